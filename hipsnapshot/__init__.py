@@ -1,0 +1,44 @@
+"""hipsnapshot: distributed checkpointing for PyTorch on AMD Instinct MI355X.
+
+Public API (same surface as TorchSnapshot, reference `torchsnapshot/__init__.py:10-41`):
+``Snapshot``, ``PendingSnapshot``, ``Stateful``, ``StateDict``, ``RNGState``,
+``__version__``.
+"""
+
+import sys as _sys
+
+import torch as _torch  # noqa: F401  (load torch's HIP runtime before our .so)
+
+from .snapshot import PendingSnapshot, Snapshot
+from .stateful import AppState, RNGState, StateDict, Stateful
+from .version import __hipsnapshot_version__, __version__
+
+
+def _is_notebook() -> bool:
+    try:
+        from IPython import get_ipython  # type: ignore
+
+        shell = get_ipython()
+        return shell is not None and ("Terminal" not in type(shell).__name__)
+    except Exception:
+        return False
+
+
+if _is_notebook():  # pragma: no cover - Jupyter/Colab nest their own loop
+    try:
+        import nest_asyncio  # type: ignore
+
+        nest_asyncio.apply()
+    except Exception:
+        pass
+
+__all__ = [
+    "Snapshot",
+    "PendingSnapshot",
+    "Stateful",
+    "StateDict",
+    "RNGState",
+    "AppState",
+    "__version__",
+    "__hipsnapshot_version__",
+]

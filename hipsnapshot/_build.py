@@ -1,0 +1,73 @@
+"""In-tree build of hipsnapshot's native libraries.
+
+* ``_hsio.so``  -- C++17 file-I/O engine (g++/clang++, no HIP), used on every box.
+* ``_hsgpu.so`` -- HIP data plane for gfx950 (hipcc --offload-arch=gfx950).
+
+Both are plain C ABIs loaded with ctypes, so they build in seconds without
+torch headers and travel with the repository snapshot to the GPU box.
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+HSIO_SO = os.path.join(PKG_DIR, "_hsio.so")
+HSGPU_SO = os.path.join(PKG_DIR, "_hsgpu.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+GPU_ARCH = os.environ.get("HIPSNAPSHOT_GPU_ARCH", "gfx950")
+
+
+def _stale(out: str, srcs) -> bool:
+    if not os.path.exists(out):
+        return True
+    mtime = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > mtime for s in srcs)
+
+
+def _run(cmd) -> None:
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"native build failed: {' '.join(cmd)}\n{proc.stdout}")
+
+
+def _atomic_build(out: str, cmd_for) -> None:
+    tmp = f"{out}.{os.getpid()}.tmp"
+    _run(cmd_for(tmp))
+    os.replace(tmp, out)
+
+
+def build_hsio(force: bool = False) -> str:
+    src = os.path.join(CSRC, "hsio.cpp")
+    if force or _stale(HSIO_SO, [src]):
+        cxx = shutil.which("g++") or shutil.which("c++") or os.path.join(ROCM, "llvm/bin/clang++")
+        _atomic_build(HSIO_SO, lambda out: [cxx, "-O3", "-std=c++17", "-fPIC", "-shared",
+                                            "-pthread", "-Wall", "-o", out, src])
+    return HSIO_SO
+
+
+def build_hsgpu(force: bool = False) -> str:
+    srcs = [os.path.join(CSRC, "hsgpu.hip")]
+    if force or _stale(HSGPU_SO, srcs):
+        hipcc = os.path.join(ROCM, "bin", "hipcc")
+        if not os.path.exists(hipcc):
+            hipcc = shutil.which("hipcc") or hipcc
+        _atomic_build(HSGPU_SO, lambda out: [hipcc, f"--offload-arch={GPU_ARCH}", "-O3",
+                                             "-std=c++17", "-fPIC", "-shared", "-Wall",
+                                             "-o", out] + srcs)
+    return HSGPU_SO
+
+
+def build_all(force: bool = False) -> None:
+    build_hsio(force)
+    build_hsgpu(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print(HSIO_SO)
+    print(HSGPU_SO)

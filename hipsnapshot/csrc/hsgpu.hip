@@ -1,0 +1,726 @@
+// hsgpu: MI355X (gfx950 / CDNA4) data plane for hipsnapshot.
+//
+// What the reference does through ATen on the GPU
+// (/root/reference/torchsnapshot/io_preparers/tensor.py:247-254 pageable
+// .to("cpu") in a 4-thread pool; batcher.py:141-156 slab alloc + per-member
+// DtoD + .cpu(); tensor.py:329-358 and sharded_tensor.py:278-309 host copy_ +
+// narrow for restore/resharding) is re-designed here as:
+//
+//   * a caching PINNED host pool (hipHostMalloc, 2 MiB granularity, reused
+//     across snapshots) so every DtoH/HtoD is a DMA into page-locked memory,
+//   * per-(device, slot) non-blocking copy streams ordered after the producer
+//     stream with an event (no device-wide sync, no default-stream stalls),
+//   * ONE batched strided copy/cast kernel (hs_copy_nd) that serves as
+//       K2  strided -> contiguous pack,
+//       K3  multi-tensor slab gather (descriptor table, one launch),
+//       K6  contiguous -> strided scatter with dtype conversion on restore,
+//       K7  resharding: every saved-shard x local-shard overlap in one launch,
+//     and can target host-mapped pinned memory directly (kernel stores over
+//     PCIe, "pack-to-host") or HBM (async-snapshot arena),
+//   * K5/K9 blockwise OCP-fp8 (e4m3fn) quantize / dequantize kernels.
+//
+// Work decomposition: every descriptor is cut into tiles of a fixed number of
+// elements; a tile table is built on the host and the grid walks it with a
+// grid-stride loop (grid capped at 256 CUs x 8), so thousands of tiny tensors
+// and a few huge ones share one launch and fill all 256 CUs.  Each lane moves
+// 16 bytes per access (dwordx4) wherever alignment allows (CDNA guide,
+// Guideline 13).  Wave size is 64 everywhere.
+//
+// C ABI (ctypes); no torch headers.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+constexpr int kMaxDims = 8;
+constexpr int kBlock = 256;            // 4 waves of 64
+constexpr int64_t kTileBytes = 1 << 20;  // 1 MiB of output per tile
+constexpr size_t kPinnedGranule = size_t(2) << 20;
+
+// dtype codes shared with python (hipsnapshot/ops/native.py)
+enum DType : int32_t {
+  kRaw1 = 0, kRaw2 = 1, kRaw4 = 2, kRaw8 = 3, kRaw16 = 4,  // same-type copies
+  kF16 = 10, kBF16 = 11, kF32 = 12, kF64 = 13,
+};
+
+struct CopyDesc {
+  const char* src;
+  char* dst;
+  int64_t numel;
+  int32_t ndim;
+  int32_t src_dtype;
+  int32_t dst_dtype;
+  int32_t flags;  // bit0: both fully contiguous & same type -> byte copy
+  int64_t sizes[kMaxDims];
+  int64_t src_strides[kMaxDims];  // in elements
+  int64_t dst_strides[kMaxDims];
+};
+
+struct Tile {
+  int32_t desc;
+  int32_t pad;
+  int64_t begin;  // element (or byte for flag-0 byte copies) range
+  int64_t end;
+};
+
+thread_local char g_err[512];
+
+void set_err(const char* what, hipError_t e) {
+  snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HS_CHECK(expr)                      \
+  do {                                      \
+    hipError_t _e = (expr);                 \
+    if (_e != hipSuccess) {                 \
+      set_err(#expr, _e);                   \
+      return -static_cast<int>(_e) - 1;     \
+    }                                       \
+  } while (0)
+
+__device__ __forceinline__ int elem_size(int32_t dt) {
+  switch (dt) {
+    case kRaw1: return 1;
+    case kRaw2: case kF16: case kBF16: return 2;
+    case kRaw4: case kF32: return 4;
+    case kRaw8: case kF64: return 8;
+    default: return 16;
+  }
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  // round-to-nearest-even, NaN preserved (matches torch's c10::BFloat16)
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+__device__ __forceinline__ double load_as_f64(const char* p, int32_t dt) {
+  switch (dt) {
+    case kF16: return static_cast<double>(static_cast<float>(*reinterpret_cast<const _Float16*>(p)));
+    case kBF16: return static_cast<double>(bf16_to_f32(*reinterpret_cast<const uint16_t*>(p)));
+    case kF32: return static_cast<double>(*reinterpret_cast<const float*>(p));
+    default: return *reinterpret_cast<const double*>(p);
+  }
+}
+
+__device__ __forceinline__ float load_as_f32(const char* p, int32_t dt) {
+  switch (dt) {
+    case kF16: return static_cast<float>(*reinterpret_cast<const _Float16*>(p));
+    case kBF16: return bf16_to_f32(*reinterpret_cast<const uint16_t*>(p));
+    case kF32: return *reinterpret_cast<const float*>(p);
+    default: return static_cast<float>(*reinterpret_cast<const double*>(p));
+  }
+}
+
+__device__ __forceinline__ void store_from_f32(char* p, int32_t dt, float v) {
+  switch (dt) {
+    case kF16: *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(v); break;
+    case kBF16: *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(v); break;
+    case kF32: *reinterpret_cast<float*>(p) = v; break;
+    default: *reinterpret_cast<double*>(p) = static_cast<double>(v); break;
+  }
+}
+
+__device__ __forceinline__ void store_from_f64(char* p, int32_t dt, double v) {
+  switch (dt) {
+    case kF16: *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(static_cast<float>(v)); break;
+    case kBF16: *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(static_cast<float>(v)); break;
+    case kF32: *reinterpret_cast<float*>(p) = static_cast<float>(v); break;
+    default: *reinterpret_cast<double*>(p) = v; break;
+  }
+}
+
+// Contiguous same-type byte copy of [begin, end) bytes: dwordx4 body when both
+// pointers are 16-B aligned at the tile start, byte loop otherwise.
+__device__ void copy_bytes(const char* __restrict__ src, char* __restrict__ dst,
+                           int64_t begin, int64_t end) {
+  const char* s = src + begin;
+  char* d = dst + begin;
+  int64_t n = end - begin;
+  if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+    const int64_t nv = n >> 4;
+    const uint4* sv = reinterpret_cast<const uint4*>(s);
+    uint4* dv = reinterpret_cast<uint4*>(d);
+    int64_t i = threadIdx.x;
+    // 4 independent 16-B loads in flight per lane before the stores
+    for (; i + 3 * kBlock < nv; i += 4 * kBlock) {
+      uint4 a = sv[i], b = sv[i + kBlock], c = sv[i + 2 * kBlock], e = sv[i + 3 * kBlock];
+      dv[i] = a; dv[i + kBlock] = b; dv[i + 2 * kBlock] = c; dv[i + 3 * kBlock] = e;
+    }
+    for (; i < nv; i += kBlock) dv[i] = sv[i];
+    for (int64_t j = (nv << 4) + threadIdx.x; j < n; j += kBlock) d[j] = s[j];
+  } else if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 3) == 0) {
+    const int64_t nv = n >> 2;
+    const uint32_t* sv = reinterpret_cast<const uint32_t*>(s);
+    uint32_t* dv = reinterpret_cast<uint32_t*>(d);
+    for (int64_t i = threadIdx.x; i < nv; i += kBlock) dv[i] = sv[i];
+    for (int64_t j = (nv << 2) + threadIdx.x; j < n; j += kBlock) d[j] = s[j];
+  } else {
+    for (int64_t j = threadIdx.x; j < n; j += kBlock) d[j] = s[j];
+  }
+}
+
+template <int ES>
+struct RawT;
+template <> struct RawT<1> { using T = uint8_t; };
+template <> struct RawT<2> { using T = uint16_t; };
+template <> struct RawT<4> { using T = uint32_t; };
+template <> struct RawT<8> { using T = uint64_t; };
+template <> struct RawT<16> { using T = uint4; };
+
+// Each lane owns kRun consecutive logical elements: decode the N-d index once,
+// then walk with carry propagation (one divide chain per run instead of per
+// element).  ND is a template parameter so the coordinate arrays stay in VGPRs
+// (a runtime-indexed array would spill to scratch -- CDNA guide 5.4 rule 20);
+// the host collapses mergeable dims first so ND <= 4 covers practically every
+// view (narrow/transpose/column shard).
+constexpr int kRun = 8;
+
+template <int ND>
+__device__ __forceinline__ void decode(const CopyDesc& d, int64_t linear, int64_t* coord,
+                                       int64_t* soff, int64_t* doff) {
+  int64_t s = 0, t = 0;
+#pragma unroll
+  for (int k = ND - 1; k >= 0; --k) {
+    const int64_t sz = d.sizes[k];
+    int64_t c;
+    if (k == 0) {
+      c = linear;
+    } else {
+      c = linear % sz;
+      linear /= sz;
+    }
+    coord[k] = c;
+    s += c * d.src_strides[k];
+    t += c * d.dst_strides[k];
+  }
+  *soff = s;
+  *doff = t;
+}
+
+template <int ND>
+__device__ __forceinline__ void advance(const CopyDesc& d, int64_t* coord, int64_t* soff,
+                                        int64_t* doff) {
+#pragma unroll
+  for (int k = ND - 1; k >= 0; --k) {
+    coord[k] += 1;
+    *soff += d.src_strides[k];
+    *doff += d.dst_strides[k];
+    if (k == 0 || coord[k] < d.sizes[k]) return;
+    *soff -= coord[k] * d.src_strides[k];
+    *doff -= coord[k] * d.dst_strides[k];
+    coord[k] = 0;
+  }
+}
+
+template <int ND, int ES>
+__device__ void copy_strided_same(const CopyDesc& d, int64_t begin, int64_t end) {
+  using T = typename RawT<ES>::T;
+  const T* __restrict__ src = reinterpret_cast<const T*>(d.src);
+  T* __restrict__ dst = reinterpret_cast<T*>(d.dst);
+  for (int64_t base = begin + int64_t(threadIdx.x) * kRun; base < end;
+       base += int64_t(kBlock) * kRun) {
+    int64_t coord[ND];
+    int64_t so, dof;
+    decode<ND>(d, base, coord, &so, &dof);
+    const int64_t cnt = min(int64_t(kRun), end - base);
+    T buf[kRun];
+    int64_t doffs[kRun];
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      if (r < cnt) {
+        buf[r] = src[so];
+        doffs[r] = dof;
+        advance<ND>(d, coord, &so, &dof);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      if (r < cnt) dst[doffs[r]] = buf[r];
+    }
+  }
+}
+
+template <int ND>
+__device__ void copy_strided_cast(const CopyDesc& d, int64_t begin, int64_t end) {
+  const int ses = elem_size(d.src_dtype);
+  const int des = elem_size(d.dst_dtype);
+  const bool wide = (d.src_dtype == kF64) || (d.dst_dtype == kF64);
+  for (int64_t base = begin + int64_t(threadIdx.x) * kRun; base < end;
+       base += int64_t(kBlock) * kRun) {
+    int64_t coord[ND];
+    int64_t so, dof;
+    decode<ND>(d, base, coord, &so, &dof);
+    const int64_t lim = min(base + kRun, end);
+    for (int64_t e = base; e < lim; ++e) {
+      const char* sp = d.src + so * ses;
+      char* dp = d.dst + dof * des;
+      if (wide) store_from_f64(dp, d.dst_dtype, load_as_f64(sp, d.src_dtype));
+      else store_from_f32(dp, d.dst_dtype, load_as_f32(sp, d.src_dtype));
+      advance<ND>(d, coord, &so, &dof);
+    }
+  }
+}
+
+template <int ND>
+__device__ __forceinline__ void copy_tile_nd(const CopyDesc& d, int64_t b, int64_t e) {
+  if (d.src_dtype == d.dst_dtype || d.src_dtype < kF16) {
+    switch (elem_size(d.src_dtype)) {
+      case 1: copy_strided_same<ND, 1>(d, b, e); break;
+      case 2: copy_strided_same<ND, 2>(d, b, e); break;
+      case 4: copy_strided_same<ND, 4>(d, b, e); break;
+      case 8: copy_strided_same<ND, 8>(d, b, e); break;
+      default: copy_strided_same<ND, 16>(d, b, e); break;
+    }
+  } else {
+    copy_strided_cast<ND>(d, b, e);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+hs_copy_nd(const CopyDesc* __restrict__ descs, const Tile* __restrict__ tiles, int64_t ntiles) {
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const Tile tile = tiles[t];
+    const CopyDesc& d = descs[tile.desc];
+    if (d.flags & 1) {
+      copy_bytes(d.src, d.dst, tile.begin, tile.end);
+    } else {
+      switch (d.ndim) {
+        case 1: copy_tile_nd<1>(d, tile.begin, tile.end); break;
+        case 2: copy_tile_nd<2>(d, tile.begin, tile.end); break;
+        case 3: copy_tile_nd<3>(d, tile.begin, tile.end); break;
+        case 4: copy_tile_nd<4>(d, tile.begin, tile.end); break;
+        case 5: copy_tile_nd<5>(d, tile.begin, tile.end); break;
+        case 6: copy_tile_nd<6>(d, tile.begin, tile.end); break;
+        case 7: copy_tile_nd<7>(d, tile.begin, tile.end); break;
+        default: copy_tile_nd<8>(d, tile.begin, tile.end); break;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp8 (OCP e4m3fn) blockwise quantization.  One 64-lane wave owns one block of
+// `block` elements (block = 64 * VPT); amax via 64-wide xor-shuffle reduction,
+// scale = amax / 448, payload via v_cvt_pk_fp8_f32 (gfx950: OCP encoding).
+// ---------------------------------------------------------------------------
+
+constexpr float kFp8Max = 448.0f;
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <int VPT>
+__global__ void __launch_bounds__(kBlock)
+hs_fp8_quant(const char* __restrict__ src, int32_t src_dtype, int64_t n,
+             uint8_t* __restrict__ out, float* __restrict__ scales) {
+  constexpr int kBlk = 64 * VPT;
+  const int lane = threadIdx.x & 63;
+  const int64_t nblocks = (n + kBlk - 1) / kBlk;
+  const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  const int ses = (src_dtype == kF32) ? 4 : 2;
+  for (int64_t b = wave0; b < nblocks; b += nwaves) {
+    const int64_t e0 = b * kBlk + int64_t(lane) * VPT;
+    float v[VPT];
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int64_t e = e0 + j;
+      v[j] = (e < n) ? load_as_f32(src + e * ses, src_dtype) : 0.f;
+      amax = fmaxf(amax, fabsf(v[j]));
+    }
+    amax = wave_max(amax);
+    const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
+    const float inv = 1.f / scale;
+    if (lane == 0) scales[b] = scale;
+    uint32_t words[(VPT + 3) / 4];
+#pragma unroll
+    for (int w = 0; w < (VPT + 3) / 4; ++w) {
+      float a0 = fminf(fmaxf(v[4 * w + 0] * inv, -kFp8Max), kFp8Max);
+      float a1 = (4 * w + 1 < VPT) ? fminf(fmaxf(v[4 * w + 1] * inv, -kFp8Max), kFp8Max) : 0.f;
+      float a2 = (4 * w + 2 < VPT) ? fminf(fmaxf(v[4 * w + 2] * inv, -kFp8Max), kFp8Max) : 0.f;
+      float a3 = (4 * w + 3 < VPT) ? fminf(fmaxf(v[4 * w + 3] * inv, -kFp8Max), kFp8Max) : 0.f;
+      int word = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+      word = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, word, true);
+      words[w] = static_cast<uint32_t>(word);
+    }
+    if (e0 + VPT <= n && (VPT % 4) == 0) {
+#pragma unroll
+      for (int w = 0; w < VPT / 4; ++w)
+        reinterpret_cast<uint32_t*>(out + e0)[w] = words[w];
+    } else {
+      for (int j = 0; j < VPT; ++j)
+        if (e0 + j < n) out[e0 + j] = static_cast<uint8_t>(words[j >> 2] >> (8 * (j & 3)));
+    }
+  }
+}
+
+template <int VPT>
+__global__ void __launch_bounds__(kBlock)
+hs_fp8_dequant(const uint8_t* __restrict__ q, const float* __restrict__ scales, int64_t n,
+               char* __restrict__ dst, int32_t dst_dtype) {
+  constexpr int kBlk = 64 * VPT;
+  const int des = (dst_dtype == kF32) ? 4 : (dst_dtype == kF64 ? 8 : 2);
+  const int64_t nthreads = int64_t(gridDim.x) * kBlock;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i * 4 < n; i += nthreads) {
+    const int64_t e0 = i * 4;
+    uint32_t word;
+    if (e0 + 4 <= n) {
+      word = reinterpret_cast<const uint32_t*>(q)[i];
+    } else {
+      word = 0;
+      for (int j = 0; j < 4 && e0 + j < n; ++j) word |= uint32_t(q[e0 + j]) << (8 * j);
+    }
+    const float s = scales[e0 / kBlk];
+    float f[4];
+    f[0] = __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(word), 0);
+    f[1] = __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(word), 1);
+    f[2] = __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(word), 2);
+    f[3] = __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(word), 3);
+    for (int j = 0; j < 4 && e0 + j < n; ++j) store_from_f32(dst + (e0 + j) * des, dst_dtype, f[j] * s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side state: pinned pool, copy streams, launch helpers.
+// ---------------------------------------------------------------------------
+
+struct PinnedPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> free_blocks;      // size -> ptr
+  std::unordered_map<void*, size_t> live;       // ptr -> size
+  size_t cached_bytes = 0;                        // total allocated (live + free)
+  size_t in_use_bytes = 0;
+};
+PinnedPool g_pool;
+
+struct StreamKey {
+  int dev, slot;
+  bool operator<(const StreamKey& o) const { return dev != o.dev ? dev < o.dev : slot < o.slot; }
+};
+std::mutex g_stream_mu;
+std::map<StreamKey, hipStream_t> g_streams;
+std::map<StreamKey, hipEvent_t> g_events;
+
+int get_stream(int dev, int slot, hipStream_t* out, hipEvent_t* ev) {
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  StreamKey k{dev, slot};
+  auto it = g_streams.find(k);
+  if (it == g_streams.end()) {
+    HS_CHECK(hipSetDevice(dev));
+    hipStream_t s;
+    HS_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipEvent_t e;
+    HS_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    g_streams[k] = s;
+    g_events[k] = e;
+    it = g_streams.find(k);
+  }
+  *out = it->second;
+  *ev = g_events[k];
+  return 0;
+}
+
+// Build the tile table for a descriptor batch.
+void build_tiles(const CopyDesc* descs, int n, std::vector<Tile>* tiles) {
+  for (int i = 0; i < n; ++i) {
+    const CopyDesc& d = descs[i];
+    int64_t total, step;
+    if (d.flags & 1) {
+      int es = 1;
+      switch (d.src_dtype) {
+        case kRaw1: es = 1; break;
+        case kRaw2: case kF16: case kBF16: es = 2; break;
+        case kRaw4: case kF32: es = 4; break;
+        case kRaw8: case kF64: es = 8; break;
+        default: es = 16;
+      }
+      total = d.numel * es;  // bytes
+      step = kTileBytes;
+    } else {
+      total = d.numel;
+      step = 64 * 1024;  // elements per tile on the strided/cast path
+    }
+    for (int64_t b = 0; b < total; b += step) {
+      tiles->push_back(Tile{i, 0, b, std::min(total, b + step)});
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hsg_last_error() { return g_err; }
+
+int hsg_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ---- pinned pool ----------------------------------------------------------
+
+void* hsg_pinned_acquire(uint64_t nbytes) {
+  size_t want = (std::max<size_t>(nbytes, 1) + kPinnedGranule - 1) / kPinnedGranule * kPinnedGranule;
+  {
+    std::lock_guard<std::mutex> g(g_pool.mu);
+    auto it = g_pool.free_blocks.lower_bound(want);
+    // best fit, but do not hand out a block more than 2x the request
+    if (it != g_pool.free_blocks.end() && it->first <= 2 * want) {
+      void* p = it->second;
+      size_t sz = it->first;
+      g_pool.free_blocks.erase(it);
+      g_pool.live[p] = sz;
+      g_pool.in_use_bytes += sz;
+      return p;
+    }
+  }
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    // out of pinnable memory: drop the cache and retry once
+    std::vector<void*> drop;
+    {
+      std::lock_guard<std::mutex> g(g_pool.mu);
+      for (auto& kv : g_pool.free_blocks) { drop.push_back(kv.second); g_pool.cached_bytes -= kv.first; }
+      g_pool.free_blocks.clear();
+    }
+    for (void* q : drop) (void)hipHostFree(q);
+    e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      set_err("hipHostMalloc", e);
+      return nullptr;
+    }
+  }
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  g_pool.live[p] = want;
+  g_pool.cached_bytes += want;
+  g_pool.in_use_bytes += want;
+  return p;
+}
+
+int hsg_pinned_release(void* p) {
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  auto it = g_pool.live.find(p);
+  if (it == g_pool.live.end()) return -1;
+  g_pool.free_blocks.emplace(it->second, p);
+  g_pool.in_use_bytes -= it->second;
+  g_pool.live.erase(it);
+  return 0;
+}
+
+void hsg_pinned_stats(uint64_t* cached, uint64_t* in_use) {
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  *cached = g_pool.cached_bytes;
+  *in_use = g_pool.in_use_bytes;
+}
+
+uint64_t hsg_pinned_trim() {
+  std::vector<std::pair<size_t, void*>> drop;
+  {
+    std::lock_guard<std::mutex> g(g_pool.mu);
+    for (auto& kv : g_pool.free_blocks) drop.emplace_back(kv.first, kv.second);
+    g_pool.free_blocks.clear();
+    for (auto& kv : drop) g_pool.cached_bytes -= kv.first;
+  }
+  uint64_t freed = 0;
+  for (auto& kv : drop) { (void)hipHostFree(kv.second); freed += kv.first; }
+  return freed;
+}
+
+// ---- DMA copies on side streams --------------------------------------------
+
+// Copy `n` bytes between host and device on copy stream (dev, slot), ordered
+// after all work already queued on `producer` (a torch stream, may be null).
+// kind: 0 = D2H, 1 = H2D, 2 = D2D.  If `sync` is nonzero the call blocks until
+// the copy is done (ctypes releases the GIL around it).
+int hsg_memcpy(int dev, int slot, void* dst, const void* src, uint64_t n, int kind,
+               void* producer, int sync) {
+  HS_CHECK(hipSetDevice(dev));
+  hipStream_t s;
+  hipEvent_t ev;
+  int r = get_stream(dev, slot, &s, &ev);
+  if (r) return r;
+  if (producer) {
+    HS_CHECK(hipEventRecord(ev, static_cast<hipStream_t>(producer)));
+    HS_CHECK(hipStreamWaitEvent(s, ev, 0));
+  }
+  hipMemcpyKind k = kind == 0 ? hipMemcpyDeviceToHost
+                  : kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  if (n) HS_CHECK(hipMemcpyAsync(dst, src, n, k, s));
+  if (sync) HS_CHECK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// Make `consumer` (torch stream) wait for everything queued on copy stream
+// (dev, slot) -- used after H2D restores so the trainer sees the data.
+int hsg_stream_join(int dev, int slot, void* consumer) {
+  HS_CHECK(hipSetDevice(dev));
+  hipStream_t s;
+  hipEvent_t ev;
+  int r = get_stream(dev, slot, &s, &ev);
+  if (r) return r;
+  HS_CHECK(hipEventRecord(ev, s));
+  HS_CHECK(hipStreamWaitEvent(static_cast<hipStream_t>(consumer), ev, 0));
+  return 0;
+}
+
+int hsg_stream_sync(int dev, int slot) {
+  HS_CHECK(hipSetDevice(dev));
+  hipStream_t s;
+  hipEvent_t ev;
+  int r = get_stream(dev, slot, &s, &ev);
+  if (r) return r;
+  HS_CHECK(hipStreamSynchronize(s));
+  return 0;
+}
+
+void* hsg_copy_stream(int dev, int slot) {
+  hipStream_t s;
+  hipEvent_t ev;
+  if (get_stream(dev, slot, &s, &ev)) return nullptr;
+  return s;
+}
+
+int hsg_sync_stream_handle(void* stream) {
+  HS_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+uint64_t hsg_desc_size() { return sizeof(CopyDesc); }
+
+// Batched strided copy / cast.  `descs` is a host array of `n` CopyDesc (see
+// hipsnapshot/ops/native.py for the packing); `scratch` is a device (or
+// host-mapped) workspace of at least hsg_copy_workspace_bytes() bytes used for
+// the descriptor + tile tables (copied H2D on `stream`, so the host arrays may
+// be reused as soon as this returns).  `stream` == null -> copy stream (dev,slot).
+uint64_t hsg_copy_workspace_bytes(const void* descs, int n) {
+  std::vector<Tile> tiles;
+  build_tiles(static_cast<const CopyDesc*>(descs), n, &tiles);
+  return sizeof(CopyDesc) * n + sizeof(Tile) * tiles.size() + 256;
+}
+
+int hsg_copy_nd(int dev, const void* descs, int n, void* workspace, uint64_t ws_bytes,
+                void* pinned_stage, void* stream, int sync) {
+  HS_CHECK(hipSetDevice(dev));
+  if (n <= 0) return 0;
+  std::vector<Tile> tiles;
+  const CopyDesc* d = static_cast<const CopyDesc*>(descs);
+  build_tiles(d, n, &tiles);
+  if (tiles.empty()) return 0;
+  const size_t dbytes = sizeof(CopyDesc) * n;
+  const size_t tbytes = sizeof(Tile) * tiles.size();
+  const size_t toff = (dbytes + 255) / 256 * 256;
+  if (toff + tbytes > ws_bytes) {
+    snprintf(g_err, sizeof(g_err), "workspace too small: need %zu have %llu", toff + tbytes,
+             (unsigned long long)ws_bytes);
+    return -1000;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // stage tables through pinned memory so the H2D is a true async DMA
+  char* stage = static_cast<char*>(pinned_stage);
+  std::memcpy(stage, d, dbytes);
+  std::memcpy(stage + toff, tiles.data(), tbytes);
+  char* ws = static_cast<char*>(workspace);
+  HS_CHECK(hipMemcpyAsync(ws, stage, toff + tbytes, hipMemcpyHostToDevice, s));
+  const int64_t ntiles = static_cast<int64_t>(tiles.size());
+  const int grid = static_cast<int>(std::min<int64_t>(ntiles, 256 * 8));
+  hipLaunchKernelGGL(hs_copy_nd, dim3(grid), dim3(kBlock), 0, s,
+                     reinterpret_cast<const CopyDesc*>(ws),
+                     reinterpret_cast<const Tile*>(ws + toff), ntiles);
+  HS_CHECK(hipGetLastError());
+  if (sync) HS_CHECK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// fp8 quantize: src (bf16/f16/f32, contiguous, device) -> out fp8 bytes [n] +
+// scales fp32 [ceil(n/block)], block = 64*vpt with vpt in {2,4,8,16}.
+int hsg_fp8_quantize(int dev, const void* src, int src_dtype, int64_t n, void* out,
+                     void* scales, int vpt, void* stream) {
+  HS_CHECK(hipSetDevice(dev));
+  if (n <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t blk = 64LL * vpt;
+  const int64_t nblocks = (n + blk - 1) / blk;
+  const int64_t waves_per_wg = kBlock / 64;
+  const int grid = static_cast<int>(std::min<int64_t>((nblocks + waves_per_wg - 1) / waves_per_wg, 256 * 8));
+  const char* sp = static_cast<const char*>(src);
+  uint8_t* op = static_cast<uint8_t*>(out);
+  float* sc = static_cast<float*>(scales);
+  switch (vpt) {
+    case 2: hipLaunchKernelGGL(hs_fp8_quant<2>, dim3(grid), dim3(kBlock), 0, s, sp, src_dtype, n, op, sc); break;
+    case 4: hipLaunchKernelGGL(hs_fp8_quant<4>, dim3(grid), dim3(kBlock), 0, s, sp, src_dtype, n, op, sc); break;
+    case 8: hipLaunchKernelGGL(hs_fp8_quant<8>, dim3(grid), dim3(kBlock), 0, s, sp, src_dtype, n, op, sc); break;
+    case 16: hipLaunchKernelGGL(hs_fp8_quant<16>, dim3(grid), dim3(kBlock), 0, s, sp, src_dtype, n, op, sc); break;
+    default: snprintf(g_err, sizeof(g_err), "unsupported vpt %d", vpt); return -1001;
+  }
+  HS_CHECK(hipGetLastError());
+  return 0;
+}
+
+int hsg_fp8_dequantize(int dev, const void* q, const void* scales, int64_t n, void* dst,
+                       int dst_dtype, int vpt, void* stream) {
+  HS_CHECK(hipSetDevice(dev));
+  if (n <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t words = (n + 3) / 4;
+  const int grid = static_cast<int>(std::min<int64_t>((words + kBlock - 1) / kBlock, 256 * 8));
+  const uint8_t* qp = static_cast<const uint8_t*>(q);
+  const float* sc = static_cast<const float*>(scales);
+  char* dp = static_cast<char*>(dst);
+  switch (vpt) {
+    case 2: hipLaunchKernelGGL(hs_fp8_dequant<2>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;
+    case 4: hipLaunchKernelGGL(hs_fp8_dequant<4>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;
+    case 8: hipLaunchKernelGGL(hs_fp8_dequant<8>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;
+    case 16: hipLaunchKernelGGL(hs_fp8_dequant<16>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;
+    default: snprintf(g_err, sizeof(g_err), "unsupported vpt %d", vpt); return -1001;
+  }
+  HS_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ---- managed (UVM) memory helpers (fbgemm uvm_to_cpu equivalent, K11) --------
+
+int hsg_is_managed(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return attr.isManaged ? 1 : 0;
+}
+
+void* hsg_managed_alloc(int dev, uint64_t n) {
+  if (hipSetDevice(dev) != hipSuccess) return nullptr;
+  void* p = nullptr;
+  hipError_t e = hipMallocManaged(&p, n, hipMemAttachGlobal);
+  if (e != hipSuccess) { set_err("hipMallocManaged", e); return nullptr; }
+  return p;
+}
+
+int hsg_managed_free(void* p) {
+  HS_CHECK(hipFree(p));
+  return 0;
+}
+
+}  // extern "C"

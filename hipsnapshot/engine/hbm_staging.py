@@ -1,0 +1,109 @@
+"""Async-take "freeze" of device state into spare HBM.
+
+The reference makes ``async_take`` consistent by finishing every DtoH copy
+before returning (`/root/reference/torchsnapshot/scheduler.py:330-337`), so the
+trainer is blocked for state_bytes / PCIe bandwidth (>= 4.6 s for a full
+288 GB MI355X at 63 GB/s).  MI355X has 288 GB of HBM3E per GPU and ~5-6 TB/s of
+copy bandwidth, so instead:
+
+1. every CUDA source of the pending write requests (plain tensors, chunk and
+   shard views, members of device slabs -- strided or not) is described in
+   ONE ``hs_copy_nd`` descriptor table;
+2. one kernel launch on the trainer's current stream copies them all into a
+   freshly allocated HBM arena (stream order makes the copy consistent with
+   everything the trainer already enqueued and everything it enqueues later,
+   without any host synchronisation);
+3. the stagers are re-pointed at arena views and wait on an event recorded
+   after the launch; the background commit thread drains the arena to storage.
+
+Falls back (per device) to the host-staging path when the arena does not fit
+in free HBM minus ``HBM_STAGING_RESERVE_BYTES``.
+"""
+
+from __future__ import annotations
+
+import logging
+from collections import defaultdict
+from typing import Dict, List
+
+import torch
+
+from .. import knobs
+from ..io_types import WriteReq
+from ..ops import native
+
+logger = logging.getLogger(__name__)
+
+_ALIGN = 256
+
+
+def _collect(write_reqs: List[WriteReq]):
+    """(stager-like object with .tensor/.producer) for every CUDA source."""
+    from ..io.batcher import GPUBatchedBufferStager
+    from ..io.tensor import TensorBufferStager
+
+    out = []
+    for wr in write_reqs:
+        st = wr.buffer_stager
+        if isinstance(st, TensorBufferStager) and st.tensor.is_cuda \
+                and st._tensor_prepare_func is None:
+            out.append(st)
+        elif isinstance(st, GPUBatchedBufferStager):
+            out.extend(m for _, m in st.members)
+    return out
+
+
+def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
+    """Returns {device: arena_bytes} for the devices that were frozen."""
+    if not native.gpu_available():
+        return {}
+    stagers = _collect(write_reqs)
+    if not stagers:
+        return {}
+    by_dev = defaultdict(list)
+    for st in stagers:
+        by_dev[st.tensor.device.index if st.tensor.device.index is not None
+               else torch.cuda.current_device()].append(st)
+    frozen = {}
+    for dev, sts in by_dev.items():
+        offs, total = [], 0
+        for st in sts:
+            offs.append(total)
+            nb = st.tensor.numel() * st.tensor.element_size()
+            total += (nb + _ALIGN - 1) // _ALIGN * _ALIGN
+        free, _ = torch.cuda.mem_get_info(dev)
+        if total + knobs.hbm_staging_reserve_bytes() > free:
+            logger.info(f"HBM staging skipped on cuda:{dev}: need {total} B, free {free} B")
+            continue
+        stream = torch.cuda.current_stream(dev)
+        with torch.cuda.device(dev):
+            arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
+            batch = native.CopyBatch()
+            views = []
+            for st, off in zip(sts, offs):
+                t = st.tensor.detach()
+                view = arena[off: off + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
+                if t.numel():
+                    batch.add(t.data_ptr(), t.dtype, t.stride(), view.data_ptr(), t.dtype,
+                              view.stride(), list(t.shape), t.element_size())
+                views.append(view)
+            # producers may differ from the current stream: order after them
+            for p in {st.producer for st in sts if st.producer}:
+                if p != stream.cuda_stream:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.ExternalStream(p))
+                    stream.wait_event(ev)
+            keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
+            done = torch.cuda.Event()
+            done.record(stream)
+        for st, view in zip(sts, views):
+            st.tensor = view
+            st.producer = 0
+            st.frozen = True
+            st.wait_event = done
+        # keep the descriptor tables alive until the copy ran
+        done_keep = (keep, done)
+        for st in sts:
+            st.arena_keepalive = done_keep
+        frozen[dev] = total
+    return frozen

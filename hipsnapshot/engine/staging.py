@@ -1,0 +1,242 @@
+"""Device <-> host staging on MI355X.
+
+Every GPU byte that leaves or enters HBM goes through here:
+
+* D2H of one tensor: pinned pool block + ``hipMemcpyAsync`` on a per-thread
+  copy stream ordered after the producer stream (SDMA, no pageable bounce) --
+  replaces the reference's pageable ``tensor.to("cpu")`` in a 4-thread pool
+  (`/root/reference/torchsnapshot/io_preparers/tensor.py:247-254`).
+* non-contiguous views are packed by the ``hs_copy_nd`` kernel straight into
+  host-mapped pinned memory (K2 fused with the transfer).
+* slabs of small tensors are gathered into one device buffer by ONE kernel
+  launch and moved with ONE DMA (K3; reference `batcher.py:101-159` did one DtoD
+  per member and a pageable ``.cpu()``).
+* restore: raw bytes land in pinned memory, one H2D DMA to a device scratch,
+  then ONE ``hs_copy_nd`` launch scatters (and casts) into every destination
+  view (K6/K7; reference `tensor.py:329-358`, `sharded_tensor.py:278-309` did a
+  host ``copy_`` per region).
+
+CPU tensors are never moved through the GPU.
+"""
+
+from __future__ import annotations
+
+import threading
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from ..format.serialization import contiguous_cpu_bytes_view, tensor_from_bytes
+from ..io_types import StagedBuffer, buffer_address
+from ..ops import native
+
+_tls = threading.local()
+_slot_lock = threading.Lock()
+_next_slot = [0]
+NUM_COPY_SLOTS = 4
+
+
+def copy_slot() -> int:
+    """A copy-stream slot per OS thread (concurrent DMAs from executor threads)."""
+    s = getattr(_tls, "slot", None)
+    if s is None:
+        with _slot_lock:
+            s = _next_slot[0] % NUM_COPY_SLOTS
+            _next_slot[0] += 1
+        _tls.slot = s
+    return s
+
+
+def device_of(t: torch.Tensor) -> int:
+    idx = t.device.index
+    return torch.cuda.current_device() if idx is None else idx
+
+
+def producer_stream_handle(t: torch.Tensor) -> int:
+    """The stream that produces ``t`` (current stream of its device, captured
+    on the calling thread -- call at plan time on the training thread)."""
+    if not t.is_cuda:
+        return 0
+    return int(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _pinned_staged(nbytes: int) -> Tuple[native.PinnedBuffer, StagedBuffer]:
+    pb = native.PinnedBuffer(nbytes)
+    return pb, StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
+
+
+def _elem_strides_ok(t: torch.Tensor) -> bool:
+    return t.dim() <= native.MAX_DIMS
+
+
+def d2h_tensor(t: torch.Tensor, producer: int) -> StagedBuffer:
+    """Copy a CUDA tensor's logical bytes (C order) into a pinned block."""
+    nbytes = t.numel() * t.element_size()
+    pb, staged = _pinned_staged(nbytes)
+    if nbytes == 0:
+        return staged
+    dev = device_of(t)
+    slot = copy_slot()
+    try:
+        if t.is_contiguous():
+            native.memcpy(dev, slot, pb.ptr, t.data_ptr(), nbytes, native.D2H, producer, sync=True)
+        else:
+            # pack-to-host: kernel stores the packed view over PCIe into the
+            # host-mapped pinned block, ordered after the producer stream.
+            native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
+            batch = native.CopyBatch()
+            batch.add(t.data_ptr(), t.dtype, t.stride(), pb.ptr, t.dtype,
+                      _contig_strides(t.shape), list(t.shape), t.element_size())
+            batch.launch(dev, native.copy_stream(dev, slot), sync=True)
+    except BaseException:
+        staged.release()
+        raise
+    return staged
+
+
+def _contig_strides(shape: Sequence[int]) -> List[int]:
+    st = [1] * len(shape)
+    for i in range(len(shape) - 2, -1, -1):
+        st[i] = st[i + 1] * max(int(shape[i + 1]), 1)
+    return st
+
+
+def cpu_tensor_bytes(t: torch.Tensor, copy: bool) -> StagedBuffer:
+    """Host bytes of a CPU tensor; zero-copy unless ``copy`` (async snapshot)."""
+    t = t.detach()
+    if copy or not t.is_contiguous():
+        nbytes = t.numel() * t.element_size()
+        if native.hsgpu_loaded() and native.gpu_available() and nbytes >= (1 << 20):
+            # pinned destination: the block is reused across snapshots
+            pb, staged = _pinned_staged(nbytes)
+            dst = pb.as_tensor(nbytes).view(t.dtype).view(t.shape) if nbytes else None
+            if dst is not None:
+                dst.copy_(t)
+            return staged
+        out = torch.empty(t.shape, dtype=t.dtype)
+        out.copy_(t)
+        t = out
+    mv = contiguous_cpu_bytes_view(t)
+    return StagedBuffer(mv, keepalive=t)
+
+
+def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int,
+                   producers: Sequence[int], via_device_slab: bool = True) -> StagedBuffer:
+    """Pack many CUDA tensors into one host slab: ``members`` = (tensor, offset).
+
+    Default path: one ``hs_copy_nd`` launch gathers every member into a device
+    slab (HBM-speed), then ONE SDMA transfer moves the slab to pinned memory.
+    If the device slab cannot be allocated the kernel writes the members
+    straight into host-mapped pinned memory instead.
+    """
+    pb, staged = _pinned_staged(total_bytes)
+    if total_bytes == 0 or not members:
+        return staged
+    dev = device_of(members[0][0])
+    slot = copy_slot()
+    stream = native.copy_stream(dev, slot)
+    try:
+        for producer in producers:
+            native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
+        slab = None
+        if via_device_slab:
+            try:
+                slab = torch.empty(total_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+            except torch.cuda.OutOfMemoryError:
+                slab = None
+        base = slab.data_ptr() if slab is not None else pb.ptr
+        batch = native.CopyBatch()
+        for t, off in members:
+            batch.add(t.data_ptr(), t.dtype, t.stride(), base + off, t.dtype,
+                      _contig_strides(t.shape), list(t.shape), t.element_size())
+        keep = batch.launch(dev, stream, sync=False)
+        if slab is not None:
+            native.memcpy(dev, slot, pb.ptr, slab.data_ptr(), total_bytes, native.D2H, None,
+                          sync=False)
+        native.stream_sync(dev, slot)
+        if keep is not None:
+            keep[0].release()
+        del slab
+    except BaseException:
+        staged.release()
+        raise
+    return staged
+
+
+def h2d_into(dst: torch.Tensor, host_addr: int, nbytes: int, src_dtype: torch.dtype,
+             src_shape: Sequence[int], producer: int = 0) -> None:
+    """Load C-order bytes at ``host_addr`` (ideally pinned) into CUDA ``dst``.
+
+    Same dtype + contiguous destination -> one DMA.  Otherwise one DMA into a
+    device scratch followed by one scatter/cast kernel launch.
+    """
+    dev = device_of(dst)
+    slot = copy_slot()
+    if dst.dtype == src_dtype and dst.is_contiguous() and list(dst.shape) == list(src_shape):
+        native.memcpy(dev, slot, dst.data_ptr(), host_addr, nbytes, native.H2D, producer or None,
+                      sync=True)
+        return
+    scatter_host_regions(host_addr, nbytes, [(src_dtype, src_shape, 0, None, dst)], dev,
+                         producer)
+
+
+def scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
+                         producer: int = 0) -> None:
+    """One H2D of ``nbytes`` at ``host_addr`` then ONE kernel launch that copies
+    every region into its destination view.
+
+    ``regions``: list of (src_dtype, src_shape, byte_offset_in_buffer,
+    narrows or None, dst_view) where ``narrows`` is a list of
+    (dim, start, length) applied to the source tensor view before copying.
+    """
+    slot = copy_slot()
+    scratch = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
+    # order after pending work on the destinations' stream (captured at plan time)
+    native.memcpy(dev, slot, scratch.data_ptr(), host_addr, nbytes, native.H2D, producer or None,
+                  sync=False)
+    batch = native.CopyBatch()
+    fallbacks = []
+    for src_dtype, src_shape, off, narrows, dst in regions:
+        es = torch.empty(0, dtype=src_dtype).element_size()
+        n = 1
+        for z in src_shape:
+            n *= int(z)
+        src = scratch[off: off + n * es].view(src_dtype).view(list(src_shape))
+        if narrows:
+            for d, s, ln in narrows:
+                src = src.narrow(d, s, ln)
+        if native.can_cast_on_device(src_dtype, dst.dtype) and dst.dim() <= native.MAX_DIMS:
+            batch.add(src.data_ptr(), src.dtype, src.stride(), dst.data_ptr(), dst.dtype,
+                      dst.stride(), list(src.shape), src.element_size())
+        else:
+            fallbacks.append((src, dst))
+    keep = batch.launch(dev, native.copy_stream(dev, slot), sync=False)
+    native.stream_sync(dev, slot)
+    if keep is not None:
+        keep[0].release()
+    if fallbacks:
+        # integer<->float and other exotic casts: ATen on the current stream
+        for src, dst in fallbacks:
+            dst.copy_(src)
+        torch.cuda.synchronize(dev)
+    del scratch
+
+
+def host_view_as_tensor(buf, dtype: torch.dtype, shape: Sequence[int]) -> torch.Tensor:
+    return tensor_from_bytes(buf, dtype, shape)
+
+
+def staged_from_tensor_storage(t: torch.Tensor) -> Optional[StagedBuffer]:
+    """Writable host destination aliasing a contiguous CPU tensor's bytes."""
+    if t.device.type != "cpu" or not t.is_contiguous() or t.is_quantized:
+        return None
+    if t.numel() == 0:
+        return None
+    mv = memoryview(t.detach().reshape(-1).view(torch.uint8).numpy()).cast("B")
+    return StagedBuffer(mv, addr=t.data_ptr(), keepalive=t)
+
+
+def host_buffer_addr(buf) -> int:
+    if isinstance(buf, StagedBuffer):
+        return buf.addr
+    return buffer_address(buf)

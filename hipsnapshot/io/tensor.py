@@ -1,0 +1,304 @@
+"""Plain-tensor write/read planning: ``TensorEntry`` + stager + consumer.
+
+Behavioural reference: `/root/reference/torchsnapshot/io_preparers/tensor.py:47-403`
+(serializer choice, in-place load when dtype+shape match, tiled reads under a
+buffer limit, quantized-aware ``tensor_copy``).  What is different:
+
+* staging of CUDA tensors goes through ``engine.staging`` (pinned pool + SDMA
+  on a side stream, or the pack kernel for strided views), never pageable
+  ``.cpu()``;
+* async snapshots copy EVERY host tensor before returning (the reference's
+  enum-vs-string comparison made that copy dead code);
+* ``_tensor_prepare_func`` output is what gets staged (reference staged the
+  original tensor, Appendix C #2);
+* reads land directly in the destination: CPU targets are filled in place by
+  the storage engine (no intermediate buffer), CUDA targets get a pinned
+  buffer followed by DMA (+ cast kernel when the dtype/strides differ);
+* opt-in ``hipsnapshot_fp8_block`` serializer (GPU fp8 quantized save).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import math
+from concurrent.futures import Executor
+from typing import Any, Callable, List, Optional, Tuple, Union
+
+import torch
+
+from ..format.manifest import ChunkedTensorEntry, TensorEntry
+from ..format.serialization import (
+    SUPPORTED_QUANTIZED_DTYPES,
+    Serializer,
+    dtype_to_element_size,
+    dtype_to_string,
+    is_buffer_protocol_dtype,
+    string_to_dtype,
+    tensor_from_bytes,
+    torch_load_from_bytes,
+    torch_save_as_bytes,
+)
+from ..io_types import BufferConsumer, BufferStager, Future, ReadReq, StagedBuffer, WriteReq
+from ..engine import staging
+
+PrepareFunc = Callable[[torch.Tensor, bool], torch.Tensor]
+
+
+async def run_in_executor(executor: Optional[Executor], fn, *args):
+    if executor is None:
+        return fn(*args)
+    return await asyncio.get_running_loop().run_in_executor(executor, fn, *args)
+
+
+def tensor_nbytes_from_entry(entry: Union[TensorEntry, ChunkedTensorEntry]) -> int:
+    n = 1
+    for s in entry.shape:
+        n *= int(s)
+    return n * dtype_to_element_size(string_to_dtype(entry.dtype))
+
+
+def is_uvm_like(t: torch.Tensor) -> bool:
+    from ..ops.uvm import is_uvm_tensor
+
+    return is_uvm_tensor(t)
+
+
+class TensorIOPreparer:
+    @staticmethod
+    def prepare_write(storage_path: str, tensor: torch.Tensor, is_async_snapshot: bool = False,
+                      _tensor_prepare_func: Optional[PrepareFunc] = None,
+                      serializer: Optional[str] = None) -> Tuple[TensorEntry, List[WriteReq]]:
+        proc = tensor if _tensor_prepare_func is None else _tensor_prepare_func(tensor, True)
+        if proc.shape != tensor.shape:
+            raise RuntimeError(
+                "_tensor_prepare_func shouldn't change the tensor's shape "
+                f"(changed from {tensor.shape} to {proc.shape}).")
+        quant = None
+        if serializer == Serializer.FP8_BLOCK.value:
+            from ..ops.quant import fp8_entry_quant_info, fp8_supported
+
+            if not fp8_supported(proc):
+                serializer = None
+            else:
+                quant = fp8_entry_quant_info(proc)
+        if serializer is None:
+            serializer = (Serializer.BUFFER_PROTOCOL.value if is_buffer_protocol_dtype(proc.dtype)
+                          else Serializer.TORCH_SAVE.value)
+        entry = TensorEntry(location=storage_path, serializer=serializer,
+                            dtype=dtype_to_string(proc.dtype), shape=list(proc.shape),
+                            replicated=False, quant=quant)
+        stager = TensorBufferStager(tensor=tensor, entry=entry,
+                                    is_async_snapshot=is_async_snapshot,
+                                    _tensor_prepare_func=_tensor_prepare_func)
+        return entry, [WriteReq(path=storage_path, buffer_stager=stager)]
+
+    @classmethod
+    def prepare_read(cls, entry: TensorEntry, tensor_out: Optional[torch.Tensor] = None,
+                     buffer_size_limit_bytes: Optional[int] = None
+                     ) -> Tuple[List[ReadReq], Future]:
+        if tensor_out is None or not cls.can_load_inplace(entry, tensor_out):
+            tensor_out = cls.empty_tensor_from_entry(entry)
+        if (buffer_size_limit_bytes is not None
+                and entry.serializer == Serializer.BUFFER_PROTOCOL.value):
+            return cls.prepare_read_tiled(entry, tensor_out, buffer_size_limit_bytes)
+        consumer = TensorBufferConsumer(tensor=tensor_out, entry=entry)
+        return [ReadReq(path=entry.location, byte_range=entry.byte_range_tuple,
+                        buffer_consumer=consumer)], Future(obj=tensor_out)
+
+    @classmethod
+    def prepare_read_tiled(cls, entry: TensorEntry, tensor_out: torch.Tensor,
+                           buffer_size_limit_bytes: int) -> Tuple[List[ReadReq], Future]:
+        """Split one blob into byte-ranged reads of <= limit bytes (dim-0 tiles
+        of the flattened tensor when it is viewable as 1-D, else dim-0 chunks)."""
+        total = tensor_nbytes_from_entry(entry)
+        n_chunks = max(1, math.ceil(total / max(buffer_size_limit_bytes, 1)))
+        target = tensor_out
+        try:
+            target = tensor_out.view(-1)
+        except RuntimeError:
+            pass
+        es = dtype_to_element_size(string_to_dtype(entry.dtype))
+        chunks = torch.chunk(target, chunks=n_chunks, dim=0) if target.numel() else [target]
+        base = entry.byte_range[0] if entry.byte_range is not None else 0
+        offset = 0
+        reqs = []
+        for ch in chunks:
+            nb = ch.numel() * es
+            sub = TensorEntry(location=entry.location, serializer=entry.serializer,
+                              dtype=entry.dtype, shape=list(ch.shape),
+                              replicated=entry.replicated)
+            reqs.append(ReadReq(path=entry.location,
+                                byte_range=(base + offset, base + offset + nb),
+                                buffer_consumer=TensorBufferConsumer(tensor=ch, entry=sub)))
+            offset += nb
+        return reqs, Future(obj=tensor_out)
+
+    @staticmethod
+    def get_tensor_size_from_entry(entry) -> int:
+        return tensor_nbytes_from_entry(entry)
+
+    @staticmethod
+    def can_load_inplace(entry: Union[TensorEntry, ChunkedTensorEntry], obj: Any) -> bool:
+        if not isinstance(obj, torch.Tensor) or _is_dtensor(obj):
+            return False
+        return string_to_dtype(entry.dtype) == obj.dtype and list(entry.shape) == list(obj.shape)
+
+    @staticmethod
+    def empty_tensor_from_entry(entry: Union[TensorEntry, ChunkedTensorEntry]) -> torch.Tensor:
+        dtype = string_to_dtype(entry.dtype)
+        if dtype in SUPPORTED_QUANTIZED_DTYPES:
+            raise RuntimeError("Allocating an empty quantized tensor is not supported yet.")
+        return torch.empty(list(entry.shape), dtype=dtype)
+
+
+def _is_dtensor(t) -> bool:
+    try:
+        from torch.distributed.tensor import DTensor
+    except Exception:  # pragma: no cover
+        return False
+    return isinstance(t, DTensor)
+
+
+class TensorBufferStager(BufferStager):
+    def __init__(self, tensor: torch.Tensor, entry: TensorEntry, is_async_snapshot: bool,
+                 _tensor_prepare_func: Optional[PrepareFunc] = None) -> None:
+        self.tensor = tensor
+        self.entry = entry
+        self.is_async_snapshot = is_async_snapshot
+        self._tensor_prepare_func = _tensor_prepare_func
+        self.producer = staging.producer_stream_handle(tensor)
+        # set by the async-take HBM snapshot: tensor already copied to an
+        # arena that nobody else mutates -> no extra host copy needed
+        self.frozen = False
+        self.wait_event = None  # torch.cuda.Event guarding a frozen HBM copy
+
+    def _source(self) -> torch.Tensor:
+        t = self.tensor
+        if self._tensor_prepare_func is not None:
+            t = self._tensor_prepare_func(t, False)
+        return t.detach()
+
+    async def stage_buffer(self, executor: Optional[Executor] = None):
+        t = self._source()
+        ser = self.entry.serializer
+        if ser == Serializer.BUFFER_PROTOCOL.value:
+            if t.is_cuda:
+                return await run_in_executor(executor, self._d2h, t)
+            # async snapshots must not alias live host memory (Appendix C #1);
+            # a prepare-func result that owns fresh storage needs no copy.
+            fresh = (self._tensor_prepare_func is not None
+                     and t.untyped_storage().data_ptr()
+                     != self.tensor.untyped_storage().data_ptr())
+            copy = self.is_async_snapshot and not self.frozen and not fresh
+            return await run_in_executor(executor, staging.cpu_tensor_bytes, t, copy)
+        if ser == Serializer.FP8_BLOCK.value:
+            from ..ops.quant import stage_fp8
+
+            return await run_in_executor(executor, stage_fp8, t, self.entry, self.producer)
+        if ser == Serializer.TORCH_SAVE.value:
+            return await run_in_executor(executor, _torch_save_tensor, t)
+        raise ValueError(f"Unrecognized serializer: {ser}.")
+
+    def _d2h(self, t: torch.Tensor):
+        if self.wait_event is not None:
+            self.wait_event.synchronize()
+        return staging.d2h_tensor(t, self.producer)
+
+    def get_staging_cost_bytes(self) -> int:
+        n = tensor_nbytes_from_entry(self.entry)
+        return 2 * n if self.entry.serializer == Serializer.TORCH_SAVE.value else n
+
+
+def _torch_save_tensor(t: torch.Tensor) -> bytes:
+    if t.is_cuda:
+        t = t.cpu()
+    elif t.numel() != t.untyped_storage().nbytes() // max(t.element_size(), 1):
+        # a view of a larger storage: torch.save would write the whole storage
+        t = t.clone()
+    return torch_save_as_bytes(t)
+
+
+def deserialize_tensor(buf, entry: TensorEntry) -> torch.Tensor:
+    if entry.serializer == Serializer.TORCH_SAVE.value:
+        # tensor payloads (complex / quantized dtypes) load weights-only
+        return torch_load_from_bytes(buf, trusted=False)
+    if entry.serializer == Serializer.BUFFER_PROTOCOL.value:
+        return tensor_from_bytes(buf, string_to_dtype(entry.dtype), entry.shape)
+    if entry.serializer == Serializer.FP8_BLOCK.value:
+        from ..ops.quant import dequantize_host_fp8
+
+        return dequantize_host_fp8(buf, entry)
+    raise ValueError(f"Unrecognized serializer: {entry.serializer}.")
+
+
+class TensorBufferConsumer(BufferConsumer):
+    def __init__(self, tensor: torch.Tensor, entry: TensorEntry) -> None:
+        self.tensor = tensor
+        self.entry = entry
+        self.producer = staging.producer_stream_handle(tensor)
+        self._direct = False
+
+    def _nbytes(self) -> int:
+        return tensor_nbytes_from_entry(self.entry)
+
+    def get_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
+        if self.entry.serializer != Serializer.BUFFER_PROTOCOL.value:
+            return None
+        t = self.tensor
+        if (not t.is_cuda and t.dtype == string_to_dtype(self.entry.dtype)
+                and nbytes == self._nbytes() and list(t.shape) == list(self.entry.shape)):
+            dest = staging.staged_from_tensor_storage(t)
+            if dest is not None:
+                self._direct = True
+                return dest
+        if t.is_cuda:
+            from ..ops import native
+
+            pb = native.PinnedBuffer(nbytes)
+            return StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
+        return None
+
+    async def consume_buffer(self, buf, executor: Optional[Executor] = None) -> None:
+        if self._direct:
+            return  # bytes were read straight into the destination tensor
+        await run_in_executor(executor, self._consume_sync, buf)
+
+    def _consume_sync(self, buf) -> None:
+        t = self.tensor
+        if (t.is_cuda and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value):
+            staging.h2d_into(t, staging.host_buffer_addr(buf), self._nbytes(),
+                             string_to_dtype(self.entry.dtype), self.entry.shape, self.producer)
+            return
+        loaded = deserialize_tensor(buf, self.entry)
+        tensor_copy(t, loaded)
+
+    def get_consuming_cost_bytes(self) -> int:
+        n = self._nbytes()
+        return 2 * n if self.entry.serializer == Serializer.TORCH_SAVE.value else n
+
+
+def _q_params_equal(lhs: torch.Tensor, rhs: torch.Tensor) -> bool:
+    if lhs.qscheme() != rhs.qscheme():
+        return False
+    if lhs.qscheme() == torch.per_tensor_affine:
+        return lhs.q_scale() == rhs.q_scale() and lhs.q_zero_point() == rhs.q_zero_point()
+    if lhs.qscheme() in (torch.per_channel_affine, torch.per_channel_affine_float_qparams):
+        return (torch.equal(lhs.q_per_channel_scales(), rhs.q_per_channel_scales())
+                and torch.equal(lhs.q_per_channel_zero_points(), rhs.q_per_channel_zero_points())
+                and lhs.q_per_channel_axis() == rhs.q_per_channel_axis())
+    raise RuntimeError(f"Unrecognized qscheme {lhs.qscheme()}")
+
+
+def tensor_copy(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """``dst.copy_(src)`` that also handles quantized <-> float and qparam changes.
+
+    Quantized sources are dequantized when the destination is not quantized,
+    has another qscheme/dtype, or is a view whose qparams differ (copying then
+    would silently re-label the view's data under the parent's qparams).
+    """
+    if src.is_quantized and (
+            not dst.is_quantized or dst.qscheme() != src.qscheme() or dst.dtype != src.dtype
+            or (dst._is_view() and not _q_params_equal(dst, src))):
+        src = src.dequantize()
+    with torch.no_grad():
+        dst.detach().copy_(src)

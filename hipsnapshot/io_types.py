@@ -1,0 +1,175 @@
+"""Request / buffer types shared by the planners, the engine and storage plugins.
+
+Mirrors the reference's contract (`/root/reference/torchsnapshot/io_types.py:16-111`):
+a write is ``WriteReq(path, buffer_stager)`` whose stager produces the bytes,
+a read is ``ReadReq(path, buffer_consumer, byte_range)`` whose consumer eats
+them, and storage plugins only see ``WriteIO`` / ``ReadIO``.
+
+Differences that matter for MI355X:
+
+* ``StagedBuffer`` carries the host address of the bytes (a pinned pool block,
+  a CPU tensor's storage, ...) plus a ``release`` hook, so the native I/O
+  engine writes straight from pinned memory and the block returns to the pool
+  the moment the write completes.
+* a ``BufferConsumer`` may offer a destination (``get_read_dest``) so storage
+  reads land directly in pinned memory or in the restore target's storage.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import io
+from abc import ABC, abstractmethod
+from concurrent.futures import Executor
+from dataclasses import dataclass, field
+from typing import Any, Callable, Generic, Optional, Tuple, TypeVar, Union
+
+import numpy as np
+
+BufferType = Union[bytes, bytearray, memoryview]
+T = TypeVar("T")
+
+
+def buffer_address(buf) -> int:
+    if len(memoryview(buf)) == 0:
+        return 0
+    return int(np.frombuffer(buf, dtype=np.uint8).ctypes.data)
+
+
+class StagedBuffer:
+    """Bytes ready for storage: ``view`` + raw ``addr`` + release hook."""
+
+    __slots__ = ("view", "addr", "_release", "keepalive")
+
+    def __init__(self, view: BufferType, addr: Optional[int] = None,
+                 release: Optional[Callable[[], None]] = None, keepalive: Any = None) -> None:
+        mv = memoryview(view)
+        if mv.format != "B" or mv.ndim != 1:
+            mv = mv.cast("B")
+        self.view = mv
+        self.addr = buffer_address(mv) if addr is None else addr
+        self._release = release
+        self.keepalive = keepalive
+
+    @property
+    def nbytes(self) -> int:
+        return self.view.nbytes
+
+    def release(self) -> None:
+        rel, self._release = self._release, None
+        self.keepalive = None
+        if rel is not None:
+            rel()
+
+
+def as_staged(buf: Union[StagedBuffer, BufferType]) -> StagedBuffer:
+    return buf if isinstance(buf, StagedBuffer) else StagedBuffer(buf)
+
+
+class BufferStager(ABC):
+    @abstractmethod
+    async def stage_buffer(self, executor: Optional[Executor] = None) -> Union[StagedBuffer, BufferType]:
+        ...
+
+    @abstractmethod
+    def get_staging_cost_bytes(self) -> int:
+        ...
+
+
+@dataclass
+class WriteReq:
+    path: str
+    buffer_stager: BufferStager
+
+
+class BufferConsumer(ABC):
+    @abstractmethod
+    async def consume_buffer(self, buf: BufferType, executor: Optional[Executor] = None) -> None:
+        ...
+
+    @abstractmethod
+    def get_consuming_cost_bytes(self) -> int:
+        ...
+
+    def get_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
+        """Optionally provide a writable destination for the raw bytes."""
+        return None
+
+
+@dataclass
+class ReadReq:
+    path: str
+    buffer_consumer: BufferConsumer
+    byte_range: Optional[Tuple[int, int]] = None
+
+
+@dataclass
+class Future(Generic[T]):
+    obj: Optional[T] = None
+
+
+@dataclass
+class WriteIO:
+    path: str
+    buf: BufferType
+    addr: Optional[int] = None
+
+
+@dataclass
+class ReadIO:
+    path: str
+    byte_range: Optional[Tuple[int, int]] = None
+    buf: Any = field(default_factory=io.BytesIO)
+    dest: Optional[StagedBuffer] = None
+
+    def data(self) -> BufferType:
+        """The bytes read (memoryview/bytes), whatever the plugin produced."""
+        b = self.buf
+        if isinstance(b, io.BytesIO):
+            return b.getbuffer()
+        return b
+
+
+class StoragePlugin(ABC):
+    """Async storage backend; the ``sync_*`` helpers drive a given loop."""
+
+    @abstractmethod
+    async def write(self, write_io: WriteIO) -> None:
+        ...
+
+    @abstractmethod
+    async def read(self, read_io: ReadIO) -> None:
+        ...
+
+    @abstractmethod
+    async def delete(self, path: str) -> None:
+        ...
+
+    async def delete_dir(self, path: str) -> None:
+        raise NotImplementedError(f"{type(self).__name__} does not implement delete_dir")
+
+    @abstractmethod
+    async def close(self) -> None:
+        ...
+
+    def sync_write(self, write_io: WriteIO, event_loop: Optional[asyncio.AbstractEventLoop] = None) -> None:
+        _run(self.write(write_io), event_loop)
+
+    def sync_read(self, read_io: ReadIO, event_loop: Optional[asyncio.AbstractEventLoop] = None) -> None:
+        _run(self.read(read_io), event_loop)
+
+    def sync_delete(self, path: str, event_loop: Optional[asyncio.AbstractEventLoop] = None) -> None:
+        _run(self.delete(path), event_loop)
+
+    def sync_close(self, event_loop: Optional[asyncio.AbstractEventLoop] = None) -> None:
+        _run(self.close(), event_loop)
+
+
+def _run(coro, loop: Optional[asyncio.AbstractEventLoop]):
+    if loop is None:
+        loop = asyncio.new_event_loop()
+        try:
+            return loop.run_until_complete(coro)
+        finally:
+            loop.close()
+    return loop.run_until_complete(coro)

@@ -1,0 +1,486 @@
+"""ctypes bindings for the native libraries (``_hsio.so`` and ``_hsgpu.so``).
+
+Loading policy:
+
+* ``_hsio.so`` (file I/O engine) is built on demand if missing -- it only needs
+  a C++ compiler -- and is used on every machine.
+* ``_hsgpu.so`` (HIP data plane) is REQUIRED whenever a GPU is visible: GPU
+  tensors never silently fall back to ATen copies.  ``require_gpu_lib()`` raises
+  with the build command if the library is missing or fails to load.
+
+``torch`` is always imported before ``_hsgpu.so`` is dlopen'ed so the HIP
+runtime resolved for our library is the one torch already loaded (same SONAME
+``libamdhip64.so.7``) -- one HIP runtime, shared streams and contexts.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import logging
+import os
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _build
+
+logger = logging.getLogger(__name__)
+
+_lock = threading.Lock()
+_hsio_lib: Optional[ctypes.CDLL] = None
+_hsgpu_lib: Optional[ctypes.CDLL] = None
+_hsgpu_error: Optional[str] = None
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_int64 = ctypes.c_int64
+c_uint64 = ctypes.c_uint64
+c_char_p = ctypes.c_char_p
+
+
+def _declare(lib: ctypes.CDLL, name: str, restype, argtypes) -> None:
+    fn = getattr(lib, name)
+    fn.restype = restype
+    fn.argtypes = argtypes
+
+
+# ---------------------------------------------------------------------------
+# _hsio.so
+# ---------------------------------------------------------------------------
+
+def hsio() -> ctypes.CDLL:
+    global _hsio_lib
+    if _hsio_lib is not None:
+        return _hsio_lib
+    with _lock:
+        if _hsio_lib is None:
+            path = _build.HSIO_SO
+            if not os.path.exists(path):
+                _build.build_hsio()
+            lib = ctypes.CDLL(path)
+            _declare(lib, "hsio_create", c_void_p, [c_int])
+            _declare(lib, "hsio_destroy", None, [c_void_p])
+            _declare(lib, "hsio_eventfd", c_int, [c_void_p])
+            _declare(lib, "hsio_submit_write", c_int64,
+                     [c_void_p, c_char_p, c_void_p, c_uint64, c_uint64, c_int])
+            _declare(lib, "hsio_submit_read", c_int64,
+                     [c_void_p, c_char_p, c_void_p, c_uint64, c_uint64, c_int])
+            _declare(lib, "hsio_submit_delete", c_int64, [c_void_p, c_char_p])
+            _declare(lib, "hsio_poll", c_int,
+                     [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64), c_int])
+            _declare(lib, "hsio_write_sync", c_int64,
+                     [c_void_p, c_char_p, c_void_p, c_uint64, c_uint64, c_int])
+            _declare(lib, "hsio_read_sync", c_int64,
+                     [c_void_p, c_char_p, c_void_p, c_uint64, c_uint64, c_int])
+            _declare(lib, "hsio_file_size", c_int64, [c_char_p])
+            _declare(lib, "hsio_alloc_aligned", c_void_p, [c_uint64])
+            _declare(lib, "hsio_free_aligned", None, [c_void_p])
+            _declare(lib, "hsio_parallel_memcpy", None, [c_void_p, c_void_p, c_uint64, c_int])
+            _hsio_lib = lib
+    return _hsio_lib
+
+
+IO_DIRECT = 1
+IO_SYNC = 2
+IO_MKDIRS = 4
+IO_APPEND = 8
+
+
+class IOEngine:
+    """A C++ worker pool bound to one process (re-created after fork)."""
+
+    def __init__(self, nthreads: int) -> None:
+        self.lib = hsio()
+        self.nthreads = nthreads
+        self.pid = os.getpid()
+        self.handle = self.lib.hsio_create(nthreads)
+        self.efd = self.lib.hsio_eventfd(self.handle)
+        self._ids = (c_int64 * 256)()
+        self._res = (c_int64 * 256)()
+
+    def submit_write(self, path: str, addr: int, nbytes: int, offset: int, flags: int) -> int:
+        return self.lib.hsio_submit_write(self.handle, path.encode(), addr, nbytes, offset, flags)
+
+    def submit_read(self, path: str, addr: int, nbytes: int, offset: int, flags: int) -> int:
+        return self.lib.hsio_submit_read(self.handle, path.encode(), addr, nbytes, offset, flags)
+
+    def submit_delete(self, path: str) -> int:
+        return self.lib.hsio_submit_delete(self.handle, path.encode())
+
+    def poll(self) -> List[tuple]:
+        out = []
+        while True:
+            k = self.lib.hsio_poll(self.handle, self._ids, self._res, 256)
+            for i in range(k):
+                out.append((self._ids[i], self._res[i]))
+            if k < 256:
+                return out
+
+    def write_sync(self, path: str, addr: int, nbytes: int, offset: int, flags: int) -> int:
+        return self.lib.hsio_write_sync(self.handle, path.encode(), addr, nbytes, offset, flags)
+
+    def read_sync(self, path: str, addr: int, nbytes: int, offset: int, flags: int) -> int:
+        return self.lib.hsio_read_sync(self.handle, path.encode(), addr, nbytes, offset, flags)
+
+    def close(self) -> None:
+        if self.handle and os.getpid() == self.pid:
+            self.lib.hsio_destroy(self.handle)
+        self.handle = None
+
+
+_engines = {}
+
+
+def io_engine(nthreads: int = 16) -> IOEngine:
+    """Process-wide shared engine (per thread count)."""
+    key = (os.getpid(), nthreads)
+    eng = _engines.get(key)
+    if eng is None:
+        with _lock:
+            eng = _engines.get(key)
+            if eng is None:
+                eng = IOEngine(nthreads)
+                _engines[key] = eng
+    return eng
+
+
+def file_size(path: str) -> int:
+    r = hsio().hsio_file_size(path.encode())
+    if r < 0:
+        raise OSError(-r, os.strerror(-r), path)
+    return r
+
+
+def parallel_memcpy(dst: int, src: int, nbytes: int, nthreads: int = 8) -> None:
+    hsio().hsio_parallel_memcpy(dst, src, nbytes, nthreads)
+
+
+def address_of(buf) -> int:
+    """Address of a writable/readable contiguous buffer (memoryview/bytearray/ndarray)."""
+    if isinstance(buf, torch.Tensor):
+        return buf.data_ptr()
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    return arr.ctypes.data
+
+
+# ---------------------------------------------------------------------------
+# _hsgpu.so
+# ---------------------------------------------------------------------------
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available()
+
+
+def _load_hsgpu() -> Optional[ctypes.CDLL]:
+    global _hsgpu_lib, _hsgpu_error
+    if _hsgpu_lib is not None or _hsgpu_error is not None:
+        return _hsgpu_lib
+    with _lock:
+        if _hsgpu_lib is not None or _hsgpu_error is not None:
+            return _hsgpu_lib
+        path = _build.HSGPU_SO
+        try:
+            if not os.path.exists(path):
+                _build.build_hsgpu()
+            lib = ctypes.CDLL(path)
+        except Exception as e:  # noqa: BLE001
+            _hsgpu_error = f"{type(e).__name__}: {e}"
+            return None
+        _declare(lib, "hsg_last_error", c_char_p, [])
+        _declare(lib, "hsg_device_count", c_int, [])
+        _declare(lib, "hsg_pinned_acquire", c_void_p, [c_uint64])
+        _declare(lib, "hsg_pinned_release", c_int, [c_void_p])
+        _declare(lib, "hsg_pinned_stats", None, [ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)])
+        _declare(lib, "hsg_pinned_trim", c_uint64, [])
+        _declare(lib, "hsg_memcpy", c_int,
+                 [c_int, c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_int])
+        _declare(lib, "hsg_stream_join", c_int, [c_int, c_int, c_void_p])
+        _declare(lib, "hsg_stream_sync", c_int, [c_int, c_int])
+        _declare(lib, "hsg_copy_stream", c_void_p, [c_int, c_int])
+        _declare(lib, "hsg_sync_stream_handle", c_int, [c_void_p])
+        _declare(lib, "hsg_desc_size", c_uint64, [])
+        _declare(lib, "hsg_copy_workspace_bytes", c_uint64, [c_void_p, c_int])
+        _declare(lib, "hsg_copy_nd", c_int,
+                 [c_int, c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_int])
+        _declare(lib, "hsg_fp8_quantize", c_int,
+                 [c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_int, c_void_p])
+        _declare(lib, "hsg_fp8_dequantize", c_int,
+                 [c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_void_p])
+        _declare(lib, "hsg_is_managed", c_int, [c_void_p])
+        _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
+        _declare(lib, "hsg_managed_free", c_int, [c_void_p])
+        if lib.hsg_desc_size() != COPY_DESC_DTYPE.itemsize:
+            _hsgpu_error = (f"CopyDesc layout mismatch: native {lib.hsg_desc_size()} "
+                            f"vs python {COPY_DESC_DTYPE.itemsize}")
+            return None
+        _hsgpu_lib = lib
+    return _hsgpu_lib
+
+
+def hsgpu_loaded() -> bool:
+    return _load_hsgpu() is not None
+
+
+def require_gpu_lib() -> ctypes.CDLL:
+    lib = _load_hsgpu()
+    if lib is None:
+        raise RuntimeError(
+            "hipsnapshot's HIP data plane (_hsgpu.so) is unavailable: "
+            f"{_hsgpu_error}. Build it with `python -m hipsnapshot._build` "
+            "(hipcc --offload-arch=gfx950).")
+    return lib
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        lib = _load_hsgpu()
+        msg = lib.hsg_last_error().decode() if lib is not None else "?"
+        raise HipError(f"{what} failed ({rc}): {msg}")
+
+
+# ---- pinned host memory ---------------------------------------------------
+
+class PinnedBuffer:
+    """A page-locked host block from the native caching pool.
+
+    ``view`` is a writable memoryview over the first ``nbytes`` bytes; the
+    block goes back to the pool on :meth:`release` (idempotent) or GC.
+    """
+
+    __slots__ = ("ptr", "nbytes", "_released", "_cbuf", "__weakref__")
+
+    def __init__(self, nbytes: int) -> None:
+        lib = require_gpu_lib()
+        ptr = lib.hsg_pinned_acquire(max(int(nbytes), 1))
+        if not ptr:
+            raise MemoryError(f"pinned allocation of {nbytes} bytes failed: "
+                              f"{lib.hsg_last_error().decode()}")
+        self.ptr = ptr
+        self.nbytes = int(nbytes)
+        self._released = False
+        self._cbuf = (ctypes.c_char * max(self.nbytes, 1)).from_address(ptr)
+
+    @property
+    def view(self) -> memoryview:
+        return memoryview(self._cbuf).cast("B")[: self.nbytes]
+
+    def as_tensor(self, nbytes: Optional[int] = None) -> torch.Tensor:
+        n = self.nbytes if nbytes is None else nbytes
+        if n == 0:
+            return torch.empty(0, dtype=torch.uint8)
+        return torch.frombuffer(self._cbuf, dtype=torch.uint8, count=n)
+
+    def release(self) -> None:
+        if not self._released:
+            self._released = True
+            lib = _load_hsgpu()
+            if lib is not None:
+                lib.hsg_pinned_release(self.ptr)
+
+    def __del__(self) -> None:  # pragma: no cover - GC path
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+def pinned_stats() -> tuple:
+    lib = require_gpu_lib()
+    a, b = c_uint64(), c_uint64()
+    lib.hsg_pinned_stats(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def pinned_trim() -> int:
+    return int(require_gpu_lib().hsg_pinned_trim())
+
+
+# ---- DMA ------------------------------------------------------------------
+
+D2H, H2D, D2D = 0, 1, 2
+
+
+def _stream_handle(stream) -> int:
+    if stream is None:
+        return 0
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)
+
+
+def memcpy(dev: int, slot: int, dst: int, src: int, nbytes: int, kind: int,
+           producer=None, sync: bool = True) -> None:
+    lib = require_gpu_lib()
+    _check(lib.hsg_memcpy(dev, slot, dst, src, nbytes, kind, _stream_handle(producer),
+                          1 if sync else 0), "hsg_memcpy")
+
+
+def copy_stream(dev: int, slot: int) -> int:
+    h = require_gpu_lib().hsg_copy_stream(dev, slot)
+    if not h:
+        raise HipError("hsg_copy_stream failed")
+    return h
+
+
+def stream_join(dev: int, slot: int, consumer) -> None:
+    _check(require_gpu_lib().hsg_stream_join(dev, slot, _stream_handle(consumer)),
+           "hsg_stream_join")
+
+
+def stream_sync(dev: int, slot: int) -> None:
+    _check(require_gpu_lib().hsg_stream_sync(dev, slot), "hsg_stream_sync")
+
+
+def sync_stream_handle(handle: int) -> None:
+    _check(require_gpu_lib().hsg_sync_stream_handle(handle), "hsg_sync_stream_handle")
+
+
+# ---- batched strided copy / cast --------------------------------------------
+
+MAX_DIMS = 8
+COPY_DESC_DTYPE = np.dtype([
+    ("src", np.uint64), ("dst", np.uint64), ("numel", np.int64),
+    ("ndim", np.int32), ("src_dtype", np.int32), ("dst_dtype", np.int32),
+    ("flags", np.int32),
+    ("sizes", np.int64, (MAX_DIMS,)), ("src_strides", np.int64, (MAX_DIMS,)),
+    ("dst_strides", np.int64, (MAX_DIMS,)),
+])
+
+_RAW_CODE = {1: 0, 2: 1, 4: 2, 8: 3, 16: 4}
+_FLOAT_CODE = {torch.float16: 10, torch.bfloat16: 11, torch.float32: 12, torch.float64: 13}
+
+
+def dtype_code(dtype: torch.dtype) -> int:
+    return _FLOAT_CODE.get(dtype, -1)
+
+
+def can_cast_on_device(src: torch.dtype, dst: torch.dtype) -> bool:
+    if src == dst:
+        return True
+    return src in _FLOAT_CODE and dst in _FLOAT_CODE
+
+
+def collapse_dims(sizes: Sequence[int], s_strides: Sequence[int],
+                  d_strides: Sequence[int]) -> tuple:
+    """Drop size-1 dims and merge adjacent dims that are jointly contiguous."""
+    dims = [(int(z), int(a), int(b)) for z, a, b in zip(sizes, s_strides, d_strides) if z != 1]
+    if not dims:
+        return [1], [1], [1]
+    out = [dims[0]]
+    for z, a, b in dims[1:]:
+        pz, pa, pb = out[-1]
+        if pa == a * z and pb == b * z:
+            out[-1] = (pz * z, a, b)
+        else:
+            out.append((z, a, b))
+    return [d[0] for d in out], [d[1] for d in out], [d[2] for d in out]
+
+
+class CopyBatch:
+    """Accumulates strided copy/cast descriptors executed by ONE kernel launch."""
+
+    def __init__(self) -> None:
+        self.rows: List[tuple] = []
+
+    def __len__(self) -> int:
+        return len(self.rows)
+
+    def add(self, src_ptr: int, src_dtype: torch.dtype, src_strides: Sequence[int],
+            dst_ptr: int, dst_dtype: torch.dtype, dst_strides: Sequence[int],
+            sizes: Sequence[int], elem_size: int) -> None:
+        numel = 1
+        for z in sizes:
+            numel *= int(z)
+        if numel == 0:
+            return
+        z, a, b = collapse_dims(sizes, src_strides, dst_strides)
+        if len(z) > MAX_DIMS:
+            raise ValueError(f"too many non-mergeable dims ({len(z)}) for the copy kernel")
+        if src_dtype == dst_dtype or elem_size == 16:
+            sc = dc = _RAW_CODE[elem_size]
+        else:
+            sc, dc = dtype_code(src_dtype), dtype_code(dst_dtype)
+            if sc < 0 or dc < 0:
+                raise ValueError(f"device cast {src_dtype}->{dst_dtype} unsupported")
+        flags = 1 if (sc == dc and len(z) == 1 and a[0] == 1 and b[0] == 1) else 0
+        self.rows.append((src_ptr, dst_ptr, numel, len(z), sc, dc, flags, z, a, b))
+
+    def pack(self) -> np.ndarray:
+        arr = np.zeros(len(self.rows), dtype=COPY_DESC_DTYPE)
+        for i, (sp, dp, numel, nd, sc, dc, fl, z, a, b) in enumerate(self.rows):
+            arr[i]["src"] = sp
+            arr[i]["dst"] = dp
+            arr[i]["numel"] = numel
+            arr[i]["ndim"] = nd
+            arr[i]["src_dtype"] = sc
+            arr[i]["dst_dtype"] = dc
+            arr[i]["flags"] = fl
+            arr[i]["sizes"][:nd] = z
+            arr[i]["src_strides"][:nd] = a
+            arr[i]["dst_strides"][:nd] = b
+        return arr
+
+    def launch(self, dev: int, stream_handle: int, sync: bool = True) -> None:
+        """Run all descriptors in one launch on ``stream_handle``.
+
+        The descriptor/tile tables go through a pinned staging block and a
+        device workspace that are kept alive until the stream has passed them
+        (``sync=True``) -- callers that pass ``sync=False`` must keep the
+        returned objects alive until they synchronize the stream.
+        """
+        if not self.rows:
+            return None
+        lib = require_gpu_lib()
+        arr = self.pack()
+        ws_bytes = int(lib.hsg_copy_workspace_bytes(arr.ctypes.data, len(arr)))
+        stage = PinnedBuffer(ws_bytes)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+        rc = lib.hsg_copy_nd(dev, arr.ctypes.data, len(arr), ws.data_ptr(), ws_bytes,
+                             stage.ptr, stream_handle, 1 if sync else 0)
+        _check(rc, "hsg_copy_nd")
+        if sync:
+            stage.release()
+            return None
+        return (stage, ws)
+
+
+def tensor_copy_descriptor(batch: CopyBatch, src: torch.Tensor, dst: torch.Tensor) -> None:
+    """Queue ``dst.copy_(src)`` (same shape; any strides; float casts allowed)."""
+    if list(src.shape) != list(dst.shape):
+        raise ValueError(f"shape mismatch {src.shape} vs {dst.shape}")
+    es = src.element_size()
+    batch.add(src.data_ptr(), src.dtype, src.stride(), dst.data_ptr(), dst.dtype,
+              dst.stride(), list(src.shape), es if src.dtype == dst.dtype else es)
+
+
+# ---- fp8 ----------------------------------------------------------------------
+
+def fp8_quantize(dev: int, src: torch.Tensor, out: torch.Tensor, scales: torch.Tensor,
+                 vpt: int, stream_handle: int) -> None:
+    lib = require_gpu_lib()
+    _check(lib.hsg_fp8_quantize(dev, src.data_ptr(), dtype_code(src.dtype), src.numel(),
+                                out.data_ptr(), scales.data_ptr(), vpt, stream_handle),
+           "hsg_fp8_quantize")
+
+
+def fp8_dequantize(dev: int, q: torch.Tensor, scales: torch.Tensor, dst: torch.Tensor,
+                   vpt: int, stream_handle: int) -> None:
+    lib = require_gpu_lib()
+    _check(lib.hsg_fp8_dequantize(dev, q.data_ptr(), scales.data_ptr(), q.numel(),
+                                  dst.data_ptr(), dtype_code(dst.dtype), vpt, stream_handle),
+           "hsg_fp8_dequantize")
+
+
+# ---- managed memory -------------------------------------------------------------
+
+def is_managed_ptr(ptr: int) -> bool:
+    lib = _load_hsgpu()
+    if lib is None or not gpu_available():
+        return False
+    return bool(lib.hsg_is_managed(ptr))

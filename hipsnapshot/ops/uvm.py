@@ -1,0 +1,78 @@
+"""Managed-memory (UVM) tensors -- the fbgemm ``uvm_tensor`` equivalent (K11).
+
+Reference: `/root/reference/torchsnapshot/uvm_tensor.py:11-42` binds fbgemm_gpu's
+``new_managed_tensor / is_uvm_tensor / uvm_to_cpu``.  fbgemm is not available
+for this stack, so managed memory is allocated natively with
+``hipMallocManaged`` (``_hsgpu.so``) and exposed to torch as a CUDA tensor via
+``torch.from_blob``-style storage wrapping; detection uses
+``hipPointerGetAttributes(...).isManaged``.  Staging a UVM tensor goes
+through the same SDMA path as any other device tensor (the driver migrates
+pages as needed), i.e. no separate ``uvm_to_cpu`` copy.
+"""
+
+from __future__ import annotations
+
+import weakref
+from typing import Dict, List
+
+import torch
+
+from . import native
+
+_managed: Dict[int, int] = {}
+
+
+def is_uvm_tensor(t: torch.Tensor) -> bool:
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        return False
+    ptr = t.untyped_storage().data_ptr()
+    if ptr in _managed:
+        return True
+    return native.is_managed_ptr(ptr)
+
+
+def uvm_to_cpu(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().cpu()
+
+
+def new_managed_tensor(shape: List[int], dtype: torch.dtype = torch.float32,
+                       device: int = 0) -> torch.Tensor:
+    """Allocate a managed-memory tensor visible to the given HIP device."""
+    lib = native.require_gpu_lib()
+    numel = 1
+    for s in shape:
+        numel *= int(s)
+    nbytes = max(numel * torch.empty(0, dtype=dtype).element_size(), 1)
+    ptr = lib.hsg_managed_alloc(device, nbytes)
+    if not ptr:
+        raise MemoryError(f"hipMallocManaged({nbytes}) failed: {lib.hsg_last_error().decode()}")
+    _managed[ptr] = nbytes
+
+    def _free(p=ptr):
+        _managed.pop(p, None)
+        lib.hsg_managed_free(p)
+
+    # wrap as a CUDA tensor through DLPack-free __cuda_array_interface__
+    class _Holder:
+        pass
+
+    holder = _Holder()
+    holder.__cuda_array_interface__ = {
+        "shape": tuple(int(s) for s in shape),
+        "typestr": _typestr(dtype),
+        "data": (ptr, False),
+        "version": 3,
+        "strides": None,
+    }
+    with torch.cuda.device(device):
+        t = torch.as_tensor(holder, device=f"cuda:{device}")
+    weakref.finalize(t.untyped_storage(), _free)
+    return t
+
+
+def _typestr(dtype: torch.dtype) -> str:
+    return {
+        torch.float32: "<f4", torch.float16: "<f2", torch.float64: "<f8",
+        torch.int64: "<i8", torch.int32: "<i4", torch.int16: "<i2", torch.int8: "|i1",
+        torch.uint8: "|u1", torch.bool: "|b1", torch.bfloat16: "<V2",
+    }[dtype]

@@ -1,0 +1,165 @@
+"""Write-load balancing of replicated state across ranks.
+
+Reference: `/root/reference/torchsnapshot/partitioner.py:24-316`.  Same outcome --
+each replicated blob is written by exactly one rank, replicated
+``ChunkedTensorEntry``s are split chunk by chunk, and per-rank (non-replicated)
+bytes are accounted for -- but a different protocol:
+
+* ONE all-gather of ``(non_replicated_bytes, {path: (digest, [chunk bytes])})``
+  (digest = dtype/shape/chunk layout) instead of gathering whole entries and
+  then broadcasting rank 0's plan (two collectives, CO6);
+* every rank then computes the SAME plan locally and deterministically;
+* longest-processing-time-first greedy (largest unit to the least-loaded
+  rank, ties -> lowest rank) instead of manifest order, which bounds the
+  imbalance at 4/3 of optimal.  With 8 ranks on one node this is what keeps
+  all 8 PCIe links busy for the whole D2H phase.
+"""
+
+from __future__ import annotations
+
+import copy
+import hashlib
+import os
+from collections import defaultdict
+from typing import Dict, List, Tuple
+
+from ..format.manifest import ChunkedTensorEntry, Entry, is_replicated
+from ..io_types import WriteReq
+from .comm import Comm
+
+
+def estimate_write_req_bytes(wr: WriteReq) -> int:
+    st = wr.buffer_stager
+    entry = getattr(st, "entry", None)
+    if entry is not None and getattr(entry, "type", None) == "Tensor":
+        from ..io.tensor import tensor_nbytes_from_entry
+
+        return tensor_nbytes_from_entry(entry)
+    return st.get_staging_cost_bytes()
+
+
+def _digest(entry: Entry) -> str:
+    if isinstance(entry, ChunkedTensorEntry):
+        key = repr((entry.dtype, list(entry.shape),
+                    [(c.offsets, c.sizes, c.tensor.dtype, c.tensor.serializer)
+                     for c in entry.chunks]))
+    else:
+        key = repr(entry.to_dict())
+    return hashlib.sha1(key.encode()).hexdigest()
+
+
+def plan_partition(rank_sizes: List[int], path_loads: Dict[str, List[int]],
+                   subpartitionable: Dict[str, bool]) -> Dict[Tuple[str, int], int]:
+    """Deterministic greedy LPT: (path, write_req_idx) -> owner rank."""
+    loads = list(rank_sizes)
+    units: List[Tuple[int, str, int, List[int]]] = []  # (-size, path, idx, idxs)
+    for path in sorted(path_loads):
+        sizes = path_loads[path]
+        if subpartitionable.get(path, False):
+            for i, s in enumerate(sizes):
+                units.append((-s, path, i, [i]))
+        else:
+            units.append((-sum(sizes), path, -1, list(range(len(sizes)))))
+    units.sort(key=lambda u: (u[0], u[1], u[2]))
+    owner: Dict[Tuple[str, int], int] = {}
+    for neg, path, _i, idxs in units:
+        r = min(range(len(loads)), key=lambda k: (loads[k], k))
+        loads[r] += -neg
+        for i in idxs:
+            owner[(path, i)] = r
+    return owner
+
+
+def partition_write_reqs(entries: Dict[str, Entry], write_reqs: Dict[str, List[WriteReq]],
+                         pg: Comm) -> Tuple[Dict[str, Entry], Dict[str, List[WriteReq]]]:
+    if not set(write_reqs).issubset(entries):
+        raise RuntimeError("Not all entries associated with the write reqs are passed in. "
+                           f"Missing: {set(write_reqs) - set(entries)}.")
+    if os.environ.get("TORCH_SNAPSHOT_DISABLE_PARTITIONER") or \
+            os.environ.get("HIPSNAPSHOT_DISABLE_PARTITIONER"):
+        # every rank writes its own copy of the replicated state, but only
+        # rank 0's copy is referenced by the manifest (others are skipped).
+        if pg.get_rank() == 0:
+            return entries, write_reqs
+        keep = {k: v for k, v in entries.items() if not is_replicated(v)}
+        return keep, {k: v for k, v in write_reqs.items() if k in keep}
+
+    rep_entries = {k: v for k, v in entries.items() if is_replicated(v)}
+    non_rep_bytes = sum(estimate_write_req_bytes(wr) for k, wrs in write_reqs.items()
+                        if k not in rep_entries for wr in wrs)
+    local = {k: (_digest(rep_entries[k]),
+                 [estimate_write_req_bytes(wr) for wr in write_reqs.get(k, [])])
+             for k in rep_entries}
+    ws = pg.get_world_size()
+    gathered: List = [None] * ws
+    pg.all_gather_object(gathered, (non_rep_bytes, local))
+    rank_sizes = [g[0] for g in gathered]
+    path_loads = {k: v[1] for k, v in gathered[0][1].items()}
+    subpart = {}
+    for k in path_loads:
+        digests = {g[1][k][0] if k in g[1] else None for g in gathered}
+        subpart[k] = isinstance(rep_entries.get(k), ChunkedTensorEntry) and len(digests) == 1
+    owner = plan_partition(rank_sizes, path_loads, subpart)
+
+    me = pg.get_rank()
+    new_entries: Dict[str, Entry] = {k: v for k, v in entries.items() if not is_replicated(v)}
+    new_reqs: Dict[str, List[WriteReq]] = {k: v for k, v in write_reqs.items()
+                                           if k in new_entries}
+    mine = sorted((p, i) for (p, i), r in owner.items() if r == me and p in rep_entries)
+    for path, idx in mine:
+        entry = rep_entries[path]
+        wrs = write_reqs.get(path, [])
+        if isinstance(entry, ChunkedTensorEntry) and subpart.get(path):
+            if path not in new_entries:
+                e = copy.copy(entry)
+                e.chunks = []
+                new_entries[path] = e
+            new_entries[path].chunks.append(entry.chunks[idx])
+        else:
+            new_entries[path] = entry
+        if idx < len(wrs):
+            new_reqs.setdefault(path, []).append(wrs[idx])
+    return new_entries, new_reqs
+
+
+def _merge_replicated_chunked(rank_to_entries: List[Dict[str, Entry]]) -> None:
+    groups: Dict[str, List[ChunkedTensorEntry]] = defaultdict(list)
+    for entries in rank_to_entries:
+        for path, e in entries.items():
+            if is_replicated(e) and isinstance(e, ChunkedTensorEntry):
+                groups[path].append(e)
+    for path, group in groups.items():
+        merged = ChunkedTensorEntry(dtype=group[0].dtype, shape=group[0].shape,
+                                    chunks=sorted((c for e in group for c in e.chunks),
+                                                  key=lambda c: c.offsets),
+                                    replicated=True)
+        for entries in rank_to_entries:
+            if path in entries:
+                entries[path] = merged
+
+
+def consolidate_replicated_entries(rank_to_entries: List[Dict[str, Entry]],
+                                   dedup: bool = True) -> List[Dict[str, Entry]]:
+    """Merge partitioned replicated entries; with ``dedup`` they live only in
+    rank 0's manifest (on-disk format rule)."""
+    _merge_replicated_chunked(rank_to_entries)
+    replicated: Dict[str, Entry] = {}
+    for entries in rank_to_entries:
+        for path in list(entries):
+            e = entries[path]
+            if not is_replicated(e):
+                continue
+            replicated.setdefault(path, e)
+            del entries[path]
+    for rank, entries in enumerate(rank_to_entries):
+        if dedup and rank != 0:
+            continue
+        entries.update(replicated)
+    return rank_to_entries
+
+
+def consolidate_replicated_entries_dist(entries: Dict[str, Entry], pg: Comm,
+                                        dedup: bool = True) -> Dict[str, Entry]:
+    gathered: List = [None] * pg.get_world_size()
+    pg.all_gather_object(gathered, entries)
+    return consolidate_replicated_entries(gathered, dedup=dedup)[pg.get_rank()]
