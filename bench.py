@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Headline benchmark: checkpoint save GB/s + time-to-unblock, Llama-3-8B FSDP.
+
+BASELINE.json metric: "checkpoint save GB/s + time-to-unblock, Llama-3-8B FSDP
+at 1/2/4/8 MI355X".  One *step* = one ``Snapshot.take`` of the full FSDP2
+(DTensor, Shard(0)) Llama-3-8B model state (8.03 B bf16 params = 16.06 GB,
+random init, synthetic) to local storage, committed (metadata written after
+every rank finished).  The total model is fixed as N grows -> strong scaling;
+``value`` is the whole-job GB/s = model bytes / step time (max over ranks).
+
+After the timed steps, ``async_take`` is run ``--async-iters`` times and its
+time-to-unblock (max over ranks) is reported in ``time_to_unblock_ms``.
+
+Launch: ``python bench.py`` (1 GPU) or
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import socket
+import sys
+import time
+
+# published reference numbers: DDP 20 GB save on p4d.24xlarge,
+# local FS -- 1 GPU 13.91 s (1.44 GB/s), 1 node x 8 GPUs 3.38 s (5.92 GB/s)
+BASELINE_GBPS = {1: 20.0 / 13.91, 8: 20.0 / 3.38}
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _default_dir() -> str:
+    for cand in (os.environ.get("HIPSNAPSHOT_BENCH_DIR"), "/var/tmp", "/tmp"):
+        if cand and os.path.isdir(cand) and os.access(cand, os.W_OK):
+            return os.path.join(cand, "hipsnapshot_bench")
+    return "hipsnapshot_bench"
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3_8b", choices=["llama3_8b", "llama3_70b", "tiny"])
+    ap.add_argument("--path", default=None)
+    ap.add_argument("--async-iters", type=int, default=2)
+    ap.add_argument("--no-restore-check", action="store_true")
+    ap.add_argument("--fsync", action="store_true")
+    ap.add_argument("--direct-io", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    torchrun = "RANK" in os.environ and "WORLD_SIZE" in os.environ
+    if not torchrun:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using WORLD_SIZE",
+              file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist.init_process_group("nccl", device_id=dev)
+
+    from hipsnapshot import Snapshot
+    from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+    from hipsnapshot.ops import native
+
+    native.require_gpu_lib()  # the HIP data plane must be the one running
+    cfg = {"llama3_8b": LlamaConfig.llama3_8b, "llama3_70b": LlamaConfig.llama3_70b,
+           "tiny": LlamaConfig.tiny}[args.model]()
+    from torch.distributed.device_mesh import init_device_mesh
+
+    mesh = init_device_mesh("cuda", (world,))
+    model = build_fsdp_llama(cfg, dev, torch.bfloat16, mesh=mesh)
+    torch.cuda.synchronize()
+    local_bytes = sum(p._local_tensor.numel() * p._local_tensor.element_size()
+                      for p in model.parameters())
+    t = torch.tensor([local_bytes], dtype=torch.int64, device=dev)
+    dist.all_reduce(t)
+    total_bytes = int(t.item())
+
+    root = args.path or _default_dir()
+    path = os.path.join(root, "ckpt")
+    if rank == 0:
+        shutil.rmtree(root, ignore_errors=True)
+        os.makedirs(root, exist_ok=True)
+    dist.barrier()
+    opts = {"fsync": args.fsync, "direct_io": args.direct_io}
+    app_state = {"model": model}
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+
+    def log(msg):
+        if rank == 0:
+            print(msg, file=sys.stderr, flush=True)
+
+    for i in range(args.warmup):
+        t0 = time.monotonic()
+        Snapshot.take(path, app_state, storage_options=opts)
+        log(f"warmup {i}: {time.monotonic() - t0:.3f}s")
+
+    barrier_sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ts = time.perf_counter()
+        Snapshot.take(path, app_state, storage_options=opts)
+        log(f"step {i}: {time.perf_counter() - ts:.3f}s")
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    elapsed = float(e.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    gbps = total_bytes / (ms_per_step / 1e3) / 1e9
+
+    # async_take: time-to-unblock
+    unblock = []
+    drain = []
+    for i in range(args.async_iters):
+        barrier_sync()
+        ts = time.perf_counter()
+        pending = Snapshot.async_take(path + "_async", app_state, storage_options=opts)
+        tu = time.perf_counter() - ts
+        pending.wait()
+        torch.cuda.synchronize()
+        td = time.perf_counter() - ts
+        u = torch.tensor([tu, td], dtype=torch.float64, device=dev)
+        dist.all_reduce(u, op=dist.ReduceOp.MAX)
+        unblock.append(float(u[0].item()) * 1e3)
+        drain.append(float(u[1].item()) * 1e3)
+        log(f"async {i}: unblock {unblock[-1]:.1f} ms, total {drain[-1]:.1f} ms")
+
+    restore_ok = None
+    if not args.no_restore_check:
+        # bitwise restore check of one sharded parameter
+        p = dict(model.named_parameters())["layers.0.attention.wq.weight"]
+        ref = p._local_tensor.clone()
+        p._local_tensor.zero_()
+        barrier_sync()
+        tr = time.perf_counter()
+        Snapshot(path).restore(app_state)
+        barrier_sync()
+        restore_s = time.perf_counter() - tr
+        restore_ok = bool(torch.equal(ref, p._local_tensor))
+        log(f"restore: {restore_s:.3f}s ({total_bytes / restore_s / 1e9:.2f} GB/s) ok={restore_ok}")
+
+    base = BASELINE_GBPS.get(world)
+    if rank == 0:
+        out = {
+            "metric": "checkpoint save GB/s + time-to-unblock, Llama-3-8B FSDP",
+            "value": round(gbps, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(gbps / base, 3) if base else None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights)",
+            "config": {"model": {"llama3_8b": "Llama-3-8B", "llama3_70b": "Llama-3-70B",
+                                 "tiny": "tiny-llama"}[args.model],
+                       "global_batch": None, "seq_len": None,
+                       "parallelism": f"fsdp{world}",
+                       "checkpoint_bytes": total_bytes,
+                       "storage": "local fs" + (" fsync" if args.fsync else "")},
+            "time_to_unblock_ms": round(min(unblock), 2) if unblock else None,
+            "async_total_ms": round(min(drain), 2) if drain else None,
+            "restore_bitwise_ok": restore_ok,
+            "baseline_note": "reference DDP 20GB save, p4d: 1 GPU 1.44 GB/s, 8 GPU 5.92 GB/s; "
+                             "no published number for 2/4 GPUs",
+        }
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    if rank == 0:
+        shutil.rmtree(root, ignore_errors=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Data-plane microbenchmarks on one MI355X (prints one JSON line per test).
+
+* d2h_sdma      : hipMemcpyAsync D2H into the pinned pool, 1 and 4 streams
+* d2h_kernel    : hs_copy_nd storing straight into host-mapped pinned memory
+* d2h_torch     : torch ``.cpu()`` (pageable; what the reference does)
+* gather_hbm    : hs_copy_nd multi-tensor gather, HBM -> HBM (GB/s of payload)
+* pack_strided  : hs_copy_nd strided (transposed) -> contiguous, HBM -> HBM
+* fs_write      : native engine pwrite of pinned buffers (buffered / O_DIRECT)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import threading
+import time
+
+import torch
+
+from hipsnapshot.ops import native
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def timeit(fn, iters=5):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return min(ts), sorted(ts)[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mb", type=int, default=1024)
+    ap.add_argument("--dir", default="/tmp/hs_micro")
+    ap.add_argument("--skip-fs", action="store_true")
+    args = ap.parse_args()
+    dev = 0
+    n = args.mb << 20
+    src = torch.empty(n, dtype=torch.uint8, device="cuda:0").random_(0, 255)
+    pb = native.PinnedBuffer(n)
+
+    def sdma1():
+        native.memcpy(dev, 0, pb.ptr, src.data_ptr(), n, native.D2H, None, sync=True)
+
+    best, med = timeit(sdma1)
+    emit(test="d2h_sdma_1stream", GBps=n / best / 1e9, median_GBps=n / med / 1e9, bytes=n)
+
+    def sdma4():
+        q = n // 4
+        th = [threading.Thread(target=native.memcpy,
+                               args=(dev, i, pb.ptr + i * q, src.data_ptr() + i * q, q,
+                                     native.D2H, None, True)) for i in range(4)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+
+    best, med = timeit(sdma4)
+    emit(test="d2h_sdma_4stream", GBps=n / best / 1e9, median_GBps=n / med / 1e9)
+
+    stream = native.copy_stream(dev, 0)
+
+    def kern():
+        b = native.CopyBatch()
+        b.add(src.data_ptr(), torch.uint8, [1], pb.ptr, torch.uint8, [1], [n], 1)
+        b.launch(dev, stream, sync=True)
+
+    best, med = timeit(kern)
+    emit(test="d2h_kernel_hostmapped", GBps=n / best / 1e9, median_GBps=n / med / 1e9)
+
+    def tcpu():
+        src.cpu()
+
+    best, med = timeit(tcpu, 3)
+    emit(test="d2h_torch_pageable", GBps=n / best / 1e9, median_GBps=n / med / 1e9)
+
+    # H2D
+    def h2d():
+        native.memcpy(dev, 0, src.data_ptr(), pb.ptr, n, native.H2D, None, sync=True)
+
+    best, med = timeit(h2d)
+    emit(test="h2d_sdma_1stream", GBps=n / best / 1e9, median_GBps=n / med / 1e9)
+
+    # multi-tensor gather HBM->HBM: 2000 tensors of mixed sizes
+    sizes = [(4096 * 4096 * 2) if i % 10 == 0 else (4096 * 2 * (1 + i % 7)) for i in range(2000)]
+    ts = [torch.empty(s // 2, dtype=torch.bfloat16, device="cuda:0").normal_() for s in sizes]
+    total = sum(sizes)
+    dst = torch.empty(total + 256 * len(ts), dtype=torch.uint8, device="cuda:0")
+    offs, o = [], 0
+    for s in sizes:
+        offs.append(o)
+        o += (s + 255) // 256 * 256
+
+    def gather():
+        b = native.CopyBatch()
+        for t, off in zip(ts, offs):
+            b.add(t.data_ptr(), t.dtype, [1], dst.data_ptr() + off, t.dtype, [1], [t.numel()], 2)
+        b.launch(dev, int(torch.cuda.current_stream().cuda_stream), sync=True)
+
+    best, med = timeit(gather)
+    emit(test="gather_hbm_2000_tensors", GBps=total / best / 1e9, median_GBps=total / med / 1e9,
+         bytes=total, note="payload bytes/s (read+write = 2x)")
+
+    def torch_gather():
+        for t, off in zip(ts, offs):
+            dst[off:off + t.numel() * 2].view(torch.bfloat16).copy_(t)
+
+    best, med = timeit(torch_gather, 3)
+    emit(test="gather_hbm_torch_copy_loop", GBps=total / best / 1e9, median_GBps=total / med / 1e9)
+
+    # strided pack: transpose view of 8192x8192 bf16
+    a = torch.empty(8192, 8192, dtype=torch.bfloat16, device="cuda:0").normal_()
+    at = a.t()
+    out = torch.empty(8192 * 8192, dtype=torch.bfloat16, device="cuda:0")
+
+    def pack():
+        b = native.CopyBatch()
+        b.add(at.data_ptr(), at.dtype, at.stride(), out.data_ptr(), at.dtype, [8192, 1],
+              [8192, 8192], 2)
+        b.launch(dev, int(torch.cuda.current_stream().cuda_stream), sync=True)
+
+    best, med = timeit(pack)
+    nb = a.numel() * 2
+    emit(test="pack_transpose_8192sq_bf16", GBps=nb / best / 1e9, median_GBps=nb / med / 1e9)
+    assert torch.equal(out.view(8192, 8192), at.contiguous())
+
+    def tpack():
+        out.view(8192, 8192).copy_(at)
+
+    best, med = timeit(tpack)
+    emit(test="pack_transpose_torch", GBps=nb / best / 1e9, median_GBps=nb / med / 1e9)
+
+    # column shard (narrow on dim 1) pack
+    col = a[:, 1024:3072]
+    out2 = torch.empty(col.numel(), dtype=torch.bfloat16, device="cuda:0")
+
+    def colpack():
+        b = native.CopyBatch()
+        b.add(col.data_ptr(), col.dtype, col.stride(), out2.data_ptr(), col.dtype, [2048, 1],
+              list(col.shape), 2)
+        b.launch(dev, int(torch.cuda.current_stream().cuda_stream), sync=True)
+
+    best, med = timeit(colpack)
+    nb2 = col.numel() * 2
+    emit(test="pack_column_shard_bf16", GBps=nb2 / best / 1e9, median_GBps=nb2 / med / 1e9)
+    assert torch.equal(out2.view(col.shape), col.contiguous())
+
+    if not args.skip_fs:
+        os.makedirs(args.dir, exist_ok=True)
+        eng = native.IOEngine(16)
+        nfiles = 16
+        per = 256 << 20
+        bufs = [native.PinnedBuffer(per) for _ in range(nfiles)]
+        for direct in (0, 1):
+            flags = native.IO_MKDIRS | (native.IO_DIRECT if direct else 0)
+            t0 = time.perf_counter()
+            ids = [eng.submit_write(f"{args.dir}/f{i}", b.ptr, per, 0, flags)
+                   for i, b in enumerate(bufs)]
+            done = 0
+            while done < len(ids):
+                r = eng.poll()
+                for _, res in r:
+                    assert res >= 0, res
+                done += len(r)
+                if not r:
+                    time.sleep(0.0005)
+            dt = time.perf_counter() - t0
+            emit(test="fs_write_16x256MB", direct=direct, GBps=nfiles * per / dt / 1e9)
+        import shutil
+
+        shutil.rmtree(args.dir, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -440,25 +440,38 @@ int get_stream(int dev, int slot, hipStream_t* out, hipEvent_t* ev) {
   return 0;
 }
 
-// Build the tile table for a descriptor batch.
+// Build the tile table for a descriptor batch.  Tile size adapts to the
+// batch so that a launch always has >= ~4096 tiles when there is enough work
+// (>> 256 CUs: every CU gets several 4-wave workgroups and enough loads in
+// flight to reach HBM / PCIe bandwidth), and never below 32 KiB (tile-table
+// overhead) or above 1 MiB.
+int elem_bytes_host(int32_t dt) {
+  switch (dt) {
+    case kRaw1: return 1;
+    case kRaw2: case kF16: case kBF16: return 2;
+    case kRaw4: case kF32: return 4;
+    case kRaw8: case kF64: return 8;
+    default: return 16;
+  }
+}
+
 void build_tiles(const CopyDesc* descs, int n, std::vector<Tile>* tiles) {
+  int64_t total_bytes = 0;
+  for (int i = 0; i < n; ++i) total_bytes += descs[i].numel * elem_bytes_host(descs[i].src_dtype);
+  int64_t tile_bytes = total_bytes / 4096;
+  tile_bytes = (tile_bytes + 16383) / 16384 * 16384;
+  tile_bytes = std::max<int64_t>(32 << 10, std::min<int64_t>(kTileBytes, tile_bytes));
   for (int i = 0; i < n; ++i) {
     const CopyDesc& d = descs[i];
+    const int es = elem_bytes_host(d.src_dtype);
     int64_t total, step;
     if (d.flags & 1) {
-      int es = 1;
-      switch (d.src_dtype) {
-        case kRaw1: es = 1; break;
-        case kRaw2: case kF16: case kBF16: es = 2; break;
-        case kRaw4: case kF32: es = 4; break;
-        case kRaw8: case kF64: es = 8; break;
-        default: es = 16;
-      }
       total = d.numel * es;  // bytes
-      step = kTileBytes;
+      step = tile_bytes;
     } else {
       total = d.numel;
-      step = 64 * 1024;  // elements per tile on the strided/cast path
+      // elements per tile on the strided/cast path (multiple of the per-block run)
+      step = std::max<int64_t>(kBlock * 8, tile_bytes / es / (kBlock * 8) * (kBlock * 8));
     }
     for (int64_t b = 0; b < total; b += step) {
       tiles->push_back(Tile{i, 0, b, std::min(total, b + step)});

@@ -203,8 +203,11 @@ class Engine {
       int r = MkdirsFor(j.path);
       if (r < 0) return r;
     }
+    // Overwrite in place instead of O_TRUNC: re-taking a snapshot to the same
+    // path then rewrites the page-cache pages it already owns (truncating and
+    // re-allocating 16 GB of page cache costs ~1 s per take on a 3 TB host);
+    // the stale tail, if any, is cut with ftruncate below.
     int oflags = O_WRONLY | O_CREAT | O_CLOEXEC;
-    if (!(j.flags & kFlagAppend)) oflags |= O_TRUNC;
     int fd = ::open(j.path.c_str(), oflags, 0644);
     if (fd < 0) return -errno;
     int64_t res = 0;
@@ -222,6 +225,12 @@ class Engine {
       }
     }
     res = full_pwrite(fd, j.buf + body, j.nbytes - body, j.offset + body);
+    if (res >= 0 && !(j.flags & kFlagAppend) && j.offset == 0) {
+      struct stat st;
+      if (::fstat(fd, &st) == 0 && static_cast<size_t>(st.st_size) != j.nbytes) {
+        if (::ftruncate(fd, static_cast<off_t>(j.nbytes)) != 0) res = -errno;
+      }
+    }
     if (res >= 0 && (j.flags & kFlagSync)) {
       if (::fdatasync(fd) != 0) res = -errno;
     }

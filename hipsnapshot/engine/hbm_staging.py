@@ -107,3 +107,20 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
             st.arena_keepalive = done_keep
         frozen[dev] = total
     return frozen
+
+
+def is_deferrable(wr: WriteReq) -> bool:
+    """A write whose bytes are already captured (frozen HBM copy or eagerly
+    serialized object) can run entirely after ``async_take`` returns."""
+    from ..io.batcher import GPUBatchedBufferStager
+    from ..io.object import ObjectBufferStager
+    from ..io.tensor import TensorBufferStager
+
+    st = wr.buffer_stager
+    if isinstance(st, ObjectBufferStager):
+        return True
+    if isinstance(st, TensorBufferStager):
+        return st.frozen
+    if isinstance(st, GPUBatchedBufferStager):
+        return all(m.frozen for _, m in st.members)
+    return False

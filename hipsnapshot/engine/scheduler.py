@@ -190,6 +190,41 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     return PendingIOWork(io_tasks, executor, stats, failure)
 
 
+class DeferredIOWork:
+    """``PendingIOWork`` for an async take whose device state was frozen in
+    HBM: the immediate part (host tensors, already copied) is staged before
+    ``async_take`` returns; the deferred part (HBM arena -> pinned -> storage)
+    runs its whole pipeline in the background commit thread."""
+
+    def __init__(self, first: PendingIOWork, deferred: List[WriteReq], storage: StoragePlugin,
+                 memory_budget_bytes: int, rank: int) -> None:
+        self.first = first
+        self.deferred = deferred
+        self.storage = storage
+        self.budget = memory_budget_bytes
+        self.rank = rank
+        self.stats = first.stats
+        self._second: Optional[PendingIOWork] = None
+
+    async def complete(self) -> None:
+        async def run_deferred() -> None:
+            p = await execute_write_reqs(self.deferred, self.storage, self.budget, self.rank)
+            self._second = p
+            await p.complete()
+
+        res = await asyncio.gather(self.first.complete(), run_deferred(), return_exceptions=True)
+        if self._second is not None:
+            self.stats.bytes_written += self._second.stats.bytes_written
+            self.stats.n_reqs += self._second.stats.n_reqs
+        self.stats.t_done = time.monotonic()
+        for r in res:
+            if isinstance(r, BaseException):
+                raise r
+
+    def sync_complete(self, event_loop: asyncio.AbstractEventLoop) -> None:
+        event_loop.run_until_complete(self.complete())
+
+
 def sync_execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                             memory_budget_bytes: int, rank: int,
                             event_loop: asyncio.AbstractEventLoop) -> PendingIOWork:

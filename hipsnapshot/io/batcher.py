@@ -47,10 +47,14 @@ def _align(n: int, a: int) -> int:
 
 
 class Slab:
-    def __init__(self, device: Optional[torch.device]) -> None:
+    def __init__(self, device: Optional[torch.device], name: Optional[str] = None) -> None:
         self.device = device
         self.members: List[Tuple[Tuple[int, int], TensorBufferStager]] = []
-        self.location = os.path.join("batched", str(uuid.uuid4()))
+        # Deterministic names (``batched/<prefix>_<device>_<k>``) when the
+        # caller provides a prefix: re-taking a snapshot to the same path then
+        # overwrites its slabs like every other blob instead of leaking
+        # uuid-named files; uuid4 names otherwise (reference behaviour).
+        self.location = os.path.join("batched", name or str(uuid.uuid4()))
         self.sz_bytes = 0
 
     def add(self, nbytes: int, stager: TensorBufferStager, align: int) -> Tuple[int, int]:
@@ -120,7 +124,8 @@ class GPUBatchedBufferStager(BufferStager):
 
 
 def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
-                         slab_size_threshold_bytes: Optional[int] = None
+                         slab_size_threshold_bytes: Optional[int] = None,
+                         name_prefix: Optional[str] = None
                          ) -> Tuple[List[Entry], List[WriteReq]]:
     threshold = slab_size_threshold_bytes or knobs.get_slab_size_threshold_bytes()
     align = knobs.slab_align()
@@ -138,9 +143,16 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
             out.append(wr)
             continue
         dev = t.device if t.is_cuda else None
-        lst = slabs.setdefault(dev, [Slab(dev)])
+
+        def _new_slab(k: int) -> Slab:
+            if name_prefix is None:
+                return Slab(dev)
+            tag = f"cuda{dev.index}" if dev is not None else "cpu"
+            return Slab(dev, f"{name_prefix}_{tag}_{k}")
+
+        lst = slabs.setdefault(dev, [_new_slab(0)])
         if lst[-1].members and _align(lst[-1].sz_bytes, align) + nbytes >= threshold:
-            lst.append(Slab(dev))
+            lst.append(_new_slab(len(lst)))
         lo, hi = lst[-1].add(nbytes, st, align)
         relocation[wr.path] = (lst[-1].location, lo, hi)
     for lst in slabs.values():
@@ -161,13 +173,26 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
 
 
 class BatchedBufferConsumer(BufferConsumer):
+    """Consumes one merged ranged read that covers several entries.
+
+    Members that restore into HBM (plain tensors, DTensor/ShardedTensor
+    shards) expose ``device_regions``; all of them are served by ONE H2D DMA
+    of the merged pinned buffer and ONE scatter/cast kernel launch per device.
+    """
+
     def __init__(self, members: List[Tuple[Tuple[int, int], BufferConsumer]],
                  buf_sz_bytes: int) -> None:
         self.members = members
         self.buf_sz_bytes = buf_sz_bytes
-        self._gpu = [(rng, c) for rng, c in members if _gpu_raw_consumer(c)]
-        gpu_ids = {id(c) for _, c in self._gpu}
-        self._other = [(rng, c) for rng, c in members if id(c) not in gpu_ids]
+        self._gpu = []
+        self._other = []
+        for rng, c in members:
+            fn = getattr(c, "device_regions", None)
+            regions = fn(rng[0]) if fn is not None else None
+            if regions:
+                self._gpu.append((rng, c, regions))
+            else:
+                self._other.append((rng, c))
 
     # reference-compatible attribute
     @property
@@ -193,21 +218,15 @@ class BatchedBufferConsumer(BufferConsumer):
         addr = staging.host_buffer_addr(buf)
         by_dev: Dict[int, list] = defaultdict(list)
         producers = {}
-        for (lo, hi), c in self._gpu:
-            dev = staging.device_of(c.tensor)
-            by_dev[dev].append((string_to_dtype(c.entry.dtype), c.entry.shape, lo, None, c.tensor))
-            producers.setdefault(dev, c.producer)
+        for _rng, c, regions in self._gpu:
+            dev = staging.device_of(regions[0][4])
+            by_dev[dev].extend(regions)
+            producers.setdefault(dev, getattr(c, "producer", 0))
         for dev, regions in by_dev.items():
             staging.scatter_host_regions(addr, self.buf_sz_bytes, regions, dev, producers[dev])
 
     def get_consuming_cost_bytes(self) -> int:
         return self.buf_sz_bytes + sum(c.get_consuming_cost_bytes() for _, c in self.members)
-
-
-def _gpu_raw_consumer(c: BufferConsumer) -> bool:
-    return (type(c) is TensorBufferConsumer and c.tensor.is_cuda
-            and c.entry.serializer == Serializer.BUFFER_PROTOCOL.value
-            and c.tensor.dim() <= 8)
 
 
 def batch_read_requests(read_reqs: List[ReadReq]) -> List[ReadReq]:

@@ -285,6 +285,13 @@ class ShardedTensorBufferConsumer(BufferConsumer):
         n = tensor_nbytes_from_entry(self.entry)
         return 2 * n if self.entry.serializer == Serializer.TORCH_SAVE.value else n
 
+    def device_regions(self, base: int):
+        if not self._gpu:
+            return None
+        dtype = string_to_dtype(self.entry.dtype)
+        return [(dtype, self.entry.shape, base, [(d, so, ln) for d, so, _do, ln in r.narrows],
+                 _narrow_dst(r.dst, r.narrows)) for r in self.regions]
+
 
 def _narrow_dst(dst: torch.Tensor, narrows) -> torch.Tensor:
     for dim, _so, do, ln in narrows:

@@ -276,6 +276,14 @@ class TensorBufferConsumer(BufferConsumer):
         n = self._nbytes()
         return 2 * n if self.entry.serializer == Serializer.TORCH_SAVE.value else n
 
+    def device_regions(self, base: int):
+        """Scatter regions for a merged (batched) GPU restore, or None."""
+        t = self.tensor
+        if (t.is_cuda and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value
+                and t.dim() <= 8 and list(t.shape) == list(self.entry.shape)):
+            return [(string_to_dtype(self.entry.dtype), self.entry.shape, base, None, t)]
+        return None
+
 
 def _q_params_equal(lhs: torch.Tensor, rhs: torch.Tensor) -> bool:
     if lhs.qscheme() != rhs.qscheme():

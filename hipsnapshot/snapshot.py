@@ -173,12 +173,25 @@ class Snapshot:
                                storage=storage, event_loop=loop, storage_options=storage_options,
                                nonce=nonce)
 
+    @staticmethod
+    def _uncommit(storage: StoragePlugin, loop: asyncio.AbstractEventLoop) -> None:
+        """A snapshot exists iff its metadata exists: drop an older commit at
+        this path before its blobs get overwritten."""
+        try:
+            storage.sync_delete(SNAPSHOT_METADATA_FNAME, loop)
+        except (FileNotFoundError, KeyError):
+            pass
+        except Exception as e:  # noqa: BLE001 - e.g. plugins without delete
+            logger.debug(f"could not remove previous metadata: {e}")
+
     @classmethod
     def _take_impl(cls, path: str, app_state: AppState, replicated: Set[str],
                    global_keys: List[str], comm: Comm, storage: StoragePlugin,
                    loop: asyncio.AbstractEventLoop, is_async: bool,
                    prepare_func: Optional[PrepareFunc], quantize: Optional[List[str]]
                    ) -> Tuple[PendingIOWork, SnapshotMetadata]:
+        if comm.get_rank() == 0:
+            cls._uncommit(storage, loop)
         app_state = dict(app_state)
         rng_item = cls._pop_rng_state(app_state)
         manifest: Dict[str, Entry] = {}
@@ -228,17 +241,25 @@ class Snapshot:
         object_entries, path_reqs = partition_write_reqs(object_entries, path_reqs, comm)
         write_reqs = [wr for wrs in path_reqs.values() for wr in wrs]
         if not knobs.is_batching_disabled():
-            _, write_reqs = batch_write_requests(list(object_entries.values()), write_reqs)
+            _, write_reqs = batch_write_requests(list(object_entries.values()), write_reqs,
+                                                 name_prefix=f"r{rank}")
         manifest.update(primitives)
         manifest.update(object_entries)
         manifest = cls._gather_manifest(manifest, comm)
 
+        budget = get_process_memory_budget_bytes(comm)
+        deferred: List[WriteReq] = []
         if is_async and knobs.async_hbm_staging_enabled():
-            from .engine.hbm_staging import freeze_device_state
+            from .engine.hbm_staging import freeze_device_state, is_deferrable
 
             freeze_device_state(write_reqs)
-        budget = get_process_memory_budget_bytes(comm)
+            deferred = [wr for wr in write_reqs if is_deferrable(wr)]
+            write_reqs = [wr for wr in write_reqs if not is_deferrable(wr)]
         pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop)
+        if deferred:
+            from .engine.scheduler import DeferredIOWork
+
+            pending = DeferredIOWork(pending, deferred, storage, budget, rank)
         metadata = SnapshotMetadata(version=__version__, world_size=comm.get_world_size(),
                                     manifest=manifest)
         return pending, metadata

@@ -141,6 +141,18 @@ class FSStoragePlugin(StoragePlugin):
         read_io.buf = dest_view
         self.bytes_read += n
 
+    async def commit_metadata(self, path: str, buf: bytes) -> None:
+        """Atomic commit: write a temp file then rename it into place."""
+        final = self._abs(path)
+        tmp = f"{final}.tmp.{os.getpid()}"
+        os.makedirs(os.path.dirname(final) or ".", exist_ok=True)
+        with open(tmp, "wb") as f:
+            f.write(buf)
+            if self.fsync:
+                f.flush()
+                os.fsync(f.fileno())
+        os.replace(tmp, final)
+
     async def delete(self, path: str) -> None:
         os.remove(self._abs(path))
 
