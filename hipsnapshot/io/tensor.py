@@ -97,6 +97,13 @@ class TensorIOPreparer:
                      buffer_size_limit_bytes: Optional[int] = None
                      ) -> Tuple[List[ReadReq], Future]:
         if tensor_out is None or not cls.can_load_inplace(entry, tensor_out):
+            if entry.serializer == Serializer.TORCH_SAVE.value:
+                # the payload carries its own tensor (quantized params etc.):
+                # hand the loaded object out instead of pre-allocating
+                fut = Future()
+                consumer = TensorBufferConsumer(tensor=None, entry=entry, future=fut)
+                return [ReadReq(path=entry.location, byte_range=entry.byte_range_tuple,
+                                buffer_consumer=consumer)], fut
             tensor_out = cls.empty_tensor_from_entry(entry)
         if (buffer_size_limit_bytes is not None
                 and entry.serializer == Serializer.BUFFER_PROTOCOL.value):
@@ -232,17 +239,19 @@ def deserialize_tensor(buf, entry: TensorEntry) -> torch.Tensor:
 
 
 class TensorBufferConsumer(BufferConsumer):
-    def __init__(self, tensor: torch.Tensor, entry: TensorEntry) -> None:
+    def __init__(self, tensor: Optional[torch.Tensor], entry: TensorEntry,
+                 future: Optional[Future] = None) -> None:
         self.tensor = tensor
         self.entry = entry
-        self.producer = staging.producer_stream_handle(tensor)
+        self.future = future
+        self.producer = staging.producer_stream_handle(tensor) if tensor is not None else 0
         self._direct = False
 
     def _nbytes(self) -> int:
         return tensor_nbytes_from_entry(self.entry)
 
     def get_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
-        if self.entry.serializer != Serializer.BUFFER_PROTOCOL.value:
+        if self.entry.serializer != Serializer.BUFFER_PROTOCOL.value or self.tensor is None:
             return None
         t = self.tensor
         if (not t.is_cuda and t.dtype == string_to_dtype(self.entry.dtype)
@@ -265,6 +274,9 @@ class TensorBufferConsumer(BufferConsumer):
 
     def _consume_sync(self, buf) -> None:
         t = self.tensor
+        if t is None:
+            self.future.obj = deserialize_tensor(buf, self.entry)
+            return
         if (t.is_cuda and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value):
             staging.h2d_into(t, staging.host_buffer_addr(buf), self._nbytes(),
                              string_to_dtype(self.entry.dtype), self.entry.shape, self.producer)
@@ -279,8 +291,8 @@ class TensorBufferConsumer(BufferConsumer):
     def device_regions(self, base: int):
         """Scatter regions for a merged (batched) GPU restore, or None."""
         t = self.tensor
-        if (t.is_cuda and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value
-                and t.dim() <= 8 and list(t.shape) == list(self.entry.shape)):
+        if (t is not None and t.is_cuda
+                and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value and t.dim() <= 8 and list(t.shape) == list(self.entry.shape)):
             return [(string_to_dtype(self.entry.dtype), self.entry.shape, base, None, t)]
         return None
 

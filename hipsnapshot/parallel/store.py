@@ -88,6 +88,7 @@ class LinearBarrier:
         self.leader_rank = leader_rank
         self.arrived = False
         self.departed = False
+        self._errored = False
 
     def _key(self, rank: int) -> str:
         return f"{self.prefix}_{rank}"
@@ -99,7 +100,8 @@ class LinearBarrier:
             raise RuntimeError("Can't call .arrive() on a completed barrier.")
         self.arrived = True
         if self.rank != self.leader_rank:
-            self.store.set(self._key(self.rank), "")
+            if not self._errored:  # never overwrite a reported error
+                self.store.set(self._key(self.rank), "")
             return
         peers = [self._key(r) for r in range(self.world_size) if r != self.leader_rank]
         if peers:
@@ -127,4 +129,5 @@ class LinearBarrier:
             raise RuntimeError(err.decode() if isinstance(err, bytes) else str(err))
 
     def report_error(self, err: str) -> None:
+        self._errored = True
         self.store.set(self._key(self.rank), f"Rank {self.rank} encountered error: {err}")

@@ -1,0 +1,220 @@
+"""Worker bodies for multi-process tests (module-level so spawn can import them)."""
+
+import os
+import time
+from datetime import timedelta
+
+import torch
+import torch.distributed as dist
+
+from hipsnapshot import Snapshot, StateDict
+from hipsnapshot.parallel.comm import Comm
+from hipsnapshot.utils.test_utils import assert_state_dict_eq
+
+
+def _ddp_model(seed: int):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+
+
+def ddp_take(path: str, chunk_bytes=None):
+    from hipsnapshot.knobs import override_max_chunk_size_bytes
+
+    rank = dist.get_rank()
+    model = torch.nn.parallel.DistributedDataParallel(_ddp_model(0))
+    per_rank = StateDict(rank=rank, t=torch.full((4,), float(rank)))
+    app = {"model": model, "per_rank": per_rank}
+    if chunk_bytes:
+        with override_max_chunk_size_bytes(chunk_bytes):
+            Snapshot.take(path, app)
+    else:
+        Snapshot.take(path, app)
+
+
+def ddp_restore(path: str, saved_world: int):
+    rank = dist.get_rank()
+    model = torch.nn.parallel.DistributedDataParallel(_ddp_model(100 + rank))
+    per_rank = StateDict(rank=-1)
+    snap = Snapshot(path)
+    snap.restore({"model": model, "per_rank": per_rank})
+    ref = _ddp_model(0)
+    assert_state_dict_eq(model.module.state_dict(), ref.state_dict())
+    if rank < saved_world:
+        assert per_rank["rank"] == rank and torch.equal(per_rank["t"], torch.full((4,), float(rank)))
+    else:
+        assert per_rank["rank"] == -1  # new rank: per-rank state is not available
+    man = snap.get_manifest()
+    # replicated entries are stored once, under rank 0
+    assert any(k.startswith("0/model/") for k in man)
+    assert not any(k.startswith("1/model/") for k in man)
+    rep = [e for k, e in man.items() if k.startswith("0/model/") and hasattr(e, "location")]
+    assert all(e.replicated for e in rep)
+
+
+def write_load_balance(path: str):
+    """Replicated big tensors must be spread over ranks by the partitioner."""
+    from hipsnapshot.knobs import override_is_batching_disabled
+
+    rank = dist.get_rank()
+    sd = StateDict({f"w{i}": torch.full((1000 * (i + 1),), float(i)) for i in range(8)})
+    with override_is_batching_disabled(True):
+        Snapshot.take(path, {"sd": sd}, replicated=["**"])
+    dist.barrier()
+    if rank == 0:
+        man = Snapshot(path).get_manifest()
+        assert all(man[f"0/sd/w{i}"].replicated for i in range(8))
+        assert all(man[f"0/sd/w{i}"].location.startswith("replicated/") for i in range(8))
+    out = StateDict({f"w{i}": torch.zeros(1000 * (i + 1)) for i in range(8)})
+    Snapshot(path).restore({"sd": out})
+    for i in range(8):
+        assert torch.equal(out[f"w{i}"], torch.full((1000 * (i + 1),), float(i)))
+
+
+def partition_plan_check():
+    from hipsnapshot.parallel.partitioner import partition_write_reqs
+    from hipsnapshot.io.preparer import prepare_write
+    from hipsnapshot.knobs import override_max_chunk_size_bytes
+
+    comm = Comm()
+    rank = comm.get_rank()
+    ws = comm.get_world_size()
+    entries, reqs = {}, {}
+    with override_max_chunk_size_bytes(4000):
+        for i in range(6):
+            t = torch.ones(1000 * (i + 1))
+            e, w = prepare_write(t, f"sd/t{i}", rank, replicated=True)
+            entries[f"sd/t{i}"], reqs[f"sd/t{i}"] = e, w
+    new_entries, new_reqs = partition_write_reqs(entries, reqs, comm)
+    mine = sum(len(v) for v in new_reqs.values())
+    gathered = [None] * ws
+    comm.all_gather_object(gathered, (mine, sorted(new_reqs)))
+    total = sum(len(v) for v in reqs.values())
+    assert sum(g[0] for g in gathered) == total, gathered
+    # balanced within one unit (chunks are ~4000 B each)
+    counts = [g[0] for g in gathered]
+    assert max(counts) - min(counts) <= 2, counts
+
+
+def fsdp_take(path: str):
+    from torch.distributed.device_mesh import init_device_mesh
+    from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+
+    mesh = init_device_mesh("cpu", (dist.get_world_size(),))
+    model = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cpu"), torch.float32, mesh=mesh)
+    Snapshot.take(path, {"model": model})
+    full = {k: v.full_tensor() for k, v in model.state_dict().items()}
+    if dist.get_rank() == 0:
+        torch.save(full, path + "_ref.pt")
+
+
+def fsdp_restore(path: str):
+    from torch.distributed.device_mesh import init_device_mesh
+    from hipsnapshot.models.llama import Llama, LlamaConfig
+    from torch.distributed.fsdp import fully_shard
+
+    ws = dist.get_world_size()
+    mesh = init_device_mesh("cpu", (ws,))
+    with torch.device("meta"):
+        model = Llama(LlamaConfig.tiny())
+    for layer in model.layers:
+        fully_shard(layer, mesh=mesh)
+    fully_shard(model, mesh=mesh)
+    model.to_empty(device="cpu")
+    for p in model.parameters():
+        p._local_tensor.zero_()
+    Snapshot(path).restore({"model": model})
+    ref = torch.load(path + "_ref.pt", weights_only=True)
+    for k, v in model.state_dict().items():
+        assert torch.equal(v.full_tensor(), ref[k]), k
+    # read_object of a sharded entry into a plain tensor (whole global tensor)
+    w = torch.zeros_like(ref["layers.0.attention.wq.weight"])
+    Snapshot(path).read_object("0/model/layers.0.attention.wq.weight", obj_out=w)
+    assert torch.equal(w, ref["layers.0.attention.wq.weight"])
+
+
+class FaultyPlugin:
+    pass
+
+
+def async_take_ok(path: str):
+    rank = dist.get_rank()
+    t = torch.full((1000,), float(rank))
+    sd = StateDict(t=t, step=rank)
+    pending = Snapshot.async_take(path, {"sd": sd})
+    t.fill_(-1)  # must not leak into the snapshot
+    snap = pending.wait()
+    assert pending.done()
+    out = StateDict()
+    snap.restore({"sd": out})
+    assert torch.equal(out["t"], torch.full((1000,), float(rank))) and out["step"] == rank
+
+
+def async_take_faulty(path: str):
+    import asyncio
+    from unittest import mock
+
+    from hipsnapshot.storage.fs import FSStoragePlugin
+
+    rank = dist.get_rank()
+
+    class Faulty(FSStoragePlugin):
+        async def write(self, write_io):
+            if rank == 1 and not write_io.path.startswith(".snapshot"):
+                await asyncio.sleep(0.2)
+                raise OSError("injected failure")
+            await super().write(write_io)
+
+    with mock.patch("hipsnapshot.storage.fs.FSStoragePlugin", Faulty):
+        pending = Snapshot.async_take(path, {"sd": StateDict(t=torch.ones(100) * rank)})
+        try:
+            pending.wait()
+            raised = False
+        except RuntimeError as e:
+            raised = True
+            assert "injected failure" in str(e) or "encountered error" in str(e), str(e)
+    assert raised, "every rank must observe the failure"
+    dist.barrier()
+    assert not os.path.exists(os.path.join(path, ".snapshot_metadata"))
+
+
+def linear_barrier(prefix: str, skip_arrive_rank: int = -1, error_rank: int = -1):
+    from hipsnapshot.parallel.store import LinearBarrier, get_or_create_store
+
+    comm = Comm()
+    store = get_or_create_store(comm)
+    rank, ws = comm.get_rank(), comm.get_world_size()
+    b = LinearBarrier(prefix, store, rank, ws, leader_rank=0)
+    if rank == error_rank:
+        b.report_error("boom")
+        return
+    if rank == skip_arrive_rank:
+        return
+    try:
+        b.arrive(timeout=timedelta(seconds=3))
+        b.depart(timeout=timedelta(seconds=3))
+        assert error_rank < 0 and skip_arrive_rank < 0
+    except RuntimeError as e:
+        assert error_rank >= 0 or skip_arrive_rank >= 0, e
+        if error_rank >= 0:
+            assert "boom" in str(e)
+    except Exception as e:  # store timeout
+        assert skip_arrive_rank >= 0, e
+
+
+def comm_collectives():
+    comm = Comm()
+    rank, ws = comm.get_rank(), comm.get_world_size()
+    big = "x" * (200_000 * (rank + 1))  # > 64 KiB frame -> second round
+    out = [None] * ws
+    comm.all_gather_object(out, {"r": rank, "big": big})
+    for r in range(ws):
+        assert out[r]["r"] == r and len(out[r]["big"]) == 200_000 * (r + 1)
+    small = [None] * ws
+    comm.all_gather_object(small, rank * 10)
+    assert small == [r * 10 for r in range(ws)]
+    obj = [f"from0-{rank}"]
+    comm.broadcast_object_list(obj, src=0)
+    assert obj == ["from0-0"]
+    res = [None]
+    comm.scatter_object_list(res, [f"s{r}" for r in range(ws)] if rank == 0 else None, src=0)
+    assert res[0] == f"s{rank}"

@@ -1,0 +1,57 @@
+"""Multi-process CPU (gloo) tests: DDP replication + partitioning + elastic
+upscale, FSDP2/DTensor resharding across world sizes, async take with fault
+injection, store barrier, object collectives."""
+
+import pytest
+
+import dist_workers as W
+from hipsnapshot.utils.test_utils import run_distributed
+
+pytestmark = pytest.mark.multiproc
+
+
+def test_comm_collectives():
+    run_distributed(W.comm_collectives, 3)
+
+
+@pytest.mark.parametrize("chunk", [None, 700])
+def test_ddp_take_restore_and_upscale(tmp_path, chunk):
+    p = str(tmp_path / f"ddp_{chunk}")
+    run_distributed(W.ddp_take, 2, p, chunk)
+    run_distributed(W.ddp_restore, 2, p, 2)
+    run_distributed(W.ddp_restore, 3, p, 2)  # elastic: a new rank joins
+
+
+def test_replicated_write_load_balance(tmp_path):
+    run_distributed(W.write_load_balance, 3, str(tmp_path / "lb"))
+
+
+def test_partition_plan():
+    run_distributed(W.partition_plan_check, 4)
+
+
+@pytest.mark.parametrize("save_ws,load_ws", [(2, 2), (2, 1), (2, 3), (4, 2)])
+def test_fsdp2_dtensor_resharding(tmp_path, save_ws, load_ws):
+    p = str(tmp_path / "fsdp")
+    run_distributed(W.fsdp_take, save_ws, p)
+    run_distributed(W.fsdp_restore, load_ws, p)
+
+
+def test_async_take(tmp_path):
+    run_distributed(W.async_take_ok, 2, str(tmp_path / "a"))
+
+
+def test_async_take_fault_injection(tmp_path):
+    run_distributed(W.async_take_faulty, 2, str(tmp_path / "f"))
+
+
+def test_linear_barrier():
+    run_distributed(W.linear_barrier, 3, "lb_ok")
+
+
+def test_linear_barrier_error_propagation():
+    run_distributed(W.linear_barrier, 3, "lb_err", -1, 1)
+
+
+def test_linear_barrier_timeout():
+    run_distributed(W.linear_barrier, 2, "lb_to", 1, -1)

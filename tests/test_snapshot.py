@@ -1,0 +1,185 @@
+"""Single-process end-to-end take/restore (reference: tests/test_snapshot.py,
+test_rng_state.py, test_read_object.py, test_fs_storage_plugin.py)."""
+
+import json
+import os
+from collections import OrderedDict
+
+import pytest
+import torch
+
+from hipsnapshot import RNGState, Snapshot, StateDict
+from hipsnapshot.knobs import override_max_chunk_size_bytes, override_slab_size_threshold_bytes
+from hipsnapshot.utils.test_utils import assert_state_dict_eq, rand_tensor
+
+
+def _model():
+    return torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 8))
+
+
+def test_state_dict_odd_keys(tmp_path, toggle_batching):
+    sd = StateDict({"a/b": torch.randn(3), "%2F": 1, "": {"": [torch.ones(2)]}, 7: "seven",
+                    "nested": OrderedDict(x=1.5, y=[b"raw", True, None])})
+    Snapshot.take(str(tmp_path / "s"), {"sd": sd})
+    out = StateDict()
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    assert_state_dict_eq(dict(out), dict(sd))
+
+
+@pytest.mark.parametrize("opt_cls", [torch.optim.Adagrad, torch.optim.Adam, torch.optim.SGD])
+def test_model_and_optimizer(tmp_path, toggle_batching, opt_cls):
+    torch.manual_seed(0)
+    m = _model()
+    kw = {"momentum": 0.9} if opt_cls is torch.optim.SGD else {}
+    o = opt_cls(m.parameters(), lr=0.1, **kw)
+    for _ in range(2):
+        m(torch.randn(4, 32)).sum().backward()
+        o.step()
+    Snapshot.take(str(tmp_path / "s"), {"m": m, "o": o})
+    m2 = _model()
+    o2 = opt_cls(m2.parameters(), lr=0.5, **kw)
+    m2(torch.randn(4, 32)).sum().backward()
+    o2.step()
+    Snapshot(str(tmp_path / "s")).restore({"m": m2, "o": o2})
+    assert_state_dict_eq(m.state_dict(), m2.state_dict())
+    assert_state_dict_eq(o.state_dict(), o2.state_dict())
+
+
+def test_differing_structure_restore(tmp_path):
+    """Restore only fills what the target asks for, adds what the snapshot has."""
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(a=torch.ones(2), b=2)})
+    out = StateDict(c=3)
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    assert set(out.keys()) == {"a", "b", "c"}
+
+
+def test_inplace_restore_keeps_storage(tmp_path):
+    t = torch.randn(64, 64)
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(t=t)})
+    target = torch.zeros(64, 64)
+    ptr = target.data_ptr()
+    sd = StateDict(t=target)
+    Snapshot(str(tmp_path / "s")).restore({"sd": sd})
+    assert sd["t"].data_ptr() == ptr and torch.equal(target, t)
+
+
+def test_chunked_and_slabbed(tmp_path, toggle_batching):
+    ts = {f"t{i}": rand_tensor([50 + i, 17], dt) for i, dt in
+          enumerate([torch.float32, torch.bfloat16, torch.int64, torch.bool, torch.float16])}
+    with override_max_chunk_size_bytes(1000), override_slab_size_threshold_bytes(3000):
+        Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(ts)})
+    man = Snapshot(str(tmp_path / "s")).get_manifest()
+    assert man["0/sd/t0"].type == "ChunkedTensor"
+    out = StateDict({k: torch.zeros_like(v) for k, v in ts.items()})
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    assert_state_dict_eq(dict(out), ts)
+
+
+def test_rng_state_invariant(tmp_path):
+    torch.manual_seed(42)
+
+    class Mutator:
+        def state_dict(self):
+            torch.rand(10)  # side effect on the RNG
+            return {"x": 1}
+
+        def load_state_dict(self, sd):
+            torch.rand(10)
+
+    app = {"rng": RNGState(), "mut": Mutator()}
+    Snapshot.take(str(tmp_path / "s"), app)
+    after_take = torch.rand(5)
+    torch.rand(100)
+    Snapshot(str(tmp_path / "s")).restore(app)
+    assert torch.equal(torch.rand(5), after_take)
+
+
+def test_multiple_rng_states_rejected(tmp_path):
+    with pytest.raises(RuntimeError):
+        Snapshot.take(str(tmp_path / "s"), {"a": RNGState(), "b": RNGState()})
+
+
+def test_non_stateful_rejected(tmp_path):
+    with pytest.raises(TypeError):
+        Snapshot.take(str(tmp_path / "s"), {"a": {"not": "stateful"}})
+
+
+def test_read_object(tmp_path):
+    sd = StateDict(t=torch.randn(100, 10), p=3.5, s="hi", big=torch.arange(10000))
+    Snapshot.take(str(tmp_path / "s"), {"sd": sd})
+    snap = Snapshot(str(tmp_path / "s"))
+    assert snap.read_object("0/sd/p") == 3.5
+    assert snap.read_object("0/sd/s") == "hi"
+    assert torch.equal(snap.read_object("0/sd/t"), sd["t"])
+    out = torch.zeros(100, 10)
+    assert snap.read_object("0/sd/t", obj_out=out) is out and torch.equal(out, sd["t"])
+    assert torch.equal(snap.read_object("0/sd/big", memory_budget_bytes=1000), sd["big"])
+    with pytest.raises(RuntimeError):
+        snap.read_object("0/sd/missing")
+
+
+def test_object_entries_weights_only_and_trust(tmp_path):
+    class Custom:
+        def __init__(self):
+            self.v = 5
+
+    import builtins
+
+    builtins._HsTestCustom = Custom  # make it picklable by reference
+    Custom.__module__, Custom.__qualname__ = "builtins", "_HsTestCustom"
+    try:
+        sd = StateDict(obj={1, 2, 3}, custom=Custom())
+        Snapshot.take(str(tmp_path / "s"), {"sd": sd})
+        snap = Snapshot(str(tmp_path / "s"))
+        # sets are allow-listed in weights_only loading
+        assert snap.read_object("0/sd/obj") == {1, 2, 3}
+        with pytest.raises(Exception):
+            snap.read_object("0/sd/custom")
+        trusted = Snapshot(str(tmp_path / "s"), trust_objects=True)
+        assert trusted.read_object("0/sd/custom").v == 5
+    finally:
+        del builtins._HsTestCustom
+
+
+def test_metadata_format_on_disk(tmp_path):
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(a=torch.ones(3), b=1)})
+    md = json.loads((tmp_path / "s" / ".snapshot_metadata").read_text())
+    assert md["version"] == "0.1.0" and md["world_size"] == 1
+    assert md["manifest"]["0/sd"] == {"type": "dict", "keys": ["a", "b"]}
+    assert md["manifest"]["0/sd/b"]["type"] == "int"
+    assert md["manifest"]["0/sd/a"]["serializer"] == "buffer_protocol"
+
+
+def test_retake_same_path_overwrites(tmp_path):
+    p = str(tmp_path / "s")
+    Snapshot.take(p, {"sd": StateDict(a=torch.ones(1000), b=torch.zeros(10))})
+    Snapshot.take(p, {"sd": StateDict(a=torch.full((10,), 2.0))})
+    out = StateDict()
+    Snapshot(p).restore({"sd": out})
+    assert torch.equal(out["a"], torch.full((10,), 2.0)) and "b" not in out
+    # deterministic slab names: no stale blobs accumulate
+    assert len(os.listdir(tmp_path / "s" / "batched")) == 1
+
+
+def test_memory_storage_plugin():
+    from hipsnapshot.storage.memory import clear_memory_store
+
+    sd = StateDict(a=torch.randn(10), b="x")
+    Snapshot.take("memory://bucket/snap", {"sd": sd})
+    out = StateDict()
+    Snapshot("memory://bucket/snap").restore({"sd": out})
+    assert torch.equal(out["a"], sd["a"]) and out["b"] == "x"
+    clear_memory_store("bucket")
+
+
+def test_quantize_fp8_cpu(tmp_path):
+    w = torch.randn(300, 70)
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w, i=torch.arange(5))},
+                  quantize=["sd/w"])
+    man = Snapshot(str(tmp_path / "s")).get_manifest()
+    assert man["0/sd/w"].serializer == "hipsnapshot_fp8_block"
+    assert man["0/sd/w"].quant["block"] == 128
+    out = StateDict(w=torch.zeros(300, 70), i=torch.zeros(5, dtype=torch.int64))
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    rel = (out["w"] - w).abs().max() / w.abs().max()
+    assert rel < 0.08 and torch.equal(out["i"], torch.arange(5))
