@@ -138,7 +138,16 @@ __device__ __forceinline__ void store_from_f32(char* p, int32_t dt, float v) {
 
 __device__ __forceinline__ void store_from_f64(char* p, int32_t dt, double v) {
   switch (dt) {
-    case kF16: *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(static_cast<float>(v)); break;
+    case kF16: {
+      // f64 -> f16 with ONE rounding (torch semantics): round-to-odd into
+      // f32 (truncate + sticky bit), then RNE to f16.  A plain f64->f32->f16
+      // chain double-rounds ~1 in 8k values.
+      float f = __double2float_rz(v);
+      if (static_cast<double>(f) != v && (__float_as_uint(f) & 0x7f800000u) != 0x7f800000u)
+        f = __uint_as_float(__float_as_uint(f) | 1u);
+      *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(f);
+      break;
+    }
     case kBF16: *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(static_cast<float>(v)); break;
     case kF32: *reinterpret_cast<float*>(p) = static_cast<float>(v); break;
     default: *reinterpret_cast<double*>(p) = v; break;
@@ -349,16 +358,17 @@ hs_fp8_quant(const char* __restrict__ src, int32_t src_dtype, int64_t n,
       amax = fmaxf(amax, fabsf(v[j]));
     }
     amax = wave_max(amax);
+    // correctly rounded division everywhere (no reciprocal-multiply): the
+    // payload is bit-identical to the fp32 torch reference of the same rule
     const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
-    const float inv = 1.f / scale;
     if (lane == 0) scales[b] = scale;
     uint32_t words[(VPT + 3) / 4];
 #pragma unroll
     for (int w = 0; w < (VPT + 3) / 4; ++w) {
-      float a0 = fminf(fmaxf(v[4 * w + 0] * inv, -kFp8Max), kFp8Max);
-      float a1 = (4 * w + 1 < VPT) ? fminf(fmaxf(v[4 * w + 1] * inv, -kFp8Max), kFp8Max) : 0.f;
-      float a2 = (4 * w + 2 < VPT) ? fminf(fmaxf(v[4 * w + 2] * inv, -kFp8Max), kFp8Max) : 0.f;
-      float a3 = (4 * w + 3 < VPT) ? fminf(fmaxf(v[4 * w + 3] * inv, -kFp8Max), kFp8Max) : 0.f;
+      float a0 = fminf(fmaxf(v[4 * w + 0] / scale, -kFp8Max), kFp8Max);
+      float a1 = (4 * w + 1 < VPT) ? fminf(fmaxf(v[4 * w + 1] / scale, -kFp8Max), kFp8Max) : 0.f;
+      float a2 = (4 * w + 2 < VPT) ? fminf(fmaxf(v[4 * w + 2] / scale, -kFp8Max), kFp8Max) : 0.f;
+      float a3 = (4 * w + 3 < VPT) ? fminf(fmaxf(v[4 * w + 3] / scale, -kFp8Max), kFp8Max) : 0.f;
       int word = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
       word = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, word, true);
       words[w] = static_cast<uint32_t>(word);

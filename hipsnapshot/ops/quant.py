@@ -61,7 +61,9 @@ def quantize_reference(x: torch.Tensor, block: int):
     padded[:n] = flat
     blocks = padded.view(nblocks, block)
     amax = blocks.abs().amax(dim=1)
-    scale = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    # tensor/tensor division (correctly rounded; a Python-scalar divisor is
+    # lowered to a reciprocal multiply by torch and differs by 1 ulp)
+    scale = torch.where(amax > 0, amax / torch.full_like(amax, FP8_MAX), torch.ones_like(amax))
     q = (blocks / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
     return q.reshape(-1)[:n], scale
 

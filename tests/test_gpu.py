@@ -1,0 +1,246 @@
+"""MI355X tests: HIP kernel numerics vs PyTorch references, and GPU snapshot paths.
+
+Every test here runs the native HIP data plane (``_hsgpu.so``); nothing falls
+back to ATen silently -- ``native.require_gpu_lib()`` raises if the library is
+missing.
+"""
+
+import os
+
+import pytest
+import torch
+
+from hipsnapshot import Snapshot, StateDict
+from hipsnapshot.knobs import override_knob, override_slab_size_threshold_bytes
+from hipsnapshot.ops import native
+from hipsnapshot.utils.test_utils import assert_state_dict_eq, run_distributed
+
+pytestmark = pytest.mark.gpu
+
+FLOATS = [torch.float32, torch.bfloat16, torch.float16, torch.float64]
+
+
+def _launch(batch, dev=0):
+    batch.launch(dev, int(torch.cuda.current_stream().cuda_stream), sync=True)
+
+
+def test_pinned_pool_and_dma(gpu):
+    n = (64 << 20) + 123
+    src = torch.randint(0, 255, (n,), dtype=torch.uint8, device=gpu)
+    pb = native.PinnedBuffer(n)
+    native.memcpy(0, 0, pb.ptr, src.data_ptr(), n, native.D2H,
+                  torch.cuda.current_stream(), sync=True)
+    assert torch.equal(pb.as_tensor(n), src.cpu())
+    dst = torch.empty_like(src)
+    native.memcpy(0, 1, dst.data_ptr(), pb.ptr, n, native.H2D, None, sync=True)
+    assert torch.equal(dst, src)
+    cached, in_use = native.pinned_stats()
+    assert in_use >= n
+    ptr = pb.ptr
+    pb.release()
+    pb2 = native.PinnedBuffer(n)  # served from the cache
+    assert pb2.ptr == ptr
+    pb2.release()
+
+
+@pytest.mark.parametrize("dtype", [torch.uint8, torch.bfloat16, torch.float32, torch.int64,
+                                   torch.complex64, torch.bool])
+def test_gather_contiguous_many_tensors(gpu, dtype):
+    torch.manual_seed(0)
+    sizes = [1, 7, 64, 1000, 4097, 65536 + 3, 1 << 20, 3]
+    ts = [torch.randn(s, device=gpu).to(dtype) if dtype != torch.uint8 else
+          torch.randint(0, 255, (s,), dtype=dtype, device=gpu) for s in sizes]
+    es = ts[0].element_size()
+    total = sum(t.numel() * es for t in ts) + 64 * len(ts)
+    out = torch.zeros(total, dtype=torch.uint8, device=gpu)
+    b = native.CopyBatch()
+    offs, o = [], 3  # deliberately misaligned first offset
+    for t in ts:
+        offs.append(o)
+        b.add(t.data_ptr(), t.dtype, t.stride(), out.data_ptr() + o, t.dtype, [1], [t.numel()], es)
+        o += t.numel() * es + 5
+    _launch(b)
+    for t, off in zip(ts, offs):
+        got = out[off: off + t.numel() * es]
+        assert torch.equal(got, t.contiguous().view(torch.uint8).view(-1) if dtype != torch.bool
+                           else t.view(torch.uint8))
+
+
+@pytest.mark.parametrize("make", [
+    lambda a: a.t(),
+    lambda a: a[:, 100:900],
+    lambda a: a[::3, 5::7],
+    lambda a: a.view(32, 32, 1024).permute(2, 0, 1),
+    lambda a: a[7],
+    lambda a: a.view(4, 8, 32, 1024)[:, 2:5, ::2, 1:1000].transpose(0, 3),
+])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.int8, torch.float64])
+def test_strided_pack_matches_contiguous(gpu, make, dtype):
+    a = torch.randn(1024, 1024, device=gpu).to(dtype)
+    v = make(a)
+    out = torch.empty(v.numel(), dtype=dtype, device=gpu)
+    b = native.CopyBatch()
+    st = [1] * v.dim()
+    for i in range(v.dim() - 2, -1, -1):
+        st[i] = st[i + 1] * v.shape[i + 1]
+    b.add(v.data_ptr(), dtype, v.stride(), out.data_ptr(), dtype, st, list(v.shape),
+          v.element_size())
+    _launch(b)
+    assert torch.equal(out.view(v.shape), v.contiguous())
+
+
+@pytest.mark.parametrize("src_dtype", FLOATS, ids=str)
+@pytest.mark.parametrize("dst_dtype", FLOATS, ids=str)
+def test_scatter_cast_vs_torch(gpu, src_dtype, dst_dtype):
+    torch.manual_seed(1)
+    src = (torch.randn(257, 129, device=gpu, dtype=torch.float64) * 100).to(src_dtype)
+    big = torch.zeros(300, 400, dtype=dst_dtype, device=gpu)
+    dst = big[10:267, 50:179]  # strided destination
+    b = native.CopyBatch()
+    b.add(src.data_ptr(), src_dtype, src.stride(), dst.data_ptr(), dst_dtype, dst.stride(),
+          list(src.shape), src.element_size())
+    _launch(b)
+    ref = src.to(dst_dtype)
+    assert torch.equal(dst, ref), (dst - ref).abs().max()
+    assert big[:10].abs().sum() == 0 and big[:, :50].abs().sum() == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("n", [1, 127, 128, 1000, 1 << 20])
+@pytest.mark.parametrize("vpt", [2, 8])
+def test_fp8_quant_dequant_vs_reference(gpu, dtype, n, vpt):
+    from hipsnapshot.ops.quant import dequantize_reference, quantize_reference
+
+    torch.manual_seed(2)
+    x = (torch.randn(n, device=gpu) * torch.logspace(-3, 3, n, device=gpu)).to(dtype)
+    block = 64 * vpt
+    nblocks = (n + block - 1) // block
+    q = torch.empty(n, dtype=torch.uint8, device=gpu)
+    sc = torch.empty(nblocks, dtype=torch.float32, device=gpu)
+    stream = int(torch.cuda.current_stream().cuda_stream)
+    native.fp8_quantize(0, x, q, sc, vpt, stream)
+    rq, rs = quantize_reference(x, block)
+    torch.cuda.synchronize()
+    assert torch.equal(sc, rs), (sc - rs).abs().max()
+    mism = (q != rq.view(torch.uint8)).sum().item()
+    assert mism == 0, f"{mism} fp8 codes differ from torch's float8_e4m3fn cast"
+    out = torch.empty(n, dtype=dtype, device=gpu)
+    native.fp8_dequantize(0, q, sc, out, vpt, stream)
+    ref = dequantize_reference(rq, rs, block, dtype)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+def test_gpu_snapshot_roundtrip(gpu, tmp_path):
+    torch.manual_seed(3)
+    a = torch.randn(512, 256, device=gpu)
+    sd = StateDict(
+        w=torch.randn(1000, 300, device=gpu, dtype=torch.bfloat16),
+        t=a.t(),                                   # strided view
+        col=a[:, 10:100],                          # column shard-like view
+        small=[torch.randn(i + 1, device=gpu) for i in range(50)],  # slab members
+        i64=torch.arange(1000, device=gpu),
+        cpu=torch.randn(77),
+        step=3,
+    )
+    ref = {k: (v.clone() if isinstance(v, torch.Tensor) else
+               [x.clone() for x in v] if isinstance(v, list) else v) for k, v in sd.items()}
+    with override_slab_size_threshold_bytes(1 << 20):
+        Snapshot.take(str(tmp_path / "s"), {"sd": sd})
+    out = StateDict(
+        w=torch.zeros(1000, 300, device=gpu, dtype=torch.bfloat16),
+        t=torch.zeros(256, 512, device=gpu),
+        col=torch.zeros(1024, 180, device=gpu)[::2, ::2],   # strided destination
+        small=[torch.zeros(i + 1, device=gpu) for i in range(50)],
+        i64=torch.zeros(1000, dtype=torch.int64, device=gpu),
+        cpu=torch.zeros(77),
+    )
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    torch.cuda.synchronize()
+    assert_state_dict_eq({k: out[k] for k in ref}, ref)
+
+
+def test_gpu_restore_with_dtype_cast(gpu, tmp_path):
+    w = torch.randn(300, 200, device=gpu)
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)})
+    out = torch.zeros(300, 200, device=gpu, dtype=torch.bfloat16)
+    Snapshot(str(tmp_path / "s")).read_object("0/sd/w", obj_out=out)
+    # dtype differs -> not in place; result returned on host, cast on copy
+    got = Snapshot(str(tmp_path / "s")).read_object("0/sd/w")
+    assert torch.equal(got, w.cpu())
+
+
+def test_async_take_hbm_freeze_is_consistent(gpu, tmp_path):
+    w = torch.randn(4096, 1024, device=gpu)
+    small = torch.randn(100, device=gpu)
+    ref_w, ref_s = w.clone(), small.clone()
+    pending = Snapshot.async_take(str(tmp_path / "s"), {"sd": StateDict(w=w, s=small)})
+    w.add_(1.0)        # enqueued after the freeze on the same stream
+    small.mul_(0)
+    pending.wait()
+    out = StateDict(w=torch.zeros_like(w), s=torch.zeros_like(small))
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    assert torch.equal(out["w"], ref_w) and torch.equal(out["s"], ref_s)
+
+
+def test_async_take_host_fallback_when_hbm_short(gpu, tmp_path):
+    w = torch.randn(1024, 1024, device=gpu)
+    ref = w.clone()
+    with override_knob("HBM_STAGING_RESERVE_BYTES", str(1 << 50)):
+        pending = Snapshot.async_take(str(tmp_path / "s"), {"sd": StateDict(w=w)})
+    w.zero_()
+    pending.wait()
+    assert torch.equal(Snapshot(str(tmp_path / "s")).read_object("0/sd/w"), ref.cpu())
+
+
+def test_fp8_quantized_save_gpu(gpu, tmp_path):
+    from hipsnapshot.ops.quant import dequantize_reference, quantize_reference
+
+    w = torch.randn(1000, 333, device=gpu, dtype=torch.bfloat16)
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/*"])
+    out = torch.zeros_like(w)
+    Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=out)})
+    q, s = quantize_reference(w, 128)
+    ref = dequantize_reference(q, s, 128, torch.bfloat16).view(w.shape)
+    assert torch.equal(out, ref)
+    size = sum(os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(tmp_path / "s")
+               for f in fs if not f.startswith("."))
+    assert size < w.numel() * 2 * 0.55  # ~half of the bf16 bytes
+
+
+def test_uvm_managed_tensor(gpu, tmp_path):
+    from hipsnapshot.ops.uvm import is_uvm_tensor, new_managed_tensor
+
+    t = new_managed_tensor([256, 64], torch.float32, 0)
+    t.copy_(torch.randn(256, 64, device=gpu))
+    assert is_uvm_tensor(t) and not is_uvm_tensor(torch.zeros(3, device=gpu))
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(t=t)})
+    out = new_managed_tensor([256, 64], torch.float32, 0)
+    out.zero_()
+    Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(t=out)})
+    torch.cuda.synchronize()
+    assert torch.equal(out, t)
+
+
+def _fsdp_gpu_worker(path):
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+
+    from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+
+    mesh = init_device_mesh("cuda", (dist.get_world_size(),))
+    m = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cuda", 0), torch.bfloat16, mesh=mesh)
+    ref = {k: v.full_tensor().clone() for k, v in m.state_dict().items()}
+    Snapshot.take(path, {"model": m})
+    pending = Snapshot.async_take(path + "_a", {"model": m})
+    pending.wait()
+    for p in m.parameters():
+        p._local_tensor.zero_()
+    Snapshot(path + "_a").restore({"model": m})
+    torch.cuda.synchronize()
+    for k, v in m.state_dict().items():
+        assert torch.equal(v.full_tensor(), ref[k]), k
+
+
+def test_fsdp2_rccl_single_rank(gpu, tmp_path):
+    run_distributed(_fsdp_gpu_worker, 1, str(tmp_path / "f"), backend="nccl")
