@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""DLRM with large row-wise sharded embedding tables on managed (UVM) memory.
+
+BASELINE config 4 (TorchRec DLRM, 100 GB tables, uvm_tensor path); reference
+script /root/reference/benchmarks/torchrec/main.py:54-151 (sync vs async take,
+time-to-unblock).  Tables are DTensor(Shard(0)) over the ranks; ``--uvm``
+puts every local shard in hipMallocManaged memory.
+"""
+
+import argparse
+import os
+import shutil
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from common import Timer, emit, init_dist, log, max_over_ranks, sync  # noqa: E402
+from hipsnapshot import Snapshot  # noqa: E402
+from hipsnapshot.models.dlrm import DLRM  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--total-gb", type=float, default=8.0, help="total embedding bytes (all ranks)")
+    ap.add_argument("--tables", type=int, default=8)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--uvm", action="store_true")
+    ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    args = ap.parse_args()
+    rank, ws, dev = init_dist()
+    from torch.distributed.device_mesh import init_device_mesh
+
+    mesh = init_device_mesh(dev.type, (ws,))
+    rows = int(args.total_gb * 1e9 / 4 / args.dim / args.tables)
+    model = DLRM([rows] * args.tables, dim=args.dim, device=dev, mesh=mesh, uvm=args.uvm)
+    nbytes = sum(p.numel() * 4 for p in model.parameters())
+    log(f"DLRM: {args.tables} tables x {rows} rows x {args.dim} (uvm={args.uvm}), "
+        f"{nbytes / 1e9:.2f} GB")
+    root = os.path.join(args.work_dir, "hs_dlrm")
+    if rank == 0:
+        shutil.rmtree(root, ignore_errors=True)
+    sync(dev)
+    Snapshot.take(root + "/warm", {"model": model})
+    sync(dev)
+    with Timer() as t:
+        Snapshot.take(root + "/sync", {"model": model})
+        sync(dev)
+    sync_s = max_over_ranks(t.s, dev)
+    sync(dev)
+    with Timer() as tu:
+        pending = Snapshot.async_take(root + "/async", {"model": model})
+    unblock = max_over_ranks(tu.s, dev)
+    pending.wait()
+    sync(dev)
+    emit({"bench": "dlrm_uvm" if args.uvm else "dlrm_hbm", "world_size": ws, "bytes": nbytes,
+          "sync_take_s": round(sync_s, 3), "sync_GBps": round(nbytes / sync_s / 1e9, 2),
+          "async_unblock_ms": round(unblock * 1e3, 1)})
+    if rank == 0:
+        shutil.rmtree(root, ignore_errors=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
