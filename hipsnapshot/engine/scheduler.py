@@ -130,6 +130,9 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     io_tasks: set = set()
     io_sem = asyncio.Semaphore(io_concurrency)
     wake = asyncio.Event()
+    from ..utils.tracing import WriteReporter
+
+    reporter = WriteReporter(rank, memory_budget_bytes)
 
     async def _write(wr: WriteReq, buf: StagedBuffer, cost: int) -> None:
         try:
@@ -162,6 +165,8 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             done, _ = await asyncio.wait(waiters | {waiter}, return_when=asyncio.FIRST_COMPLETED)
             if not waiter.done():
                 waiter.cancel()
+            reporter.maybe_report(len(pending), len(staging), len(io_tasks), in_use[0],
+                                  stats.bytes_written)
             for task in done:
                 if task is waiter:
                     continue

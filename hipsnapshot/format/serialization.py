@@ -172,10 +172,74 @@ def torch_load_from_bytes(buf, trusted: bool = False):
     """Load a ``torch_save`` payload.
 
     ``weights_only=True`` by default: torch >= 2.6 refuses arbitrary pickled
-    objects (reference quirk).  Snapshots written by this
-    process are trusted (``trusted=True``) -- see ``knobs.trust_object_payloads``.
+    objects (reference quirk).  Full unpickling
+    (``trusted=True``) only happens when the caller opted in
+    (``Snapshot(..., trust_objects=True)`` / ``HIPSNAPSHOT_TRUST_OBJECTS=1``).
     """
     bio = io.BytesIO(bytes(buf) if not isinstance(buf, (bytes, bytearray)) else buf)
     if trusted:
         return torch.load(bio, weights_only=False, map_location="cpu")
     return torch.load(bio, weights_only=True, map_location="cpu")
+
+
+# ---------------------------------------------------------------------------
+# compact quantized-tensor encodings (reference serialization.py:257-456; the
+# reference never selects them on its main path -- we read them when present
+# and offer them as a weights-only-safe alternative to torch.save)
+# ---------------------------------------------------------------------------
+
+import struct as _struct
+
+_Q_CODES = {torch.qint8: 0, torch.quint8: 1, torch.qint32: 2}
+_Q_FROM = {v: k for k, v in _Q_CODES.items()}
+_Q_INT = {torch.qint8: torch.int8, torch.quint8: torch.uint8, torch.qint32: torch.int32}
+
+
+def per_tensor_qtensor_as_bytes(t: torch.Tensor) -> bytes:
+    if not t.is_quantized or t.qscheme() not in (torch.per_tensor_affine,
+                                                 torch.per_tensor_symmetric):
+        raise ValueError("expected a per-tensor quantized tensor")
+    shape = list(t.shape)
+    head = _struct.pack(f"<BdqI{len(shape)}q", _Q_CODES[t.dtype], float(t.q_scale()),
+                        int(t.q_zero_point()), len(shape), *shape)
+    return head + bytes(contiguous_cpu_bytes_view(t.int_repr().contiguous()))
+
+
+def per_tensor_qtensor_from_bytes(buf) -> torch.Tensor:
+    mv = memoryview(buf).cast("B")
+    code, scale, zp, ndim = _struct.unpack_from("<BdqI", mv, 0)
+    off = _struct.calcsize("<BdqI")
+    shape = list(_struct.unpack_from(f"<{ndim}q", mv, off))
+    off += 8 * ndim
+    dtype = _Q_FROM[code]
+    ints = tensor_from_bytes(bytes(mv[off:]), _Q_INT[dtype], shape)
+    return torch._make_per_tensor_quantized_tensor(ints, scale, zp)
+
+
+def per_channel_qtensor_as_bytes(t: torch.Tensor) -> bytes:
+    if not t.is_quantized or t.qscheme() not in (torch.per_channel_affine,
+                                                 torch.per_channel_symmetric):
+        raise ValueError("expected a per-channel quantized tensor")
+    shape = list(t.shape)
+    axis = t.q_per_channel_axis()
+    scales = t.q_per_channel_scales().to(torch.float64).contiguous()
+    zps = t.q_per_channel_zero_points().to(torch.int64).contiguous()
+    head = _struct.pack(f"<BqI{len(shape)}q", _Q_CODES[t.dtype], axis, len(shape), *shape)
+    return (head + bytes(contiguous_cpu_bytes_view(scales)) + bytes(contiguous_cpu_bytes_view(zps))
+            + bytes(contiguous_cpu_bytes_view(t.int_repr().contiguous())))
+
+
+def per_channel_qtensor_from_bytes(buf) -> torch.Tensor:
+    mv = memoryview(buf).cast("B")
+    code, axis, ndim = _struct.unpack_from("<BqI", mv, 0)
+    off = _struct.calcsize("<BqI")
+    shape = list(_struct.unpack_from(f"<{ndim}q", mv, off))
+    off += 8 * ndim
+    nch = shape[axis]
+    scales = tensor_from_bytes(bytes(mv[off: off + 8 * nch]), torch.float64, [nch])
+    off += 8 * nch
+    zps = tensor_from_bytes(bytes(mv[off: off + 8 * nch]), torch.int64, [nch])
+    off += 8 * nch
+    dtype = _Q_FROM[code]
+    ints = tensor_from_bytes(bytes(mv[off:]), _Q_INT[dtype], shape)
+    return torch._make_per_channel_quantized_tensor(ints, scales, zps, axis)

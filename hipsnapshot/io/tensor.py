@@ -235,6 +235,14 @@ def deserialize_tensor(buf, entry: TensorEntry) -> torch.Tensor:
         from ..ops.quant import dequantize_host_fp8
 
         return dequantize_host_fp8(buf, entry)
+    if entry.serializer == Serializer.PER_TENSOR_QTENSOR.value:
+        from ..format.serialization import per_tensor_qtensor_from_bytes
+
+        return per_tensor_qtensor_from_bytes(buf)
+    if entry.serializer == Serializer.PER_CHANNEL_QTENSOR.value:
+        from ..format.serialization import per_channel_qtensor_from_bytes
+
+        return per_channel_qtensor_from_bytes(buf)
     raise ValueError(f"Unrecognized serializer: {entry.serializer}.")
 
 

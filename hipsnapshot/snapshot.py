@@ -65,6 +65,7 @@ from .parallel.partitioner import consolidate_replicated_entries, partition_writ
 from .parallel.store import LinearBarrier, get_or_create_store
 from .stateful import AppState, RNGState, Stateful
 from .storage.registry import url_to_storage_plugin_in_event_loop
+from .utils.tracing import roctx_range
 from .version import __version__
 
 logger = logging.getLogger(__name__)
@@ -126,13 +127,17 @@ class Snapshot:
         path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
         storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
         try:
-            pending, metadata = cls._take_impl(path, app_state, rep, keys, comm, storage, loop,
-                                               False, _custom_tensor_prepare_func, quantize)
+            with roctx_range("hipsnapshot.take.plan_and_stage"):
+                pending, metadata = cls._take_impl(path, app_state, rep, keys, comm, storage,
+                                                   loop, False, _custom_tensor_prepare_func,
+                                                   quantize)
             t_staged = time.monotonic()
-            pending.sync_complete(loop)
-            comm.barrier()
-            if comm.get_rank() == 0:
-                cls._write_snapshot_metadata(metadata, storage, loop)
+            with roctx_range("hipsnapshot.take.drain_io"):
+                pending.sync_complete(loop)
+            with roctx_range("hipsnapshot.take.commit"):
+                comm.barrier()
+                if comm.get_rank() == 0:
+                    cls._write_snapshot_metadata(metadata, storage, loop)
         finally:
             storage.sync_close(loop)
             loop.close()

@@ -56,3 +56,26 @@ def test_zero_size():
     t = torch.empty(0, 3)
     assert contiguous_cpu_bytes_view(t).nbytes == 0
     assert tensor_from_bytes(b"", torch.float32, [0, 3]).shape == (0, 3)
+
+
+def test_per_tensor_qtensor_codec():
+    from hipsnapshot.format.serialization import (per_tensor_qtensor_as_bytes,
+                                                  per_tensor_qtensor_from_bytes)
+
+    for dt in (torch.qint8, torch.quint8, torch.qint32):
+        q = torch.quantize_per_tensor(torch.rand(5, 7) * 5, 0.05, 3, dt)
+        back = per_tensor_qtensor_from_bytes(per_tensor_qtensor_as_bytes(q))
+        assert tensor_eq(back, q) and back.q_scale() == q.q_scale()
+
+
+def test_per_channel_qtensor_codec():
+    from hipsnapshot.format.serialization import (per_channel_qtensor_as_bytes,
+                                                  per_channel_qtensor_from_bytes)
+
+    x = torch.rand(6, 4, 3) * 4
+    q = torch.quantize_per_channel(x, torch.rand(4) + 0.01, torch.randint(0, 10, (4,)), 1,
+                                   torch.quint8)
+    back = per_channel_qtensor_from_bytes(per_channel_qtensor_as_bytes(q))
+    assert torch.equal(back.int_repr(), q.int_repr())
+    assert torch.equal(back.q_per_channel_scales(), q.q_per_channel_scales().double())
+    assert back.q_per_channel_axis() == 1

@@ -1,0 +1,85 @@
+"""DeepSpeed trick (duck-typed fake engine), RSS profiler, knobs."""
+
+import torch
+
+from hipsnapshot import knobs
+from hipsnapshot.tricks.deepspeed import Zero3StateAdapter, patch_engine_to_use_hipsnapshot
+from hipsnapshot.utils.rss_profiler import measure_rss_deltas
+
+
+class _FakeZero3:
+    def __init__(self):
+        self.state = {"fp32_flat": torch.randn(1000), "step": 3}
+        self.persistent_parameters = []
+        self.loaded = None
+
+    def state_dict(self):
+        return self.state
+
+    def load_state_dict(self, state_dict):
+        self.state = state_dict
+
+    def _rigid_load_state_dict(self, state_dict, load_optimizer_states=True):
+        self.loaded = state_dict
+
+
+_FakeZero3.__name__ = "DeepSpeedZeroOptimizer_Stage3"
+
+
+class _FakeEngine:
+    def __init__(self):
+        self.optimizer = _FakeZero3()
+        self.config = {"zero_optimization": {"stage": 3}}
+        self.global_rank = 0
+        self.copied = None
+
+    def _copy_recovery_script(self, path):
+        self.copied = path
+
+    def zero_load_from_fp32_weights(self):
+        return False
+
+
+def test_deepspeed_trick_roundtrip(tmp_path):
+    eng = _FakeEngine()
+    patch_engine_to_use_hipsnapshot(eng)
+    eng._save_zero_checkpoint(str(tmp_path / "z"), "tag")
+    assert eng.copied == str(tmp_path / "z")
+    eng2 = _FakeEngine()
+    eng2._hipsnapshot_pending = eng._hipsnapshot_pending
+    patch_engine_to_use_hipsnapshot(eng2)
+    assert eng2._load_zero_checkpoint(str(tmp_path / "z"), "tag")
+    assert torch.equal(eng2.optimizer.loaded["fp32_flat"], eng.optimizer.state["fp32_flat"])
+    assert eng2.optimizer.loaded["step"] == 3
+
+
+def test_deepspeed_trick_rejects_non_zero3():
+    eng = _FakeEngine()
+    eng.optimizer = object()
+    import pytest
+
+    with pytest.raises(RuntimeError):
+        patch_engine_to_use_hipsnapshot(eng)
+    assert isinstance(Zero3StateAdapter(_FakeZero3()).state_dict(), dict)
+
+
+def test_rss_profiler():
+    deltas = []
+    with measure_rss_deltas(deltas, interval_s=0.01):
+        x = torch.ones(50_000_000)  # 200 MB
+        x.add_(1)
+    assert max(deltas) > 100 * 2 ** 20
+
+
+def test_knob_overrides_and_legacy_names(monkeypatch):
+    assert knobs.get_max_chunk_size_bytes() == 512 * 1024 * 1024
+    with knobs.override_max_chunk_size_bytes(123):
+        assert knobs.get_max_chunk_size_bytes() == 123
+    assert knobs.get_max_chunk_size_bytes() == 512 * 1024 * 1024
+    monkeypatch.setenv("TORCHSNAPSHOT_SLAB_SIZE_THRESHOLD_BYTES_OVERRIDE", "77")
+    assert knobs.get_slab_size_threshold_bytes() == 77
+    with knobs.override_slab_size_threshold_bytes(5):
+        assert knobs.get_slab_size_threshold_bytes() == 5
+        assert knobs.get_max_shard_size_bytes() == 512 * 1024 * 1024
+    monkeypatch.setenv("TORCHSNAPSHOT_DISABLE_BATCHING", "1")
+    assert knobs.is_batching_disabled()
