@@ -37,6 +37,7 @@
 #include <map>
 #include <mutex>
 #include <unordered_map>
+#include <type_traits>
 #include <vector>
 
 namespace {
@@ -138,16 +139,10 @@ __device__ __forceinline__ void store_from_f32(char* p, int32_t dt, float v) {
 
 __device__ __forceinline__ void store_from_f64(char* p, int32_t dt, double v) {
   switch (dt) {
-    case kF16: {
-      // f64 -> f16 with ONE rounding (torch semantics): round-to-odd into
-      // f32 (truncate + sticky bit), then RNE to f16.  A plain f64->f32->f16
-      // chain double-rounds ~1 in 8k values.
-      float f = __double2float_rz(v);
-      if (static_cast<double>(f) != v && (__float_as_uint(f) & 0x7f800000u) != 0x7f800000u)
-        f = __uint_as_float(__float_as_uint(f) | 1u);
-      *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(f);
-      break;
-    }
+    // f64 -> f16 goes through f32 (two RNE roundings) exactly like torch's
+    // copy_ on ROCm (c10::Half is constructed from float); measured on MI355X:
+    // a single-rounding conversion differs from torch in ~1e-4 of values.
+    case kF16: *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(static_cast<float>(v)); break;
     case kBF16: *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(static_cast<float>(v)); break;
     case kF32: *reinterpret_cast<float*>(p) = static_cast<float>(v); break;
     default: *reinterpret_cast<double*>(p) = v; break;
@@ -301,13 +296,82 @@ __device__ __forceinline__ void copy_tile_nd(const CopyDesc& d, int64_t b, int64
   }
 }
 
+// ---- rows mode (flags & 2): 2-D copy whose inner dim is contiguous on both
+// sides (column shards, narrowed views).  Work unit = one vector of `vw` bytes
+// (vw = flags >> 8, the widest power of two dividing the row length, both row
+// strides and both base addresses); the tile range indexes the flattened
+// (row, vector) space so long and short rows balance the same way.
+template <int VW>
+__device__ void copy_rows(const CopyDesc& d, int64_t begin, int64_t end, int es) {
+  using V = typename RawT<VW>::T;
+  const int64_t vpr = d.sizes[1] * es / VW;  // vectors per row
+  const int64_t s_row = d.src_strides[0] * es, d_row = d.dst_strides[0] * es;
+  for (int64_t v = begin + threadIdx.x; v < end; v += kBlock) {
+    const int64_t r = v / vpr, c = v - r * vpr;
+    const V* s = reinterpret_cast<const V*>(d.src + r * s_row) + c;
+    V* o = reinterpret_cast<V*>(d.dst + r * d_row) + c;
+    *o = *s;
+  }
+}
+
+// ---- transpose mode (flags & 4): canonical [B, I, J] with src contiguous along
+// I and dst contiguous along J.  64x64 tiles staged through LDS (padded to 65
+// words per row: conflict-free column reads), loads coalesced along I, stores
+// coalesced along J.  A tile range is a range of 64x64 blocks.
+template <int ES>
+__device__ void transpose_blocks(const CopyDesc& d, int64_t begin, int64_t end, char* lds_raw) {
+  using T = typename RawT<ES>::T;
+  using W = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
+  W(*lds)[65] = reinterpret_cast<W(*)[65]>(lds_raw);
+  const int64_t I = d.sizes[1], J = d.sizes[2];
+  const int64_t ti_n = (I + 63) / 64, tj_n = (J + 63) / 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int64_t blk = begin; blk < end; ++blk) {
+    const int64_t b = blk / (ti_n * tj_n);
+    const int64_t rr = blk - b * (ti_n * tj_n);
+    const int64_t i0 = (rr / tj_n) * 64, j0 = (rr % tj_n) * 64;
+    const T* src = reinterpret_cast<const T*>(d.src) + b * d.src_strides[0];
+    T* dst = reinterpret_cast<T*>(d.dst) + b * d.dst_strides[0];
+    const int64_t sj = d.src_strides[2], di = d.dst_strides[1];
+#pragma unroll 4
+    for (int jj = ty; jj < 64; jj += kBlock / 64) {
+      const int64_t i = i0 + tx, j = j0 + jj;
+      if (i < I && j < J) lds[jj][tx] = static_cast<W>(src[i + j * sj]);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int ii = ty; ii < 64; ii += kBlock / 64) {
+      const int64_t i = i0 + ii, j = j0 + tx;
+      if (i < I && j < J) dst[i * di + j] = static_cast<T>(lds[tx][ii]);
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void __launch_bounds__(kBlock)
 hs_copy_nd(const CopyDesc* __restrict__ descs, const Tile* __restrict__ tiles, int64_t ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const Tile tile = tiles[t];
     const CopyDesc& d = descs[tile.desc];
     if (d.flags & 1) {
       copy_bytes(d.src, d.dst, tile.begin, tile.end);
+    } else if (d.flags & 2) {
+      const int es = elem_size(d.src_dtype);
+      switch (d.flags >> 8) {
+        case 16: copy_rows<16>(d, tile.begin, tile.end, es); break;
+        case 8: copy_rows<8>(d, tile.begin, tile.end, es); break;
+        case 4: copy_rows<4>(d, tile.begin, tile.end, es); break;
+        case 2: copy_rows<2>(d, tile.begin, tile.end, es); break;
+        default: copy_rows<1>(d, tile.begin, tile.end, es); break;
+      }
+    } else if (d.flags & 4) {
+      switch (elem_size(d.src_dtype)) {
+        case 1: transpose_blocks<1>(d, tile.begin, tile.end, lds_raw); break;
+        case 2: transpose_blocks<2>(d, tile.begin, tile.end, lds_raw); break;
+        case 4: transpose_blocks<4>(d, tile.begin, tile.end, lds_raw); break;
+        default: transpose_blocks<8>(d, tile.begin, tile.end, lds_raw); break;
+      }
     } else {
       switch (d.ndim) {
         case 1: copy_tile_nd<1>(d, tile.begin, tile.end); break;
@@ -478,6 +542,13 @@ void build_tiles(const CopyDesc* descs, int n, std::vector<Tile>* tiles) {
     if (d.flags & 1) {
       total = d.numel * es;  // bytes
       step = tile_bytes;
+    } else if (d.flags & 2) {
+      const int vw = d.flags >> 8;
+      total = d.sizes[0] * (d.sizes[1] * es / vw);  // vectors
+      step = std::max<int64_t>(kBlock, tile_bytes / vw);
+    } else if (d.flags & 4) {
+      total = d.sizes[0] * ((d.sizes[1] + 63) / 64) * ((d.sizes[2] + 63) / 64);  // 64x64 blocks
+      step = std::max<int64_t>(1, tile_bytes / (64 * 64 * es));
     } else {
       total = d.numel;
       // elements per tile on the strided/cast path (multiple of the per-block run)
@@ -668,7 +739,15 @@ int hsg_copy_nd(int dev, const void* descs, int n, void* workspace, uint64_t ws_
   HS_CHECK(hipMemcpyAsync(ws, stage, toff + tbytes, hipMemcpyHostToDevice, s));
   const int64_t ntiles = static_cast<int64_t>(tiles.size());
   const int grid = static_cast<int>(std::min<int64_t>(ntiles, 256 * 8));
-  hipLaunchKernelGGL(hs_copy_nd, dim3(grid), dim3(kBlock), 0, s,
+  // dynamic LDS only when a transpose descriptor is present (64x65 words)
+  size_t lds = 0;
+  for (int i = 0; i < n; ++i) {
+    if (d[i].flags & 4) {
+      const size_t w = elem_bytes_host(d[i].src_dtype) == 8 ? 8 : 4;
+      lds = std::max(lds, 64 * 65 * w);
+    }
+  }
+  hipLaunchKernelGGL(hs_copy_nd, dim3(grid), dim3(kBlock), lds, s,
                      reinterpret_cast<const CopyDesc*>(ws),
                      reinterpret_cast<const Tile*>(ws + toff), ntiles);
   HS_CHECK(hipGetLastError());

@@ -78,6 +78,11 @@ class LocalBox:
         self.sharding_dim = sharding_dim
 
 
+# (global shape, mesh, coordinate, placements) -> (local shape, global offset);
+# the same layouts recur every snapshot of a training job
+_LAYOUT_CACHE: dict = {}
+
+
 def _dtensor_boxes(dt, for_write: bool) -> List[LocalBox]:
     from torch.distributed.tensor._utils import compute_local_shape_and_global_offset
 
@@ -97,7 +102,14 @@ def _dtensor_boxes(dt, for_write: bool) -> List[LocalBox]:
         for mdim, p in enumerate(placements):
             if isinstance(p, Replicate) and coord[mdim] != 0:
                 return []
-    shape, offset = compute_local_shape_and_global_offset(dt.shape, mesh, placements)
+    key = (tuple(dt.shape), id(mesh), tuple(coord), tuple(placements))
+    hit = _LAYOUT_CACHE.get(key)
+    if hit is None:
+        hit = compute_local_shape_and_global_offset(dt.shape, mesh, placements)
+        if len(_LAYOUT_CACHE) > 65536:
+            _LAYOUT_CACHE.clear()
+        _LAYOUT_CACHE[key] = hit
+    shape, offset = hit
     local = dt._local_tensor
     sdim = next((p.dim for p in placements if isinstance(p, DShard)), 0)
     if local.dim() == 0 and len(shape) == 0:

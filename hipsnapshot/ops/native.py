@@ -382,6 +382,35 @@ def collapse_dims(sizes: Sequence[int], s_strides: Sequence[int],
     return [d[0] for d in out], [d[1] for d in out], [d[2] for d in out]
 
 
+def _fast_mode(src_ptr: int, dst_ptr: int, z, a, b, es: int):
+    """Pick a specialised kernel path for a same-dtype strided copy.
+
+    * rows (flags 2): 2-D, inner dim contiguous on both sides -> vectorised
+      row copies (column shards, narrowed views); vector width in flags >> 8.
+    * transpose (flags 4): src contiguous along one dim, dst along another ->
+      LDS-tiled 64x64 transpose; canonical dims [B, I, J].
+    """
+    if len(z) == 2 and a[1] == 1 and b[1] == 1:
+        row_bytes = z[1] * es
+        vw = 16
+        while vw > 1 and (row_bytes % vw or src_ptr % vw or dst_ptr % vw
+                          or (a[0] * es) % vw or (b[0] * es) % vw):
+            vw //= 2
+        return 2 | (vw << 8), z, a, b
+    if len(z) in (2, 3):
+        i = next((k for k in range(len(z)) if a[k] == 1), None)
+        j = next((k for k in range(len(z)) if b[k] == 1), None)
+        if i is None or j is None or i == j:
+            return None
+        rest = [k for k in range(len(z)) if k not in (i, j)]
+        order = rest + [i, j]
+        zz, aa, bb = [z[k] for k in order], [a[k] for k in order], [b[k] for k in order]
+        if len(zz) == 2:
+            zz, aa, bb = [1] + zz, [0] + aa, [0] + bb
+        return 4, zz, aa, bb
+    return None
+
+
 class CopyBatch:
     """Accumulates strided copy/cast descriptors executed by ONE kernel launch."""
 
@@ -409,6 +438,10 @@ class CopyBatch:
             if sc < 0 or dc < 0:
                 raise ValueError(f"device cast {src_dtype}->{dst_dtype} unsupported")
         flags = 1 if (sc == dc and len(z) == 1 and a[0] == 1 and b[0] == 1) else 0
+        if not flags and sc == dc and elem_size <= 8:
+            mode = _fast_mode(src_ptr, dst_ptr, z, a, b, elem_size)
+            if mode is not None:
+                flags, z, a, b = mode
         self.rows.append((src_ptr, dst_ptr, numel, len(z), sc, dc, flags, z, a, b))
 
     def pack(self) -> np.ndarray:
