@@ -233,7 +233,7 @@ def batch_read_requests(read_reqs: List[ReadReq]) -> List[ReadReq]:
     out: List[ReadReq] = []
     grouped: Dict[str, List[ReadReq]] = defaultdict(list)
     for rr in read_reqs:
-        if rr.byte_range is None:
+        if rr.byte_range is None or not rr.mergeable:
             out.append(rr)
         else:
             grouped[rr.path].append(rr)

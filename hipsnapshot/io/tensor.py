@@ -43,6 +43,11 @@ from ..engine import staging
 
 PrepareFunc = Callable[[torch.Tensor, bool], torch.Tensor]
 
+# reads above this size are split into AUTO_TILE_BYTES ranged reads that run
+# concurrently on the I/O engine and overlap with the H2D DMA of earlier tiles
+AUTO_TILE_THRESHOLD_BYTES = 256 << 20
+AUTO_TILE_BYTES = 64 << 20
+
 
 async def run_in_executor(executor: Optional[Executor], fn, *args):
     if executor is None:
@@ -105,9 +110,12 @@ class TensorIOPreparer:
                 return [ReadReq(path=entry.location, byte_range=entry.byte_range_tuple,
                                 buffer_consumer=consumer)], fut
             tensor_out = cls.empty_tensor_from_entry(entry)
-        if (buffer_size_limit_bytes is not None
-                and entry.serializer == Serializer.BUFFER_PROTOCOL.value):
-            return cls.prepare_read_tiled(entry, tensor_out, buffer_size_limit_bytes)
+        if entry.serializer == Serializer.BUFFER_PROTOCOL.value:
+            if buffer_size_limit_bytes is not None:
+                return cls.prepare_read_tiled(entry, tensor_out, buffer_size_limit_bytes)
+            if tensor_nbytes_from_entry(entry) > AUTO_TILE_THRESHOLD_BYTES:
+                # large blobs: parallel ranged reads pipelined with H2D
+                return cls.prepare_read_tiled(entry, tensor_out, AUTO_TILE_BYTES)
         consumer = TensorBufferConsumer(tensor=tensor_out, entry=entry)
         return [ReadReq(path=entry.location, byte_range=entry.byte_range_tuple,
                         buffer_consumer=consumer)], Future(obj=tensor_out)
@@ -136,7 +144,8 @@ class TensorIOPreparer:
                               replicated=entry.replicated)
             reqs.append(ReadReq(path=entry.location,
                                 byte_range=(base + offset, base + offset + nb),
-                                buffer_consumer=TensorBufferConsumer(tensor=ch, entry=sub)))
+                                buffer_consumer=TensorBufferConsumer(tensor=ch, entry=sub),
+                                mergeable=False))
             offset += nb
         return reqs, Future(obj=tensor_out)
 

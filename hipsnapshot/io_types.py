@@ -101,6 +101,9 @@ class ReadReq:
     path: str
     buffer_consumer: BufferConsumer
     byte_range: Optional[Tuple[int, int]] = None
+    # False for tiles of one large tensor: merging them back into one read
+    # would defeat the memory budget / read-H2D pipelining they exist for
+    mergeable: bool = True
 
 
 @dataclass
