@@ -410,9 +410,12 @@ class Snapshot:
                 if not ignored:
                     out.append(os.path.join(key, "**"))
                     continue
-                for name, _ in itertools.chain(val.named_parameters(), val.named_buffers()):
-                    if name not in ignored:
-                        out.append(os.path.join(key, name))
+                # parameters_to_ignore holds names relative to the wrapped
+                # module; state_dict keys carry DDP's "module." prefix
+                inner = val.module
+                for name, _ in itertools.chain(inner.named_parameters(), inner.named_buffers()):
+                    if name not in ignored and f"module.{name}" not in ignored:
+                        out.append(os.path.join(key, f"module.{name}"))
         return out
 
     @classmethod

@@ -218,3 +218,39 @@ def comm_collectives():
     res = [None]
     comm.scatter_object_list(res, [f"s{r}" for r in range(ws)] if rank == 0 else None, src=0)
     assert res[0] == f"s{rank}"
+
+
+def replication_globs(path: str):
+    """replicated = glob matched on ALL ranks, present on all ranks, not sharded."""
+    rank = dist.get_rank()
+    sd = StateDict(common=torch.ones(4), only_rank0=torch.ones(2),
+                   per=torch.full((3,), float(rank)), nested={"a": torch.zeros(2), "b": 1})
+    if rank != 0:
+        del sd["only_rank0"]
+    # rank 1 passes an extra glob that rank 0 does not: it must be ignored
+    globs = ["sd/common", "sd/only_rank0", "sd/nested/*"] + (["sd/per"] if rank == 1 else [])
+    Snapshot.take(path, {"sd": sd}, replicated=globs)
+    man = Snapshot(path).get_manifest()
+    assert man["0/sd/common"].replicated and man["0/sd/nested/a"].replicated
+    assert man["0/sd/nested/b"].replicated  # primitives can be replicated too
+    assert not man["0/sd/only_rank0"].replicated  # absent on rank 1
+    assert not man["0/sd/per"].replicated and "1/sd/per" in man
+    assert "1/sd/common" not in man  # replicated entries live under rank 0 only
+
+
+def ddp_infer_replication(path: str, ignore: bool):
+    rank = dist.get_rank()
+    torch.manual_seed(0)
+    inner = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 2))
+    if ignore:
+        torch.nn.parallel.DistributedDataParallel._set_params_and_buffers_to_ignore_for_model(
+            inner, ["1.weight"])
+    model = torch.nn.parallel.DistributedDataParallel(inner)
+    Snapshot.take(path, {"ddp": model})
+    man = Snapshot(path).get_manifest()
+    if ignore:
+        assert not man["0/ddp/module.1.weight"].replicated
+        assert f"{1}/ddp/module.1.weight" in man
+        assert man["0/ddp/module.0.weight"].replicated
+    else:
+        assert all(e.replicated for k, e in man.items() if hasattr(e, "location"))

@@ -55,3 +55,12 @@ def test_linear_barrier_error_propagation():
 
 def test_linear_barrier_timeout():
     run_distributed(W.linear_barrier, 2, "lb_to", 1, -1)
+
+
+def test_replication_glob_semantics(tmp_path):
+    run_distributed(W.replication_globs, 2, str(tmp_path / "g"))
+
+
+@pytest.mark.parametrize("ignore", [False, True])
+def test_ddp_replication_inference(tmp_path, ignore):
+    run_distributed(W.ddp_infer_replication, 2, str(tmp_path / f"d{ignore}"), ignore)
