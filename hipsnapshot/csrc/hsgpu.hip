@@ -475,6 +475,97 @@ hs_fp8_dequant(const uint8_t* __restrict__ q, const float* __restrict__ scales, 
 }
 
 // ---------------------------------------------------------------------------
+// Hadamard-rotated fp8 (MFMA).  The flat tensor is viewed as rows of 32
+// ("groups"); every group is rotated by the 32x32 Sylvester Hadamard matrix H
+// (entries +-1, H*H = 32 I) before blockwise e4m3 quantization, which spreads
+// outliers across the group and cuts fp8 error on heavy-tailed weights.
+//
+// One wave owns a tile of 32 groups (1024 elements) and computes
+// Y[32x32] = X[32x32] * H with 16 x v_mfma_f32_32x32x2_f32 (exact f32 inputs,
+// k-ordered fmaf chain -> bit-reproducible by a sequential fp32 reference).
+// Operand maps (CDNA guide 3): lane l, r = l&31, h = l>>5:
+//   A[i=r][k=h] per instruction t -> X[row r][2t+h];  B[k=h][j=r] -> H[2t+h][r]
+//   C/D reg i -> row (i&3) + 8(i>>2) + 4h, col r
+// so register quad g4 of lane-half h is exactly quantization block 2*g4+h of
+// the tile (4 rows x 32 cols = 128 elements): amax = 4 regs + xor-shuffle over
+// the 32 lanes of the half.  Restore inverts with X = (Y' * H) / 32.
+// ---------------------------------------------------------------------------
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float hada(int k, int c) {
+  return (__popc(k & c) & 1) ? -1.f : 1.f;
+}
+
+__global__ void __launch_bounds__(kBlock)
+hs_fp8_hadamard_quant(const char* __restrict__ src, int32_t src_dtype, int64_t n, int64_t n_pad,
+                      uint8_t* __restrict__ out, float* __restrict__ scales) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int ses = (src_dtype == kF32) ? 4 : 2;
+  const int64_t ntiles = (n_pad + 1023) / 1024;
+  const int64_t nblocks = (n_pad + 127) / 128;
+  const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
+    const int64_t rowbase = (tile * 32 + r) * 32;  // flat index of X[row r][0]
+    floatx16 acc = {};
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int64_t e = rowbase + 2 * t + h;
+      const float a = (e < n) ? load_as_f32(src + e * ses, src_dtype) : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, hada(2 * t + h, r), acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      float amax = fmaxf(fmaxf(fabsf(acc[4 * g4]), fabsf(acc[4 * g4 + 1])),
+                         fmaxf(fabsf(acc[4 * g4 + 2]), fabsf(acc[4 * g4 + 3])));
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+      const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
+      const int64_t blk = tile * 8 + 2 * g4 + h;
+      if (r == 0 && blk < nblocks) scales[blk] = scale;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = q + 8 * g4 + 4 * h;
+        const int64_t e = (tile * 32 + row) * 32 + r;
+        const float v = fminf(fmaxf(acc[4 * g4 + q] / scale, -kFp8Max), kFp8Max);
+        if (e < n_pad) out[e] = static_cast<uint8_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+hs_fp8_hadamard_dequant(const uint8_t* __restrict__ q, const float* __restrict__ scales,
+                        int64_t n, int64_t n_pad, char* __restrict__ dst, int32_t dst_dtype) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int des = (dst_dtype == kF32) ? 4 : (dst_dtype == kF64 ? 8 : 2);
+  const int64_t ntiles = (n_pad + 1023) / 1024;
+  const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
+    const int64_t grow = tile * 32 + r;  // global group (row) index
+    const int64_t rowbase = grow * 32;
+    const float s = (rowbase < n_pad) ? scales[rowbase / 128] : 0.f;
+    floatx16 acc = {};
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int64_t e = rowbase + 2 * t + h;
+      const float y = (e < n_pad) ? __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(q[e]), 0) * s : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(y, hada(2 * t + h, r), acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+      const int64_t e = (tile * 32 + row) * 32 + r;
+      if (e < n) store_from_f32(dst + e * des, dst_dtype, acc[i] * (1.f / 32.f));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side state: pinned pool, copy streams, launch helpers.
 // ---------------------------------------------------------------------------
 
@@ -797,6 +888,37 @@ int hsg_fp8_dequantize(int dev, const void* q, const void* scales, int64_t n, vo
     case 16: hipLaunchKernelGGL(hs_fp8_dequant<16>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;
     default: snprintf(g_err, sizeof(g_err), "unsupported vpt %d", vpt); return -1001;
   }
+  HS_CHECK(hipGetLastError());
+  return 0;
+}
+
+// Hadamard-rotated fp8: payload `out` has n_pad = round_up(n, 32) bytes,
+// `scales` ceil(n_pad / 128) floats.
+int hsg_fp8_hadamard_quantize(int dev, const void* src, int src_dtype, int64_t n, void* out,
+                              void* scales, void* stream) {
+  HS_CHECK(hipSetDevice(dev));
+  if (n <= 0) return 0;
+  const int64_t n_pad = (n + 31) / 32 * 32;
+  const int64_t ntiles = (n_pad + 1023) / 1024;
+  const int grid = static_cast<int>(std::min<int64_t>((ntiles + 3) / 4, 256 * 8));
+  hipLaunchKernelGGL(hs_fp8_hadamard_quant, dim3(grid), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const char*>(src), src_dtype,
+                     n, n_pad, static_cast<uint8_t*>(out), static_cast<float*>(scales));
+  HS_CHECK(hipGetLastError());
+  return 0;
+}
+
+int hsg_fp8_hadamard_dequantize(int dev, const void* q, const void* scales, int64_t n, void* dst,
+                                int dst_dtype, void* stream) {
+  HS_CHECK(hipSetDevice(dev));
+  if (n <= 0) return 0;
+  const int64_t n_pad = (n + 31) / 32 * 32;
+  const int64_t ntiles = (n_pad + 1023) / 1024;
+  const int grid = static_cast<int>(std::min<int64_t>((ntiles + 3) / 4, 256 * 8));
+  hipLaunchKernelGGL(hs_fp8_hadamard_dequant, dim3(grid), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(q),
+                     static_cast<const float*>(scales), n, n_pad, static_cast<char*>(dst),
+                     dst_dtype);
   HS_CHECK(hipGetLastError());
   return 0;
 }

@@ -242,11 +242,13 @@ def _expected_read_bytes(rr: ReadReq) -> Optional[int]:
         return rr.byte_range[1] - rr.byte_range[0]
     c = rr.buffer_consumer
     entry = getattr(c, "entry", None)
-    if entry is not None and getattr(entry, "type", None) == "Tensor" \
-            and entry.serializer == "buffer_protocol":
-        from ..io.tensor import tensor_nbytes_from_entry
+    if entry is not None and getattr(entry, "type", None) == "Tensor":
+        if entry.serializer == "buffer_protocol":
+            from ..io.tensor import tensor_nbytes_from_entry
 
-        return tensor_nbytes_from_entry(entry)
+            return tensor_nbytes_from_entry(entry)
+        if getattr(entry, "quant", None):
+            return int(entry.quant["total_bytes"])
     return None
 
 

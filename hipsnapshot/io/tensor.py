@@ -267,7 +267,17 @@ class TensorBufferConsumer(BufferConsumer):
     def _nbytes(self) -> int:
         return tensor_nbytes_from_entry(self.entry)
 
+    def _fp8_on_device(self) -> bool:
+        t = self.tensor
+        return (t is not None and t.is_cuda and self.entry.serializer == Serializer.FP8_BLOCK.value
+                and t.is_contiguous() and t.dtype == string_to_dtype(self.entry.dtype))
+
     def get_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
+        if self._fp8_on_device():
+            from ..ops import native
+
+            pb = native.PinnedBuffer(nbytes)
+            return StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
         if self.entry.serializer != Serializer.BUFFER_PROTOCOL.value or self.tensor is None:
             return None
         t = self.tensor
@@ -293,6 +303,19 @@ class TensorBufferConsumer(BufferConsumer):
         t = self.tensor
         if t is None:
             self.future.obj = deserialize_tensor(buf, self.entry)
+            return
+        if self._fp8_on_device() and isinstance(buf, StagedBuffer):
+            # raw blob -> HBM by DMA, dequantized on the GPU into the target
+            from ..ops import native
+            from ..ops.quant import dequantize_device
+
+            dev = staging.device_of(t)
+            total = self.entry.quant["total_bytes"]
+            blob = torch.empty(total, dtype=torch.uint8, device=t.device)
+            native.memcpy(dev, staging.copy_slot(), blob.data_ptr(), buf.addr, total, native.H2D,
+                          None, sync=True)
+            dequantize_device(blob, self.entry, t)
+            torch.cuda.current_stream(t.device).synchronize()
             return
         if (t.is_cuda and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value):
             staging.h2d_into(t, staging.host_buffer_addr(buf), self._nbytes(),

@@ -208,6 +208,10 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_int, c_void_p])
         _declare(lib, "hsg_fp8_dequantize", c_int,
                  [c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_void_p])
+        _declare(lib, "hsg_fp8_hadamard_quantize", c_int,
+                 [c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p])
+        _declare(lib, "hsg_fp8_hadamard_dequantize", c_int,
+                 [c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p])
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
@@ -508,6 +512,29 @@ def fp8_dequantize(dev: int, q: torch.Tensor, scales: torch.Tensor, dst: torch.T
     _check(lib.hsg_fp8_dequantize(dev, q.data_ptr(), scales.data_ptr(), q.numel(),
                                   dst.data_ptr(), dtype_code(dst.dtype), vpt, stream_handle),
            "hsg_fp8_dequantize")
+
+
+def fp8_hadamard_quantize(dev: int, src: torch.Tensor, out: torch.Tensor, scales: torch.Tensor,
+                          stream_handle: int) -> None:
+    """MFMA Hadamard-32 rotation + blockwise e4m3 quantization (see hsgpu.hip)."""
+    lib = require_gpu_lib()
+    n = src.numel()
+    n_pad = (n + 31) // 32 * 32
+    assert out.numel() >= n_pad and scales.numel() >= (n_pad + 127) // 128
+    assert src.is_contiguous() and dtype_code(src.dtype) in (10, 11, 12)
+    _check(lib.hsg_fp8_hadamard_quantize(dev, src.data_ptr(), dtype_code(src.dtype), n,
+                                         out.data_ptr(), scales.data_ptr(), stream_handle),
+           "hsg_fp8_hadamard_quantize")
+
+
+def fp8_hadamard_dequantize(dev: int, q: torch.Tensor, scales: torch.Tensor, dst: torch.Tensor,
+                            stream_handle: int) -> None:
+    lib = require_gpu_lib()
+    n = dst.numel()
+    assert q.numel() >= (n + 31) // 32 * 32 and dst.is_contiguous()
+    _check(lib.hsg_fp8_hadamard_dequantize(dev, q.data_ptr(), scales.data_ptr(), n,
+                                           dst.data_ptr(), dtype_code(dst.dtype), stream_handle),
+           "hsg_fp8_hadamard_dequantize")
 
 
 # ---- managed memory -------------------------------------------------------------

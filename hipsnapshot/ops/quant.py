@@ -1,22 +1,37 @@
 """Blockwise OCP-fp8 (e4m3fn) quantized save / dequantized restore (K5/K9).
 
 Opt-in (``Snapshot.take(..., quantize=["model/**"])``): floating tensors are
-written as 1 byte/element plus one fp32 scale per block of ``64*vpt``
-elements (default vpt=2 -> 128-element blocks), halving bf16 checkpoint bytes
-(quartering fp32).  Layout of a blob: ``[fp8 payload (n bytes, padded to 16)]
-[fp32 scales]``; the entry's ``quant`` field records
-``{"format": "fp8_e4m3fn_block", "block": B, "orig_dtype": ..., "payload_bytes": ...}``
-and ``dtype`` stays the ORIGINAL dtype so restore targets match in place.
+written as 1 byte/element plus one fp32 scale per 128-element block, halving
+bf16 checkpoint bytes (quartering fp32).  The entry's ``dtype`` stays the
+ORIGINAL dtype so restore targets match in place; ``quant`` records the
+layout::
 
-On a GPU the quantizer is the ``hs_fp8_quant`` HIP kernel (one wave per block,
-64-lane xor-shuffle amax, ``v_cvt_pk_fp8_f32`` -- gfx950 converts to OCP
-e4m3fn natively); restore runs ``hs_fp8_dequant`` on the device.  CPU tensors
-use the bit-identical torch reference below (same scale rule, same RNE
-conversion via ``torch.float8_e4m3fn``).
+    {"format": "fp8_e4m3fn_block", "block": 128, "rotation": "hadamard32"|"none",
+     "payload_bytes": P, "nblocks": B, "total_bytes": P + 4B, ...}
+
+blob = ``[fp8 payload (P bytes)][B fp32 scales]``.
+
+rotation ``"hadamard32"`` (opt-in, ``HIPSNAPSHOT_FP8_ROTATION=hadamard32``): the flat
+tensor is cut into groups of 32 elements and each group is multiplied by the
+32x32 Sylvester Hadamard matrix H (+-1 entries) before quantization; restore
+computes ``(Y' H) / 32``.  The rotation spreads outliers over the group; for
+e4m3 that only pays when a block's dynamic range exceeds the format's (see
+``default_rotation``), so it is off by default.  On MI355X both directions run on the
+matrix cores (``v_mfma_f32_32x32x2_f32``, exact f32 k-ordered FMA chains) in
+``hs_fp8_hadamard_quant/dequant``; the torch references below use the same
+sequential k order, so GPU and CPU produce bit-identical blobs.
+
+rotation ``"none"`` (default): plain blockwise quantization (``hs_fp8_quant`` kernel:
+one wave per block, 64-lane xor-shuffle amax, ``v_cvt_pk_fp8_f32`` -- gfx950
+converts to OCP e4m3fn natively).
+
+Scale rule (both): ``scale = amax / 448`` (correctly rounded; 1 when the block
+is all zeros), ``q = e4m3fn(clamp(y / scale))`` with round-to-nearest-even.
 """
 
 from __future__ import annotations
 
+import os
 from typing import Any, Dict
 
 import torch
@@ -27,10 +42,22 @@ from ..io_types import StagedBuffer
 
 FP8_MAX = 448.0
 DEFAULT_VPT = 2
+GROUP = 32
 
 
 def block_elems(vpt: int = DEFAULT_VPT) -> int:
     return 64 * vpt
+
+
+def default_rotation() -> str:
+    # Measured (tests/test_quant.py::test_rotation_error_tradeoff): e4m3 is a
+    # floating format, so an outlier only costs its own relative precision;
+    # rotating spreads the outlier's absolute error over its whole group.  On
+    # Student-t(2) weights the rotated L2 error is ~1.6x the plain one, so the
+    # rotation is opt-in; it pays when a block's dynamic range exceeds e4m3's
+    # ~2^15 (values far below amax would otherwise fall into subnormals).
+    r = os.environ.get("HIPSNAPSHOT_FP8_ROTATION", "none").lower()
+    return r if r in ("hadamard32", "none") else "none"
 
 
 def fp8_supported(t: torch.Tensor) -> bool:
@@ -38,33 +65,48 @@ def fp8_supported(t: torch.Tensor) -> bool:
         and t.numel() > 0
 
 
-def _layout(n: int, block: int):
-    payload = (n + 15) // 16 * 16
-    nblocks = (n + block - 1) // block
-    return payload, nblocks, payload + 4 * nblocks
+def _round_up(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
 
 
-def fp8_entry_quant_info(t: torch.Tensor, vpt: int = DEFAULT_VPT) -> Dict[str, Any]:
-    block = block_elems(vpt)
-    payload, nblocks, total = _layout(t.numel(), block)
-    return {"format": "fp8_e4m3fn_block", "block": block, "vpt": vpt,
+def fp8_entry_quant_info(t: torch.Tensor, vpt: int = DEFAULT_VPT,
+                         rotation: str = None) -> Dict[str, Any]:
+    rotation = rotation or default_rotation()
+    n = t.numel()
+    if rotation == "hadamard32":
+        block = 128
+        n_q = _round_up(n, GROUP)
+    else:
+        block = block_elems(vpt)
+        n_q = n
+    payload = _round_up(n_q, 16)
+    nblocks = (n_q + block - 1) // block
+    return {"format": "fp8_e4m3fn_block", "block": block, "vpt": vpt, "rotation": rotation,
             "orig_dtype": dtype_to_string(t.dtype), "payload_bytes": payload,
-            "nblocks": nblocks, "total_bytes": total}
+            "nblocks": nblocks, "total_bytes": payload + 4 * nblocks}
 
 
-def quantize_reference(x: torch.Tensor, block: int):
-    """Torch fp32 reference: scale = amax/448 per block (1 if amax == 0)."""
-    flat = x.detach().reshape(-1).float()
-    n = flat.numel()
-    nblocks = (n + block - 1) // block
-    padded = torch.zeros(nblocks * block, dtype=torch.float32, device=flat.device)
-    padded[:n] = flat
-    blocks = padded.view(nblocks, block)
+# ---------------------------------------------------------------------------
+# torch fp32 references
+# ---------------------------------------------------------------------------
+
+def _scale_and_quant(blocks: torch.Tensor):
     amax = blocks.abs().amax(dim=1)
     # tensor/tensor division (correctly rounded; a Python-scalar divisor is
     # lowered to a reciprocal multiply by torch and differs by 1 ulp)
     scale = torch.where(amax > 0, amax / torch.full_like(amax, FP8_MAX), torch.ones_like(amax))
     q = (blocks / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q, scale
+
+
+def quantize_reference(x: torch.Tensor, block: int):
+    """Plain blockwise reference: returns (q[n] e4m3fn, scale[nblocks])."""
+    flat = x.detach().reshape(-1).float()
+    n = flat.numel()
+    nblocks = (n + block - 1) // block
+    padded = torch.zeros(nblocks * block, dtype=torch.float32, device=flat.device)
+    padded[:n] = flat
+    q, scale = _scale_and_quant(padded.view(nblocks, block))
     return q.reshape(-1)[:n], scale
 
 
@@ -77,10 +119,55 @@ def dequantize_reference(q: torch.Tensor, scale: torch.Tensor, block: int,
     return (padded.view(nblocks, block) * scale[:, None]).reshape(-1)[:n].to(dtype)
 
 
+def hadamard_matrix(n: int = GROUP, device=None) -> torch.Tensor:
+    idx = torch.arange(n, device=device)
+    bits = (idx[:, None] & idx[None, :])
+    parity = torch.zeros_like(bits)
+    for b in range(n.bit_length()):
+        parity ^= (bits >> b) & 1
+    return 1.0 - 2.0 * parity.float()
+
+
+def _rotate_sequential(rows: torch.Tensor) -> torch.Tensor:
+    """rows[R, 32] @ H with a k-ordered fp32 FMA chain (= MFMA f32 semantics)."""
+    h = hadamard_matrix(GROUP, rows.device)
+    acc = torch.zeros_like(rows)
+    for k in range(GROUP):
+        acc = acc + rows[:, k:k + 1] * h[k][None, :]  # x * +-1 is exact: one rounding
+    return acc
+
+
+def hadamard_quantize_reference(x: torch.Tensor, block: int = 128):
+    """Returns (q[n_pad] e4m3fn, scale[nblocks]) with n_pad = round_up(n, 32)."""
+    flat = x.detach().reshape(-1).float()
+    n = flat.numel()
+    n_pad = _round_up(n, GROUP)
+    nblocks = (n_pad + block - 1) // block
+    rows = torch.zeros(nblocks * block // GROUP, GROUP, dtype=torch.float32, device=flat.device)
+    rows.view(-1)[:n] = flat
+    y = _rotate_sequential(rows).reshape(nblocks, block)
+    q, scale = _scale_and_quant(y)
+    return q.reshape(-1)[:n_pad], scale
+
+
+def hadamard_dequantize_reference(q: torch.Tensor, scale: torch.Tensor, n: int,
+                                  dtype: torch.dtype, block: int = 128) -> torch.Tensor:
+    n_pad = q.numel()
+    y = q.float().reshape(-1)
+    s = scale.repeat_interleave(block)[:n_pad]
+    rows = (y * s).view(-1, GROUP)
+    x = _rotate_sequential(rows) * (1.0 / GROUP)
+    return x.reshape(-1)[:n].to(dtype)
+
+
+# ---------------------------------------------------------------------------
+# staging (save) and decoding (restore)
+# ---------------------------------------------------------------------------
+
 def stage_fp8(t: torch.Tensor, entry: TensorEntry, producer: int) -> StagedBuffer:
     """Quantize ``t`` and return the blob bytes in host memory."""
     info = entry.quant
-    block, vpt = info["block"], info["vpt"]
+    rot = info.get("rotation", "none")
     payload, nblocks, total = info["payload_bytes"], info["nblocks"], info["total_bytes"]
     if t.is_cuda:
         from ..engine import staging
@@ -88,22 +175,39 @@ def stage_fp8(t: torch.Tensor, entry: TensorEntry, producer: int) -> StagedBuffe
 
         dev = staging.device_of(t)
         src = t if t.is_contiguous() else t.contiguous()
-        blob = torch.empty(total, dtype=torch.uint8, device=t.device)
+        blob = torch.zeros(total, dtype=torch.uint8, device=t.device)
         stream = torch.cuda.current_stream(t.device)
         if producer and producer != stream.cuda_stream:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.ExternalStream(producer))
             stream.wait_event(ev)
-        native.fp8_quantize(dev, src, blob[:payload], blob[payload:].view(torch.float32),
-                            vpt, int(stream.cuda_stream))
+        scales = blob[payload:].view(torch.float32)
+        if rot == "hadamard32":
+            native.fp8_hadamard_quantize(dev, src, blob[:payload], scales,
+                                         int(stream.cuda_stream))
+        else:
+            native.fp8_quantize(dev, src, blob[:payload], scales, info["vpt"],
+                                int(stream.cuda_stream))
         return staging.d2h_tensor(blob, int(stream.cuda_stream))
-    q, scale = quantize_reference(t, block)
+    if rot == "hadamard32":
+        q, scale = hadamard_quantize_reference(t, info["block"])
+    else:
+        q, scale = quantize_reference(t, info["block"])
     blob = torch.zeros(total, dtype=torch.uint8)
-    blob[: t.numel()] = q.view(torch.uint8)
+    blob[: q.numel()] = q.view(torch.uint8)
     blob[payload:] = scale.view(torch.uint8)
     from ..format.serialization import contiguous_cpu_bytes_view
 
     return StagedBuffer(contiguous_cpu_bytes_view(blob), keepalive=blob)
+
+
+def _split_blob(raw: torch.Tensor, info: Dict[str, Any], n: int):
+    rot = info.get("rotation", "none")
+    nq = _round_up(n, GROUP) if rot == "hadamard32" else n
+    q = raw[:nq]
+    scale = raw[info["payload_bytes"]: info["payload_bytes"] + 4 * info["nblocks"]].view(
+        torch.float32)
+    return rot, q, scale
 
 
 def dequantize_host_fp8(buf, entry: TensorEntry) -> torch.Tensor:
@@ -114,11 +218,14 @@ def dequantize_host_fp8(buf, entry: TensorEntry) -> torch.Tensor:
         n *= int(s)
     mv = memoryview(buf.view if isinstance(buf, StagedBuffer) else buf).cast("B")
     raw = torch.frombuffer(bytearray(mv[: info["total_bytes"]]), dtype=torch.uint8)
-    q = raw[:n].view(torch.float8_e4m3fn)
-    scale = raw[info["payload_bytes"]: info["payload_bytes"] + 4 * info["nblocks"]].view(
-        torch.float32)
-    return dequantize_reference(q, scale, info["block"], string_to_dtype(entry.dtype)).view(
-        list(entry.shape))
+    rot, q, scale = _split_blob(raw, info, n)
+    dtype = string_to_dtype(entry.dtype)
+    if rot == "hadamard32":
+        out = hadamard_dequantize_reference(q.view(torch.float8_e4m3fn), scale, n, dtype,
+                                            info["block"])
+    else:
+        out = dequantize_reference(q.view(torch.float8_e4m3fn), scale, info["block"], dtype)
+    return out.view(list(entry.shape))
 
 
 def dequantize_device(blob_dev: torch.Tensor, entry: TensorEntry, dst: torch.Tensor) -> None:
@@ -127,8 +234,10 @@ def dequantize_device(blob_dev: torch.Tensor, entry: TensorEntry, dst: torch.Ten
 
     info = entry.quant
     n = dst.numel()
-    stream = torch.cuda.current_stream(dst.device)
-    native.fp8_dequantize(dst.device.index or 0, blob_dev[:n],
-                          blob_dev[info["payload_bytes"]: info["payload_bytes"]
-                                   + 4 * info["nblocks"]].view(torch.float32),
-                          dst, info["vpt"], int(stream.cuda_stream))
+    rot, q, scale = _split_blob(blob_dev, info, n)
+    stream = int(torch.cuda.current_stream(dst.device).cuda_stream)
+    dev = dst.device.index or 0
+    if rot == "hadamard32":
+        native.fp8_hadamard_dequantize(dev, q, scale, dst, stream)
+    else:
+        native.fp8_dequantize(dev, q, scale, dst, info["vpt"], stream)

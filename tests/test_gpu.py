@@ -131,6 +131,46 @@ def test_fp8_quant_dequant_vs_reference(gpu, dtype, n, vpt):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("n", [1, 31, 1000, 1024, 65536 + 77, 3 << 20])
+def test_fp8_hadamard_mfma_vs_reference(gpu, dtype, n):
+    """MFMA (v_mfma_f32_32x32x2_f32) rotation + quantization is bit-identical to
+    the k-ordered fp32 torch reference, in both directions."""
+    from hipsnapshot.ops.quant import hadamard_dequantize_reference, hadamard_quantize_reference
+
+    torch.manual_seed(4)
+    x = (torch.randn(n, device=gpu) * 3).to(dtype)
+    n_pad = (n + 31) // 32 * 32
+    nblocks = (n_pad + 127) // 128
+    q = torch.zeros(n_pad, dtype=torch.uint8, device=gpu)
+    sc = torch.empty(nblocks, dtype=torch.float32, device=gpu)
+    stream = int(torch.cuda.current_stream().cuda_stream)
+    native.fp8_hadamard_quantize(0, x, q, sc, stream)
+    rq, rs = hadamard_quantize_reference(x, 128)
+    torch.cuda.synchronize()
+    assert torch.equal(sc, rs), (sc - rs).abs().max()
+    assert torch.equal(q, rq.view(torch.uint8)), (q != rq.view(torch.uint8)).sum()
+    out = torch.empty(n, dtype=dtype, device=gpu)
+    native.fp8_hadamard_dequantize(0, q, sc, out, stream)
+    ref = hadamard_dequantize_reference(rq, rs, n, dtype)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max()
+
+
+def test_fp8_hadamard_snapshot_gpu(gpu, tmp_path):
+    from hipsnapshot.ops.quant import hadamard_dequantize_reference, hadamard_quantize_reference
+    from hipsnapshot.utils.test_utils import env
+
+    w = torch.randn(777, 333, device=gpu, dtype=torch.bfloat16)
+    with env(HIPSNAPSHOT_FP8_ROTATION="hadamard32"):
+        Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/*"])
+    out = torch.zeros_like(w)
+    Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=out)})
+    q, s = hadamard_quantize_reference(w, 128)
+    ref = hadamard_dequantize_reference(q, s, w.numel(), torch.bfloat16).view(w.shape)
+    assert torch.equal(out, ref)
+
+
 def test_gpu_snapshot_roundtrip(gpu, tmp_path):
     torch.manual_seed(3)
     a = torch.randn(512, 256, device=gpu)
