@@ -142,7 +142,14 @@ __device__ __forceinline__ void store_from_f64(char* p, int32_t dt, double v) {
     // f64 -> f16 goes through f32 (two RNE roundings) exactly like torch's
     // copy_ on ROCm (c10::Half is constructed from float); measured on MI355X:
     // a single-rounding conversion differs from torch in ~1e-4 of values.
-    case kF16: *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(static_cast<float>(v)); break;
+    case kF16: {
+      // the empty asm pins the f32 intermediate: without it LLVM folds the two
+      // fptruncs into one f64->f16 rounding, which torch does not do
+      float f = static_cast<float>(v);
+      asm volatile("" : "+v"(f));
+      *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(f);
+      break;
+    }
     case kBF16: *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(static_cast<float>(v)); break;
     case kF32: *reinterpret_cast<float*>(p) = static_cast<float>(v); break;
     default: *reinterpret_cast<double*>(p) = v; break;
