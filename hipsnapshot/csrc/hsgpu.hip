@@ -711,13 +711,28 @@ void* hsg_pinned_acquire(uint64_t nbytes) {
   return p;
 }
 
+// Blocks released while the pool caches more than this are returned to the
+// driver instead of being kept (bounds pinned host memory per process).
+uint64_t g_pool_limit = ~uint64_t(0);
+
+void hsg_pinned_set_limit(uint64_t bytes) { g_pool_limit = bytes; }
+
 int hsg_pinned_release(void* p) {
-  std::lock_guard<std::mutex> g(g_pool.mu);
-  auto it = g_pool.live.find(p);
-  if (it == g_pool.live.end()) return -1;
-  g_pool.free_blocks.emplace(it->second, p);
-  g_pool.in_use_bytes -= it->second;
-  g_pool.live.erase(it);
+  void* drop = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_pool.mu);
+    auto it = g_pool.live.find(p);
+    if (it == g_pool.live.end()) return -1;
+    g_pool.in_use_bytes -= it->second;
+    if (g_pool.cached_bytes > g_pool_limit) {
+      g_pool.cached_bytes -= it->second;
+      drop = p;
+    } else {
+      g_pool.free_blocks.emplace(it->second, p);
+    }
+    g_pool.live.erase(it);
+  }
+  if (drop) (void)hipHostFree(drop);
   return 0;
 }
 

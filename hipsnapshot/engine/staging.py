@@ -190,13 +190,30 @@ def scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
     (dim, start, length) applied to the source tensor view before copying.
     """
     slot = copy_slot()
-    scratch = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
     # order after pending work on the destinations' stream (captured at plan time)
-    native.memcpy(dev, slot, scratch.data_ptr(), host_addr, nbytes, native.H2D, producer or None,
+    native.memcpy(dev, slot, 0, 0, 0, native.H2D, producer or None, sync=False)
+    # Regions whose source bytes are one contiguous range and whose destination
+    # is a contiguous tensor of the same dtype/shape go host -> destination with
+    # one DMA each (no scratch, no kernel: the common FSDP/DTensor restore).
+    kernel_regions = []
+    for region in regions:
+        src_dtype, src_shape, off, narrows, dst = region
+        rng = _contiguous_src_range(src_dtype, src_shape, off, narrows)
+        if (rng is not None and dst.dtype == src_dtype and dst.is_contiguous()
+                and dst.numel() * dst.element_size() == rng[1]):
+            native.memcpy(dev, slot, dst.data_ptr(), host_addr + rng[0], rng[1], native.H2D,
+                          None, sync=False)
+        else:
+            kernel_regions.append(region)
+    if not kernel_regions:
+        native.stream_sync(dev, slot)
+        return
+    scratch = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
+    native.memcpy(dev, slot, scratch.data_ptr(), host_addr, nbytes, native.H2D, None,
                   sync=False)
     batch = native.CopyBatch()
     fallbacks = []
-    for src_dtype, src_shape, off, narrows, dst in regions:
+    for src_dtype, src_shape, off, narrows, dst in kernel_regions:
         es = torch.empty(0, dtype=src_dtype).element_size()
         n = 1
         for z in src_shape:
@@ -220,6 +237,19 @@ def scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
             dst.copy_(src)
         torch.cuda.synchronize(dev)
     del scratch
+
+
+def _contiguous_src_range(src_dtype: torch.dtype, src_shape: Sequence[int], off: int, narrows):
+    """(byte offset, nbytes) of a region's source when it is one contiguous
+    byte range of the host buffer, else None (computed on the meta device)."""
+    src = torch.empty(list(src_shape), dtype=src_dtype, device="meta")
+    if narrows:
+        for d, s, ln in narrows:
+            src = src.narrow(d, s, ln)
+    if not src.is_contiguous():
+        return None
+    es = src.element_size()
+    return off + src.storage_offset() * es, src.numel() * es
 
 
 def host_view_as_tensor(buf, dtype: torch.dtype, shape: Sequence[int]) -> torch.Tensor:

@@ -194,6 +194,9 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_pinned_release", c_int, [c_void_p])
         _declare(lib, "hsg_pinned_stats", None, [ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_pinned_trim", c_uint64, [])
+        _declare(lib, "hsg_pinned_set_limit", None, [c_uint64])
+        lim = os.environ.get("HIPSNAPSHOT_PINNED_POOL_MAX_BYTES")
+        lib.hsg_pinned_set_limit(int(lim) if lim else 64 << 30)
         _declare(lib, "hsg_memcpy", c_int,
                  [c_int, c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_int])
         _declare(lib, "hsg_stream_join", c_int, [c_int, c_int, c_void_p])
