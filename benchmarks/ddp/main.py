@@ -30,11 +30,23 @@ def main():
     ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
     ap.add_argument("--torch-save", action="store_true")
     ap.add_argument("--repeats", type=int, default=2)
+    ap.add_argument("--model", default="many_params", choices=["many_params", "llama3_8b"],
+                    help="llama3_8b = BASELINE config 2 (Llama-3-8B DDP bf16, partitioned save)")
     args = ap.parse_args()
     rank, ws, dev = init_dist()
-    model = DDP(ManyParams(args.n_params, args.param_mb, dev), device_ids=[dev.index]
-                if dev.type == "cuda" else None, gradient_as_bucket_view=True)
-    nbytes = args.n_params * args.param_mb * 1000 * 1000
+    if args.model == "llama3_8b":
+        from hipsnapshot.models.llama import Llama, LlamaConfig, init_weights_
+
+        with torch.device("meta"):
+            inner = Llama(LlamaConfig.llama3_8b()).to(torch.bfloat16)
+        inner.to_empty(device=dev)
+        init_weights_(inner)
+        nbytes = sum(p.numel() * p.element_size() for p in inner.parameters())
+    else:
+        inner = ManyParams(args.n_params, args.param_mb, dev)
+        nbytes = args.n_params * args.param_mb * 1000 * 1000
+    model = DDP(inner, device_ids=[dev.index] if dev.type == "cuda" else None,
+                gradient_as_bucket_view=True)
     log(f"model size: {nbytes / 1e9:.1f} GB, world size {ws}")
     root = os.path.join(args.work_dir, "hs_ddp_bench")
     if rank == 0:
@@ -49,8 +61,8 @@ def main():
         s = max_over_ranks(t.s, dev)
         log(f"hipsnapshot take {i}: {s:.2f}s ({nbytes / s / 1e9:.2f} GB/s)")
         best = s if best is None else min(best, s)
-    ref = {1: 13.91, 8: 3.38}.get(ws)
-    out = {"bench": "ddp_20gb_save", "world_size": ws, "bytes": nbytes, "seconds": round(best, 3),
+    ref = {1: 13.91, 8: 3.38}.get(ws) if args.model == "many_params" else None
+    out = {"bench": "ddp_20gb_save" if args.model == "many_params" else "llama3_8b_ddp_save", "world_size": ws, "bytes": nbytes, "seconds": round(best, 3),
            "GBps": round(nbytes / best / 1e9, 3),
            "reference_seconds": ref, "speedup_vs_reference": round(ref / best, 2) if ref else None}
     if args.torch_save and rank == 0:
