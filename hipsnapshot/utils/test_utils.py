@@ -56,7 +56,39 @@ def _dense(t: Any) -> Any:
     return t
 
 
+def _is_sharded_tensor(t: Any) -> bool:
+    try:
+        from torch.distributed._shard.sharded_tensor import ShardedTensor
+    except Exception:  # pragma: no cover
+        return False
+    return isinstance(t, ShardedTensor)
+
+
+def sharded_tensor_eq(a: Any, b: Any) -> bool:
+    """Local comparison of two ShardedTensors (no collective): same global
+    metadata and bitwise-equal local shards at the same offsets
+    (reference: `/root/reference/torchsnapshot/test_utils.py:65-101`)."""
+    if not (_is_sharded_tensor(a) and _is_sharded_tensor(b)):
+        return False
+    ma, mb = a.metadata(), b.metadata()
+    if list(ma.size) != list(mb.size) or ma.tensor_properties.dtype != mb.tensor_properties.dtype:
+        return False
+    if [(s.shard_offsets, s.shard_sizes) for s in ma.shards_metadata] != \
+            [(s.shard_offsets, s.shard_sizes) for s in mb.shards_metadata]:
+        return False
+    la, lb = a.local_shards(), b.local_shards()
+    if len(la) != len(lb):
+        return False
+    for x, y in zip(la, lb):
+        if x.metadata.shard_offsets != y.metadata.shard_offsets or \
+                not tensor_eq(x.tensor, y.tensor):
+            return False
+    return True
+
+
 def tensor_eq(a: torch.Tensor, b: torch.Tensor) -> bool:
+    if _is_sharded_tensor(a) or _is_sharded_tensor(b):
+        return sharded_tensor_eq(a, b)
     a, b = _dense(a), _dense(b)
     if a.is_quantized != b.is_quantized:
         return False

@@ -72,6 +72,68 @@ def test_sharded_tensor_resharding_all_spec_pairs(tmp_path, subdivide):
     run_distributed(_worker, 1, str(tmp_path), subdivide)
 
 
+def _rank_specs(ws: int):
+    """Specs whose shards live on different ranks of a ``ws``-rank group."""
+    from torch.distributed._shard.metadata import ShardMetadata
+    from torch.distributed._shard.sharding_spec import ChunkShardingSpec, EnumerableShardingSpec
+
+    pl = [f"rank:{r}/cpu" for r in range(ws)]
+    return [
+        ChunkShardingSpec(dim=0, placements=pl),
+        ChunkShardingSpec(dim=1, placements=pl[::-1]),
+        EnumerableShardingSpec([
+            ShardMetadata([0, 0], [37, 64], pl[0]),
+            ShardMetadata([37, 0], [27, 20], pl[1 % ws]),
+            ShardMetadata([37, 20], [27, 44], pl[-1]),
+        ]),
+    ]
+
+
+def _multirank_worker(tmp: str, subdivide: bool) -> None:
+    """Every rank saves its local shards; every (src, dst) spec pair restores
+    across ranks; read_object of the whole tensor (with and without a memory
+    budget) works on every rank (reference:
+    tests/test_sharded_tensor_io_preparer.py:101-175, tests/test_read_object.py:43-140)."""
+    import torch.distributed as dist
+    from torch.distributed._shard import sharded_tensor
+
+    from hipsnapshot import Snapshot, StateDict
+    from hipsnapshot.knobs import override_max_shard_size_bytes
+    from hipsnapshot.utils.test_utils import sharded_tensor_eq
+
+    ws = dist.get_world_size()
+    specs = _rank_specs(ws)
+    for i, (src, dst) in enumerate(itertools.product(specs, specs)):
+        torch.manual_seed(i)  # same global values on every rank
+        full = torch.randn(64, 64)
+        st = sharded_tensor.zeros(src, 64, 64)
+        for s in st.local_shards():
+            o, z = s.metadata.shard_offsets, s.metadata.shard_sizes
+            s.tensor.copy_(full[o[0]:o[0] + z[0], o[1]:o[1] + z[1]])
+        path = f"{tmp}/m{i}"
+        if subdivide:
+            with override_max_shard_size_bytes(1024):
+                Snapshot.take(path, {"sd": StateDict(st=st)})
+        else:
+            Snapshot.take(path, {"sd": StateDict(st=st)})
+        out = sharded_tensor.zeros(dst, 64, 64)
+        Snapshot(path).restore({"sd": StateDict(st=out)})
+        for s in out.local_shards():
+            o, z = s.metadata.shard_offsets, s.metadata.shard_sizes
+            assert torch.equal(s.tensor, full[o[0]:o[0] + z[0], o[1]:o[1] + z[1]]), (i, o)
+        if src is dst:
+            assert sharded_tensor_eq(out, st)
+        for budget in (None, 4096):
+            plain = torch.zeros(64, 64)
+            Snapshot(path).read_object("0/sd/st", obj_out=plain, memory_budget_bytes=budget)
+            assert torch.equal(plain, full), (i, budget)
+
+
+@pytest.mark.parametrize("subdivide", [False, True])
+def test_sharded_tensor_multirank_resharding(tmp_path, subdivide):
+    run_distributed(_multirank_worker, 3, str(tmp_path), subdivide)
+
+
 def test_subdivide_shard_math():
     from hipsnapshot.io.sharded import ShardedTensorIOPreparer
 
