@@ -33,6 +33,7 @@ import psutil
 
 from .. import knobs
 from ..io_types import ReadIO, ReadReq, StagedBuffer, StoragePlugin, WriteIO, WriteReq, as_staged
+from ..utils.tracing import timeline
 
 logger = logging.getLogger(__name__)
 
@@ -137,7 +138,10 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     async def _write(wr: WriteReq, buf: StagedBuffer, cost: int) -> None:
         try:
             async with io_sem:
+                t_w = time.perf_counter()
                 await storage.write(WriteIO(path=wr.path, buf=buf.view, addr=buf.addr))
+                timeline.add("write", "io", t_w, time.perf_counter(), path=wr.path,
+                             bytes=buf.nbytes)
             stats.bytes_written += buf.nbytes
         except BaseException as e:  # noqa: BLE001
             failure.append(e)
@@ -156,7 +160,7 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                 wr = pending.popleft()
                 in_use[0] += cost
                 task = asyncio.ensure_future(wr.buffer_stager.stage_buffer(executor))
-                staging[task] = (wr, cost)
+                staging[task] = (wr, cost, time.perf_counter())
             if failure:
                 break
             waiters = set(staging)
@@ -170,13 +174,15 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             for task in done:
                 if task is waiter:
                     continue
-                wr, cost = staging.pop(task)
+                wr, cost, t_s = staging.pop(task)
                 exc = task.exception()
                 if exc is not None:
                     in_use[0] -= cost
                     failure.append(exc)
                     continue
                 buf = as_staged(task.result())
+                timeline.add("stage", "stage", t_s, time.perf_counter(), path=wr.path,
+                             bytes=buf.nbytes)
                 stats.bytes_staged += buf.nbytes
                 io_tasks.add(asyncio.ensure_future(_write(wr, buf, cost)))
         if failure:
@@ -275,11 +281,16 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                 dest = rr.buffer_consumer.get_read_dest(nbytes)
             read_io = ReadIO(path=rr.path, byte_range=rr.byte_range, dest=dest)
             async with io_sem:
+                t_r = time.perf_counter()
                 await storage.read(read_io)
+                t_c = time.perf_counter()
             data = read_io.data()
-            stats.bytes_written += memoryview(data).nbytes
+            nb = memoryview(data).nbytes
+            timeline.add("read", "io", t_r, t_c, path=rr.path, bytes=nb)
+            stats.bytes_written += nb
             await rr.buffer_consumer.consume_buffer(dest if dest is not None else data,
                                                     executor)
+            timeline.add("consume", "stage", t_c, time.perf_counter(), path=rr.path, bytes=nb)
         finally:
             if dest is not None:
                 dest.release()

@@ -22,6 +22,7 @@ CPU tensors are never moved through the GPU.
 from __future__ import annotations
 
 import threading
+import time
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -29,6 +30,7 @@ import torch
 from ..format.serialization import contiguous_cpu_bytes_view, tensor_from_bytes
 from ..io_types import StagedBuffer, buffer_address
 from ..ops import native
+from ..utils.tracing import timeline
 
 _tls = threading.local()
 _slot_lock = threading.Lock()
@@ -77,6 +79,7 @@ def d2h_tensor(t: torch.Tensor, producer: int) -> StagedBuffer:
         return staged
     dev = device_of(t)
     slot = copy_slot()
+    t_s = time.perf_counter()
     try:
         if t.is_contiguous():
             native.memcpy(dev, slot, pb.ptr, t.data_ptr(), nbytes, native.D2H, producer, sync=True)
@@ -91,6 +94,7 @@ def d2h_tensor(t: torch.Tensor, producer: int) -> StagedBuffer:
     except BaseException:
         staged.release()
         raise
+    timeline.add("d2h", "d2h", t_s, time.perf_counter(), bytes=nbytes, slot=slot)
     return staged
 
 
@@ -135,6 +139,7 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
     dev = device_of(members[0][0])
     slot = copy_slot()
     stream = native.copy_stream(dev, slot)
+    t_s = time.perf_counter()
     try:
         for producer in producers:
             native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
@@ -160,6 +165,8 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
     except BaseException:
         staged.release()
         raise
+    timeline.add("gather_d2h", "d2h", t_s, time.perf_counter(), bytes=total_bytes,
+                 members=len(members), slot=slot)
     return staged
 
 
@@ -182,6 +189,12 @@ def h2d_into(dst: torch.Tensor, host_addr: int, nbytes: int, src_dtype: torch.dt
 
 def scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
                          producer: int = 0) -> None:
+    with timeline.span("h2d_scatter", "h2d", bytes=nbytes, regions=len(regions)):
+        _scatter_host_regions(host_addr, nbytes, regions, dev, producer)
+
+
+def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
+                          producer: int = 0) -> None:
     """One H2D of ``nbytes`` at ``host_addr`` then ONE kernel launch that copies
     every region into its destination view.
 

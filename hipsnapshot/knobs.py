@@ -9,6 +9,8 @@ Every variable is read as ``HIPSNAPSHOT_<NAME>`` first and the reference's
 MI355X-specific knobs:
 
 * ``HIPSNAPSHOT_IO_THREADS`` (16) -- native I/O engine workers per storage plugin.
+* ``HIPSNAPSHOT_IO_READ_SPLIT_BYTES`` (8 MiB) -- reads larger than 1.5x this are
+  split across I/O workers (parallel page-cache reads of one file; 0 = off).
 * ``HIPSNAPSHOT_STAGE_THREADS`` (4) -- concurrent staging jobs (DMA/pack/serialize).
 * ``HIPSNAPSHOT_FS_DIRECT_IO`` (0) -- O_DIRECT for the aligned body of blobs.
 * ``HIPSNAPSHOT_FS_FSYNC`` (0) -- fdatasync every blob (durable checkpoints).
@@ -83,6 +85,10 @@ def get_memory_budget_override() -> Optional[int]:
 
 def get_io_threads() -> int:
     return _get_int("IO_THREADS", 16)
+
+
+def get_io_read_split_bytes() -> int:
+    return _get_int("IO_READ_SPLIT_BYTES", 8 * 1024 * 1024)
 
 
 def get_stage_threads() -> int:

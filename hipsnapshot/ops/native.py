@@ -63,6 +63,7 @@ def hsio() -> ctypes.CDLL:
             _declare(lib, "hsio_create", c_void_p, [c_int])
             _declare(lib, "hsio_destroy", None, [c_void_p])
             _declare(lib, "hsio_eventfd", c_int, [c_void_p])
+            _declare(lib, "hsio_set_read_split", None, [c_void_p, c_uint64])
             _declare(lib, "hsio_submit_write", c_int64,
                      [c_void_p, c_char_p, c_void_p, c_uint64, c_uint64, c_int])
             _declare(lib, "hsio_submit_read", c_int64,
@@ -97,6 +98,9 @@ class IOEngine:
         self.pid = os.getpid()
         self.handle = self.lib.hsio_create(nthreads)
         self.efd = self.lib.hsio_eventfd(self.handle)
+        from .. import knobs
+
+        self.lib.hsio_set_read_split(self.handle, knobs.get_io_read_split_bytes())
         self._ids = (c_int64 * 256)()
         self._res = (c_int64 * 256)()
 

@@ -65,7 +65,7 @@ from .parallel.partitioner import consolidate_replicated_entries, partition_writ
 from .parallel.store import LinearBarrier, get_or_create_store
 from .stateful import AppState, RNGState, Stateful
 from .storage.registry import url_to_storage_plugin_in_event_loop
-from .utils.tracing import roctx_range
+from .utils.tracing import roctx_range, timeline
 from .version import __version__
 
 logger = logging.getLogger(__name__)
@@ -124,7 +124,8 @@ class Snapshot:
         loop = asyncio.new_event_loop()
         comm = Comm(pg)
         t0 = time.monotonic()
-        path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
+        with timeline.span("coalesce"):
+            path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
         storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
         try:
             with roctx_range("hipsnapshot.take.plan_and_stage"):
@@ -132,15 +133,16 @@ class Snapshot:
                                                    loop, False, _custom_tensor_prepare_func,
                                                    quantize)
             t_staged = time.monotonic()
-            with roctx_range("hipsnapshot.take.drain_io"):
+            with roctx_range("hipsnapshot.take.drain_io"), timeline.span("drain_io"):
                 pending.sync_complete(loop)
-            with roctx_range("hipsnapshot.take.commit"):
+            with roctx_range("hipsnapshot.take.commit"), timeline.span("commit"):
                 comm.barrier()
                 if comm.get_rank() == 0:
                     cls._write_snapshot_metadata(metadata, storage, loop)
         finally:
             storage.sync_close(loop)
             loop.close()
+        timeline.dump("take", comm.get_rank())
         TakeStats.last = {"stage_s": t_staged - t0, "total_s": time.monotonic() - t0,
                           "bytes": float(pending.stats.bytes_written)}
         snap = cls(path=path, pg=pg, storage_options=storage_options)
@@ -196,7 +198,8 @@ class Snapshot:
                    prepare_func: Optional[PrepareFunc], quantize: Optional[List[str]]
                    ) -> Tuple[PendingIOWork, SnapshotMetadata]:
         if comm.get_rank() == 0:
-            cls._uncommit(storage, loop)
+            with timeline.span("uncommit"):
+                cls._uncommit(storage, loop)
         app_state = dict(app_state)
         rng_item = cls._pop_rng_state(app_state)
         manifest: Dict[str, Entry] = {}
@@ -211,16 +214,20 @@ class Snapshot:
             flattened.update(f)
         for key in global_keys:
             if key in app_state:
-                m, f = flatten(app_state[key].state_dict(), prefix=key)
+                with timeline.span("state_dict", key=key):
+                    m, f = flatten(app_state[key].state_dict(), prefix=key)
                 manifest.update(m)
                 flattened.update(f)
             # user state_dict() implementations may run collectives: keep them
             # from interleaving across ranks
-            comm.barrier()
+            with timeline.span("barrier"):
+                comm.barrier()
         if rng_item is not None:
             rng_item[1].load_state_dict(rng_sd)
 
-        rep_paths = cls._calculate_replicated_entries(flattened, replicated, comm)
+        with timeline.span("replicated_entries"):
+            rep_paths = cls._calculate_replicated_entries(flattened, replicated, comm)
+        t_prep = time.perf_counter()
         from .format.serialization import Serializer
 
         object_entries: Dict[str, Entry] = {}
@@ -243,24 +250,30 @@ class Snapshot:
             else:
                 object_entries[logical] = entry
                 path_reqs[logical] = wrs
-        object_entries, path_reqs = partition_write_reqs(object_entries, path_reqs, comm)
+        timeline.add("prepare_write", "phase", t_prep, time.perf_counter(), n=len(flattened))
+        with timeline.span("partition"):
+            object_entries, path_reqs = partition_write_reqs(object_entries, path_reqs, comm)
         write_reqs = [wr for wrs in path_reqs.values() for wr in wrs]
         if not knobs.is_batching_disabled():
-            _, write_reqs = batch_write_requests(list(object_entries.values()), write_reqs,
-                                                 name_prefix=f"r{rank}")
+            with timeline.span("batch"):
+                _, write_reqs = batch_write_requests(list(object_entries.values()), write_reqs,
+                                                     name_prefix=f"r{rank}")
         manifest.update(primitives)
         manifest.update(object_entries)
-        manifest = cls._gather_manifest(manifest, comm)
+        with timeline.span("gather_manifest"):
+            manifest = cls._gather_manifest(manifest, comm)
 
         budget = get_process_memory_budget_bytes(comm)
         deferred: List[WriteReq] = []
         if is_async and knobs.async_hbm_staging_enabled():
             from .engine.hbm_staging import freeze_device_state, is_deferrable
 
-            freeze_device_state(write_reqs)
+            with timeline.span("hbm_freeze"):
+                freeze_device_state(write_reqs)
             deferred = [wr for wr in write_reqs if is_deferrable(wr)]
             write_reqs = [wr for wr in write_reqs if not is_deferrable(wr)]
-        pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop)
+        with timeline.span("stage", n=len(write_reqs)):
+            pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop)
         if deferred:
             from .engine.scheduler import DeferredIOWork
 
@@ -285,13 +298,15 @@ class Snapshot:
             comm.all_gather_object(gathered, list(app_state.keys()))
             keys = sorted(set(itertools.chain.from_iterable(gathered)))
             for key in keys:
-                self._load_stateful(key, app_state.get(key), storage, comm, loop)
+                with timeline.span("load_stateful", key=key):
+                    self._load_stateful(key, app_state.get(key), storage, comm, loop)
                 comm.barrier()
             if rng_item is not None:
                 self._load_stateful(rng_item[0], rng_item[1], storage, comm, loop)
         finally:
             storage.sync_close(loop)
             loop.close()
+        timeline.dump("restore", comm.get_rank())
 
     def _load_stateful(self, key: str, stateful: Optional[Stateful], storage: StoragePlugin,
                        comm: Comm, loop: asyncio.AbstractEventLoop) -> None:
@@ -320,7 +335,8 @@ class Snapshot:
         if not knobs.is_batching_disabled():
             reads = batch_read_requests(reads)
         budget = get_process_memory_budget_bytes(comm)
-        sync_execute_read_reqs(reads, storage, budget, comm.get_rank(), loop)
+        with timeline.span("read_pipeline", n=len(reads)):
+            sync_execute_read_reqs(reads, storage, budget, comm.get_rank(), loop)
         state_dict = inflate(containers, {k: f.obj for k, f in futs.items()}, prefix=key)
         stateful.load_state_dict(state_dict)
 

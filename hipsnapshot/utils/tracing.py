@@ -93,3 +93,63 @@ class WriteReporter:
                 f"written={bytes_written / 1e9:8.3f}GB")
         logger.debug(line)
         return line
+
+
+class Timeline:
+    """Per-process span recorder dumped as a Chrome/Perfetto trace.
+
+    Enabled with ``HIPSNAPSHOT_TIMELINE=<path prefix>``: every take / restore
+    writes ``<prefix>.rank<R>.<op><N>.json`` with one complete event per
+    planning phase, per staged request (D2H / gather) and per storage write or
+    read, on the thread that ran it.  Open it in ui.perfetto.dev next to a
+    ``rocprofv3 --kernel-trace`` of the same run to see where a snapshot's
+    wall time goes.  Disabled, ``span`` costs one attribute check.
+    """
+
+    def __init__(self) -> None:
+        self.prefix = os.environ.get("HIPSNAPSHOT_TIMELINE") or None
+        self.events: list = []
+        self.t0 = time.perf_counter()
+        self.counts: dict = {}
+
+    @property
+    def enabled(self) -> bool:
+        return self.prefix is not None
+
+    def add(self, name: str, cat: str, t_start: float, t_end: float, **args) -> None:
+        if self.prefix is None:
+            return
+        import threading
+
+        self.events.append({"name": name, "cat": cat, "ph": "X",
+                            "ts": (t_start - self.t0) * 1e6, "dur": (t_end - t_start) * 1e6,
+                            "pid": os.getpid(), "tid": threading.get_ident() % 100000,
+                            "args": args})
+
+    @contextlib.contextmanager
+    def span(self, name: str, cat: str = "phase", **args):
+        if self.prefix is None:
+            yield
+            return
+        t = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.add(name, cat, t, time.perf_counter(), **args)
+
+    def dump(self, op: str, rank: int) -> Optional[str]:
+        if self.prefix is None or not self.events:
+            return None
+        import json
+
+        n = self.counts.get(op, 0)
+        self.counts[op] = n + 1
+        path = f"{self.prefix}.rank{rank}.{op}{n}.json"
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump({"traceEvents": self.events, "displayTimeUnit": "ms"}, f)
+        self.events = []
+        return path
+
+
+timeline = Timeline()

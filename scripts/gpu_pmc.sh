@@ -18,4 +18,5 @@ for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LD
   dirs="$dirs $REPO/gpurun_out/raw_$tag"
 done
 python3 $REPO/scripts/pmc_summary.py $REPO/gpurun_out/pmc_summary $dirs || exit 1
+for d in $dirs; do f=$(ls $d/*counter_collection.csv | head -1); head -40 $f > $d.sample.csv; done
 rm -rf $dirs

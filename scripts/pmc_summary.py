@@ -18,6 +18,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
     name = name.split("(")[0]
     return name if len(name) <= 60 else name[:57] + "..."
 
@@ -70,6 +71,21 @@ def main():
         fh.write("|" + "---|" * len(fields) + "\n")
         for r in rows:
             fh.write("| " + " | ".join(str(r.get(f, "")) for f in fields) + " |\n")
+    # per-dispatch table (dispatch order = program order; lets a caller map
+    # dispatches of one kernel to the microbench case that issued them)
+    disp_ids = sorted({(dk[1], k) for k in vals for c in vals[k] for dk in vals[k][c]},
+                      key=lambda x: int(x[0] or 0))
+    with open(out_prefix + "_dispatches.csv", "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["dispatch", "kernel", "dur_us"] + counters)
+        for did, k in disp_ids:
+            row = [did, k]
+            dur = [v for (dd, i), v in durs.get(k, {}).items() if i == did]
+            row.append(round(dur[0], 2) if dur else "")
+            for c in counters:
+                xs = [v for (dd, i), v in vals[k].get(c, {}).items() if i == did]
+                row.append(xs[0] if xs else "")
+            w.writerow(row)
     print(open(out_prefix + ".md").read())
 
 

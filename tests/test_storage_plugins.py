@@ -4,6 +4,7 @@ MemoryviewStream (reference tests: test_fs_storage_plugin.py,
 test_s3_storage_plugin.py, test_gcs_storage_plugin.py, test_memoryview_stream.py)."""
 
 import asyncio
+import ctypes
 import datetime
 import io
 import os
@@ -67,6 +68,42 @@ def test_fs_engine_write_read_ranged_and_overwrite(tmp_path):
         await p.close()
 
     run(body())
+
+
+@pytest.mark.parametrize("direct", [0, 1])
+def test_engine_split_reads(tmp_path, direct):
+    from hipsnapshot.ops import native
+
+    eng = native.IOEngine(4)
+    eng.lib.hsio_set_read_split(eng.handle, 64 << 10)
+    data = os.urandom((3 << 20) + 12345)
+    path = str(tmp_path / "big.bin")
+    with open(path, "wb") as f:
+        f.write(data)
+    pb = native.hsio().hsio_alloc_aligned(len(data))
+    try:
+        buf = (ctypes.c_char * len(data)).from_address(pb)
+        flags = native.IO_DIRECT if direct else 0
+        jid = eng.submit_read(path, pb, len(data), 0, flags)
+        got = {}
+        while jid not in got:
+            got.update(dict(eng.poll()))
+        assert got[jid] == len(data) and bytes(buf) == data
+        # ranged + reading past EOF: the sum of the parts is the short count
+        jid = eng.submit_read(path, pb, 1 << 20, len(data) - 100_000, flags)
+        got = {}
+        while jid not in got:
+            got.update(dict(eng.poll()))
+        assert got[jid] == 100_000 and bytes(buf[:100_000]) == data[-100_000:]
+        # missing file: one error for the whole group
+        jid = eng.submit_read(str(tmp_path / "nope"), pb, 1 << 20, 0, 0)
+        got = {}
+        while jid not in got:
+            got.update(dict(eng.poll()))
+        assert got[jid] < 0
+    finally:
+        native.hsio().hsio_free_aligned(pb)
+        eng.close()
 
 
 def test_fs_engine_direct_io_and_fsync(tmp_path):

@@ -83,3 +83,29 @@ def test_knob_overrides_and_legacy_names(monkeypatch):
         assert knobs.get_max_shard_size_bytes() == 512 * 1024 * 1024
     monkeypatch.setenv("TORCHSNAPSHOT_DISABLE_BATCHING", "1")
     assert knobs.is_batching_disabled()
+
+
+def test_timeline_trace(tmp_path, monkeypatch):
+    import json
+
+    from hipsnapshot import Snapshot, StateDict
+    from hipsnapshot.utils import tracing
+
+    tl = tracing.Timeline()
+    tl.prefix = str(tmp_path / "tl")
+    monkeypatch.setattr(tracing, "timeline", tl)
+    import hipsnapshot.engine.scheduler as sched
+    import hipsnapshot.snapshot as snap_mod
+
+    monkeypatch.setattr(sched, "timeline", tl)
+    monkeypatch.setattr(snap_mod, "timeline", tl)
+    sd = StateDict(a=torch.randn(1000), b=torch.randn(50, 50), n=3)
+    Snapshot.take(str(tmp_path / "s"), {"sd": sd})
+    Snapshot(str(tmp_path / "s")).restore({"sd": sd})
+    take = json.load(open(tmp_path / "tl.rank0.take0.json"))["traceEvents"]
+    names = {e["name"] for e in take}
+    assert {"coalesce", "prepare_write", "stage", "drain_io", "commit", "write"} <= names
+    assert all(e["ph"] == "X" and e["dur"] >= 0 for e in take)
+    assert sum(e["args"].get("bytes", 0) for e in take if e["name"] == "write") > 0
+    rest = json.load(open(tmp_path / "tl.rank0.restore0.json"))["traceEvents"]
+    assert {"load_stateful", "read"} <= {e["name"] for e in rest}
