@@ -42,16 +42,16 @@ def _atomic_build(out: str, cmd_for) -> None:
 
 
 def build_hsio(force: bool = False) -> str:
-    src = os.path.join(CSRC, "hsio.cpp")
-    if force or _stale(HSIO_SO, [src]):
+    srcs = [os.path.join(CSRC, "hsio.cpp"), os.path.join(CSRC, "hsz_cpu.cpp")]
+    if force or _stale(HSIO_SO, srcs):
         cxx = shutil.which("g++") or shutil.which("c++") or os.path.join(ROCM, "llvm/bin/clang++")
         _atomic_build(HSIO_SO, lambda out: [cxx, "-O3", "-std=c++17", "-fPIC", "-shared",
-                                            "-pthread", "-Wall", "-o", out, src])
+                                            "-pthread", "-Wall", "-o", out] + srcs)
     return HSIO_SO
 
 
 def build_hsgpu(force: bool = False) -> str:
-    srcs = [os.path.join(CSRC, "hsgpu.hip")]
+    srcs = [os.path.join(CSRC, "hsgpu.hip"), os.path.join(CSRC, "hsz.hip")]
     if force or _stale(HSGPU_SO, srcs):
         hipcc = os.path.join(ROCM, "bin", "hipcc")
         if not os.path.exists(hipcc):

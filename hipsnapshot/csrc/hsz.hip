@@ -1,0 +1,561 @@
+// hsz: HSZ1 lossless exponent-nibble codec on gfx950 (format: hipsnapshot/ops/codec.py).
+//
+// Encode (before D2H) = 3 launches on the caller's stream:
+//   hsz_analyze<W>  one workgroup per 256 KiB frame: 2048-sample LDS histogram
+//                   -> 15-entry dictionary (wave-wide argmax), then a full pass
+//                   counting escapes -> frame mode + coded size
+//   hsz_layout      one workgroup: exclusive scan of frame sizes, blob header +
+//                   frame table, total size for the host
+//   hsz_encode<W>   one workgroup per frame: 8 elements per lane per step,
+//                   coalesced 16-B loads, nibble codes via an LDS code table,
+//                   low-byte plane stores; the rare escapes go to an LDS list
+//                   and are written in element order by rank
+// Decode (after H2D) = 1 launch, one workgroup per frame (escape positions are
+// collected from the nibble plane first, then every element is rebuilt).
+//
+// A frame is one workgroup (4 waves): a 512 MiB blob has 2048 frames, 8x the
+// CU count, so the grid fills the chip; all traffic is streaming HBM
+// (read 2 B + write 1.5 B per bf16 element encoded).
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kSample = 2048;
+constexpr int kMaxEsc = 1024;
+constexpr int kHeader = 64;
+constexpr int kFrameHeader = 32;
+constexpr int kEsc = 15;
+
+struct FrameMeta {
+  uint32_t mode;
+  uint32_t n_esc;
+  uint32_t nsel;  // dictionary entries actually selected (rest are 0 padding)
+  uint32_t pad;
+  uint8_t dict[16];
+  uint64_t size;    // padded frame bytes
+  uint64_t offset;  // absolute offset in the blob
+};
+
+__device__ __forceinline__ uint64_t align16(uint64_t n) { return (n + 15) & ~uint64_t(15); }
+
+__device__ __forceinline__ int block_sum(int v, int* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wid] = v;
+  __syncthreads();
+  int t = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return t;
+}
+
+// The 15 most frequent values of hist (count desc, value asc); zero counts are
+// never chosen.  Runs on wave 0; results in dict / code_of (LDS).
+__device__ void build_dict(const uint32_t* hist, uint8_t* dict, uint8_t* code_of, int* nsel) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    uint64_t key[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int v = lane * 4 + j;
+      key[j] = (uint64_t(hist[v]) << 8) | uint64_t(255 - v);
+    }
+    int k = 0;
+    for (; k < 15; ++k) {
+      uint64_t best = key[0];
+#pragma unroll
+      for (int j = 1; j < 4; ++j) best = key[j] > best ? key[j] : best;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t other = __shfl_xor(best, o, 64);
+        best = other > best ? other : best;
+      }
+      if ((best >> 8) == 0) break;
+      const int v = 255 - int(best & 255);
+      if (lane == 0) dict[k] = uint8_t(v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (v == lane * 4 + j) key[j] = 0;
+    }
+    if (lane == 0) *nsel = k;
+    for (int j = k + lane; j < 16; j += 64) dict[j] = 0;
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[v] = kEsc;
+  __syncthreads();
+  if (threadIdx.x < *nsel) code_of[dict[threadIdx.x]] = uint8_t(threadIdx.x);
+  __syncthreads();
+}
+
+template <int W>
+__global__ void __launch_bounds__(kThreads)
+hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+            FrameMeta* __restrict__ meta) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint8_t dict[16];
+  __shared__ uint8_t code_of[256];
+  __shared__ int nsel;
+  __shared__ int red[4];
+  const uint64_t f = blockIdx.x;
+  const uint64_t base = f * frame_bytes;
+  const uint64_t len = min(uint64_t(frame_bytes), logical - base);
+  const uint64_t n = len / W;
+  const uint8_t* s = src + base;
+  for (int v = threadIdx.x; v < 256; v += kThreads) hist[v] = 0;
+  __syncthreads();
+  const uint64_t stride = n / kSample > 0 ? n / kSample : 1;
+  for (int i = threadIdx.x; i < kSample; i += kThreads) {
+    const uint64_t idx = uint64_t(i) * stride;
+    if (idx < n) atomicAdd(&hist[s[idx * W + W - 1]], 1u);
+  }
+  __syncthreads();
+  build_dict(hist, dict, code_of, &nsel);
+  int esc = 0;
+  if (((reinterpret_cast<uintptr_t>(s)) & 15) == 0) {
+    const uint64_t nv = (n * W) / 16;  // whole 16-B vectors of elements
+    const uint4* sv = reinterpret_cast<const uint4*>(s);
+    for (uint64_t i = threadIdx.x; i < nv; i += kThreads) {
+      const uint4 v = sv[i];
+      const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int p = W - 1; p < 16; p += W) esc += code_of[(wd[p >> 2] >> (8 * (p & 3))) & 255] == kEsc;
+    }
+    for (uint64_t e = nv * 16 / W + threadIdx.x; e < n; e += kThreads)
+      esc += code_of[s[e * W + W - 1]] == kEsc;
+  } else {
+    for (uint64_t e = threadIdx.x; e < n; e += kThreads) esc += code_of[s[e * W + W - 1]] == kEsc;
+  }
+  const int total = block_sum(esc, red);
+  if (threadIdx.x == 0) {
+    const uint64_t coded = kFrameHeader + (n + 1) / 2 + uint64_t(W - 1) * n + total + (len - n * W);
+    const uint64_t raw = kFrameHeader + len;
+    FrameMeta m;
+    m.mode = (total <= kMaxEsc && coded < raw && n > 0) ? 1 : 0;
+    m.n_esc = m.mode ? total : 0;
+    m.nsel = m.mode ? nsel : 0;
+    m.pad = 0;
+    for (int j = 0; j < 16; ++j) m.dict[j] = m.mode ? dict[j] : 0;
+    m.size = align16(m.mode ? coded : raw);
+    m.offset = 0;
+    meta[f] = m;
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+hsz_layout(FrameMeta* __restrict__ meta, uint32_t n_frames, uint8_t* __restrict__ out,
+           uint64_t logical, uint32_t w, uint32_t frame_bytes, uint64_t* __restrict__ total) {
+  __shared__ uint64_t part[1024];
+  __shared__ uint64_t carry;
+  const uint64_t start = align16(kHeader + 8ull * (n_frames + 1));
+  if (threadIdx.x == 0) carry = start;
+  __syncthreads();
+  uint64_t* table = reinterpret_cast<uint64_t*>(out + kHeader);
+  for (uint32_t c = 0; c < n_frames; c += 1024) {
+    const uint32_t i = c + threadIdx.x;
+    const uint64_t v = i < n_frames ? meta[i].size : 0;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+      const uint64_t add = threadIdx.x >= uint32_t(o) ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += add;
+      __syncthreads();
+    }
+    if (i < n_frames) {
+      const uint64_t off = carry + part[threadIdx.x] - v;
+      meta[i].offset = off;
+      table[i] = off;
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    table[n_frames] = carry;
+    *total = carry;
+    uint32_t* h32 = reinterpret_cast<uint32_t*>(out);
+    h32[0] = 0x315a5348u;  // "HSZ1"
+    h32[1] = 1;
+    *reinterpret_cast<uint64_t*>(out + 8) = logical;
+    h32[4] = w;
+    h32[5] = frame_bytes;
+    h32[6] = n_frames;
+    for (int j = 7; j < 16; ++j) h32[j] = 0;
+    for (uint64_t p = kHeader + 8ull * (n_frames + 1); p < start; ++p) out[p] = 0;
+  }
+}
+
+// Writes frame f's escape values in element order: entries (idx, value) were
+// appended in arbitrary order; each one's rank = #entries with a smaller idx.
+__device__ void write_escapes(const uint32_t* eidx, const uint8_t* evals, int n_esc,
+                              uint8_t* dst) {
+  for (int i = threadIdx.x; i < n_esc; i += kThreads) {
+    const uint32_t me = eidx[i];
+    int rank = 0;
+    for (int j = 0; j < n_esc; ++j) rank += eidx[j] < me;
+    dst[rank] = evals[i];
+  }
+}
+
+template <int W>
+__global__ void __launch_bounds__(kThreads)
+hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+           const FrameMeta* __restrict__ meta, uint8_t* __restrict__ out) {
+  __shared__ uint8_t code_of[256];
+  __shared__ uint32_t eidx[kMaxEsc];
+  __shared__ uint8_t evals[kMaxEsc];
+  __shared__ int ecount;
+  const uint64_t f = blockIdx.x;
+  const uint64_t base = f * frame_bytes;
+  const uint64_t len = min(uint64_t(frame_bytes), logical - base);
+  const uint64_t n = len / W;
+  const uint8_t* s = src + base;
+  const FrameMeta m = meta[f];
+  uint8_t* fr = out + m.offset;
+  if (threadIdx.x < kFrameHeader) {
+    uint8_t b = 0;
+    const int t = threadIdx.x;
+    if (t == 0) b = uint8_t(m.mode);
+    else if (t >= 4 && t < 8) b = uint8_t(m.n_esc >> (8 * (t - 4)));
+    else if (t >= 8 && t < 24) b = m.dict[t - 8];
+    fr[t] = b;
+  }
+  uint8_t* body = fr + kFrameHeader;
+  const uint64_t padded_end = m.size - kFrameHeader;  // body bytes incl. padding
+  if (m.mode == 0) {
+    if ((((reinterpret_cast<uintptr_t>(s)) | reinterpret_cast<uintptr_t>(body)) & 15) == 0) {
+      const uint64_t nv = len / 16;
+      const uint4* sv = reinterpret_cast<const uint4*>(s);
+      uint4* dv = reinterpret_cast<uint4*>(body);
+      for (uint64_t i = threadIdx.x; i < nv; i += kThreads) dv[i] = sv[i];
+      for (uint64_t j = nv * 16 + threadIdx.x; j < padded_end; j += kThreads)
+        body[j] = j < len ? s[j] : 0;
+    } else {
+      for (uint64_t j = threadIdx.x; j < padded_end; j += kThreads) body[j] = j < len ? s[j] : 0;
+    }
+    return;
+  }
+  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[v] = kEsc;
+  if (threadIdx.x == 0) ecount = 0;
+  __syncthreads();
+  if (threadIdx.x < m.nsel) code_of[m.dict[threadIdx.x]] = uint8_t(threadIdx.x);
+  __syncthreads();
+  uint8_t* nib = body;
+  const uint64_t nb = (n + 1) / 2;
+  uint8_t* lo = body + nb;
+  uint8_t* escp = lo + uint64_t(W - 1) * n;
+  const bool fast = (reinterpret_cast<uintptr_t>(s) & 15) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(nib) | reinterpret_cast<uintptr_t>(lo)) & 7) == 0 &&
+                    (n % 8) == 0;
+  uint64_t done = 0;
+  if (fast && W == 2) {
+    // 8 elements (16 B) per lane per step -> 4 B of nibbles + 8 B of low bytes
+    const uint64_t groups = n / 8;
+    const uint4* sv = reinterpret_cast<const uint4*>(s);
+    uint32_t* nv = reinterpret_cast<uint32_t*>(nib);
+    uint64_t* lv = reinterpret_cast<uint64_t*>(lo);
+    for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+      const uint4 v = sv[g];
+      const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+      uint32_t codes = 0;
+      uint64_t lob = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = q * 2 + h;
+          const uint32_t hi = (wd[q] >> (16 * h + 8)) & 255;
+          const uint32_t c = code_of[hi];
+          codes |= c << (4 * e);
+          lob |= uint64_t((wd[q] >> (16 * h)) & 255) << (8 * e);
+          if (c == kEsc) {
+            const int k = atomicAdd(&ecount, 1);
+            if (k < kMaxEsc) { eidx[k] = uint32_t(g * 8 + e); evals[k] = uint8_t(hi); }
+          }
+        }
+      }
+      nv[g] = codes;
+      lv[g] = lob;
+    }
+    done = n;
+  } else if (fast && W == 4) {
+    const uint64_t groups = n / 8;  // 32 B in, 4 B nibbles + 24 B low bytes
+    const uint4* sv = reinterpret_cast<const uint4*>(s);
+    uint32_t* nv = reinterpret_cast<uint32_t*>(nib);
+    for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+      const uint4 a = sv[2 * g], b = sv[2 * g + 1];
+      const uint32_t wd[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      uint32_t codes = 0;
+      uint8_t lob[24];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t hi = wd[e] >> 24;
+        const uint32_t c = code_of[hi];
+        codes |= c << (4 * e);
+        lob[3 * e] = wd[e] & 255;
+        lob[3 * e + 1] = (wd[e] >> 8) & 255;
+        lob[3 * e + 2] = (wd[e] >> 16) & 255;
+        if (c == kEsc) {
+          const int k = atomicAdd(&ecount, 1);
+          if (k < kMaxEsc) { eidx[k] = uint32_t(g * 8 + e); evals[k] = uint8_t(hi); }
+        }
+      }
+      nv[g] = codes;
+      uint64_t* lv = reinterpret_cast<uint64_t*>(lo + 24 * g);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int b8 = 0; b8 < 8; ++b8) x |= uint64_t(lob[8 * q + b8]) << (8 * b8);
+        lv[q] = x;
+      }
+    }
+    done = n;
+  }
+  if (done < n) {
+    // generic path: one element pair per lane step (partial / unaligned frames)
+    for (uint64_t p = threadIdx.x; p < nb; p += kThreads) {
+      uint8_t byte = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t e = 2 * p + h;
+        if (e >= n) break;
+        const uint8_t* el = s + e * W;
+        const uint32_t hi = el[W - 1];
+        const uint32_t c = code_of[hi];
+        byte |= uint8_t(c << (4 * h));
+        for (int b = 0; b < W - 1; ++b) lo[e * (W - 1) + b] = el[b];
+        if (c == kEsc) {
+          const int k = atomicAdd(&ecount, 1);
+          if (k < kMaxEsc) { eidx[k] = uint32_t(e); evals[k] = uint8_t(hi); }
+        }
+      }
+      nib[p] = byte;
+    }
+  }
+  __syncthreads();
+  write_escapes(eidx, evals, min(ecount, kMaxEsc), escp);
+  // tail bytes + zero padding
+  uint8_t* tail = escp + m.n_esc;
+  const uint64_t tail_len = len - n * W;
+  const uint64_t used = uint64_t(tail - body);
+  for (uint64_t j = threadIdx.x; used + j < padded_end; j += kThreads)
+    tail[j] = j < tail_len ? s[n * W + j] : 0;
+}
+
+template <int W>
+__global__ void __launch_bounds__(kThreads)
+hsz_decode(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+           uint32_t first_frame, uint64_t logical, uint32_t frame_bytes,
+           uint8_t* __restrict__ out) {
+  __shared__ uint32_t eidx[kMaxEsc];
+  __shared__ uint32_t sorted[kMaxEsc];
+  __shared__ int ecount;
+  __shared__ uint8_t dict[16];
+  const uint64_t fl = blockIdx.x;             // local frame index
+  const uint64_t f = first_frame + fl;         // global frame index
+  const uint64_t base = f * frame_bytes;
+  const uint64_t len = min(uint64_t(frame_bytes), logical - base);
+  const uint64_t n = len / W;
+  const uint8_t* fr = frames + offsets[fl];
+  uint8_t* o = out + fl * uint64_t(frame_bytes);
+  const int mode = fr[0];
+  const uint8_t* body = fr + kFrameHeader;
+  if (mode == 0) {
+    if ((((reinterpret_cast<uintptr_t>(o)) | reinterpret_cast<uintptr_t>(body)) & 15) == 0) {
+      const uint64_t nv = len / 16;
+      const uint4* sv = reinterpret_cast<const uint4*>(body);
+      uint4* dv = reinterpret_cast<uint4*>(o);
+      for (uint64_t i = threadIdx.x; i < nv; i += kThreads) dv[i] = sv[i];
+      for (uint64_t j = nv * 16 + threadIdx.x; j < len; j += kThreads) o[j] = body[j];
+    } else {
+      for (uint64_t j = threadIdx.x; j < len; j += kThreads) o[j] = body[j];
+    }
+    return;
+  }
+  const uint32_t n_esc = *reinterpret_cast<const uint32_t*>(fr + 4);
+  if (threadIdx.x < 16) dict[threadIdx.x] = fr[8 + threadIdx.x];
+  if (threadIdx.x == 0) ecount = 0;
+  __syncthreads();
+  const uint64_t nb = (n + 1) / 2;
+  const uint8_t* nib = body;
+  const uint8_t* lo = body + nb;
+  const uint8_t* escv = lo + uint64_t(W - 1) * n;
+  if (n_esc > 0) {
+    // collect escape element indices (nibble value 15), then sort them by rank
+    for (uint64_t p = threadIdx.x; p < nb; p += kThreads) {
+      const uint8_t b = nib[p];
+      if ((b & 15) == kEsc && 2 * p < n) {
+        const int k = atomicAdd(&ecount, 1);
+        if (k < kMaxEsc) eidx[k] = uint32_t(2 * p);
+      }
+      if ((b >> 4) == kEsc && 2 * p + 1 < n) {
+        const int k = atomicAdd(&ecount, 1);
+        if (k < kMaxEsc) eidx[k] = uint32_t(2 * p + 1);
+      }
+    }
+    __syncthreads();
+    const int ne = min(ecount, kMaxEsc);
+    for (int i = threadIdx.x; i < ne; i += kThreads) {
+      const uint32_t me = eidx[i];
+      int rank = 0;
+      for (int j = 0; j < ne; ++j) rank += eidx[j] < me;
+      sorted[rank] = me;
+    }
+    __syncthreads();
+  }
+  const int n_found = min(min(ecount, kMaxEsc), int(n_esc));
+  auto esc_value = [&](uint32_t e) -> uint8_t {
+    int lo_i = 0, hi_i = n_found - 1;
+    if (hi_i < 0) return 0;
+    while (lo_i < hi_i) {
+      const int mid = (lo_i + hi_i) >> 1;
+      if (sorted[mid] < e) lo_i = mid + 1; else hi_i = mid;
+    }
+    return escv[lo_i];
+  };
+  const bool fast = (reinterpret_cast<uintptr_t>(o) & 15) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(nib) | reinterpret_cast<uintptr_t>(lo)) & 7) == 0 &&
+                    (n % 8) == 0;
+  uint64_t done = 0;
+  if (fast && W == 2) {
+    const uint64_t groups = n / 8;
+    const uint32_t* nv = reinterpret_cast<const uint32_t*>(nib);
+    const uint64_t* lv = reinterpret_cast<const uint64_t*>(lo);
+    uint4* ov = reinterpret_cast<uint4*>(o);
+    for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+      const uint32_t codes = nv[g];
+      const uint64_t lob = lv[g];
+      uint32_t wd[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = q * 2 + h;
+          const uint32_t c = (codes >> (4 * e)) & 15;
+          const uint32_t hi = c == kEsc ? esc_value(uint32_t(g * 8 + e)) : dict[c];
+          x |= ((uint32_t((lob >> (8 * e)) & 255)) | (hi << 8)) << (16 * h);
+        }
+        wd[q] = x;
+      }
+      ov[g] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    }
+    done = n;
+  } else if (fast && W == 4) {
+    const uint64_t groups = n / 8;
+    const uint32_t* nv = reinterpret_cast<const uint32_t*>(nib);
+    uint4* ov = reinterpret_cast<uint4*>(o);
+    for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+      const uint32_t codes = nv[g];
+      const uint64_t* lv = reinterpret_cast<const uint64_t*>(lo + 24 * g);
+      const uint64_t l0 = lv[0], l1 = lv[1], l2 = lv[2];
+      uint32_t wd[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t c = (codes >> (4 * e)) & 15;
+        const uint32_t hi = c == kEsc ? esc_value(uint32_t(g * 8 + e)) : dict[c];
+        uint32_t b[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int bi = 3 * e + k;
+          const uint64_t src = bi < 8 ? l0 : (bi < 16 ? l1 : l2);
+          b[k] = uint32_t((src >> (8 * (bi & 7))) & 255);
+        }
+        wd[e] = b[0] | (b[1] << 8) | (b[2] << 16) | (hi << 24);
+      }
+      ov[2 * g] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+      ov[2 * g + 1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+    }
+    done = n;
+  }
+  if (done < n) {
+    for (uint64_t e = threadIdx.x; e < n; e += kThreads) {
+      const uint32_t c = (nib[e >> 1] >> (4 * (e & 1))) & 15;
+      const uint8_t hi = c == kEsc ? esc_value(uint32_t(e)) : dict[c];
+      for (int b = 0; b < W - 1; ++b) o[e * W + b] = lo[e * (W - 1) + b];
+      o[e * W + W - 1] = hi;
+    }
+  }
+  const uint8_t* tail = escv + n_esc;
+  for (uint64_t j = threadIdx.x; j < len - n * W; j += kThreads) o[n * W + j] = tail[j];
+}
+
+thread_local char g_hsz_err[256];
+
+int fail(const char* what, hipError_t e) {
+  snprintf(g_hsz_err, sizeof(g_hsz_err), "%s: %s", what, hipGetErrorString(e));
+  return -static_cast<int>(e) - 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hsg_hsz_last_error() { return g_hsz_err; }
+
+uint64_t hsg_hsz_meta_bytes(uint32_t n_frames) { return uint64_t(n_frames) * sizeof(FrameMeta); }
+
+// Encode `logical` bytes at device `src` (16-B aligned) into device `out`
+// (capacity >= max_encoded_bytes).  `meta` = device scratch of
+// hsg_hsz_meta_bytes(n_frames); `total` = device u64 receiving the blob size.
+// Everything is enqueued on `stream`; nothing synchronises.
+int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t frame_bytes,
+                   void* out, void* meta, void* total, void* stream) {
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return fail("hipSetDevice", e);
+  if (frame_bytes % 16 || frame_bytes % w) return -1000;
+  const uint32_t nf = logical ? uint32_t((logical + frame_bytes - 1) / frame_bytes) : 1;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto* src8 = static_cast<const uint8_t*>(src);
+  auto* m = static_cast<FrameMeta*>(meta);
+  auto* o = static_cast<uint8_t*>(out);
+  switch (w) {
+    case 1: hipLaunchKernelGGL(hsz_analyze<1>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m); break;
+    case 2: hipLaunchKernelGGL(hsz_analyze<2>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m); break;
+    case 4: hipLaunchKernelGGL(hsz_analyze<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m); break;
+    case 8: hipLaunchKernelGGL(hsz_analyze<8>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m); break;
+    default: return -1001;
+  }
+  hipLaunchKernelGGL(hsz_layout, dim3(1), dim3(1024), 0, s, m, nf, o, logical, uint32_t(w),
+                     frame_bytes, static_cast<uint64_t*>(total));
+  switch (w) {
+    case 1: hipLaunchKernelGGL(hsz_encode<1>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
+    case 2: hipLaunchKernelGGL(hsz_encode<2>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
+    case 4: hipLaunchKernelGGL(hsz_encode<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
+    default: hipLaunchKernelGGL(hsz_encode<8>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
+  }
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail("hsz encode launch", e);
+}
+
+// Decode `count` frames starting at global frame `first` into `out` (logical
+// bytes of those frames).  `offsets` (device, count entries) are byte offsets
+// of each frame relative to `frames`.
+int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t first,
+                   uint32_t count, uint64_t logical, int w, uint32_t frame_bytes, void* out,
+                   void* stream) {
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return fail("hipSetDevice", e);
+  if (count == 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto* fr = static_cast<const uint8_t*>(frames);
+  auto* off = static_cast<const uint64_t*>(offsets);
+  auto* o = static_cast<uint8_t*>(out);
+  switch (w) {
+    case 1: hipLaunchKernelGGL(hsz_decode<1>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
+    case 2: hipLaunchKernelGGL(hsz_decode<2>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
+    case 4: hipLaunchKernelGGL(hsz_decode<4>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
+    case 8: hipLaunchKernelGGL(hsz_decode<8>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
+    default: return -1001;
+  }
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail("hsz decode launch", e);
+}
+
+}  // extern "C"

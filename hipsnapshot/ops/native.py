@@ -79,6 +79,12 @@ def hsio() -> ctypes.CDLL:
             _declare(lib, "hsio_alloc_aligned", c_void_p, [c_uint64])
             _declare(lib, "hsio_free_aligned", None, [c_void_p])
             _declare(lib, "hsio_parallel_memcpy", None, [c_void_p, c_void_p, c_uint64, c_int])
+            _declare(lib, "hsz_max_encoded_bytes", c_uint64, [c_uint64, ctypes.c_uint32])
+            _declare(lib, "hsz_encode_cpu", c_int64,
+                     [c_void_p, c_uint64, c_int, ctypes.c_uint32, c_void_p, c_int])
+            _declare(lib, "hsz_decode_cpu", c_int,
+                     [c_void_p, c_void_p, ctypes.c_uint32, ctypes.c_uint32, c_uint64, c_int,
+                      ctypes.c_uint32, c_void_p, c_int])
             _hsio_lib = lib
     return _hsio_lib
 
@@ -222,6 +228,14 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
+        _declare(lib, "hsg_hsz_last_error", c_char_p, [])
+        _declare(lib, "hsg_hsz_meta_bytes", c_uint64, [ctypes.c_uint32])
+        _declare(lib, "hsg_hsz_encode", c_int,
+                 [c_int, c_void_p, c_uint64, c_int, ctypes.c_uint32, c_void_p, c_void_p,
+                  c_void_p, c_void_p])
+        _declare(lib, "hsg_hsz_decode", c_int,
+                 [c_int, c_void_p, c_void_p, ctypes.c_uint32, ctypes.c_uint32, c_uint64, c_int,
+                  ctypes.c_uint32, c_void_p, c_void_p])
         if lib.hsg_desc_size() != COPY_DESC_DTYPE.itemsize:
             _hsgpu_error = (f"CopyDesc layout mismatch: native {lib.hsg_desc_size()} "
                             f"vs python {COPY_DESC_DTYPE.itemsize}")
@@ -551,3 +565,52 @@ def is_managed_ptr(ptr: int) -> bool:
     if lib is None or not gpu_available():
         return False
     return bool(lib.hsg_is_managed(ptr))
+
+
+# ---- HSZ1 lossless codec (format: ops/codec.py) ---------------------------------
+
+def hsz_encode_cpu(src_addr: int, logical: int, w: int, frame_bytes: int, out_addr: int,
+                   nthreads: int = 8) -> int:
+    r = hsio().hsz_encode_cpu(src_addr, logical, w, frame_bytes, out_addr, nthreads)
+    if r < 0:
+        raise RuntimeError(f"hsz_encode_cpu failed ({r})")
+    return int(r)
+
+
+def hsz_decode_cpu(frames_addr: int, offsets_addr: int, first: int, count: int, logical: int,
+                   w: int, frame_bytes: int, out_addr: int, nthreads: int = 8) -> None:
+    r = hsio().hsz_decode_cpu(frames_addr, offsets_addr, first, count, logical, w, frame_bytes,
+                              out_addr, nthreads)
+    if r != 0:
+        raise RuntimeError(f"hsz_decode_cpu failed ({r})")
+
+
+def hsz_max_encoded_bytes(logical: int, frame_bytes: int) -> int:
+    return int(hsio().hsz_max_encoded_bytes(logical, frame_bytes))
+
+
+def _hsz_check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = require_gpu_lib().hsg_hsz_last_error().decode()
+        raise HipError(f"{what} failed ({rc}): {msg}")
+
+
+def hsz_meta_bytes(n_frames: int) -> int:
+    return int(require_gpu_lib().hsg_hsz_meta_bytes(n_frames))
+
+
+def hsz_encode_gpu(dev: int, src_addr: int, logical: int, w: int, frame_bytes: int,
+                   out_addr: int, meta_addr: int, total_addr: int, stream_handle: int) -> None:
+    """Enqueue the 3 encode kernels on ``stream_handle`` (no synchronisation)."""
+    assert src_addr % 16 == 0 and out_addr % 16 == 0, "HSZ1 buffers must be 16-B aligned"
+    _hsz_check(require_gpu_lib().hsg_hsz_encode(dev, src_addr, logical, w, frame_bytes,
+                                                out_addr, meta_addr, total_addr, stream_handle),
+               "hsg_hsz_encode")
+
+
+def hsz_decode_gpu(dev: int, frames_addr: int, offsets_addr: int, first: int, count: int,
+                   logical: int, w: int, frame_bytes: int, out_addr: int,
+                   stream_handle: int) -> None:
+    _hsz_check(require_gpu_lib().hsg_hsz_decode(dev, frames_addr, offsets_addr, first, count,
+                                                logical, w, frame_bytes, out_addr,
+                                                stream_handle), "hsg_hsz_decode")

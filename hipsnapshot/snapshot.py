@@ -176,6 +176,7 @@ class Snapshot:
             loop.close()
             raise
         TakeStats.last = {"unblock_s": time.monotonic() - t0}
+        timeline.dump("async_take", comm.get_rank())
         return PendingSnapshot(path=path, pending_io_work=pending, comm=comm, metadata=metadata,
                                storage=storage, event_loop=loop, storage_options=storage_options,
                                nonce=nonce)

@@ -30,6 +30,13 @@ def union(intervals):
 def main():
     for f in sys.argv[1:]:
         ev = json.load(open(f))["traceEvents"]
+        # keep the window of this operation's top-level phases (a background
+        # async drain may have recorded spans into the same buffer)
+        top = [e for e in ev if e["cat"] == "phase" and e["name"] in
+               ("coalesce", "load_stateful")]
+        if top:
+            lo = min(e["ts"] for e in top)
+            ev = [e for e in ev if e["ts"] >= lo]
         t0 = min(e["ts"] for e in ev)
         print(f"== {f}")
         for e in ev:

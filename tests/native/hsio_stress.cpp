@@ -22,6 +22,10 @@ int64_t hsio_write_sync(void*, const char*, const void*, uint64_t, uint64_t, int
 int64_t hsio_read_sync(void*, const char*, void*, uint64_t, uint64_t, int);
 void hsio_parallel_memcpy(void*, const void*, uint64_t, int);
 void hsio_set_read_split(void*, uint64_t);
+uint64_t hsz_max_encoded_bytes(uint64_t, uint32_t);
+int64_t hsz_encode_cpu(const void*, uint64_t, int, uint32_t, void*, int);
+int hsz_decode_cpu(const void*, const uint64_t*, uint32_t, uint32_t, uint64_t, int, uint32_t,
+                   void*, int);
 }
 
 int main(int argc, char** argv) {
@@ -88,6 +92,26 @@ int main(int argc, char** argv) {
   }
   for (int i = 0; i < kFiles; ++i)
     if (std::memcmp(backs[i].data(), bufs[i].data(), bufs[i].size())) { std::fprintf(stderr, "split mismatch %d\n", i); return 1; }
+  // HSZ1 codec round trip, multi-threaded, odd length + all element widths
+  for (int w : {1, 2, 4, 8}) {
+    const uint64_t n = (3u << 20) + 13;
+    std::vector<uint8_t> src(n);
+    uint32_t x = 12345;
+    for (uint64_t i = 0; i < n; ++i) {
+      x = x * 1103515245u + 12345u;
+      src[i] = (i % w == uint64_t(w - 1)) ? uint8_t(60 + ((x >> 16) % 5)) : uint8_t(x >> 24);
+    }
+    std::vector<uint8_t> enc(hsz_max_encoded_bytes(n, 65536));
+    int64_t sz = hsz_encode_cpu(src.data(), n, w, 65536, enc.data(), 8);
+    if (sz <= 0 || uint64_t(sz) > enc.size()) { std::fprintf(stderr, "encode w=%d: %lld\n", w, (long long)sz); return 1; }
+    uint32_t nf;
+    std::memcpy(&nf, enc.data() + 24, 4);
+    std::vector<uint64_t> offs(nf + 1);
+    std::memcpy(offs.data(), enc.data() + 64, 8 * (nf + 1));
+    std::vector<uint8_t> dec(n);
+    if (hsz_decode_cpu(enc.data(), offs.data(), 0, nf, n, w, 65536, dec.data(), 8) != 0 ||
+        std::memcmp(dec.data(), src.data(), n)) { std::fprintf(stderr, "decode w=%d\n", w); return 1; }
+  }
   std::vector<char> a(64 << 20, 7), b(64 << 20, 0);
   hsio_parallel_memcpy(b.data(), a.data(), a.size(), 8);
   if (std::memcmp(a.data(), b.data(), a.size())) return 1;

@@ -329,3 +329,65 @@ def test_multirank_gpu_tensors_gloo(gpu, tmp_path, save_ws, load_ws):
     p = str(tmp_path / "mr")
     run_distributed(_multirank_gpu_worker, save_ws, p, "save", backend="gloo")
     run_distributed(_multirank_gpu_worker, load_ws, p, "load", backend="gloo")
+
+
+# ---- HSZ1 lossless codec kernels ------------------------------------------------
+
+def _codec_inputs():
+    g = torch.Generator().manual_seed(7)
+    w_bf16 = (torch.randn(3_000_001, generator=g) * 0.02).to(torch.bfloat16)
+    rnd = torch.randint(0, 256, (200_003,), dtype=torch.uint8, generator=g)
+    # escapes in every frame: 14 common high bytes + a sprinkle of rare ones
+    hi = torch.randint(60, 74, (400_000,), dtype=torch.uint8, generator=g)
+    hi[::997] = torch.randint(0, 256, (hi[::997].numel(),), dtype=torch.uint8, generator=g)
+    esc = torch.stack([torch.randint(0, 256, (400_000,), dtype=torch.uint8, generator=g), hi],
+                      1).reshape(-1)
+    return {"bf16": w_bf16.view(torch.uint8), "random": rnd, "escapes": esc,
+            "fp32": (torch.randn(500_000, generator=g) * 1e-3).view(torch.uint8)}
+
+
+@pytest.mark.parametrize("w", [1, 2, 4, 8])
+@pytest.mark.parametrize("kind", ["bf16", "random", "escapes", "fp32"])
+def test_hsz_encode_gpu_bit_exact_vs_reference(gpu, w, kind):
+    from hipsnapshot.ops import codec
+
+    host = _codec_inputs()[kind]
+    for n in (host.numel(), host.numel() - 7, 4096 * 16 + 3):
+        h = host[:n].contiguous()
+        ref = codec.encode_reference(h.numpy().tobytes(), w, 64 * 1024)
+        d = h.to(gpu)
+        s = torch.cuda.current_stream()
+        out, total, _ = codec.encode_device(d, w, int(s.cuda_stream), 64 * 1024)
+        s.synchronize()
+        nb = int(total.item())
+        assert nb == len(ref), (kind, w, n)
+        assert out[:nb].cpu().numpy().tobytes() == ref, (kind, w, n)
+        # GPU decode of the whole blob and of a middle frame range
+        hdr = codec.parse_header(ref)
+        back = torch.empty(n, dtype=torch.uint8, device=gpu)
+        codec.decode_device_into(out[:nb], hdr, back, int(s.cuda_stream))
+        assert torch.equal(back.cpu(), h), (kind, w, n)
+        if hdr.n_frames >= 3:
+            lo, _ = hdr.frame_range(1)
+            _, hi_ = hdr.frame_range(2)
+            part = torch.empty(hi_ - lo, dtype=torch.uint8, device=gpu)
+            base = hdr.offsets[1]
+            codec.decode_device_into(out[base:nb], hdr, part, int(s.cuda_stream), first=1,
+                                     count=2, blob_base=base)
+            assert torch.equal(part.cpu(), h[lo:hi_])
+
+
+def test_hsz_gpu_large_blob_ratio(gpu):
+    from hipsnapshot.ops import codec
+
+    x = (torch.randn(64 << 20, device=gpu) / 64).to(torch.bfloat16)  # 128 MiB
+    s = torch.cuda.current_stream()
+    out, total, _ = codec.encode_device(x.view(torch.uint8), 2, int(s.cuda_stream))
+    s.synchronize()
+    nb = int(total.item())
+    assert 0.74 < nb / (x.numel() * 2) < 0.77
+    nf = codec.n_frames_for(x.numel() * 2, codec.DEFAULT_FRAME_BYTES)
+    hdr = codec.parse_header(out[:codec.payload_start(nf)].cpu().numpy().tobytes())
+    back = torch.empty_like(x)
+    codec.decode_device_into(out[:nb], hdr, back.view(torch.uint8), int(s.cuda_stream))
+    assert torch.equal(back.view(torch.int16), x.view(torch.int16))

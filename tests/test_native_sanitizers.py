@@ -14,6 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = [os.path.join(ROOT, "hipsnapshot", "csrc", "hsio.cpp"),
+       os.path.join(ROOT, "hipsnapshot", "csrc", "hsz_cpu.cpp"),
        os.path.join(ROOT, "tests", "native", "hsio_stress.cpp")]
 
 
