@@ -264,6 +264,9 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                             io_concurrency: Optional[int] = None) -> PipelineStats:
     consume_threads = consume_threads or knobs.get_stage_threads()
     io_concurrency = io_concurrency or knobs.get_io_threads()
+    # reads are split across all I/O workers by the native engine, so a few
+    # whole-blob reads in flight saturate it; more would only pin more memory
+    max_inflight = knobs.get_read_inflight()
     executor = ThreadPoolExecutor(max_workers=consume_threads,
                                   thread_name_prefix=f"hipsnapshot-consume-{rank}")
     stats = PipelineStats()
@@ -273,12 +276,53 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
     inflight: set = set()
     io_sem = asyncio.Semaphore(io_concurrency)
 
+    async def _one_compressed(rr: ReadReq) -> None:
+        from ..ops import codec as hsz
+        from ..io_types import CompressedSpan
+
+        info = rr.codec
+        nf = hsz.n_frames_for(int(info["blob_bytes"]), int(info["frame_bytes"]))
+        async with io_sem:
+            t_r = time.perf_counter()
+            head_io = ReadIO(path=rr.path, byte_range=(0, hsz.payload_start(nf)))
+            await storage.read(head_io)
+            header = hsz.parse_header(head_io.data())
+            lo, hi = rr.byte_range if rr.byte_range is not None else (0, header.logical_size)
+            first, last = header.frames_covering(lo, hi)
+            c_lo, c_hi = header.offsets[first], header.offsets[last]
+            hsz.validate_offsets(header, header.offsets[-1])
+            dest = await asyncio.get_running_loop().run_in_executor(
+                None, rr.buffer_consumer.get_compressed_read_dest, c_hi - c_lo)
+            if dest is None:
+                dest = as_staged(bytearray(max(c_hi - c_lo, 1)))
+            body_io = ReadIO(path=rr.path, byte_range=(c_lo, c_hi), dest=dest)
+            if c_hi > c_lo:
+                await storage.read(body_io)
+            t_c = time.perf_counter()
+        span = CompressedSpan(dest, header, first, last, lo, hi)
+        timeline.add("read", "io", t_r, t_c, path=rr.path, bytes=c_hi - c_lo, logical=hi - lo)
+        stats.bytes_written += hi - lo
+        try:
+            await rr.buffer_consumer.consume_buffer(span, executor)
+        finally:
+            span.release()
+        timeline.add("consume", "stage", t_c, time.perf_counter(), path=rr.path, bytes=hi - lo)
+
     async def _one(rr: ReadReq, cost: int) -> None:
+        if rr.codec is not None:
+            try:
+                await _one_compressed(rr)
+            finally:
+                in_use[0] -= cost
+            return
         dest = None
         try:
             nbytes = _expected_read_bytes(rr)
             if nbytes is not None:
-                dest = rr.buffer_consumer.get_read_dest(nbytes)
+                # pinned-pool misses cost a hipHostMalloc: keep them off the
+                # event loop so completions of earlier reads are not delayed
+                dest = await asyncio.get_running_loop().run_in_executor(
+                    None, rr.buffer_consumer.get_read_dest, nbytes)
             read_io = ReadIO(path=rr.path, byte_range=rr.byte_range, dest=dest)
             async with io_sem:
                 t_r = time.perf_counter()
@@ -298,7 +342,7 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
 
     try:
         while pending or inflight:
-            while pending and len(inflight) < 2 * io_concurrency:
+            while pending and len(inflight) < max_inflight:
                 cost = pending[0].buffer_consumer.get_consuming_cost_bytes()
                 if in_use[0] + cost > memory_budget_bytes and inflight:
                     break

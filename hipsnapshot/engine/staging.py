@@ -25,6 +25,7 @@ import threading
 import time
 from typing import List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from ..format.serialization import contiguous_cpu_bytes_view, tensor_from_bytes
@@ -71,8 +72,14 @@ def _elem_strides_ok(t: torch.Tensor) -> bool:
     return t.dim() <= native.MAX_DIMS
 
 
-def d2h_tensor(t: torch.Tensor, producer: int) -> StagedBuffer:
-    """Copy a CUDA tensor's logical bytes (C order) into a pinned block."""
+def d2h_tensor(t: torch.Tensor, producer: int, codec: Optional[dict] = None) -> StagedBuffer:
+    """Copy a CUDA tensor's logical bytes (C order) into a pinned block.
+
+    With ``codec`` (HSZ1 info dict) the bytes are compressed on the GPU first
+    and only the encoded blob crosses PCIe.
+    """
+    if codec is not None:
+        return _d2h_encoded(t, producer, codec)
     nbytes = t.numel() * t.element_size()
     pb, staged = _pinned_staged(nbytes)
     if nbytes == 0:
@@ -96,6 +103,115 @@ def d2h_tensor(t: torch.Tensor, producer: int) -> StagedBuffer:
         raise
     timeline.add("d2h", "d2h", t_s, time.perf_counter(), bytes=nbytes, slot=slot)
     return staged
+
+
+def _join_current_stream(dev: int, slot: int) -> None:
+    """Order the copy stream after the current stream: memory just handed out
+    by torch's caching allocator is only safe to use in that stream's order."""
+    native.memcpy(dev, slot, 0, 0, 0, native.D2H,
+                  int(torch.cuda.current_stream(dev).cuda_stream), sync=False)
+
+
+def _read_u64_device(dev: int, slot: int, addr: int) -> int:
+    pb = native.PinnedBuffer(8)
+    try:
+        native.memcpy(dev, slot, pb.ptr, addr, 8, native.D2H, None, sync=True)
+        return int(pb.as_tensor(8).view(torch.int64)[0])
+    finally:
+        pb.release()
+
+
+def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dict
+                           ) -> StagedBuffer:
+    """HSZ1-encode a contiguous device byte tensor on the copy stream, then
+    move only the encoded bytes to a pinned block (one small sync in between
+    to learn the encoded size)."""
+    from ..ops import codec as hsz
+
+    stream = native.copy_stream(dev, slot)
+    t_s = time.perf_counter()
+    try:
+        with torch.cuda.device(dev):
+            out, total, meta = hsz.encode_device(src_u8, int(codec["w"]), 0,
+                                                 int(codec["frame_bytes"]), launch=False)
+    except torch.cuda.OutOfMemoryError:
+        return _encode_on_host(dev, slot, src_u8, codec)
+    _join_current_stream(dev, slot)
+    hsz.launch_encode(src_u8, int(codec["w"]), stream, int(codec["frame_bytes"]), out, total,
+                      meta)
+    nbytes = _read_u64_device(dev, slot, total.data_ptr())
+    pb, staged = _pinned_staged(nbytes)
+    try:
+        native.memcpy(dev, slot, pb.ptr, out.data_ptr(), nbytes, native.D2H, None, sync=True)
+    except BaseException:
+        staged.release()
+        raise
+    del out, total, meta
+    timeline.add("encode_d2h", "d2h", t_s, time.perf_counter(), bytes=nbytes,
+                 logical=src_u8.numel(), slot=slot)
+    return staged
+
+
+def _encode_on_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dict) -> StagedBuffer:
+    """Fallback when HBM is short: raw D2H, then the C++ encoder."""
+    from ..ops import codec as hsz
+
+    n = src_u8.numel()
+    raw_pb = native.PinnedBuffer(max(n, 1))
+    try:
+        if n:
+            native.memcpy(dev, slot, raw_pb.ptr, src_u8.data_ptr(), n, native.D2H, None,
+                          sync=True)
+        return _encode_host_bytes(raw_pb.ptr, n, codec)
+    finally:
+        raw_pb.release()
+
+
+def encode_host_buffer(buf: StagedBuffer, codec: dict) -> StagedBuffer:
+    """C++ HSZ1 encode of host bytes (host tensors / host slabs)."""
+    return _encode_host_bytes(buf.addr, buf.nbytes, codec)
+
+
+def _encode_host_bytes(addr: int, n: int, codec: dict) -> StagedBuffer:
+    from ..ops import codec as hsz
+
+    cap = hsz.max_encoded_bytes(n, int(codec["frame_bytes"]))
+    if native.hsgpu_loaded() and native.gpu_available():
+        pb, staged = _pinned_staged(cap)
+        out_addr, view, release, keep = pb.ptr, pb.view, pb.release, pb
+    else:
+        arr = np.empty(cap, dtype=np.uint8)
+        out_addr, view, release, keep = arr.ctypes.data, memoryview(arr), None, arr
+    try:
+        used = native.hsz_encode_cpu(addr if n else out_addr, n, int(codec["w"]),
+                                     int(codec["frame_bytes"]), out_addr)
+    except BaseException:
+        if release is not None:
+            release()
+        raise
+    return StagedBuffer(view[:used], out_addr, release=release, keepalive=keep)
+
+
+def _d2h_encoded(t: torch.Tensor, producer: int, codec: dict) -> StagedBuffer:
+    dev = device_of(t)
+    slot = copy_slot()
+    native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer or None, sync=False)
+    nbytes = t.numel() * t.element_size()
+    if t.is_contiguous() and t.data_ptr() % 16 == 0:
+        src = torch.empty(0, dtype=torch.uint8, device=t.device).set_(
+            t.untyped_storage(), t.storage_offset() * t.element_size(), (nbytes,))
+    else:
+        src = torch.empty(nbytes, dtype=torch.uint8, device=t.device)
+        _join_current_stream(dev, slot)
+        if nbytes:
+            batch = native.CopyBatch()
+            batch.add(t.data_ptr(), t.dtype, t.stride(), src.data_ptr(), t.dtype,
+                      _contig_strides(t.shape), list(t.shape), t.element_size())
+            keep = batch.launch(dev, native.copy_stream(dev, slot), sync=False)
+            native.stream_sync(dev, slot)
+            if keep is not None:
+                keep[0].release()
+    return _encode_device_to_host(dev, slot, src, codec)
 
 
 def _contig_strides(shape: Sequence[int]) -> List[int]:
@@ -125,7 +241,8 @@ def cpu_tensor_bytes(t: torch.Tensor, copy: bool) -> StagedBuffer:
 
 
 def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int,
-                   producers: Sequence[int], via_device_slab: bool = True) -> StagedBuffer:
+                   producers: Sequence[int], via_device_slab: bool = True,
+                   codec: Optional[dict] = None) -> StagedBuffer:
     """Pack many CUDA tensors into one host slab: ``members`` = (tensor, offset).
 
     Default path: one ``hs_copy_nd`` launch gathers every member into a device
@@ -133,6 +250,8 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
     If the device slab cannot be allocated the kernel writes the members
     straight into host-mapped pinned memory instead.
     """
+    if codec is not None and members:
+        return _gather_encoded(members, total_bytes, producers, codec)
     pb, staged = _pinned_staged(total_bytes)
     if total_bytes == 0 or not members:
         return staged
@@ -147,6 +266,7 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
         if via_device_slab:
             try:
                 slab = torch.empty(total_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+                _join_current_stream(dev, slot)
             except torch.cuda.OutOfMemoryError:
                 slab = None
         base = slab.data_ptr() if slab is not None else pb.ptr
@@ -168,6 +288,37 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
     timeline.add("gather_d2h", "d2h", t_s, time.perf_counter(), bytes=total_bytes,
                  members=len(members), slot=slot)
     return staged
+
+
+def _gather_encoded(members, total_bytes: int, producers, codec: dict) -> StagedBuffer:
+    """Slab gather into HBM (one launch), HSZ1 encode, D2H of the encoded bytes."""
+    dev = device_of(members[0][0])
+    slot = copy_slot()
+    stream = native.copy_stream(dev, slot)
+    for producer in producers:
+        native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
+    try:
+        slab = torch.zeros(total_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+    except torch.cuda.OutOfMemoryError:
+        # no HBM for the slab: gather into host memory, encode on the CPU
+        raw = gather_to_host(members, total_bytes, producers, via_device_slab=False)
+        try:
+            return _encode_host_bytes(raw.addr, total_bytes, codec)
+        finally:
+            raw.release()
+    # the slab comes from torch's allocator on the current stream: make the
+    # copy stream wait for its zero-fill (padding bytes are encoded too)
+    _join_current_stream(dev, slot)
+    batch = native.CopyBatch()
+    for t, off in members:
+        batch.add(t.data_ptr(), t.dtype, t.stride(), slab.data_ptr() + off, t.dtype,
+                  _contig_strides(t.shape), list(t.shape), t.element_size())
+    keep = batch.launch(dev, stream, sync=False)
+    try:
+        return _encode_device_to_host(dev, slot, slab, codec)
+    finally:
+        if keep is not None:
+            keep[0].release()
 
 
 def h2d_into(dst: torch.Tensor, host_addr: int, nbytes: int, src_dtype: torch.dtype,
@@ -222,11 +373,19 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
         native.stream_sync(dev, slot)
         return
     scratch = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
+    _join_current_stream(dev, slot)
     native.memcpy(dev, slot, scratch.data_ptr(), host_addr, nbytes, native.H2D, None,
                   sync=False)
+    _copy_regions(scratch, kernel_regions, dev, slot)
+    del scratch
+
+
+def _copy_regions(scratch: torch.Tensor, regions, dev: int, slot: int) -> None:
+    """ONE copy/cast launch from the device buffer ``scratch`` (region offsets
+    are relative to it) into every destination view, then a stream sync."""
     batch = native.CopyBatch()
     fallbacks = []
-    for src_dtype, src_shape, off, narrows, dst in kernel_regions:
+    for src_dtype, src_shape, off, narrows, dst in regions:
         es = torch.empty(0, dtype=src_dtype).element_size()
         n = 1
         for z in src_shape:
@@ -249,7 +408,56 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
         for src, dst in fallbacks:
             dst.copy_(src)
         torch.cuda.synchronize(dev)
-    del scratch
+
+
+def scatter_compressed(span, regions, dev: int, producer: int = 0) -> None:
+    """HSZ1 restore into HBM: ONE H2D of the encoded frames, ONE decode launch,
+    then the same region copy as ``scatter_host_regions``.  A single region
+    that is the whole blob, contiguous and of the stored dtype is decoded
+    straight into its destination (no scratch, no copy)."""
+    with timeline.span("h2d_decode", "h2d", bytes=span.nbytes, regions=len(regions)):
+        _scatter_compressed(span, regions, dev, producer)
+
+
+def _scatter_compressed(span, regions, dev: int, producer: int = 0) -> None:
+    from ..ops import codec as hsz
+
+    h = span.header
+    first, last = span.first, span.last
+    if last <= first:
+        return
+    slot = copy_slot()
+    native.memcpy(dev, slot, 0, 0, 0, native.H2D, producer or None, sync=False)
+    c_lo = h.offsets[first]
+    c_n = h.offsets[last] - c_lo
+    log_lo = span.frames_logical_lo
+    log_n = min(last * h.frame_bytes, h.logical_size) - log_lo
+    direct = None
+    if len(regions) == 1:
+        src_dtype, src_shape, off, narrows, dst = regions[0]
+        rng = _contiguous_src_range(src_dtype, src_shape, off, narrows)
+        if (rng is not None and rng[0] + span.lo == log_lo and rng[1] == log_n
+                and dst.dtype == src_dtype and dst.is_contiguous()
+                and dst.data_ptr() % 16 == 0):
+            direct = dst
+    enc = torch.empty(c_n, dtype=torch.uint8, device=f"cuda:{dev}")
+    offs = torch.tensor([o - c_lo for o in h.offsets[first:last]], dtype=torch.int64)
+    offs_dev = torch.empty(offs.numel(), dtype=torch.int64, device=f"cuda:{dev}")
+    out = None if direct is not None else torch.empty(log_n, dtype=torch.uint8,
+                                                     device=f"cuda:{dev}")
+    _join_current_stream(dev, slot)
+    native.memcpy(dev, slot, enc.data_ptr(), span.buf.addr, c_n, native.H2D, None, sync=False)
+    native.memcpy(dev, slot, offs_dev.data_ptr(), offs.data_ptr(), offs.numel() * 8,
+                  native.H2D, None, sync=False)
+    stream = native.copy_stream(dev, slot)
+    native.hsz_decode_gpu(dev, enc.data_ptr(), offs_dev.data_ptr(), first, last - first,
+                          h.logical_size, h.elem_width, h.frame_bytes,
+                          (direct if direct is not None else out).data_ptr(), stream)
+    if direct is not None:
+        native.stream_sync(dev, slot)
+        return
+    shift = span.lo - log_lo
+    _copy_regions(out[shift:], regions, dev, slot)
 
 
 def _contiguous_src_range(src_dtype: torch.dtype, src_shape: Sequence[int], off: int, narrows):

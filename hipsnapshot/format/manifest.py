@@ -16,9 +16,12 @@ Metadata is written as JSON (fast) and read with ``json`` first, falling back
 to YAML ``SafeLoader`` for metadata produced by YAML dumpers (JSON is a subset
 of YAML, reference `manifest.py:283-314`).
 
-hipsnapshot extension: a ``Tensor`` entry may carry an optional ``quant``
-object (only present for the opt-in fp8 serializer); it is omitted from the
-JSON when absent so ordinary snapshots are byte-compatible.
+hipsnapshot extensions: a ``Tensor`` entry may carry an optional ``quant``
+object (only present for the opt-in fp8 serializer) and an optional ``codec``
+object (opt-in lossless HSZ1 compression of the blob it lives in:
+``{"name": "hsz1", "w": 2, "frame_bytes": F, "blob_bytes": L}``, its
+``byte_range`` staying in logical bytes); both are omitted from the JSON when
+absent so ordinary snapshots are byte-compatible.
 """
 
 from __future__ import annotations
@@ -49,6 +52,7 @@ class TensorEntry(Entry):
     replicated: bool
     byte_range: Optional[List[int]]
     quant: Optional[Dict[str, Any]] = None
+    codec: Optional[Dict[str, Any]] = None
 
     def __init__(
         self,
@@ -59,6 +63,7 @@ class TensorEntry(Entry):
         replicated: bool,
         byte_range: Optional[List[int]] = None,
         quant: Optional[Dict[str, Any]] = None,
+        codec: Optional[Dict[str, Any]] = None,
     ) -> None:
         self.type = "Tensor"
         self.location = location
@@ -68,6 +73,7 @@ class TensorEntry(Entry):
         self.replicated = replicated
         self.byte_range = list(byte_range) if byte_range is not None else None
         self.quant = quant
+        self.codec = codec
 
     @property
     def byte_range_tuple(self) -> Optional[Tuple[int, int]]:
@@ -87,6 +93,8 @@ class TensorEntry(Entry):
         }
         if self.quant is not None:
             d["quant"] = self.quant
+        if self.codec is not None:
+            d["codec"] = self.codec
         return d
 
     @classmethod
@@ -99,6 +107,7 @@ class TensorEntry(Entry):
             replicated=d.get("replicated", False),
             byte_range=d.get("byte_range"),
             quant=d.get("quant"),
+            codec=d.get("codec"),
         )
 
 

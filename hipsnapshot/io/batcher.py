@@ -32,7 +32,8 @@ from .. import knobs
 from ..engine import staging
 from ..format.manifest import Entry, iter_tensor_entries
 from ..format.serialization import Serializer, string_to_dtype
-from ..io_types import BufferConsumer, BufferStager, ReadReq, StagedBuffer, WriteReq
+from ..io_types import (BufferConsumer, BufferStager, CompressedSpan, ReadReq, StagedBuffer,
+                        WriteReq)
 from .tensor import TensorBufferConsumer, TensorBufferStager, run_in_executor, tensor_nbytes_from_entry
 
 
@@ -76,11 +77,21 @@ class BatchedBufferStager(BufferStager):
     def __init__(self, members, total: int) -> None:
         self.members = members
         self.total = total
+        self.codec: Optional[dict] = None
 
     async def stage_buffer(self, executor: Optional[Executor] = None):
         return await run_in_executor(executor, self._stage_sync)
 
     def _stage_sync(self) -> StagedBuffer:
+        raw = self._gather()
+        if self.codec is None:
+            return raw
+        try:
+            return staging.encode_host_buffer(raw, self.codec)
+        finally:
+            raw.release()
+
+    def _gather(self) -> StagedBuffer:
         from ..ops import native
 
         if native.gpu_available() and native.hsgpu_loaded():
@@ -106,6 +117,7 @@ class GPUBatchedBufferStager(BufferStager):
     def __init__(self, members, total: int) -> None:
         self.members = members
         self.total = total
+        self.codec: Optional[dict] = None  # HSZ1 info when the slab is compressed
 
     async def stage_buffer(self, executor: Optional[Executor] = None):
         return await run_in_executor(executor, self._stage_sync)
@@ -117,7 +129,8 @@ class GPUBatchedBufferStager(BufferStager):
         producers = sorted({st.producer for _, st in self.members if st.producer})
         pairs = [(st._source(), lo) for (lo, _hi), st in self.members]
         return staging.gather_to_host(pairs, self.total, producers,
-                                      via_device_slab=knobs.use_gpu_gather_for_slabs())
+                                      via_device_slab=knobs.use_gpu_gather_for_slabs(),
+                                      codec=self.codec)
 
     def get_staging_cost_bytes(self) -> int:
         return self.total
@@ -207,7 +220,18 @@ class BatchedBufferConsumer(BufferConsumer):
             return StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
         return None
 
+    def get_compressed_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
+        return self.get_read_dest(nbytes)
+
     async def consume_buffer(self, buf, executor: Optional[Executor] = None) -> None:
+        if isinstance(buf, CompressedSpan):
+            if self._gpu:
+                await run_in_executor(executor, self._consume_gpu, buf)
+            if self._other:
+                mv = await run_in_executor(executor, buf.decode_host)
+                for (lo, hi), c in self._other:
+                    await c.consume_buffer(mv[lo:hi], executor=executor)
+            return
         mv = memoryview(buf.view if isinstance(buf, StagedBuffer) else buf).cast("B")
         if self._gpu:
             await run_in_executor(executor, self._consume_gpu, buf)
@@ -215,7 +239,6 @@ class BatchedBufferConsumer(BufferConsumer):
             await c.consume_buffer(mv[lo:hi], executor=executor)
 
     def _consume_gpu(self, buf) -> None:
-        addr = staging.host_buffer_addr(buf)
         by_dev: Dict[int, list] = defaultdict(list)
         producers = {}
         for _rng, c, regions in self._gpu:
@@ -223,7 +246,11 @@ class BatchedBufferConsumer(BufferConsumer):
             by_dev[dev].extend(regions)
             producers.setdefault(dev, getattr(c, "producer", 0))
         for dev, regions in by_dev.items():
-            staging.scatter_host_regions(addr, self.buf_sz_bytes, regions, dev, producers[dev])
+            if isinstance(buf, CompressedSpan):
+                staging.scatter_compressed(buf, regions, dev, producers[dev])
+            else:
+                staging.scatter_host_regions(staging.host_buffer_addr(buf), self.buf_sz_bytes,
+                                             regions, dev, producers[dev])
 
     def get_consuming_cost_bytes(self) -> int:
         return self.buf_sz_bytes + sum(c.get_consuming_cost_bytes() for _, c in self.members)
@@ -245,5 +272,6 @@ def batch_read_requests(read_reqs: List[ReadReq]) -> List[ReadReq]:
         hi = max(r.byte_range[1] for r in rrs)
         members = [((r.byte_range[0] - lo, r.byte_range[1] - lo), r.buffer_consumer) for r in rrs]
         out.append(ReadReq(path=path, byte_range=(lo, hi),
-                           buffer_consumer=BatchedBufferConsumer(members, hi - lo)))
+                           buffer_consumer=BatchedBufferConsumer(members, hi - lo),
+                           codec=rrs[0].codec))
     return out

@@ -33,7 +33,7 @@ import torch
 
 from ..format.manifest import Shard, ShardedTensorEntry, TensorEntry
 from ..format.serialization import Serializer, string_to_dtype
-from ..io_types import BufferConsumer, Future, ReadReq, StagedBuffer, WriteReq
+from ..io_types import BufferConsumer, CompressedSpan, Future, ReadReq, StagedBuffer, WriteReq
 from ..knobs import get_max_shard_size_bytes
 from ..engine import staging
 from .tensor import (
@@ -229,7 +229,8 @@ class ShardedTensorIOPreparer:
                 groups.setdefault(key, []).append(Region(box.tensor, nar))
                 entries[key] = shard.tensor
         reqs = [ReadReq(path=entries[k].location, byte_range=entries[k].byte_range_tuple,
-                        buffer_consumer=ShardedTensorBufferConsumer(regions, entries[k]))
+                        buffer_consumer=ShardedTensorBufferConsumer(regions, entries[k]),
+                        codec=entries[k].codec)
                 for k, regions in groups.items()]
         return reqs, Future(obj=obj_out)
 
@@ -275,10 +276,20 @@ class ShardedTensorBufferConsumer(BufferConsumer):
             return StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
         return None
 
+    def get_compressed_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
+        return self.get_read_dest(nbytes)
+
     async def consume_buffer(self, buf, executor: Optional[Executor] = None) -> None:
         await run_in_executor(executor, self._consume_sync, buf)
 
     def _consume_sync(self, buf) -> None:
+        if isinstance(buf, CompressedSpan):
+            if self._gpu:
+                staging.scatter_compressed(buf, self.device_regions(0),
+                                           staging.device_of(self.regions[0].dst),
+                                           self.producer)
+                return
+            buf = buf.decode_host()
         if self._gpu:
             dtype = string_to_dtype(self.entry.dtype)
             regions = [(dtype, self.entry.shape, 0,

@@ -38,7 +38,8 @@ from ..format.serialization import (
     torch_load_from_bytes,
     torch_save_as_bytes,
 )
-from ..io_types import BufferConsumer, BufferStager, Future, ReadReq, StagedBuffer, WriteReq
+from ..io_types import (BufferConsumer, BufferStager, CompressedSpan, Future, ReadReq,
+                        StagedBuffer, WriteReq)
 from ..engine import staging
 
 PrepareFunc = Callable[[torch.Tensor, bool], torch.Tensor]
@@ -108,9 +109,9 @@ class TensorIOPreparer:
                 fut = Future()
                 consumer = TensorBufferConsumer(tensor=None, entry=entry, future=fut)
                 return [ReadReq(path=entry.location, byte_range=entry.byte_range_tuple,
-                                buffer_consumer=consumer)], fut
+                                buffer_consumer=consumer, codec=entry.codec)], fut
             tensor_out = cls.empty_tensor_from_entry(entry)
-        if entry.serializer == Serializer.BUFFER_PROTOCOL.value:
+        if entry.serializer == Serializer.BUFFER_PROTOCOL.value and entry.codec is None:
             if buffer_size_limit_bytes is not None:
                 return cls.prepare_read_tiled(entry, tensor_out, buffer_size_limit_bytes)
             if tensor_nbytes_from_entry(entry) > AUTO_TILE_THRESHOLD_BYTES:
@@ -118,7 +119,7 @@ class TensorIOPreparer:
                 return cls.prepare_read_tiled(entry, tensor_out, AUTO_TILE_BYTES)
         consumer = TensorBufferConsumer(tensor=tensor_out, entry=entry)
         return [ReadReq(path=entry.location, byte_range=entry.byte_range_tuple,
-                        buffer_consumer=consumer)], Future(obj=tensor_out)
+                        buffer_consumer=consumer, codec=entry.codec)], Future(obj=tensor_out)
 
     @classmethod
     def prepare_read_tiled(cls, entry: TensorEntry, tensor_out: torch.Tensor,
@@ -187,6 +188,7 @@ class TensorBufferStager(BufferStager):
         # arena that nobody else mutates -> no extra host copy needed
         self.frozen = False
         self.wait_event = None  # torch.cuda.Event guarding a frozen HBM copy
+        self.codec: Optional[dict] = None  # HSZ1 info when the blob is compressed
 
     def _source(self) -> torch.Tensor:
         t = self.tensor
@@ -206,6 +208,8 @@ class TensorBufferStager(BufferStager):
                      and t.untyped_storage().data_ptr()
                      != self.tensor.untyped_storage().data_ptr())
             copy = self.is_async_snapshot and not self.frozen and not fresh
+            if self.codec is not None:
+                return await run_in_executor(executor, self._encode_host, t)
             return await run_in_executor(executor, staging.cpu_tensor_bytes, t, copy)
         if ser == Serializer.FP8_BLOCK.value:
             from ..ops.quant import stage_fp8
@@ -215,10 +219,17 @@ class TensorBufferStager(BufferStager):
             return await run_in_executor(executor, _torch_save_tensor, t)
         raise ValueError(f"Unrecognized serializer: {ser}.")
 
+    def _encode_host(self, t: torch.Tensor):
+        raw = staging.cpu_tensor_bytes(t, copy=False)
+        try:
+            return staging.encode_host_buffer(raw, self.codec)
+        finally:
+            raw.release()
+
     def _d2h(self, t: torch.Tensor):
         if self.wait_event is not None:
             self.wait_event.synchronize()
-        return staging.d2h_tensor(t, self.producer)
+        return staging.d2h_tensor(t, self.producer, codec=self.codec)
 
     def get_staging_cost_bytes(self) -> int:
         n = tensor_nbytes_from_entry(self.entry)
@@ -294,6 +305,15 @@ class TensorBufferConsumer(BufferConsumer):
             return StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
         return None
 
+    def get_compressed_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
+        t = self.tensor
+        if t is not None and t.is_cuda and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value:
+            from ..ops import native
+
+            pb = native.PinnedBuffer(nbytes)
+            return StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
+        return None
+
     async def consume_buffer(self, buf, executor: Optional[Executor] = None) -> None:
         if self._direct:
             return  # bytes were read straight into the destination tensor
@@ -301,6 +321,14 @@ class TensorBufferConsumer(BufferConsumer):
 
     def _consume_sync(self, buf) -> None:
         t = self.tensor
+        if isinstance(buf, CompressedSpan):
+            if (t is not None and t.is_cuda
+                    and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value):
+                staging.scatter_compressed(
+                    buf, [(string_to_dtype(self.entry.dtype), self.entry.shape, 0, None, t)],
+                    staging.device_of(t), self.producer)
+                return
+            buf = buf.decode_host()
         if t is None:
             self.future.obj = deserialize_tensor(buf, self.entry)
             return

@@ -95,6 +95,57 @@ class BufferConsumer(ABC):
         """Optionally provide a writable destination for the raw bytes."""
         return None
 
+    def get_compressed_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
+        """Destination for the ENCODED bytes of an HSZ1 blob (pinned memory
+        for consumers that decode on the GPU); None = plain host memory."""
+        return None
+
+
+class CompressedSpan:
+    """Encoded frames [first, last) of an HSZ1 blob covering the logical byte
+    range [lo, hi) a read asked for.  Consumers that restore into HBM move
+    the encoded bytes with one H2D and decode on the GPU
+    (``engine.staging.scatter_compressed``); others call ``decode_host``."""
+
+    def __init__(self, buf: "StagedBuffer", header, first: int, last: int, lo: int,
+                 hi: int) -> None:
+        self.buf = buf
+        self.header = header
+        self.first = first
+        self.last = last
+        self.lo = lo
+        self.hi = hi
+
+    @property
+    def nbytes(self) -> int:
+        return self.hi - self.lo
+
+    @property
+    def frames_logical_lo(self) -> int:
+        return self.first * self.header.frame_bytes
+
+    def decode_host(self) -> memoryview:
+        """Logical bytes [lo, hi) decoded by the C++ codec into host memory."""
+        from .ops import codec
+
+        h = self.header
+        n_log = min(self.last * h.frame_bytes, h.logical_size) - self.frames_logical_lo
+        out = np.empty(max(n_log, 1), dtype=np.uint8)
+        base = h.offsets[self.first]
+        offs = np.asarray([o - base for o in h.offsets[self.first: self.last]],
+                          dtype=np.uint64)
+        if self.last > self.first:
+            from .ops import native
+
+            native.hsz_decode_cpu(self.buf.addr, offs.ctypes.data, self.first,
+                                  self.last - self.first, h.logical_size, h.elem_width,
+                                  h.frame_bytes, out.ctypes.data)
+        shift = self.lo - self.frames_logical_lo
+        return memoryview(out)[shift: shift + self.nbytes]
+
+    def release(self) -> None:
+        self.buf.release()
+
 
 @dataclass
 class ReadReq:
@@ -104,6 +155,8 @@ class ReadReq:
     # False for tiles of one large tensor: merging them back into one read
     # would defeat the memory budget / read-H2D pipelining they exist for
     mergeable: bool = True
+    # HSZ1 info of the blob (entry.codec): byte_range is then in logical bytes
+    codec: Optional[dict] = None
 
 
 @dataclass

@@ -9,6 +9,9 @@ Every variable is read as ``HIPSNAPSHOT_<NAME>`` first and the reference's
 MI355X-specific knobs:
 
 * ``HIPSNAPSHOT_IO_THREADS`` (16) -- native I/O engine workers per storage plugin.
+* ``HIPSNAPSHOT_COMPRESSION`` (none) -- ``hsz1`` = lossless GPU compression of
+  floating-point blobs (see ``ops/codec.py``); per call via ``compression=``.
+* ``HIPSNAPSHOT_READ_INFLIGHT`` (8) -- whole-blob reads in flight during restore.
 * ``HIPSNAPSHOT_IO_READ_SPLIT_BYTES`` (8 MiB) -- reads larger than 1.5x this are
   split across I/O workers (parallel page-cache reads of one file; 0 = off).
 * ``HIPSNAPSHOT_STAGE_THREADS`` (4) -- concurrent staging jobs (DMA/pack/serialize).
@@ -85,6 +88,18 @@ def get_memory_budget_override() -> Optional[int]:
 
 def get_io_threads() -> int:
     return _get_int("IO_THREADS", 16)
+
+
+def compress_host_tensors() -> bool:
+    return _get_bool("COMPRESSION_HOST", False)
+
+
+def get_read_inflight() -> int:
+    return max(1, _get_int("READ_INFLIGHT", 8))
+
+
+def get_compression() -> str:
+    return str(_get("COMPRESSION") or "none")
 
 
 def get_io_read_split_bytes() -> int:

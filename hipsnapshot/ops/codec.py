@@ -265,7 +265,7 @@ def validate_offsets(h: Header, blob_len: int) -> None:
 
 
 def encode_device(src, elem_width: int, stream_handle: int,
-                  frame_bytes: int = DEFAULT_FRAME_BYTES):
+                  frame_bytes: int = DEFAULT_FRAME_BYTES, launch: bool = True):
     """Encode a contiguous CUDA uint8 tensor on the GPU.
 
     Returns ``(blob_tensor, nbytes_device)`` where ``blob_tensor`` has the
@@ -283,11 +283,22 @@ def encode_device(src, elem_width: int, stream_handle: int,
     out = torch.empty(max_encoded_bytes(logical, frame_bytes), dtype=torch.uint8,
                       device=src.device)
     meta = torch.empty(native.hsz_meta_bytes(nf), dtype=torch.uint8, device=src.device)
-    total = torch.zeros(1, dtype=torch.int64, device=src.device)
-    src_addr = src.data_ptr() if logical else out.data_ptr()
-    native.hsz_encode_gpu(dev, src_addr, logical, elem_width, frame_bytes, out.data_ptr(),
-                          meta.data_ptr(), total.data_ptr(), stream_handle)
+    total = torch.empty(1, dtype=torch.int64, device=src.device)
+    if launch:
+        launch_encode(src, elem_width, stream_handle, frame_bytes, out, total, meta)
     return out, total, meta
+
+
+def launch_encode(src, elem_width: int, stream_handle: int, frame_bytes: int, out, total,
+                  meta) -> None:
+    import torch
+
+    from . import native
+
+    dev = src.device.index if src.device.index is not None else torch.cuda.current_device()
+    src_addr = src.data_ptr() if src.numel() else out.data_ptr()
+    native.hsz_encode_gpu(dev, src_addr, src.numel(), elem_width, frame_bytes, out.data_ptr(),
+                          meta.data_ptr(), total.data_ptr(), stream_handle)
 
 
 def decode_device_into(blob_dev, header: Header, out_dev, stream_handle: int,

@@ -286,7 +286,7 @@ def test_fsdp2_rccl_single_rank(gpu, tmp_path):
     run_distributed(_fsdp_gpu_worker, 1, str(tmp_path / "f"), backend="nccl")
 
 
-def _multirank_gpu_worker(path, phase):
+def _multirank_gpu_worker(path, phase, compression=None):
     """Several ranks sharing cuda:0 with gloo metadata collectives: exercises
     the multi-rank take/restore logic (partitioning, manifest merge, sharded
     resharding, HBM freeze, store-barrier commit) on device tensors."""
@@ -296,7 +296,7 @@ def _multirank_gpu_worker(path, phase):
 
     rank, ws = dist.get_rank(), dist.get_world_size()
     torch.manual_seed(0)
-    full = torch.randn(96, 40, device="cuda:0")
+    full = torch.randn(96, 2048, device="cuda:0")
     mesh = init_device_mesh("cuda", (ws,))
     rows = 96 // ws
     local = full[rank * rows:(rank + 1) * rows].clone()
@@ -305,9 +305,9 @@ def _multirank_gpu_worker(path, phase):
     if phase == "save":
         Snapshot.take(path, {"m": StateDict(w=dt, rep=rep, mine=torch.full((5,), float(rank),
                                                                             device="cuda:0"))},
-                      replicated=["m/rep"])
+                      replicated=["m/rep"], compression=compression)
         p = Snapshot.async_take(path + "_a", {"m": StateDict(w=dt, rep=rep)},
-                                replicated=["m/rep"])
+                                replicated=["m/rep"], compression=compression)
         local.add_(1)  # after the freeze: must not leak
         p.wait()
         local.sub_(1)
@@ -319,7 +319,7 @@ def _multirank_gpu_worker(path, phase):
         torch.cuda.synchronize()
         assert torch.equal(out, full[rank * rows:(rank + 1) * rows]), rank
         assert torch.equal(r2, rep)
-        whole = torch.zeros(96, 40, device="cuda:0")
+        whole = torch.zeros(96, 2048, device="cuda:0")
         Snapshot(path).read_object("0/m/w", obj_out=whole)
         assert torch.equal(whole, full)
 
@@ -391,3 +391,99 @@ def test_hsz_gpu_large_blob_ratio(gpu):
     back = torch.empty_like(x)
     codec.decode_device_into(out[:nb], hdr, back.view(torch.uint8), int(s.cuda_stream))
     assert torch.equal(back.view(torch.int16), x.view(torch.int16))
+
+
+# ---- HSZ1 compressed snapshots on the GPU path ---------------------------------
+
+def _compressible_state(gpu):
+    torch.manual_seed(11)
+    a = torch.randn(512, 256, device=gpu)
+    return StateDict(
+        w=(torch.randn(1000, 300, device=gpu) * 0.02).to(torch.bfloat16),
+        big=(torch.randn(3000, 1024, device=gpu) * 0.02).to(torch.bfloat16),
+        t=a.t(),                                   # strided view, fp32
+        col=a[:, 10:100],
+        small=[torch.randn(i + 1000, device=gpu) for i in range(20)],  # slab members
+        h=torch.randn(70_001, device=gpu, dtype=torch.float16),
+        i64=torch.arange(100_000, device=gpu),
+        cpu=torch.randn(77),
+        step=3,
+    )
+
+
+def _clone_state(sd):
+    return {k: (v.clone() if isinstance(v, torch.Tensor) else
+                [x.clone() for x in v] if isinstance(v, list) else v) for k, v in sd.items()}
+
+
+@pytest.mark.parametrize("slab", [1 << 20, 64 << 20])
+def test_gpu_compressed_snapshot_roundtrip(gpu, tmp_path, slab):
+    sd = _compressible_state(gpu)
+    ref = _clone_state(sd)
+    with override_slab_size_threshold_bytes(slab):
+        snap = Snapshot.take(str(tmp_path / "s"), {"sd": sd}, compression="hsz1")
+    man = snap.get_manifest()
+    assert man["0/sd/big"].codec is not None and man["0/sd/cpu"].codec is None
+    total = sum(os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(tmp_path / "s")
+                for f in fs)
+    raw = sum(v.numel() * v.element_size() for v in ref.values() if isinstance(v, torch.Tensor))
+    assert total < raw  # the bf16 payload shrank
+    out = StateDict(
+        w=torch.zeros(1000, 300, device=gpu, dtype=torch.bfloat16),
+        big=torch.zeros(3000, 1024, device=gpu, dtype=torch.bfloat16),
+        t=torch.zeros(256, 512, device=gpu),
+        col=torch.zeros(1024, 180, device=gpu)[::2, ::2],   # strided destination
+        small=[torch.zeros(i + 1000, device=gpu) for i in range(20)],
+        h=torch.zeros(70_001, device=gpu, dtype=torch.float16),
+        i64=torch.zeros(100_000, dtype=torch.int64, device=gpu),
+        cpu=torch.zeros(77),
+    )
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    torch.cuda.synchronize()
+    assert_state_dict_eq({k: out[k] for k in ref}, ref)
+    # host read of a compressed device blob (CPU decoder)
+    got = Snapshot(str(tmp_path / "s")).read_object("0/sd/big")
+    assert torch.equal(got, ref["big"].cpu())
+
+
+def test_gpu_compressed_async_take(gpu, tmp_path):
+    w = (torch.randn(4096, 1024, device=gpu) * 0.02).to(torch.bfloat16)
+    small = torch.randn(5000, device=gpu)
+    ref_w, ref_s = w.clone(), small.clone()
+    pending = Snapshot.async_take(str(tmp_path / "s"), {"sd": StateDict(w=w, s=small)},
+                                  compression="hsz1")
+    w.add_(1.0)
+    small.mul_(0)
+    pending.wait()
+    out = StateDict(w=torch.zeros_like(w), s=torch.zeros_like(small))
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    assert torch.equal(out["w"], ref_w) and torch.equal(out["s"], ref_s)
+
+
+def _fsdp_compressed_worker(path):
+    from torch.distributed.device_mesh import init_device_mesh
+
+    from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+
+    mesh = init_device_mesh("cuda", (1,))
+    model = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cuda:0"), torch.bfloat16,
+                             mesh=mesh)
+    ref = {k: v.full_tensor().clone() for k, v in model.state_dict().items()}
+    Snapshot.take(path, {"model": model}, compression="hsz1")
+    with torch.no_grad():
+        for p in model.parameters():
+            p.to_local().zero_()
+    Snapshot(path).restore({"model": model})
+    for k, v in model.state_dict().items():
+        assert torch.equal(v.full_tensor(), ref[k]), k
+
+
+def test_gpu_compressed_fsdp2_single_rank(gpu, tmp_path):
+    run_distributed(_fsdp_compressed_worker, 1, str(tmp_path / "f"), backend="nccl")
+
+
+@pytest.mark.parametrize("save_ws,load_ws", [(2, 3)])
+def test_multirank_gpu_compressed_gloo(gpu, tmp_path, save_ws, load_ws):
+    p = str(tmp_path / "mrc")
+    run_distributed(_multirank_gpu_worker, save_ws, p, "save", "hsz1", backend="gloo")
+    run_distributed(_multirank_gpu_worker, load_ws, p, "load", "hsz1", backend="gloo")
