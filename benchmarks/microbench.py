@@ -188,6 +188,38 @@ def main():
         del blob, back
     del w
 
+    # HSZ1 lossless codec: encode (3 launches) and decode of 1 GiB bf16 in HBM
+    from hipsnapshot.ops import codec
+
+    x = (torch.randn(512 << 20, device="cuda:0") / 64).to(torch.bfloat16).view(torch.uint8)
+    st = torch.cuda.current_stream()
+    out, total, meta = codec.encode_device(x, 2, int(st.cuda_stream))
+    st.synchronize()
+    nb = int(total.item())
+    nf = codec.n_frames_for(x.numel(), codec.DEFAULT_FRAME_BYTES)
+    hdr = codec.parse_header(out[:codec.payload_start(nf)].cpu().numpy().tobytes())
+    offs = torch.tensor(hdr.offsets[:-1], dtype=torch.int64, device="cuda:0")
+    back = torch.empty_like(x)
+
+    def enc():
+        codec.launch_encode(x, 2, int(st.cuda_stream), codec.DEFAULT_FRAME_BYTES, out, total,
+                            meta)
+
+    def dec():
+        native.hsz_decode_gpu(dev, out.data_ptr(), offs.data_ptr(), 0, hdr.n_frames,
+                              hdr.logical_size, 2, hdr.frame_bytes, back.data_ptr(),
+                              int(st.cuda_stream))
+
+    best, med = timeit(enc)
+    emit(test="hsz_encode_1GiB_bf16", GBps=x.numel() / best / 1e9,
+         median_GBps=x.numel() / med / 1e9, ms=best * 1e3, ratio=nb / x.numel(),
+         note="logical bytes/s; HBM traffic = 2 reads + 0.75 write")
+    best, med = timeit(dec)
+    emit(test="hsz_decode_1GiB_bf16", GBps=x.numel() / best / 1e9,
+         median_GBps=x.numel() / med / 1e9, ms=best * 1e3)
+    assert torch.equal(back, x)
+    del x, out, back
+
     if not args.skip_fs:
         os.makedirs(args.dir, exist_ok=True)
         eng = native.IOEngine(16)
