@@ -357,7 +357,33 @@ class SnapshotMetadata:
         # Compact separators keep json on its C encoder: ~10x faster than the
         # reference's indent=2 (pure-Python encoder), which matters for the
         # merged manifest of an 8-rank FSDP job.  Any JSON/YAML reader parses it.
+        pre = self.__dict__.get("_json_async")
+        if pre is not None:
+            thread, box = pre
+            thread.join()
+            if "json" in box:
+                return box["json"]
         return json.dumps(self.to_dict(), sort_keys=False, separators=(",", ":"))
+
+    def serialize_in_background(self) -> None:
+        """Start encoding the JSON now (the commit needs it only after all
+        blobs are written): takes the merged-manifest encoding of an 8-rank
+        job off rank 0's critical path.  The manifest must not change after
+        this call; ``to_json`` joins the thread."""
+        import threading
+
+        box: Dict[str, str] = {}
+
+        def run() -> None:
+            try:
+                box["json"] = json.dumps(self.to_dict(), sort_keys=False,
+                                         separators=(",", ":"))
+            except Exception:  # noqa: BLE001 - to_json falls back to inline encoding
+                pass
+
+        t = threading.Thread(target=run, name="hipsnapshot-metadata-json", daemon=True)
+        t.start()
+        self.__dict__["_json_async"] = (t, box)
 
     # Reference name (metadata is JSON, which is valid YAML).
     to_yaml = to_json

@@ -295,6 +295,8 @@ class Snapshot:
             pending = DeferredIOWork(pending, deferred, storage, budget, rank)
         metadata = SnapshotMetadata(version=__version__, world_size=comm.get_world_size(),
                                     manifest=manifest)
+        if comm.get_rank() == 0:
+            metadata.serialize_in_background()
         return pending, metadata
 
     # --------------------------------------------------------------- restore
@@ -508,6 +510,7 @@ class Snapshot:
                                  loop: asyncio.AbstractEventLoop) -> None:
         with timeline.span("metadata_to_json", "commit"):
             buf = metadata.to_json().encode("utf-8")
+        metadata.__dict__.pop("_json_async", None)  # later edits re-encode
         commit = getattr(storage, "commit_metadata", None)
         if commit is not None:
             loop.run_until_complete(commit(SNAPSHOT_METADATA_FNAME, buf))
