@@ -63,6 +63,7 @@ def main() -> None:
     ap.add_argument("--no-restore-check", action="store_true")
     ap.add_argument("--fsync", action="store_true")
     ap.add_argument("--direct-io", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"],
                     help="hsz1 (default) = lossless GPU-side exponent-nibble compression of "
                          "the bf16 blobs, restore verified bitwise; none = raw blobs "
@@ -83,9 +84,15 @@ def main() -> None:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using WORLD_SIZE",
               file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    dist.init_process_group("nccl", device_id=dev)
+    # --backend gloo rehearses the multi-rank path with several ranks sharing
+    # one GPU (RCCL refuses that); the measured numbers are then NOT scaling data
+    gpu_index = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(gpu_index)
+    dev = torch.device("cuda", gpu_index)
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
 
     from hipsnapshot import Snapshot
     from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
@@ -169,17 +176,25 @@ def main() -> None:
     restore_gbps = None
     if not args.no_restore_check:
         # bitwise restore check of EVERY local shard (HBM holds the copies)
-        params = [p._local_tensor for p in model.parameters()]
-        refs = [p.clone() for p in params]
-        for p in params:
-            p.zero_()
+        named = list(model.named_parameters())
+        refs = [p._local_tensor.clone() for _, p in named]
+        for _, p in named:
+            p._local_tensor.zero_()
         barrier_sync()
         tr = time.perf_counter()
         Snapshot(path).restore(app_state)
         barrier_sync()
         restore_s = time.perf_counter() - tr
-        ok = torch.tensor([int(all(torch.equal(a, b) for a, b in zip(refs, params)))],
-                          device=dev)
+        # compare against the parameters as they are NOW (load_state_dict may
+        # re-point a module's parameter)
+        bad = [(n, r, p._local_tensor) for (n, p), r in zip(named, refs)
+               if not torch.equal(r, p._local_tensor)]
+        for n, r, cur in bad[:5]:
+            nz = int((cur != 0).sum().item())
+            print(f"rank {rank}: restore mismatch in {n}: shape {tuple(cur.shape)}, "
+                  f"{nz}/{cur.numel()} nonzero, first diff at "
+                  f"{int((r != cur).flatten().nonzero()[0].item())}", file=sys.stderr)
+        ok = torch.tensor([int(not bad)], device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         restore_ok = bool(ok.item())
         restore_gbps = total_bytes / restore_s / 1e9

@@ -758,17 +758,20 @@ uint64_t hsg_pinned_trim() {
 // ---- DMA copies on side streams --------------------------------------------
 
 // Copy `n` bytes between host and device on copy stream (dev, slot), ordered
-// after all work already queued on `producer` (a torch stream, may be null).
+// after all work already queued on `producer` when `has_producer` is set (a
+// torch stream; handle 0 = the legacy default stream).
 // kind: 0 = D2H, 1 = H2D, 2 = D2D.  If `sync` is nonzero the call blocks until
 // the copy is done (ctypes releases the GIL around it).
 int hsg_memcpy(int dev, int slot, void* dst, const void* src, uint64_t n, int kind,
-               void* producer, int sync) {
+               void* producer, int has_producer, int sync) {
   HS_CHECK(hipSetDevice(dev));
   hipStream_t s;
   hipEvent_t ev;
   int r = get_stream(dev, slot, &s, &ev);
   if (r) return r;
-  if (producer) {
+  // producer may be the legacy null stream (handle 0, torch's default stream):
+  // the copy streams are non-blocking, so it must be joined explicitly too
+  if (has_producer) {
     HS_CHECK(hipEventRecord(ev, static_cast<hipStream_t>(producer)));
     HS_CHECK(hipStreamWaitEvent(s, ev, 0));
   }

@@ -88,17 +88,18 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
                               view.stride(), list(t.shape), t.element_size())
                 views.append(view)
             # producers may differ from the current stream: order after them
-            for p in {st.producer for st in sts if st.producer}:
+            for p in {st.producer for st in sts if st.producer is not None}:
                 if p != stream.cuda_stream:
                     ev = torch.cuda.Event()
-                    ev.record(torch.cuda.ExternalStream(p))
+                    ev.record(torch.cuda.default_stream(dev) if p == 0
+                              else torch.cuda.ExternalStream(p))
                     stream.wait_event(ev)
             keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
             done = torch.cuda.Event()
             done.record(stream)
         for st, view in zip(sts, views):
             st.tensor = view
-            st.producer = 0
+            st.producer = None  # ordering is carried by wait_event
             st.frozen = True
             st.wait_event = done
         # keep the descriptor tables alive until the copy ran

@@ -55,11 +55,13 @@ def device_of(t: torch.Tensor) -> int:
     return torch.cuda.current_device() if idx is None else idx
 
 
-def producer_stream_handle(t: torch.Tensor) -> int:
+def producer_stream_handle(t: torch.Tensor) -> Optional[int]:
     """The stream that produces ``t`` (current stream of its device, captured
-    on the calling thread -- call at plan time on the training thread)."""
+    on the calling thread -- call at plan time on the training thread).
+    0 is torch's default (legacy null) stream -- a real producer that the
+    non-blocking copy streams must be ordered after; None = host tensor."""
     if not t.is_cuda:
-        return 0
+        return None
     return int(torch.cuda.current_stream(t.device).cuda_stream)
 
 
@@ -72,7 +74,8 @@ def _elem_strides_ok(t: torch.Tensor) -> bool:
     return t.dim() <= native.MAX_DIMS
 
 
-def d2h_tensor(t: torch.Tensor, producer: int, codec: Optional[dict] = None) -> StagedBuffer:
+def d2h_tensor(t: torch.Tensor, producer: Optional[int],
+               codec: Optional[dict] = None) -> StagedBuffer:
     """Copy a CUDA tensor's logical bytes (C order) into a pinned block.
 
     With ``codec`` (HSZ1 info dict) the bytes are compressed on the GPU first
@@ -192,10 +195,10 @@ def _encode_host_bytes(addr: int, n: int, codec: dict) -> StagedBuffer:
     return StagedBuffer(view[:used], out_addr, release=release, keepalive=keep)
 
 
-def _d2h_encoded(t: torch.Tensor, producer: int, codec: dict) -> StagedBuffer:
+def _d2h_encoded(t: torch.Tensor, producer: Optional[int], codec: dict) -> StagedBuffer:
     dev = device_of(t)
     slot = copy_slot()
-    native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer or None, sync=False)
+    native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
     nbytes = t.numel() * t.element_size()
     if t.is_contiguous() and t.data_ptr() % 16 == 0:
         src = torch.empty(0, dtype=torch.uint8, device=t.device).set_(
@@ -322,7 +325,7 @@ def _gather_encoded(members, total_bytes: int, producers, codec: dict) -> Staged
 
 
 def h2d_into(dst: torch.Tensor, host_addr: int, nbytes: int, src_dtype: torch.dtype,
-             src_shape: Sequence[int], producer: int = 0) -> None:
+             src_shape: Sequence[int], producer: Optional[int] = None) -> None:
     """Load C-order bytes at ``host_addr`` (ideally pinned) into CUDA ``dst``.
 
     Same dtype + contiguous destination -> one DMA.  Otherwise one DMA into a
@@ -331,7 +334,7 @@ def h2d_into(dst: torch.Tensor, host_addr: int, nbytes: int, src_dtype: torch.dt
     dev = device_of(dst)
     slot = copy_slot()
     if dst.dtype == src_dtype and dst.is_contiguous() and list(dst.shape) == list(src_shape):
-        native.memcpy(dev, slot, dst.data_ptr(), host_addr, nbytes, native.H2D, producer or None,
+        native.memcpy(dev, slot, dst.data_ptr(), host_addr, nbytes, native.H2D, producer,
                       sync=True)
         return
     scatter_host_regions(host_addr, nbytes, [(src_dtype, src_shape, 0, None, dst)], dev,
@@ -339,13 +342,13 @@ def h2d_into(dst: torch.Tensor, host_addr: int, nbytes: int, src_dtype: torch.dt
 
 
 def scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
-                         producer: int = 0) -> None:
+                         producer: Optional[int] = None) -> None:
     with timeline.span("h2d_scatter", "h2d", bytes=nbytes, regions=len(regions)):
         _scatter_host_regions(host_addr, nbytes, regions, dev, producer)
 
 
 def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
-                          producer: int = 0) -> None:
+                          producer: Optional[int] = None) -> None:
     """One H2D of ``nbytes`` at ``host_addr`` then ONE kernel launch that copies
     every region into its destination view.
 
@@ -355,7 +358,7 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
     """
     slot = copy_slot()
     # order after pending work on the destinations' stream (captured at plan time)
-    native.memcpy(dev, slot, 0, 0, 0, native.H2D, producer or None, sync=False)
+    native.memcpy(dev, slot, 0, 0, 0, native.H2D, producer, sync=False)
     # Regions whose source bytes are one contiguous range and whose destination
     # is a contiguous tensor of the same dtype/shape go host -> destination with
     # one DMA each (no scratch, no kernel: the common FSDP/DTensor restore).
@@ -410,7 +413,7 @@ def _copy_regions(scratch: torch.Tensor, regions, dev: int, slot: int) -> None:
         torch.cuda.synchronize(dev)
 
 
-def scatter_compressed(span, regions, dev: int, producer: int = 0) -> None:
+def scatter_compressed(span, regions, dev: int, producer: Optional[int] = None) -> None:
     """HSZ1 restore into HBM: ONE H2D of the encoded frames, ONE decode launch,
     then the same region copy as ``scatter_host_regions``.  A single region
     that is the whole blob, contiguous and of the stored dtype is decoded
@@ -419,7 +422,7 @@ def scatter_compressed(span, regions, dev: int, producer: int = 0) -> None:
         _scatter_compressed(span, regions, dev, producer)
 
 
-def _scatter_compressed(span, regions, dev: int, producer: int = 0) -> None:
+def _scatter_compressed(span, regions, dev: int, producer: Optional[int] = None) -> None:
     from ..ops import codec as hsz
 
     h = span.header
@@ -427,7 +430,7 @@ def _scatter_compressed(span, regions, dev: int, producer: int = 0) -> None:
     if last <= first:
         return
     slot = copy_slot()
-    native.memcpy(dev, slot, 0, 0, 0, native.H2D, producer or None, sync=False)
+    native.memcpy(dev, slot, 0, 0, 0, native.H2D, producer, sync=False)
     c_lo = h.offsets[first]
     c_n = h.offsets[last] - c_lo
     log_lo = span.frames_logical_lo

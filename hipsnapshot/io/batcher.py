@@ -126,7 +126,7 @@ class GPUBatchedBufferStager(BufferStager):
         for ev in {id(st.wait_event): st.wait_event for _, st in self.members
                    if st.wait_event is not None}.values():
             ev.synchronize()
-        producers = sorted({st.producer for _, st in self.members if st.producer})
+        producers = sorted({st.producer for _, st in self.members if st.producer is not None})
         pairs = [(st._source(), lo) for (lo, _hi), st in self.members]
         return staging.gather_to_host(pairs, self.total, producers,
                                       via_device_slab=knobs.use_gpu_gather_for_slabs(),
@@ -244,7 +244,7 @@ class BatchedBufferConsumer(BufferConsumer):
         for _rng, c, regions in self._gpu:
             dev = staging.device_of(regions[0][4])
             by_dev[dev].extend(regions)
-            producers.setdefault(dev, getattr(c, "producer", 0))
+            producers.setdefault(dev, getattr(c, "producer", None))
         for dev, regions in by_dev.items():
             if isinstance(buf, CompressedSpan):
                 staging.scatter_compressed(buf, regions, dev, producers[dev])

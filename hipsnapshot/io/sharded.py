@@ -266,7 +266,7 @@ class ShardedTensorBufferConsumer(BufferConsumer):
         self._gpu = (entry.serializer == Serializer.BUFFER_PROTOCOL.value
                      and all(r.dst.is_cuda for r in regions) and len(regions) > 0
                      and len({r.dst.device for r in regions}) == 1)
-        self.producer = staging.producer_stream_handle(regions[0].dst) if self._gpu else 0
+        self.producer = staging.producer_stream_handle(regions[0].dst) if self._gpu else None
 
     def get_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
         if self._gpu:

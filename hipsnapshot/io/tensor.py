@@ -272,7 +272,7 @@ class TensorBufferConsumer(BufferConsumer):
         self.tensor = tensor
         self.entry = entry
         self.future = future
-        self.producer = staging.producer_stream_handle(tensor) if tensor is not None else 0
+        self.producer = staging.producer_stream_handle(tensor) if tensor is not None else None
         self._direct = False
 
     def _nbytes(self) -> int:
@@ -340,8 +340,9 @@ class TensorBufferConsumer(BufferConsumer):
             dev = staging.device_of(t)
             total = self.entry.quant["total_bytes"]
             blob = torch.empty(total, dtype=torch.uint8, device=t.device)
+            # order after the allocator's stream (and the target's producer)
             native.memcpy(dev, staging.copy_slot(), blob.data_ptr(), buf.addr, total, native.H2D,
-                          None, sync=True)
+                          int(torch.cuda.current_stream(t.device).cuda_stream), sync=True)
             dequantize_device(blob, self.entry, t)
             torch.cuda.current_stream(t.device).synchronize()
             return

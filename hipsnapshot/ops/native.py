@@ -208,7 +208,7 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         lim = os.environ.get("HIPSNAPSHOT_PINNED_POOL_MAX_BYTES")
         lib.hsg_pinned_set_limit(int(lim) if lim else 64 << 30)
         _declare(lib, "hsg_memcpy", c_int,
-                 [c_int, c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_int])
+                 [c_int, c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_int, c_int])
         _declare(lib, "hsg_stream_join", c_int, [c_int, c_int, c_void_p])
         _declare(lib, "hsg_stream_sync", c_int, [c_int, c_int])
         _declare(lib, "hsg_copy_stream", c_void_p, [c_int, c_int])
@@ -341,8 +341,12 @@ def _stream_handle(stream) -> int:
 
 def memcpy(dev: int, slot: int, dst: int, src: int, nbytes: int, kind: int,
            producer=None, sync: bool = True) -> None:
+    """DMA on copy stream (dev, slot).  ``producer``: stream (or raw handle;
+    0 = torch's default/null stream) whose queued work must finish first;
+    None = no ordering."""
     lib = require_gpu_lib()
     _check(lib.hsg_memcpy(dev, slot, dst, src, nbytes, kind, _stream_handle(producer),
+                          int(producer is not None),
                           1 if sync else 0), "hsg_memcpy")
 
 

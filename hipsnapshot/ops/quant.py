@@ -177,9 +177,10 @@ def stage_fp8(t: torch.Tensor, entry: TensorEntry, producer: int) -> StagedBuffe
         src = t if t.is_contiguous() else t.contiguous()
         blob = torch.zeros(total, dtype=torch.uint8, device=t.device)
         stream = torch.cuda.current_stream(t.device)
-        if producer and producer != stream.cuda_stream:
+        if producer is not None and producer != stream.cuda_stream:
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.ExternalStream(producer))
+            ev.record(torch.cuda.default_stream(t.device) if producer == 0
+                      else torch.cuda.ExternalStream(producer))
             stream.wait_event(ev)
         scales = blob[payload:].view(torch.float32)
         if rot == "hadamard32":

@@ -487,3 +487,34 @@ def test_multirank_gpu_compressed_gloo(gpu, tmp_path, save_ws, load_ws):
     p = str(tmp_path / "mrc")
     run_distributed(_multirank_gpu_worker, save_ws, p, "save", "hsz1", backend="gloo")
     run_distributed(_multirank_gpu_worker, load_ws, p, "load", "hsz1", backend="gloo")
+
+
+@pytest.mark.parametrize("compression", ["none", "hsz1"])
+def test_take_orders_after_pending_default_stream_work(gpu, tmp_path, compression):
+    """Copy streams are non-blocking: a take issued while the trainer's default
+    (null) stream is still busy must wait for that work, not read stale HBM."""
+    torch.cuda.synchronize()
+    a = torch.randn(4096, 4096, device=gpu)
+    big = torch.zeros(4096, 4096, device=gpu)
+    small = [torch.zeros(1000, device=gpu) for _ in range(8)]
+    for _ in range(30):  # keep the default stream busy for a while
+        a = torch.tanh(a @ a) * 0.5
+    big.copy_(a)
+    for s in small:
+        s.copy_(a[0, :1000])
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(big=big, small=small)},
+                  compression=compression)  # no synchronize before the take
+    got = Snapshot(str(tmp_path / "s")).read_object("0/sd/big")
+    assert torch.equal(got, big.cpu())
+    assert torch.equal(Snapshot(str(tmp_path / "s")).read_object("0/sd/small/3"),
+                       small[3].cpu())
+    # restore into targets whose zeroing is still queued on the default stream
+    out_big = torch.ones_like(big)
+    out_small = [torch.ones(1000, device=gpu) for _ in range(8)]
+    for _ in range(10):
+        a = torch.tanh(a @ a) * 0.5
+    out_big.mul_(0)
+    for s in out_small:
+        s.mul_(0)
+    Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(big=out_big, small=out_small)})
+    assert torch.equal(out_big, big) and all(torch.equal(x, small[0]) for x in out_small)
