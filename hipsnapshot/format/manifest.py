@@ -386,7 +386,8 @@ class SnapshotMetadata:
         self.__dict__["_json_async"] = (t, box)
 
     # Reference name (metadata is JSON, which is valid YAML).
-    to_yaml = to_json
+    def to_yaml(self) -> str:
+        return self.to_json()
 
     @classmethod
     def from_dict(cls, d: Dict[str, Any]) -> "SnapshotMetadata":
@@ -430,3 +431,42 @@ def iter_tensor_entries(entry: Entry):
     elif isinstance(entry, ShardedTensorEntry):
         for s in entry.shards:
             yield s.tensor
+
+
+class LazySnapshotMetadata(SnapshotMetadata):
+    """Metadata assembled as JSON text (per-rank pre-encoded fragments joined
+    on the committing rank); entry objects are only materialised if someone
+    reads ``manifest``.  Keeps the 8-rank manifest encode/decode off the
+    take's critical path."""
+
+    def __init__(self, text: str, version: str, world_size: int) -> None:
+        self.version = version
+        self.world_size = world_size
+        self._text: Optional[str] = text
+        self._manifest: Optional[Manifest] = None
+
+    @property
+    def manifest(self) -> Manifest:  # type: ignore[override]
+        if self._manifest is None:
+            self._manifest = SnapshotMetadata.from_json(self._text).manifest
+        return self._manifest
+
+    @manifest.setter
+    def manifest(self, value: Manifest) -> None:
+        self._manifest = value
+        self._text = None
+
+    def to_json(self) -> str:
+        if self._text is not None and self._manifest is None:
+            return self._text
+        return SnapshotMetadata.to_json(self)
+
+
+def entry_json(entry: Entry) -> str:
+    return json.dumps(entry.to_dict(), sort_keys=False, separators=(",", ":"))
+
+
+def metadata_json_from_parts(version: str, world_size: int, parts: List[str]) -> str:
+    """``parts`` = ``'"<rank>/<path>":<entry json>'`` strings in manifest order."""
+    return ('{"version":' + json.dumps(version) + ',"world_size":' + str(int(world_size))
+            + ',"manifest":{' + ",".join(parts) + "}}")

@@ -24,6 +24,7 @@ import asyncio
 import copy
 import fnmatch
 import itertools
+import json
 import logging
 import os
 import socket
@@ -50,10 +51,14 @@ from .engine.scheduler import (
 from .format.flatten import flatten, inflate
 from .format.manifest import (
     Entry,
+    LazySnapshotMetadata,
     PrimitiveEntry,
     ShardedTensorEntry,
     SnapshotMetadata,
+    entry_json,
     is_container_entry,
+    is_replicated,
+    metadata_json_from_parts,
 )
 from .io.batcher import batch_read_requests, batch_write_requests
 from .io.preparer import prepare_read, prepare_write
@@ -276,7 +281,7 @@ class Snapshot:
         manifest.update(primitives)
         manifest.update(object_entries)
         with timeline.span("gather_manifest"):
-            manifest = cls._gather_manifest(manifest, comm)
+            metadata = cls._gather_metadata(manifest, comm)
 
         budget = get_process_memory_budget_bytes(comm)
         deferred: List[WriteReq] = []
@@ -293,10 +298,6 @@ class Snapshot:
             from .engine.scheduler import DeferredIOWork
 
             pending = DeferredIOWork(pending, deferred, storage, budget, rank)
-        metadata = SnapshotMetadata(version=__version__, world_size=comm.get_world_size(),
-                                    manifest=manifest)
-        if comm.get_rank() == 0:
-            metadata.serialize_in_background()
         return pending, metadata
 
     # --------------------------------------------------------------- restore
@@ -493,6 +494,28 @@ class Snapshot:
         gathered: List[Any] = [None] * ws
         comm.all_gather_object(gathered, mine)
         return set.intersection(*[set(g) for g in gathered])
+
+    @staticmethod
+    def _gather_metadata(manifest: Dict[str, Entry], comm: Comm) -> SnapshotMetadata:
+        """ONE all-gather of (replicated entries, pre-encoded JSON fragments of
+        every other entry).  Each rank JSON-encodes its own entries in
+        parallel; the committing rank only consolidates the replicated ones
+        and joins strings (reference: all-gather of entry objects, then rank 0
+        encodes the whole manifest, `snapshot.py:842-853`)."""
+        rep = {k: e for k, e in manifest.items() if is_replicated(e)}
+        frags = [(k, entry_json(e)) for k, e in manifest.items() if k not in rep]
+        ws = comm.get_world_size()
+        gathered: List[Any] = [None] * ws
+        comm.all_gather_object(gathered, (rep, frags))
+        rank_reps = consolidate_replicated_entries([g[0] for g in gathered])
+        parts = []
+        for rank, (_, fr) in enumerate(gathered):
+            for logical, js in fr:
+                parts.append(json.dumps(f"{rank}/{logical}") + ":" + js)
+            for logical, entry in rank_reps[rank].items():
+                parts.append(json.dumps(f"{rank}/{logical}") + ":" + entry_json(entry))
+        return LazySnapshotMetadata(metadata_json_from_parts(__version__, ws, parts),
+                                    __version__, ws)
 
     @staticmethod
     def _gather_manifest(manifest: Dict[str, Entry], comm: Comm) -> Dict[str, Entry]:

@@ -111,3 +111,41 @@ def test_unknown_entry_type_rejected():
     with pytest.raises(ValueError):
         SnapshotMetadata.from_json(json.dumps(
             {"version": "0.1.0", "world_size": 1, "manifest": {"0/x": {"type": "Bogus"}}}))
+
+
+def test_fragment_joined_metadata_matches_object_encoding():
+    """take() joins per-rank pre-encoded JSON fragments; the result must equal
+    encoding the consolidated manifest objects."""
+    import json
+
+    from hipsnapshot.format.manifest import (LazySnapshotMetadata, SnapshotMetadata, entry_json,
+                                             metadata_json_from_parts)
+    from hipsnapshot.snapshot import Snapshot
+
+    class OneRank:
+        def get_world_size(self):
+            return 1
+
+        def get_rank(self):
+            return 0
+
+        def all_gather_object(self, out, obj):
+            out[0] = obj
+
+    man = {
+        "m/w": TensorEntry("0/m/w", "buffer_protocol", "torch.float32", [3, 4], False),
+        "m/r": TensorEntry("replicated/m/r", "buffer_protocol", "torch.bfloat16", [8], True,
+                           codec={"name": "hsz1", "w": 2, "frame_bytes": 256, "blob_bytes": 16}),
+        "m/s": PrimitiveEntry.from_object("a/b\"c", replicated=False),
+    }
+    md = Snapshot._gather_metadata(dict(man), OneRank())
+    assert isinstance(md, LazySnapshotMetadata)
+    ref = SnapshotMetadata(version=md.version, world_size=1,
+                           manifest={"0/m/w": man["m/w"], "0/m/s": man["m/s"],
+                                     "0/m/r": man["m/r"]})
+    assert json.loads(md.to_json()) == ref.to_dict()
+    assert list(md.manifest) == ["0/m/w", "0/m/s", "0/m/r"]
+    assert md.manifest["0/m/r"].codec["name"] == "hsz1"
+    assert metadata_json_from_parts("0.1.0", 2, []) == \
+        '{"version":"0.1.0","world_size":2,"manifest":{}}'
+    assert json.loads(entry_json(man["m/w"])) == man["m/w"].to_dict()
