@@ -145,6 +145,18 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
     out: List[WriteReq] = []
     slabs: Dict[Optional[torch.device], List[Slab]] = {}
     relocation: Dict[str, Tuple[str, int, int]] = {}
+    # Tail taper: slabs are staged in creation order after the big blobs, and
+    # one file is written by one thread (buffered writes to a file serialize
+    # on its inode lock), so the LAST slab's write is the take's tail.  Once
+    # less than 2 slabs' worth of batchable bytes remain on a device, close
+    # slabs at a quarter of the threshold.
+    remaining: Dict[Optional[torch.device], int] = defaultdict(int)
+    for wr in write_reqs:
+        st = wr.buffer_stager
+        if is_batchable(st):
+            nb = st.tensor.numel() * st.tensor.element_size()
+            if nb < threshold:
+                remaining[st.tensor.device if st.tensor.is_cuda else None] += nb
     for wr in write_reqs:
         st = wr.buffer_stager
         if not is_batchable(st):
@@ -156,6 +168,9 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
             out.append(wr)
             continue
         dev = t.device if t.is_cuda else None
+        remaining[dev] -= nbytes
+        cap = threshold if remaining[dev] + nbytes > 2 * threshold else \
+            max(threshold // 4, min(threshold, 16 << 20))
 
         def _new_slab(k: int) -> Slab:
             if name_prefix is None:
@@ -164,7 +179,7 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
             return Slab(dev, f"{name_prefix}_{tag}_{k}")
 
         lst = slabs.setdefault(dev, [_new_slab(0)])
-        if lst[-1].members and _align(lst[-1].sz_bytes, align) + nbytes >= threshold:
+        if lst[-1].members and _align(lst[-1].sz_bytes, align) + nbytes >= cap:
             lst.append(_new_slab(len(lst)))
         lo, hi = lst[-1].add(nbytes, st, align)
         relocation[wr.path] = (lst[-1].location, lo, hi)

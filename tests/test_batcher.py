@@ -114,3 +114,18 @@ def test_merged_read_consuming_cost_counts_merged_buffer():
     (merged,) = batch_read_requests(rrs)
     lo, hi = merged.byte_range
     assert merged.buffer_consumer.get_consuming_cost_bytes() == (hi - lo) + 4 * 40
+
+
+def test_slab_tail_taper():
+    """The last slabs are closed early so the final (serial, per-file) write of
+    a take is short; packing of the bulk follows the threshold."""
+    ts = [torch.zeros(5 << 20, dtype=torch.uint8) for _ in range(40)]  # 200 MiB
+    entries, wrs = [], []
+    for i, t in enumerate(ts):
+        e, w = prepare_write(t, f"sd/{i}", 0, replicated=False)
+        entries.append(e)
+        wrs += w
+    _, batched = batch_write_requests(entries, wrs, slab_size_threshold_bytes=64 << 20)
+    sizes = [w.buffer_stager.total for w in batched]
+    assert max(sizes) < 64 << 20 and sizes[0] > 50 << 20
+    assert sizes[-1] <= 16 << 20 and sum(sizes) >= 200 << 20
