@@ -56,20 +56,34 @@ def _rank_split(metadata: SnapshotMetadata) -> Tuple[List[Dict[str, Entry]],
     return per_rank, merged
 
 
+def _fresh(entries: Dict[str, Entry]) -> Dict[str, Entry]:
+    """A copy the restore path may mutate: new dict, new container entries
+    (their ``keys`` lists are edited by the elasticity helpers); leaf entries
+    are never mutated and are shared with the cached split (a deep copy of an
+    8-rank FSDP manifest cost ~100 ms per restore)."""
+    out = {}
+    for logical, e in entries.items():
+        if is_dict_entry(e):
+            e = copy.copy(e)
+            e.keys = list(e.keys)
+        out[logical] = e
+    return out
+
+
 def get_manifest_for_rank(metadata: SnapshotMetadata, rank: int
                           ) -> Tuple[Manifest, Dict[str, ShardedTensorEntry]]:
     per_rank, merged = _rank_split(metadata)
-    merged = copy.deepcopy(merged)
+    merged = dict(merged)
     if rank < metadata.world_size:
-        local = copy.deepcopy(per_rank[rank])
+        local = _fresh(per_rank[rank])
         for logical, e in per_rank[0].items():
             if is_replicated(e):
-                local[logical] = copy.deepcopy(e)
+                local[logical] = e
         for logical, e in list(local.items()):
             if isinstance(e, ShardedTensorEntry):
                 local[logical] = merged[logical]
         return local, merged
-    local = copy.deepcopy(per_rank[0])
+    local = _fresh(per_rank[0])
     for logical in list(local):
         e = local.get(logical)
         if e is None or is_container_entry(e) or is_replicated(e):

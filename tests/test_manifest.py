@@ -149,3 +149,30 @@ def test_fragment_joined_metadata_matches_object_encoding():
     assert metadata_json_from_parts("0.1.0", 2, []) == \
         '{"version":"0.1.0","world_size":2,"manifest":{}}'
     assert json.loads(entry_json(man["m/w"])) == man["m/w"].to_dict()
+
+
+def test_manifest_for_rank_copies_are_independent():
+    """Restore mutates the per-rank view (elasticity adds/drops entries and
+    edits dict keys); the cached split must not see those edits."""
+    from hipsnapshot.format.manifest import DictEntry, Shard, ShardedTensorEntry
+
+    def te(loc):
+        return TensorEntry(loc, "buffer_protocol", "torch.float32", [2, 2], False)
+
+    man = {
+        "0/sd": DictEntry(keys=["a", "w"]),
+        "0/sd/a": te("0/sd/a"),
+        "0/sd/w": ShardedTensorEntry([Shard([0, 0], [1, 2], te("sharded/sd/w_0_0"))]),
+        "1/sd": DictEntry(keys=["a", "w"]),
+        "1/sd/a": te("1/sd/a"),
+        "1/sd/w": ShardedTensorEntry([Shard([1, 0], [1, 2], te("sharded/sd/w_1_0"))]),
+    }
+    md = SnapshotMetadata(version="0.1.0", world_size=2, manifest=man)
+    local, merged = get_manifest_for_rank(md, 0)
+    assert len(local["sd/w"].shards) == 2
+    local["sd"].keys.remove("a")
+    del local["sd/a"]
+    merged.clear()
+    again, merged2 = get_manifest_for_rank(md, 0)
+    assert again["sd"].keys == ["a", "w"] and "sd/a" in again and "sd/w" in merged2
+    assert man["0/sd"].keys == ["a", "w"]
