@@ -397,6 +397,13 @@ class SnapshotMetadata:
 
     @classmethod
     def from_json(cls, text: str) -> "SnapshotMetadata":
+        from ..utils.tracing import paused_gc
+
+        with paused_gc():
+            return cls._from_json(text)
+
+    @classmethod
+    def _from_json(cls, text: str) -> "SnapshotMetadata":
         try:
             d = json.loads(text)
         except json.JSONDecodeError:

@@ -70,7 +70,7 @@ from .parallel.partitioner import consolidate_replicated_entries, partition_writ
 from .parallel.store import LinearBarrier, get_or_create_store
 from .stateful import AppState, RNGState, Stateful
 from .storage.registry import url_to_storage_plugin_in_event_loop
-from .utils.tracing import roctx_range, timeline
+from .utils.tracing import paused_gc, roctx_range, timeline
 from .version import __version__
 
 logger = logging.getLogger(__name__)
@@ -129,6 +129,13 @@ class Snapshot:
         bf16); default from ``HIPSNAPSHOT_COMPRESSION`` ("none").
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.take")
+        with paused_gc():
+            return cls._take(path, app_state, pg, replicated, storage_options,
+                             _custom_tensor_prepare_func, quantize, compression)
+
+    @classmethod
+    def _take(cls, path, app_state, pg, replicated, storage_options,
+              _custom_tensor_prepare_func, quantize, compression) -> "Snapshot":
         cls._validate_app_state(app_state)
         loop = asyncio.new_event_loop()
         comm = Comm(pg)
@@ -174,6 +181,13 @@ class Snapshot:
         committed regardless.
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.async_take")
+        with paused_gc():
+            return cls._async_take(path, app_state, pg, replicated, storage_options,
+                                   _custom_tensor_prepare_func, quantize, compression)
+
+    @classmethod
+    def _async_take(cls, path, app_state, pg, replicated, storage_options,
+                    _custom_tensor_prepare_func, quantize, compression) -> "PendingSnapshot":
         cls._validate_app_state(app_state)
         loop = asyncio.new_event_loop()
         comm = Comm(pg)
@@ -305,6 +319,10 @@ class Snapshot:
     def restore(self, app_state: AppState) -> None:
         """Restore ``app_state`` in place from this snapshot."""
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.restore")
+        with paused_gc():
+            self._restore(app_state)
+
+    def _restore(self, app_state: AppState) -> None:
         self._validate_app_state(app_state)
         loop = asyncio.new_event_loop()
         comm = Comm(self.pg)

@@ -153,3 +153,23 @@ class Timeline:
 
 
 timeline = Timeline()
+
+
+@contextlib.contextmanager
+def paused_gc():
+    """Suspend Python's cyclic GC for a bounded critical section.
+
+    Planning a snapshot allocates tens of thousands of small objects (entries,
+    requests, futures); in a training process with a large heap that triggers
+    generation-2 collections costing 10-100 ms each in the middle of a take
+    (measured: parsing an 8-rank manifest 129 ms with GC vs 16 ms without).
+    Garbage created meanwhile is collected after the section."""
+    import gc
+
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
