@@ -1,21 +1,36 @@
-// hsz: HSZ1 lossless exponent-nibble codec on gfx950 (format: hipsnapshot/ops/codec.py).
+// hsz: HSZ1 lossless exponent-entropy codec on gfx950 (format: hipsnapshot/ops/codec.py).
 //
-// Encode (before D2H) = 3 launches on the caller's stream:
+// Encode (before D2H) = 4 launches on the caller's stream:
 //   hsz_analyze<W>  one workgroup per 256 KiB frame: 2048-sample LDS histogram
 //                   -> 15-entry dictionary (wave-wide argmax), then a full pass
-//                   counting escapes -> frame mode + coded size
+//                   over the frame.  For 2-byte elements that pass keeps one
+//                   16-bin index histogram per lane in LDS; thread 0 builds the
+//                   length-limited Huffman code and every lane sizes its own
+//                   stream, so the frame mode (raw / nibble / huffman) and the
+//                   exact coded size are known before anything is written
 //   hsz_layout      one workgroup: exclusive scan of frame sizes, blob header +
 //                   frame table, total size for the host
-//   hsz_encode<W>   one workgroup per frame: 8 elements per lane per step,
-//                   coalesced 16-B loads, nibble codes via an LDS code table,
-//                   low-byte plane stores; the rare escapes go to an LDS list
-//                   and are written in element order by rank
-// Decode (after H2D) = 1 launch, one workgroup per frame (escape positions are
-// collected from the nibble plane first, then every element is rebuilt).
+//   hsz_encode<W>   modes 0/1, one workgroup per frame: 8 elements per lane per
+//                   step, coalesced 16-B loads, nibble codes via an LDS code
+//                   table, low-byte plane stores; the rare escapes go to an LDS
+//                   list and are written in element order by rank
+//   hsz_encode2     mode 2: lane t packs the codes of element groups t, t+256,
+//                   ... into its own bit stream in LDS (stream offsets from a
+//                   block scan of the analyze pass's lane sizes) while the
+//                   low-byte plane streams out with 8-B stores; the finished
+//                   streams leave LDS with coalesced 4-B stores
+// Decode (after H2D) = 2 launches, one workgroup per frame each:
+//   hsz_decode<W>   modes 0/1 (escape positions are collected from the nibble
+//                   plane first, then every element is rebuilt)
+//   hsz_decode2     mode 2: the frame's streams are staged in LDS, lane t
+//                   decodes its stream through a 2048-entry LDS lookup table
+//                   and stores its groups as 16-B vectors (adjacent lanes ->
+//                   adjacent groups, so the stores coalesce); escapes are
+//                   patched in element order after a barrier
 //
 // A frame is one workgroup (4 waves): a 512 MiB blob has 2048 frames, 8x the
 // CU count, so the grid fills the chip; all traffic is streaming HBM
-// (read 2 B + write 1.5 B per bf16 element encoded).
+// (read 2 B + write ~1.34 B per bf16 element encoded).
 
 #include <hip/hip_runtime.h>
 
@@ -25,21 +40,28 @@
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kLanes = 256;  // mode-2 lane streams per frame == threads per workgroup
 constexpr int kSample = 2048;
 constexpr int kMaxEsc = 1024;
 constexpr int kHeader = 64;
 constexpr int kFrameHeader = 32;
 constexpr int kEsc = 15;
+constexpr int kMaxLen = 11;
+constexpr int kLut = 1 << kMaxLen;
+constexpr uint32_t kMaxCoded = 65535;
+constexpr int kLaneTable = 2 * kLanes;
 
 struct FrameMeta {
   uint32_t mode;
   uint32_t n_esc;
-  uint32_t nsel;  // dictionary entries actually selected (rest are 0 padding)
-  uint32_t pad;
+  uint32_t nsel;   // dictionary entries actually selected (rest are 0 padding)
+  uint32_t coded;  // mode 2: total stream bytes
   uint8_t dict[16];
-  uint64_t size;    // padded frame bytes
-  uint64_t offset;  // absolute offset in the blob
+  uint8_t lens[16];  // mode 2 code lengths
+  uint64_t size;     // padded frame bytes
+  uint64_t offset;   // absolute offset in the blob
 };
+// meta buffer = FrameMeta[n_frames] followed by uint16 lane_bytes[n_frames][256]
 
 __device__ __forceinline__ uint64_t align16(uint64_t n) { return (n + 15) & ~uint64_t(15); }
 
@@ -52,6 +74,24 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
   int t = red[0] + red[1] + red[2] + red[3];
   __syncthreads();
   return t;
+}
+
+// Exclusive prefix sum over the 256 threads; *total receives the sum.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int i = 0; i < wid; ++i) base += wsum[i];
+  if (threadIdx.x == 0) *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return base + x - v;
 }
 
 // The 15 most frequent values of hist (count desc, value asc); zero counts are
@@ -92,10 +132,99 @@ __device__ void build_dict(const uint32_t* hist, uint8_t* dict, uint8_t* code_of
   __syncthreads();
 }
 
+// Huffman code lengths of the 16 indices (mirror of codec.huffman_lengths).
+// One thread; the node arrays live in LDS (runtime-indexed register arrays
+// would go to scratch).  Leaves are nodes 0..15, merged nodes 16..30.
+__device__ void huffman_lengths(const uint32_t* cnt, uint8_t* lens, uint32_t* w, int* par) {
+  int k = 0;
+  for (int c = 0; c < 16; ++c) {
+    w[c] = cnt[c];
+    par[c] = cnt[c] ? -1 : -2;
+    lens[c] = 0;
+    k += cnt[c] != 0;
+  }
+  if (k == 0) return;
+  if (k == 1) {
+    for (int c = 0; c < 16; ++c)
+      if (cnt[c]) lens[c] = 1;
+    return;
+  }
+  int m = 16;
+  for (int step = 0; step < k - 1; ++step) {
+    int a = -1, b = -1;
+    for (int i = 0; i < m; ++i)
+      if (par[i] == -1 && (a < 0 || w[i] < w[a])) a = i;
+    par[a] = -3;
+    for (int i = 0; i < m; ++i)
+      if (par[i] == -1 && (b < 0 || w[i] < w[b])) b = i;
+    w[m] = w[a] + w[b];
+    par[m] = -1;
+    par[a] = m;
+    par[b] = m;
+    ++m;
+  }
+  int maxl = 0;
+  for (int c = 0; c < 16; ++c) {
+    if (!cnt[c]) continue;
+    int d = 0;
+    for (int j = c; par[j] >= 0; j = par[j]) ++d;
+    lens[c] = uint8_t(d);
+    maxl = d > maxl ? d : maxl;
+  }
+  if (maxl <= kMaxLen) return;
+  for (int c = 0; c < 16; ++c)
+    if (lens[c] > kMaxLen) lens[c] = kMaxLen;
+  for (;;) {
+    uint32_t kraft = 0;
+    for (int c = 0; c < 16; ++c)
+      if (cnt[c]) kraft += 1u << (kMaxLen - lens[c]);
+    if (kraft <= (1u << kMaxLen)) break;
+    int s = -1;
+    for (int c = 0; c < 16; ++c) {
+      if (!cnt[c] || lens[c] >= kMaxLen) continue;
+      if (s < 0 || lens[c] > lens[s] || (lens[c] == lens[s] && cnt[c] <= cnt[s])) s = c;
+    }
+    ++lens[s];
+  }
+}
+
+// Bit-reversed canonical codewords (mirror of codec.canonical_codes); one thread.
+__device__ void canonical_codes(const uint8_t* lens, uint16_t* codes) {
+  for (int c = 0; c < 16; ++c) codes[c] = 0;
+  uint32_t code = 0;
+  int prev = 0;
+  bool first = true;
+  for (int l = 1; l <= kMaxLen; ++l)
+    for (int c = 0; c < 16; ++c) {
+      if (lens[c] != l) continue;
+      if (!first) code = (code + 1) << (l - prev);
+      first = false;
+      prev = l;
+      uint32_t rev = 0;
+      for (int b = 0; b < l; ++b) rev |= ((code >> b) & 1u) << (l - 1 - b);
+      codes[c] = uint16_t(rev);
+    }
+}
+
+// The 8 high bytes of element group g (elements 8g..8g+7, 2-byte elements).
+__device__ __forceinline__ void load_group(const uint8_t* s, uint64_t g, bool aligned,
+                                           uint32_t wd[4]) {
+  if (aligned) {
+    const uint4 v = reinterpret_cast<const uint4*>(s)[g];
+    wd[0] = v.x; wd[1] = v.y; wd[2] = v.z; wd[3] = v.w;
+  } else {
+    const uint8_t* p = s + 16 * g;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      wd[q] = uint32_t(p[4 * q]) | (uint32_t(p[4 * q + 1]) << 8) | (uint32_t(p[4 * q + 2]) << 16) |
+              (uint32_t(p[4 * q + 3]) << 24);
+  }
+}
+
 template <int W>
 __global__ void __launch_bounds__(kThreads)
 hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
-            FrameMeta* __restrict__ meta) {
+            FrameMeta* __restrict__ meta, uint16_t* __restrict__ lane_bytes_all) {
   __shared__ uint32_t hist[256];
   __shared__ uint8_t dict[16];
   __shared__ uint8_t code_of[256];
@@ -115,6 +244,72 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   }
   __syncthreads();
   build_dict(hist, dict, code_of, &nsel);
+  const uint64_t tail = len - n * W;
+  const uint64_t coded1 = kFrameHeader + (n + 1) / 2 + uint64_t(W - 1) * n + tail;  // + escapes
+  const uint64_t raw = kFrameHeader + len;
+  if constexpr (W == 2) {
+    if (n > 0 && n % 8 == 0) {
+      // mode-2 sizing: one 16-bin histogram per lane (lane t owns groups t, t+256, ...)
+      __shared__ uint32_t lcnt[16 * kLanes];
+      __shared__ uint32_t fcnt[16];
+      __shared__ uint8_t hlen[16];
+      __shared__ uint32_t hw[32];
+      __shared__ int hpar[32];
+      for (int i = threadIdx.x; i < 16 * kLanes; i += kThreads) lcnt[i] = 0;
+      __syncthreads();
+      const uint64_t groups = n / 8;
+      const bool aligned = (reinterpret_cast<uintptr_t>(s) & 15) == 0;
+      for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+        uint32_t wd[4];
+        load_group(s, g, aligned, wd);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t c = code_of[(wd[q] >> (16 * h + 8)) & 255];
+            lcnt[c * kLanes + threadIdx.x] += 1;
+          }
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x < 16) {
+        uint32_t sum = 0;
+        for (int l = 0; l < kLanes; ++l) sum += lcnt[threadIdx.x * kLanes + l];
+        fcnt[threadIdx.x] = sum;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) huffman_lengths(fcnt, hlen, hw, hpar);
+      __syncthreads();
+      uint32_t bits = 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) bits += lcnt[c * kLanes + threadIdx.x] * hlen[c];
+      const uint32_t lb = (bits + 7) / 8;
+      lane_bytes_all[f * kLanes + threadIdx.x] = uint16_t(lb < 65535u ? lb : 65535u);
+      const int c_bytes = block_sum(int(lb), red);
+      if (threadIdx.x == 0) {
+        const uint32_t esc = fcnt[kEsc];
+        const uint64_t size1 = coded1 + esc;
+        const uint64_t size2 = kFrameHeader + n + kLaneTable + uint64_t(c_bytes) + esc + tail;
+        FrameMeta m;
+        m.mode = 0;
+        if (esc <= uint32_t(kMaxEsc)) {
+          if (uint32_t(c_bytes) <= kMaxCoded && size2 < size1 && size2 < raw) m.mode = 2;
+          else if (size1 < raw) m.mode = 1;
+        }
+        m.n_esc = m.mode ? esc : 0;
+        m.nsel = m.mode ? nsel : 0;
+        m.coded = m.mode == 2 ? uint32_t(c_bytes) : 0;
+        for (int j = 0; j < 16; ++j) {
+          m.dict[j] = m.mode ? dict[j] : 0;
+          m.lens[j] = m.mode == 2 ? hlen[j] : 0;
+        }
+        m.size = align16(m.mode == 2 ? size2 : (m.mode == 1 ? size1 : raw));
+        m.offset = 0;
+        meta[f] = m;
+      }
+      return;
+    }
+  }
   int esc = 0;
   if (((reinterpret_cast<uintptr_t>(s)) & 15) == 0) {
     const uint64_t nv = (n * W) / 16;  // whole 16-B vectors of elements
@@ -132,14 +327,16 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   }
   const int total = block_sum(esc, red);
   if (threadIdx.x == 0) {
-    const uint64_t coded = kFrameHeader + (n + 1) / 2 + uint64_t(W - 1) * n + total + (len - n * W);
-    const uint64_t raw = kFrameHeader + len;
+    const uint64_t coded = coded1 + total;
     FrameMeta m;
     m.mode = (total <= kMaxEsc && coded < raw && n > 0) ? 1 : 0;
     m.n_esc = m.mode ? total : 0;
     m.nsel = m.mode ? nsel : 0;
-    m.pad = 0;
-    for (int j = 0; j < 16; ++j) m.dict[j] = m.mode ? dict[j] : 0;
+    m.coded = 0;
+    for (int j = 0; j < 16; ++j) {
+      m.dict[j] = m.mode ? dict[j] : 0;
+      m.lens[j] = 0;
+    }
     m.size = align16(m.mode ? coded : raw);
     m.offset = 0;
     meta[f] = m;
@@ -180,7 +377,7 @@ hsz_layout(FrameMeta* __restrict__ meta, uint32_t n_frames, uint8_t* __restrict_
     *total = carry;
     uint32_t* h32 = reinterpret_cast<uint32_t*>(out);
     h32[0] = 0x315a5348u;  // "HSZ1"
-    h32[1] = 1;
+    h32[1] = 2;            // format version
     *reinterpret_cast<uint64_t*>(out + 8) = logical;
     h32[4] = w;
     h32[5] = frame_bytes;
@@ -202,6 +399,19 @@ __device__ void write_escapes(const uint32_t* eidx, const uint8_t* evals, int n_
   }
 }
 
+// Frame header bytes 0..31 (mode, n_esc, dict, mode-2 code lengths).
+__device__ __forceinline__ void write_frame_header(const FrameMeta& m, uint8_t* fr) {
+  if (threadIdx.x < kFrameHeader) {
+    uint8_t b = 0;
+    const int t = threadIdx.x;
+    if (t == 0) b = uint8_t(m.mode);
+    else if (t >= 4 && t < 8) b = uint8_t(m.n_esc >> (8 * (t - 4)));
+    else if (t >= 8 && t < 24) b = m.dict[t - 8];
+    else if (t >= 24) b = uint8_t(m.lens[2 * (t - 24)] | (m.lens[2 * (t - 24) + 1] << 4));
+    fr[t] = b;
+  }
+}
+
 template <int W>
 __global__ void __launch_bounds__(kThreads)
 hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
@@ -211,20 +421,14 @@ hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_byt
   __shared__ uint8_t evals[kMaxEsc];
   __shared__ int ecount;
   const uint64_t f = blockIdx.x;
+  const FrameMeta& m = meta[f];  // arrays indexed at run time: read from memory
+  if (m.mode == 2) return;  // hsz_encode2
   const uint64_t base = f * frame_bytes;
   const uint64_t len = min(uint64_t(frame_bytes), logical - base);
   const uint64_t n = len / W;
   const uint8_t* s = src + base;
-  const FrameMeta m = meta[f];
   uint8_t* fr = out + m.offset;
-  if (threadIdx.x < kFrameHeader) {
-    uint8_t b = 0;
-    const int t = threadIdx.x;
-    if (t == 0) b = uint8_t(m.mode);
-    else if (t >= 4 && t < 8) b = uint8_t(m.n_esc >> (8 * (t - 4)));
-    else if (t >= 8 && t < 24) b = m.dict[t - 8];
-    fr[t] = b;
-  }
+  write_frame_header(m, fr);
   uint8_t* body = fr + kFrameHeader;
   const uint64_t padded_end = m.size - kFrameHeader;  // body bytes incl. padding
   if (m.mode == 0) {
@@ -348,6 +552,103 @@ hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_byt
     tail[j] = j < tail_len ? s[n * W + j] : 0;
 }
 
+// Mode-2 encoder (2-byte elements).  LDS: 64 KiB stream buffer + escapes.
+__global__ void __launch_bounds__(kThreads)
+hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+            const FrameMeta* __restrict__ meta, const uint16_t* __restrict__ lane_bytes_all,
+            uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t coded[kMaxCoded + 1];
+  __shared__ uint8_t code_of[256];
+  __shared__ uint16_t hcode[16];
+  __shared__ uint8_t hlen[16];
+  __shared__ uint32_t eidx[kMaxEsc];
+  __shared__ uint8_t evals[kMaxEsc];
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t ctotal;
+  __shared__ int ecount;
+  const uint64_t f = blockIdx.x;
+  const FrameMeta& m = meta[f];  // arrays indexed at run time: read from memory
+  if (m.mode != 2) return;
+  const uint64_t base = f * frame_bytes;
+  const uint64_t len = min(uint64_t(frame_bytes), logical - base);
+  const uint64_t n = len / 2;
+  const uint8_t* s = src + base;
+  uint8_t* fr = out + m.offset;
+  write_frame_header(m, fr);
+  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[v] = kEsc;
+  if (threadIdx.x == 0) {
+    ecount = 0;
+    for (int c = 0; c < 16; ++c) hlen[c] = m.lens[c];
+    canonical_codes(hlen, hcode);
+  }
+  __syncthreads();
+  if (threadIdx.x < m.nsel) code_of[m.dict[threadIdx.x]] = uint8_t(threadIdx.x);
+  const uint32_t lb = lane_bytes_all[f * kLanes + threadIdx.x];
+  const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);  // syncs: code_of is ready
+  uint8_t* body = fr + kFrameHeader;
+  uint8_t* lo = body;
+  uint16_t* table = reinterpret_cast<uint16_t*>(body + n);  // n % 8 == 0: aligned
+  table[threadIdx.x] = uint16_t(lb);
+  uint8_t* streams = body + n + kLaneTable;
+  const uint64_t groups = n / 8;
+  const bool aligned = (reinterpret_cast<uintptr_t>(s) & 15) == 0;
+  const bool lo_aligned = (reinterpret_cast<uintptr_t>(lo) & 7) == 0;
+  uint32_t pos = loff, acc = 0;
+  int nb = 0;
+  for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+    uint32_t wd[4];
+    load_group(s, g, aligned, wd);
+    uint64_t lob = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = q * 2 + h;
+        const uint32_t hi = (wd[q] >> (16 * h + 8)) & 255;
+        lob |= uint64_t((wd[q] >> (16 * h)) & 255) << (8 * e);
+        const uint32_t c = code_of[hi];
+        if (c == kEsc) {
+          const int k = atomicAdd(&ecount, 1);
+          if (k < kMaxEsc) { eidx[k] = uint32_t(g * 8 + e); evals[k] = uint8_t(hi); }
+        }
+        acc |= uint32_t(hcode[c]) << nb;
+        nb += hlen[c];
+        while (nb >= 8) {
+          coded[pos++] = uint8_t(acc);
+          acc >>= 8;
+          nb -= 8;
+        }
+      }
+    }
+    if (lo_aligned) {
+      reinterpret_cast<uint64_t*>(lo)[g] = lob;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) lo[8 * g + e] = uint8_t(lob >> (8 * e));
+    }
+  }
+  if (nb > 0) coded[pos] = uint8_t(acc);
+  __syncthreads();
+  const uint32_t c_bytes = m.coded;
+  if ((reinterpret_cast<uintptr_t>(streams) & 3) == 0) {
+    const uint32_t nw = c_bytes / 4;
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(coded);
+    uint32_t* sw = reinterpret_cast<uint32_t*>(streams);
+    for (uint32_t i = threadIdx.x; i < nw; i += kThreads) sw[i] = cw[i];
+    for (uint32_t j = nw * 4 + threadIdx.x; j < c_bytes; j += kThreads) streams[j] = coded[j];
+  } else {
+    for (uint32_t j = threadIdx.x; j < c_bytes; j += kThreads) streams[j] = coded[j];
+  }
+  uint8_t* escp = streams + c_bytes;
+  write_escapes(eidx, evals, min(ecount, kMaxEsc), escp);
+  uint8_t* tail = escp + m.n_esc;
+  const uint64_t tail_len = len - 2 * n;
+  const uint64_t used = uint64_t(tail - body);
+  const uint64_t padded_end = m.size - kFrameHeader;
+  for (uint64_t j = threadIdx.x; used + j < padded_end; j += kThreads)
+    tail[j] = j < tail_len ? s[2 * n + j] : 0;
+}
+
 template <int W>
 __global__ void __launch_bounds__(kThreads)
 hsz_decode(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
@@ -366,6 +667,7 @@ hsz_decode(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offs
   uint8_t* o = out + fl * uint64_t(frame_bytes);
   const int mode = fr[0];
   const uint8_t* body = fr + kFrameHeader;
+  if (mode == 2) return;  // hsz_decode2
   if (mode == 0) {
     if ((((reinterpret_cast<uintptr_t>(o)) | reinterpret_cast<uintptr_t>(body)) & 15) == 0) {
       const uint64_t nv = len / 16;
@@ -486,6 +788,139 @@ hsz_decode(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offs
   for (uint64_t j = threadIdx.x; j < len - n * W; j += kThreads) o[n * W + j] = tail[j];
 }
 
+// Mode-2 decoder (2-byte elements).  A frame whose fields do not fit its
+// stored extent is left undecoded (the host validated the frame table).
+__global__ void __launch_bounds__(kThreads)
+hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+            uint32_t first_frame, uint64_t logical, uint32_t frame_bytes,
+            uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t coded[kMaxCoded + 1 + 8];
+  __shared__ uint16_t lut[kLut];
+  __shared__ uint16_t hcode[16];
+  __shared__ uint8_t hlen[16];
+  __shared__ uint8_t dict[16];
+  __shared__ uint32_t eidx[kMaxEsc];
+  __shared__ uint32_t sorted[kMaxEsc];
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t ctotal;
+  __shared__ int ecount;
+  __shared__ int valid;
+  const uint64_t fl = blockIdx.x;
+  const uint64_t f = first_frame + fl;
+  const uint64_t base = f * frame_bytes;
+  const uint64_t len = min(uint64_t(frame_bytes), logical - base);
+  const uint64_t n = len / 2;
+  const uint8_t* fr = frames + offsets[fl];
+  const uint64_t extent = offsets[fl + 1] - offsets[fl];
+  if (fr[0] != 2) return;
+  uint8_t* o = out + fl * uint64_t(frame_bytes);
+  const uint32_t n_esc = *reinterpret_cast<const uint32_t*>(fr + 4);
+  if (threadIdx.x < 16) {
+    dict[threadIdx.x] = fr[8 + threadIdx.x];
+    hlen[threadIdx.x] = (fr[24 + threadIdx.x / 2] >> (4 * (threadIdx.x & 1))) & 15;
+  }
+  if (threadIdx.x == 0) ecount = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ok = n % 8 == 0 && n_esc <= uint32_t(kMaxEsc) && kFrameHeader + n + kLaneTable <= extent;
+    for (int c = 0; c < 16; ++c) ok &= hlen[c] <= kMaxLen;
+    valid = ok;
+    canonical_codes(hlen, hcode);
+  }
+  __syncthreads();
+  if (!valid) return;
+  for (int x = threadIdx.x; x < kLut; x += kThreads) {
+    uint16_t ent = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int l = hlen[c];
+      if (l && (uint32_t(x) & ((1u << l) - 1)) == hcode[c]) ent = uint16_t(c | (l << 8));
+    }
+    lut[x] = ent;
+  }
+  const uint8_t* body = fr + kFrameHeader;
+  const uint8_t* lo = body;
+  const uint32_t lb = reinterpret_cast<const uint16_t*>(body + n)[threadIdx.x];
+  const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);
+  const uint32_t c_bytes = ctotal;
+  const uint64_t tail_len = len - 2 * n;
+  if (c_bytes > kMaxCoded ||
+      kFrameHeader + n + kLaneTable + c_bytes + n_esc + tail_len > extent)
+    return;  // uniform across the workgroup (ctotal is shared)
+  const uint8_t* streams = body + n + kLaneTable;
+  if ((reinterpret_cast<uintptr_t>(streams) & 3) == 0) {
+    const uint32_t nw = c_bytes / 4;
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(streams);
+    uint32_t* cw = reinterpret_cast<uint32_t*>(coded);
+    for (uint32_t i = threadIdx.x; i < nw; i += kThreads) cw[i] = sw[i];
+    for (uint32_t j = nw * 4 + threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
+  } else {
+    for (uint32_t j = threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
+  }
+  __syncthreads();
+  const uint64_t groups = n / 8;
+  const bool vec = ((reinterpret_cast<uintptr_t>(o) & 15) | (reinterpret_cast<uintptr_t>(lo) & 7)) == 0;
+  const uint32_t end = loff + lb;
+  uint32_t pos = loff;
+  uint64_t acc = 0;
+  int nb = 0;
+  for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+    uint64_t lob;
+    if (vec) {
+      lob = reinterpret_cast<const uint64_t*>(lo)[g];
+    } else {
+      lob = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) lob |= uint64_t(lo[8 * g + e]) << (8 * e);
+    }
+    uint32_t wd[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (nb < kMaxLen) {
+        while (nb <= 56) {
+          acc |= uint64_t(pos < end ? coded[pos] : 0) << nb;
+          ++pos;
+          nb += 8;
+        }
+      }
+      const uint32_t ent = lut[acc & (kLut - 1)];
+      uint32_t l = ent >> 8;
+      uint32_t c = ent & 15;
+      if (l == 0) { l = kMaxLen; c = 0; }  // corrupt stream: keep going, bounded
+      acc >>= l;
+      nb -= int(l);
+      uint32_t hi = dict[c];
+      if (c == kEsc) {
+        const int k = atomicAdd(&ecount, 1);
+        if (k < kMaxEsc) eidx[k] = uint32_t(g * 8 + e);
+        hi = 0;
+      }
+      wd[e >> 1] |= (uint32_t((lob >> (8 * e)) & 255) | (hi << 8)) << (16 * (e & 1));
+    }
+    if (vec) {
+      reinterpret_cast<uint4*>(o)[g] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) o[16 * g + 4 * q + b] = uint8_t(wd[q] >> (8 * b));
+    }
+  }
+  // the barrier orders every wave's element stores before the escape patches
+  __syncthreads();
+  const uint8_t* escv = streams + c_bytes;
+  const int ne = min(min(ecount, kMaxEsc), int(n_esc));
+  for (int i = threadIdx.x; i < ne; i += kThreads) {
+    const uint32_t me = eidx[i];
+    int rank = 0;
+    for (int j = 0; j < ne; ++j) rank += eidx[j] < me;
+    sorted[rank] = me;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ne; i += kThreads) o[2 * uint64_t(sorted[i]) + 1] = escv[i];
+  if (tail_len && threadIdx.x == 0) o[2 * n] = escv[n_esc];
+}
+
 thread_local char g_hsz_err[256];
 
 int fail(const char* what, hipError_t e) {
@@ -499,7 +934,9 @@ extern "C" {
 
 const char* hsg_hsz_last_error() { return g_hsz_err; }
 
-uint64_t hsg_hsz_meta_bytes(uint32_t n_frames) { return uint64_t(n_frames) * sizeof(FrameMeta); }
+uint64_t hsg_hsz_meta_bytes(uint32_t n_frames) {
+  return uint64_t(n_frames) * (sizeof(FrameMeta) + sizeof(uint16_t) * kLanes);
+}
 
 // Encode `logical` bytes at device `src` (16-B aligned) into device `out`
 // (capacity >= max_encoded_bytes).  `meta` = device scratch of
@@ -514,12 +951,13 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
   hipStream_t s = static_cast<hipStream_t>(stream);
   auto* src8 = static_cast<const uint8_t*>(src);
   auto* m = static_cast<FrameMeta*>(meta);
+  auto* lanes = reinterpret_cast<uint16_t*>(m + nf);
   auto* o = static_cast<uint8_t*>(out);
   switch (w) {
-    case 1: hipLaunchKernelGGL(hsz_analyze<1>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m); break;
-    case 2: hipLaunchKernelGGL(hsz_analyze<2>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m); break;
-    case 4: hipLaunchKernelGGL(hsz_analyze<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m); break;
-    case 8: hipLaunchKernelGGL(hsz_analyze<8>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m); break;
+    case 1: hipLaunchKernelGGL(hsz_analyze<1>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes); break;
+    case 2: hipLaunchKernelGGL(hsz_analyze<2>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes); break;
+    case 4: hipLaunchKernelGGL(hsz_analyze<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes); break;
+    case 8: hipLaunchKernelGGL(hsz_analyze<8>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes); break;
     default: return -1001;
   }
   hipLaunchKernelGGL(hsz_layout, dim3(1), dim3(1024), 0, s, m, nf, o, logical, uint32_t(w),
@@ -530,13 +968,16 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
     case 4: hipLaunchKernelGGL(hsz_encode<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
     default: hipLaunchKernelGGL(hsz_encode<8>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
   }
+  if (w == 2)
+    hipLaunchKernelGGL(hsz_encode2, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m,
+                       lanes, o);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("hsz encode launch", e);
 }
 
 // Decode `count` frames starting at global frame `first` into `out` (logical
-// bytes of those frames).  `offsets` (device, count entries) are byte offsets
-// of each frame relative to `frames`.
+// bytes of those frames).  `offsets` (device, count + 1 entries) are byte
+// offsets of each frame relative to `frames`, then the end of the last one.
 int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t first,
                    uint32_t count, uint64_t logical, int w, uint32_t frame_bytes, void* out,
                    void* stream) {
@@ -554,6 +995,9 @@ int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t fi
     case 8: hipLaunchKernelGGL(hsz_decode<8>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
     default: return -1001;
   }
+  if (w == 2)
+    hipLaunchKernelGGL(hsz_decode2, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical,
+                       frame_bytes, o);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("hsz decode launch", e);
 }

@@ -2,7 +2,9 @@
 //
 // Used for CPU tensors on save and for CPU destinations on restore.  Frames
 // are independent, so a blob is split across threads by frame; within a frame
-// the loops are plain byte loops the compiler vectorises.
+// the loops are plain byte loops the compiler vectorises.  Mode 2 (Huffman
+// coded indices, 2-byte elements) follows the NumPy reference bit for bit:
+// same code-length construction, same 256-lane stream split.
 
 #include <algorithm>
 #include <atomic>
@@ -18,8 +20,88 @@ constexpr uint32_t kMaxEsc = 1024;
 constexpr uint64_t kHeader = 64;
 constexpr uint64_t kFrameHeader = 32;
 constexpr uint8_t kEsc = 15;
+constexpr int kLanes = 256;
+constexpr uint64_t kLaneTable = 2 * kLanes;
+constexpr int kMaxLen = 11;
+constexpr uint64_t kMaxCoded = 65535;
 
 inline uint64_t align16(uint64_t n) { return (n + 15) & ~uint64_t(15); }
+
+// Code lengths of the 16 indices (mirror of codec.huffman_lengths).
+void huffman_lengths(const uint64_t cnt[16], uint8_t lens[16]) {
+  std::memset(lens, 0, 16);
+  int k = 0;
+  for (int c = 0; c < 16; ++c) k += cnt[c] != 0;
+  if (k == 0) return;
+  if (k == 1) {
+    for (int c = 0; c < 16; ++c)
+      if (cnt[c]) lens[c] = 1;
+    return;
+  }
+  // nodes 0..15 are the leaves (dead when unused), merged nodes from 16 on:
+  // the same relative order as the reference's numbering, so ties agree
+  uint64_t w[32];
+  int par[32];  // -1 live root, -2 unused leaf, >= 0 parent
+  for (int c = 0; c < 16; ++c) {
+    w[c] = cnt[c];
+    par[c] = cnt[c] ? -1 : -2;
+  }
+  int m = 16;
+  for (int step = 0; step < k - 1; ++step) {
+    int a = -1, b = -1;
+    for (int i = 0; i < m; ++i)
+      if (par[i] == -1 && (a < 0 || w[i] < w[a])) a = i;
+    par[a] = -3;
+    for (int i = 0; i < m; ++i)
+      if (par[i] == -1 && (b < 0 || w[i] < w[b])) b = i;
+    w[m] = w[a] + w[b];
+    par[m] = -1;
+    par[a] = m;
+    par[b] = m;
+    ++m;
+  }
+  int maxl = 0;
+  for (int c = 0; c < 16; ++c) {
+    if (!cnt[c]) continue;
+    int d = 0;
+    for (int j = c; par[j] >= 0; j = par[j]) ++d;
+    lens[c] = uint8_t(d);
+    maxl = std::max(maxl, d);
+  }
+  if (maxl <= kMaxLen) return;
+  for (int c = 0; c < 16; ++c)
+    if (lens[c] > kMaxLen) lens[c] = kMaxLen;
+  for (;;) {
+    uint32_t kraft = 0;
+    for (int c = 0; c < 16; ++c)
+      if (cnt[c]) kraft += 1u << (kMaxLen - lens[c]);
+    if (kraft <= (1u << kMaxLen)) break;
+    int s = -1;
+    for (int c = 0; c < 16; ++c) {
+      if (!cnt[c] || lens[c] >= kMaxLen) continue;
+      if (s < 0 || lens[c] > lens[s] || (lens[c] == lens[s] && cnt[c] <= cnt[s])) s = c;
+    }
+    ++lens[s];
+  }
+}
+
+// Bit-reversed canonical codewords (mirror of codec.canonical_codes).
+void canonical_codes(const uint8_t lens[16], uint16_t codes[16]) {
+  std::memset(codes, 0, 16 * sizeof(uint16_t));
+  uint32_t code = 0;
+  int prev = 0;
+  bool first = true;
+  for (int l = 1; l <= kMaxLen; ++l)
+    for (int c = 0; c < 16; ++c) {
+      if (lens[c] != l) continue;
+      if (!first) code = (code + 1) << (l - prev);
+      first = false;
+      prev = l;
+      uint32_t rev = 0;
+      for (int b = 0; b < l; ++b) rev |= ((code >> b) & 1u) << (l - 1 - b);
+      codes[c] = uint16_t(rev);
+    }
+}
 
 struct Plan {
   uint8_t mode = 0;
@@ -27,6 +109,9 @@ struct Plan {
   int nsel = 0;
   uint8_t dict[16] = {0};
   uint8_t code_of[256];
+  uint8_t lens[16] = {0};
+  uint16_t lane_bytes[kLanes] = {0};
+  uint64_t coded = 0;  // mode 2 stream bytes
   uint64_t size = 0;
 };
 
@@ -47,21 +132,58 @@ void plan_frame(const uint8_t* s, uint64_t len, int w, Plan* p) {
   p->nsel = k;
   std::memset(p->code_of, kEsc, 256);
   for (int j = 0; j < k; ++j) p->code_of[p->dict[j]] = uint8_t(j);
+  const bool m2 = w == 2 && n > 0 && n % 8 == 0;
   uint64_t esc = 0;
-  for (uint64_t e = 0; e < n; ++e) esc += p->code_of[s[e * w + w - 1]] == kEsc;
-  const uint64_t coded = kFrameHeader + (n + 1) / 2 + uint64_t(w - 1) * n + esc + (len - n * w);
-  const uint64_t raw = kFrameHeader + len;
-  if (n > 0 && esc <= kMaxEsc && coded < raw) {
-    p->mode = 1;
-    p->n_esc = uint32_t(esc);
-    p->size = align16(coded);
+  std::vector<uint32_t> lane_cnt;  // [lane][16]
+  uint64_t cnt[16] = {0};
+  if (m2) {
+    lane_cnt.assign(size_t(kLanes) * 16, 0);
+    for (uint64_t e = 0; e < n; ++e) {
+      const uint8_t c = p->code_of[s[2 * e + 1]];
+      ++lane_cnt[((e >> 3) & (kLanes - 1)) * 16 + c];
+    }
+    for (int l = 0; l < kLanes; ++l)
+      for (int c = 0; c < 16; ++c) cnt[c] += lane_cnt[size_t(l) * 16 + c];
+    esc = cnt[kEsc];
   } else {
-    p->mode = 0;
+    for (uint64_t e = 0; e < n; ++e) esc += p->code_of[s[e * w + w - 1]] == kEsc;
+  }
+  const uint64_t tail = len - n * w;
+  const uint64_t coded1 = kFrameHeader + (n + 1) / 2 + uint64_t(w - 1) * n + esc + tail;
+  const uint64_t raw = kFrameHeader + len;
+  p->mode = 0;
+  if (n > 0 && esc <= kMaxEsc) {
+    if (m2) {
+      huffman_lengths(cnt, p->lens);
+      uint64_t c_bytes = 0;
+      for (int l = 0; l < kLanes; ++l) {
+        uint64_t bits = 0;
+        for (int c = 0; c < 16; ++c) bits += uint64_t(lane_cnt[size_t(l) * 16 + c]) * p->lens[c];
+        const uint64_t b = (bits + 7) / 8;
+        p->lane_bytes[l] = uint16_t(std::min<uint64_t>(b, 65535));
+        c_bytes += b;
+      }
+      const uint64_t size2 = kFrameHeader + n + kLaneTable + c_bytes + esc + tail;
+      if (c_bytes <= kMaxCoded && size2 < coded1 && size2 < raw) {
+        p->mode = 2;
+        p->coded = c_bytes;
+        p->size = align16(size2);
+      }
+    }
+    if (p->mode == 0 && coded1 < raw) {
+      p->mode = 1;
+      p->size = align16(coded1);
+    }
+  }
+  if (p->mode == 0) {
     p->n_esc = 0;
     p->nsel = 0;
     std::memset(p->dict, 0, 16);
     p->size = align16(raw);
+  } else {
+    p->n_esc = uint32_t(esc);
   }
+  if (p->mode != 2) std::memset(p->lens, 0, 16);
 }
 
 void encode_frame(const uint8_t* s, uint64_t len, int w, const Plan& p, uint8_t* fr) {
@@ -77,27 +199,60 @@ void encode_frame(const uint8_t* s, uint64_t len, int w, const Plan& p, uint8_t*
     return;
   }
   const uint64_t n = len / w;
-  const uint64_t nb = (n + 1) / 2;
-  uint8_t* nib = body;
-  uint8_t* lo = body + nb;
-  uint8_t* esc = lo + uint64_t(w - 1) * n;
+  uint8_t* esc;
   uint32_t ne = 0;
-  for (uint64_t pr = 0; pr < nb; ++pr) {
-    uint8_t byte = 0;
-    for (int h = 0; h < 2; ++h) {
-      const uint64_t e = 2 * pr + h;
-      if (e >= n) break;
-      const uint8_t* el = s + e * w;
-      const uint8_t c = p.code_of[el[w - 1]];
-      byte |= uint8_t(c << (4 * h));
-      if (c == kEsc) esc[ne++] = el[w - 1];
-    }
-    nib[pr] = byte;
-  }
-  if (w == 2) {
+  if (p.mode == 2) {
+    for (int j = 0; j < 8; ++j) fr[24 + j] = uint8_t(p.lens[2 * j] | (p.lens[2 * j + 1] << 4));
+    uint16_t codes[16];
+    canonical_codes(p.lens, codes);
+    uint8_t* lo = body;
     for (uint64_t e = 0; e < n; ++e) lo[e] = s[2 * e];
+    uint8_t* table = body + n;
+    std::memcpy(table, p.lane_bytes, kLaneTable);  // little-endian host
+    uint8_t* streams = table + kLaneTable;
+    const uint64_t groups = n / 8;
+    uint64_t pos = 0;
+    for (int l = 0; l < kLanes; ++l) {
+      uint32_t acc = 0;
+      int nb = 0;
+      for (uint64_t g = uint64_t(l); g < groups; g += kLanes)
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t c = p.code_of[s[2 * (8 * g + e) + 1]];
+          acc |= uint32_t(codes[c]) << nb;
+          nb += p.lens[c];
+          while (nb >= 8) {
+            streams[pos++] = uint8_t(acc);
+            acc >>= 8;
+            nb -= 8;
+          }
+        }
+      if (nb > 0) streams[pos++] = uint8_t(acc);
+    }
+    esc = streams + p.coded;
+    for (uint64_t e = 0; e < n; ++e)
+      if (p.code_of[s[2 * e + 1]] == kEsc) esc[ne++] = s[2 * e + 1];
   } else {
-    for (uint64_t e = 0; e < n; ++e) std::memcpy(lo + e * (w - 1), s + e * w, w - 1);
+    const uint64_t nb = (n + 1) / 2;
+    uint8_t* nib = body;
+    uint8_t* lo = body + nb;
+    esc = lo + uint64_t(w - 1) * n;
+    for (uint64_t pr = 0; pr < nb; ++pr) {
+      uint8_t byte = 0;
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t e = 2 * pr + h;
+        if (e >= n) break;
+        const uint8_t* el = s + e * w;
+        const uint8_t c = p.code_of[el[w - 1]];
+        byte |= uint8_t(c << (4 * h));
+        if (c == kEsc) esc[ne++] = el[w - 1];
+      }
+      nib[pr] = byte;
+    }
+    if (w == 2) {
+      for (uint64_t e = 0; e < n; ++e) lo[e] = s[2 * e];
+    } else {
+      for (uint64_t e = 0; e < n; ++e) std::memcpy(lo + e * (w - 1), s + e * w, w - 1);
+    }
   }
   uint8_t* tail = esc + ne;
   const uint64_t tail_len = len - n * w;
@@ -106,17 +261,85 @@ void encode_frame(const uint8_t* s, uint64_t len, int w, const Plan& p, uint8_t*
   std::memset(body + used, 0, body_cap - used);
 }
 
-void decode_frame(const uint8_t* fr, uint64_t len, int w, uint8_t* o) {
+// Mode-2 frame body -> logical bytes.  `extent` = the frame's stored size.
+int decode_frame2(const uint8_t* fr, uint64_t extent, uint64_t len, uint8_t* o) {
+  uint32_t n_esc;
+  std::memcpy(&n_esc, fr + 4, 4);
+  const uint8_t* dict = fr + 8;
+  uint8_t lens[16];
+  for (int c = 0; c < 16; ++c) lens[c] = (fr[24 + c / 2] >> (4 * (c & 1))) & 15;
+  for (int c = 0; c < 16; ++c)
+    if (lens[c] > kMaxLen) return -74;
+  const uint64_t n = len / 2;
+  if (n % 8 || n_esc > kMaxEsc) return -74;
+  const uint8_t* body = fr + kFrameHeader;
+  if (kFrameHeader + n + kLaneTable > extent) return -74;
+  const uint8_t* lo = body;
+  uint16_t lane_bytes[kLanes];
+  std::memcpy(lane_bytes, body + n, kLaneTable);
+  uint64_t c_bytes = 0;
+  for (int l = 0; l < kLanes; ++l) c_bytes += lane_bytes[l];
+  const uint64_t tail = len - 2 * n;
+  if (kFrameHeader + n + kLaneTable + c_bytes + n_esc + tail > extent) return -74;
+  const uint8_t* streams = body + n + kLaneTable;
+  const uint8_t* escv = streams + c_bytes;
+  uint16_t codes[16];
+  canonical_codes(lens, codes);
+  uint16_t lut[1 << kMaxLen];
+  for (uint32_t x = 0; x < (1u << kMaxLen); ++x) {
+    uint16_t ent = 0;
+    for (int c = 0; c < 16; ++c)
+      if (lens[c] && (x & ((1u << lens[c]) - 1)) == codes[c]) ent = uint16_t(c | (lens[c] << 8));
+    lut[x] = ent;
+  }
+  std::vector<uint8_t> idx(n);
+  const uint64_t groups = n / 8;
+  uint64_t start = 0;
+  for (int l = 0; l < kLanes; ++l) {
+    const uint64_t end = start + lane_bytes[l];
+    uint64_t pos = start, acc = 0;
+    int nb = 0;
+    for (uint64_t g = uint64_t(l); g < groups; g += kLanes)
+      for (int e = 0; e < 8; ++e) {
+        while (nb <= 56 && pos < end) {
+          acc |= uint64_t(streams[pos++]) << nb;
+          nb += 8;
+        }
+        const uint16_t ent = lut[acc & ((1u << kMaxLen) - 1)];
+        const int ln = ent >> 8;
+        if (ln == 0 || ln > nb) return -74;
+        acc >>= ln;
+        nb -= ln;
+        idx[8 * g + e] = uint8_t(ent & 15);
+      }
+    start = end;
+  }
+  uint32_t ne = 0;
+  for (uint64_t e = 0; e < n; ++e) {
+    const uint8_t c = idx[e];
+    o[2 * e] = lo[e];
+    o[2 * e + 1] = c == kEsc ? (ne < n_esc ? escv[ne++] : 0) : dict[c];
+  }
+  if (tail) std::memcpy(o + 2 * n, escv + n_esc, tail);
+  return 0;
+}
+
+int decode_frame(const uint8_t* fr, uint64_t extent, uint64_t len, int w, uint8_t* o) {
   const uint8_t* body = fr + kFrameHeader;
   if (fr[0] == 0) {
+    if (kFrameHeader + len > extent) return -74;
     std::memcpy(o, body, len);
-    return;
+    return 0;
   }
+  if (fr[0] == 2) return w == 2 ? decode_frame2(fr, extent, len, o) : -74;
+  if (fr[0] != 1) return -74;
   uint32_t n_esc;
   std::memcpy(&n_esc, fr + 4, 4);
   const uint8_t* dict = fr + 8;
   const uint64_t n = len / w;
   const uint64_t nb = (n + 1) / 2;
+  if (kFrameHeader + nb + uint64_t(w - 1) * n + uint64_t(n_esc) + (len - n * w) > extent)
+    return -74;
   const uint8_t* nib = body;
   const uint8_t* lo = body + nb;
   const uint8_t* esc = lo + uint64_t(w - 1) * n;
@@ -135,6 +358,7 @@ void decode_frame(const uint8_t* fr, uint64_t len, int w, uint8_t* o) {
     d[w - 1] = hi;
   }
   std::memcpy(o + n * w, esc + n_esc, len - n * w);
+  return 0;
 }
 
 template <typename F>
@@ -183,7 +407,7 @@ int64_t hsz_encode_cpu(const void* src, uint64_t logical, int w, uint32_t frame_
   for (uint32_t f = 0; f < nf; ++f) offs[f + 1] = offs[f] + plans[f].size;
   std::memset(o, 0, start);
   std::memcpy(o, "HSZ1", 4);
-  const uint32_t ver = 1;
+  const uint32_t ver = 2;
   std::memcpy(o + 4, &ver, 4);
   std::memcpy(o + 8, &logical, 8);
   const uint32_t w32 = uint32_t(w);
@@ -198,20 +422,28 @@ int64_t hsz_encode_cpu(const void* src, uint64_t logical, int w, uint32_t frame_
 }
 
 // Decode frames [first, first+count) of a blob whose frame bytes start at
-// `frames`; offsets[i] = byte offset of frame first+i relative to `frames`.
-// Output = the logical bytes of those frames.  Returns 0 or < 0.
+// `frames`; offsets[i] (i <= count) = byte offset of frame first+i relative to
+// `frames`, offsets[count] = end of the last frame.  Output = the logical
+// bytes of those frames.  Returns 0, or < 0 for a corrupt frame.
 int hsz_decode_cpu(const void* frames, const uint64_t* offsets, uint32_t first, uint32_t count,
                    uint64_t logical, int w, uint32_t frame_bytes, void* out, int nthreads) {
   if (w < 1 || w > 8) return -22;
   const auto* fr = static_cast<const uint8_t*>(frames);
   auto* o = static_cast<uint8_t*>(out);
+  std::atomic<int> err{0};
   parallel_frames(count, nthreads, [&](uint32_t i) {
     const uint64_t f = uint64_t(first) + i;
     const uint64_t lo = f * frame_bytes;
     const uint64_t len = std::min<uint64_t>(frame_bytes, logical - lo);
-    decode_frame(fr + offsets[i], len, w, o + uint64_t(i) * frame_bytes);
+    if (offsets[i + 1] < offsets[i] + kFrameHeader) {
+      err = -74;
+      return;
+    }
+    const int r = decode_frame(fr + offsets[i], offsets[i + 1] - offsets[i], len, w,
+                               o + uint64_t(i) * frame_bytes);
+    if (r) err = r;
   });
-  return 0;
+  return err.load();
 }
 
 }  // extern "C"

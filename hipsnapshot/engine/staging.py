@@ -444,7 +444,7 @@ def _scatter_compressed(span, regions, dev: int, producer: Optional[int] = None)
                 and dst.data_ptr() % 16 == 0):
             direct = dst
     enc = torch.empty(c_n, dtype=torch.uint8, device=f"cuda:{dev}")
-    offs = torch.tensor([o - c_lo for o in h.offsets[first:last]], dtype=torch.int64)
+    offs = torch.tensor([o - c_lo for o in h.offsets[first:last + 1]], dtype=torch.int64)
     offs_dev = torch.empty(offs.numel(), dtype=torch.int64, device=f"cuda:{dev}")
     out = None if direct is not None else torch.empty(log_n, dtype=torch.uint8,
                                                      device=f"cuda:{dev}")

@@ -132,7 +132,7 @@ class CompressedSpan:
         n_log = min(self.last * h.frame_bytes, h.logical_size) - self.frames_logical_lo
         out = np.empty(max(n_log, 1), dtype=np.uint8)
         base = h.offsets[self.first]
-        offs = np.asarray([o - base for o in h.offsets[self.first: self.last]],
+        offs = np.asarray([o - base for o in h.offsets[self.first: self.last + 1]],
                           dtype=np.uint64)
         if self.last > self.first:
             from .ops import native

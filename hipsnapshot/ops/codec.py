@@ -1,4 +1,4 @@
-"""HSZ1: lossless exponent-nibble compression for floating-point checkpoint blobs.
+"""HSZ1: lossless exponent-entropy compression for floating-point checkpoint blobs.
 
 Why: a snapshot is bound by bytes moved -- PCIe D2H on one MI355X (57 GB/s
 measured), host page-cache bandwidth when 8 ranks write at once.  The high
@@ -7,33 +7,55 @@ of information for trained or initialised weights (measured in
 ``tests/test_codec.py``), the other bytes are near-random.  HSZ1 keeps the
 low bytes verbatim and codes each high byte as a 4-bit index into a per-frame
 15-entry dictionary (index 15 = escape, value stored separately): bf16 blobs
-shrink to ~75 %, fp32 to ~87.5 %, bit-exactly.  Frames that do not compress
-are stored raw, so any byte stream is accepted.
+shrink to ~75 %, fp32 to ~87.5 %, bit-exactly.  For 2-byte elements a frame
+may instead Huffman-code those 16 indices (mode 2, ~2.7 bits per element), so
+bf16 blobs shrink to ~67 %.  Frames that do not compress are stored raw, so
+any byte stream is accepted.
 
-Encoding and decoding run on the GPU (``hs_hsz_*`` kernels in
-``csrc/hsgpu.hip``) before D2H / after H2D, and on the CPU in C++
-(``hsz_*`` in ``csrc/hsio.cpp``).  This module holds the format definition,
-a NumPy reference implementation used by the tests, and the helpers that
-parse headers / map logical byte ranges to frames.
+Encoding and decoding run on the GPU (``csrc/hsz.hip``) before D2H / after
+H2D, and on the CPU in C++ (``csrc/hsz_cpu.cpp``).  This module holds the
+format definition, a NumPy reference implementation used by the tests (the
+native coders must match it byte for byte), and the helpers that parse
+headers / map logical byte ranges to frames.
 
 Blob layout (little endian)::
 
-    header   64 B   magic "HSZ1", u32 version=1, u64 logical_size,
+    header   64 B   magic "HSZ1", u32 version, u64 logical_size,
                     u32 elem_width w, u32 frame_bytes F, u32 n_frames, pad
     table    8*(n_frames+1) B   absolute offset of every frame, then the blob size
-    frame i  header 32 B  u8 mode (0 raw, 1 nibble), 3 pad, u32 n_escapes,
-                          u8 dict[16], 8 pad
+    frame i  header 32 B  u8 mode (0 raw, 1 nibble, 2 huffman), 3 pad,
+                          u32 n_escapes, u8 dict[16],
+                          u8 lens[8] (mode 2: code length of index 2j in the
+                          low nibble of byte j, of index 2j+1 in the high one)
              mode 0: the frame's logical bytes
              mode 1: nibbles   ceil(n/2) B  (element 2k low nibble, 2k+1 high)
                      low bytes (w-1)*n B   (each element without its high byte)
                      escapes   n_escapes B (high bytes of code-15 elements, in order)
                      tail      (len - n*w) B raw
+             mode 2 (w == 2 and n % 8 == 0 only):
+                     low bytes n B
+                     lane table 256 x u16: byte length of each lane's stream
+                     streams   the 256 lane streams back to back; lane t codes
+                               the indices of element groups t, t+256, t+512, ...
+                               (group g = elements 8g..8g+7) with canonical
+                               Huffman codes packed LSB-first (bit-reversed
+                               codewords), each stream zero-padded to a byte
+                     escapes   n_escapes B (element order), tail (len - 2n) B
              padded to 16 B
     where n = len // w elements of the frame's len logical bytes.
 
 Dictionary: the 15 most frequent high bytes of a deterministic 2048-element
 sample of the frame (count descending, value ascending); a frame is coded
 only if it has at most ``MAX_ESCAPES`` escapes and the coded size is smaller.
+Mode 2 code lengths come from the frame's exact index histogram (Huffman with
+deterministic tie-breaks, limited to ``HUFF_MAX_LEN`` bits: ``huffman_lengths``).
+The lane split gives one GPU lane one stream to decode while the workgroup's
+loads and stores stay coalesced.  Mode 2 is chosen when it is the smallest
+encoding and its streams fit in ``HUFF_MAX_CODED`` bytes (LDS-resident on the
+GPU).  Version-1 blobs (modes 0/1 only) decode unchanged.
+
+Native decoders take ``count + 1`` frame offsets so every frame's extent is
+known and corrupt frame bodies cannot make them read past it.
 """
 
 from __future__ import annotations
@@ -45,7 +67,7 @@ from typing import List, Tuple
 import numpy as np
 
 MAGIC = b"HSZ1"
-VERSION = 1
+VERSION = 2
 HEADER_BYTES = 64
 FRAME_HEADER_BYTES = 32
 DEFAULT_FRAME_BYTES = 256 * 1024
@@ -53,6 +75,10 @@ SAMPLE = 2048
 MAX_ESCAPES = 1024
 ESC = 15
 CODEC_NAME = "hsz1"
+LANES = 256
+LANE_TABLE_BYTES = 2 * LANES
+HUFF_MAX_LEN = 11
+HUFF_MAX_CODED = 65535
 
 
 def _align16(n: int) -> int:
@@ -101,7 +127,7 @@ def parse_header(buf) -> Header:
     if bytes(mv[:4]) != MAGIC:
         raise ValueError("not an HSZ1 blob")
     version, logical, w, fb, nf = struct.unpack_from("<IQIII", mv, 4)
-    if version != VERSION:
+    if version not in (1, VERSION):
         raise ValueError(f"unsupported HSZ1 version {version}")
     need = HEADER_BYTES + table_bytes(nf)
     if len(mv) < need:
@@ -113,6 +139,86 @@ def parse_header(buf) -> Header:
 def header_probe_bytes(max_frames: int = 4096) -> int:
     """Bytes to read to be sure to get the header of most blobs in one read."""
     return HEADER_BYTES + table_bytes(max_frames)
+
+
+# ---------------------------------------------------------------------------
+# Huffman code construction (mirrored exactly by csrc/hsz_cpu.cpp and hsz.hip)
+# ---------------------------------------------------------------------------
+
+def huffman_lengths(counts) -> List[int]:
+    """Code lengths for the 16 dictionary indices from their counts.
+
+    Huffman merges the two lightest live nodes, ties going to the lower node
+    index (leaves are numbered by ascending index value, merged nodes after
+    them in creation order).  If the longest code exceeds ``HUFF_MAX_LEN``,
+    every length is clamped and, while the Kraft sum exceeds 1, the longest
+    code shorter than the limit is lengthened by one (ties: the rarer index,
+    then the larger index).  A single used index gets length 1.
+    """
+    cnt = [int(c) for c in counts]
+    active = [c for c in range(16) if cnt[c] > 0]
+    lens = [0] * 16
+    if not active:
+        return lens
+    if len(active) == 1:
+        lens[active[0]] = 1
+        return lens
+    weight = [cnt[c] for c in active]
+    parent = [-1] * len(active)
+    alive = list(range(len(active)))
+    while len(alive) > 1:
+        a = min(alive, key=lambda i: (weight[i], i))
+        alive.remove(a)
+        b = min(alive, key=lambda i: (weight[i], i))
+        alive.remove(b)
+        weight.append(weight[a] + weight[b])
+        parent.append(-1)
+        parent[a] = parent[b] = len(weight) - 1
+        alive.append(len(weight) - 1)
+    for i, c in enumerate(active):
+        d, j = 0, i
+        while parent[j] != -1:
+            j = parent[j]
+            d += 1
+        lens[c] = d
+    if max(lens) > HUFF_MAX_LEN:
+        lens = [min(x, HUFF_MAX_LEN) for x in lens]
+        while sum(1 << (HUFF_MAX_LEN - lens[c]) for c in active) > (1 << HUFF_MAX_LEN):
+            s = max((c for c in active if lens[c] < HUFF_MAX_LEN),
+                    key=lambda c: (lens[c], -cnt[c], c))
+            lens[s] += 1
+    return lens
+
+
+def canonical_codes(lens) -> List[int]:
+    """Bit-reversed canonical codewords (LSB-first emission) for ``lens``."""
+    codes = [0] * 16
+    code, prev, first = 0, 0, True
+    for ln in range(1, HUFF_MAX_LEN + 1):
+        for c in range(16):
+            if lens[c] != ln:
+                continue
+            if not first:
+                code = (code + 1) << (ln - prev)
+            first = False
+            prev = ln
+            rev = 0
+            for k in range(ln):
+                rev |= ((code >> k) & 1) << (ln - 1 - k)
+            codes[c] = rev
+    return codes
+
+
+def decode_table(lens) -> np.ndarray:
+    """2^HUFF_MAX_LEN-entry LUT: bits 0-3 index, bits 8+ code length (0 = invalid)."""
+    codes = canonical_codes(lens)
+    lut = np.zeros(1 << HUFF_MAX_LEN, dtype=np.uint16)
+    x = np.arange(1 << HUFF_MAX_LEN)
+    for c in range(16):
+        if lens[c]:
+            hit = (x & ((1 << lens[c]) - 1)) == codes[c]
+            lut[hit] = c | (lens[c] << 8)
+    return lut
 
 
 # ---------------------------------------------------------------------------
@@ -131,12 +237,49 @@ def _frame_dict(hi: np.ndarray) -> np.ndarray:
     return d, len(chosen)
 
 
+def _raw_frame(data: np.ndarray) -> bytes:
+    return struct.pack("<B3xI16s8x", 0, 0, bytes(16)) + data.tobytes()
+
+
+def _lane_layout(codes: np.ndarray, lens: List[int]):
+    """Stream order and bit offsets of a mode-2 frame's codes.
+
+    Returns (order, bit_offset, code_length, lane_bytes): ``order`` lists the
+    element indices in stream order (lane, then group, then position in the
+    group) and ``bit_offset`` is each one's first bit in the concatenated,
+    byte-padded lane streams."""
+    g = codes.size // 8
+    grp = np.arange(g)
+    lane_of_group = grp % LANES
+    grp_order = np.lexsort((grp, lane_of_group))
+    order = (grp_order[:, None] * 8 + np.arange(8)[None, :]).reshape(-1)
+    ln = np.asarray(lens, dtype=np.int64)[codes[order]]
+    lane_of_el = lane_of_group[order // 8]
+    lane_bits = np.bincount(lane_of_el, weights=ln, minlength=LANES).astype(np.int64)
+    lane_bytes = (lane_bits + 7) // 8
+    lane_start_bit = np.concatenate([[0], np.cumsum(lane_bytes)[:-1]]) * 8
+    excl = np.concatenate([[0], np.cumsum(ln)])
+    lane_first = np.concatenate([[0], np.cumsum(np.bincount(lane_of_el, minlength=LANES))[:-1]])
+    bit_off = lane_start_bit[lane_of_el] + excl[:-1] - excl[lane_first][lane_of_el]
+    return order, bit_off, ln, lane_bytes
+
+
+def _huffman_streams(codes: np.ndarray, lens: List[int]) -> Tuple[bytes, np.ndarray]:
+    order, bit_off, ln, lane_bytes = _lane_layout(codes, lens)
+    bits = np.zeros(int(lane_bytes.sum()) * 8, dtype=np.uint8)
+    rev = np.asarray(canonical_codes(lens), dtype=np.int64)[codes[order]]
+    for k in range(HUFF_MAX_LEN):
+        m = ln > k
+        bits[bit_off[m] + k] = (rev[m] >> k) & 1
+    return np.packbits(bits, bitorder="little").tobytes(), lane_bytes
+
+
 def _encode_frame(data: np.ndarray, w: int) -> bytes:
     length = data.size
     n = length // w
     raw = FRAME_HEADER_BYTES + length
     if n == 0:
-        return struct.pack("<B3xI16s8x", 0, 0, bytes(16)) + data.tobytes()
+        return _raw_frame(data)
     el = data[: n * w].reshape(n, w)
     hi = el[:, w - 1]
     d, k = _frame_dict(hi)
@@ -145,14 +288,27 @@ def _encode_frame(data: np.ndarray, w: int) -> bytes:
     codes = code_of[hi]
     esc_mask = codes == ESC
     n_esc = int(esc_mask.sum())
-    coded = FRAME_HEADER_BYTES + (n + 1) // 2 + (w - 1) * n + n_esc + (length - n * w)
-    if n_esc > MAX_ESCAPES or coded >= raw:
-        return struct.pack("<B3xI16s8x", 0, 0, bytes(16)) + data.tobytes()
+    tail = length - n * w
+    coded = FRAME_HEADER_BYTES + (n + 1) // 2 + (w - 1) * n + n_esc + tail
+    if n_esc > MAX_ESCAPES:
+        return _raw_frame(data)
+    esc = hi[esc_mask]
+    if w == 2 and n % 8 == 0:
+        lens = huffman_lengths(np.bincount(codes, minlength=16))
+        c_bytes = int(_lane_layout(codes, lens)[3].sum())
+        size2 = FRAME_HEADER_BYTES + n + LANE_TABLE_BYTES + c_bytes + n_esc + tail
+        if c_bytes <= HUFF_MAX_CODED and size2 < coded and size2 < raw:
+            streams, lane_bytes = _huffman_streams(codes, lens)
+            lens_b = bytes(lens[2 * j] | (lens[2 * j + 1] << 4) for j in range(8))
+            return (struct.pack("<B3xI16s8s", 2, n_esc, d.tobytes(), lens_b)
+                    + el[:, 0].tobytes() + lane_bytes.astype("<u2").tobytes() + streams
+                    + esc.tobytes() + data[n * w:].tobytes())
+    if coded >= raw:
+        return _raw_frame(data)
     if n % 2:
         codes = np.concatenate([codes, np.zeros(1, dtype=np.uint8)])
     nib = (codes[0::2] | (codes[1::2] << 4)).astype(np.uint8)
     lo = np.ascontiguousarray(el[:, : w - 1]).reshape(-1)
-    esc = hi[esc_mask]
     return (struct.pack("<B3xI16s8x", 1, n_esc, d.tobytes()) + nib.tobytes() + lo.tobytes()
             + esc.tobytes() + data[n * w:].tobytes())
 
@@ -178,13 +334,54 @@ def encode_reference(data, elem_width: int = 2,
     return head + table + pad + b"".join(frames)
 
 
+def _decode_huffman_streams(streams: np.ndarray, lane_bytes: np.ndarray, n: int,
+                            lens: List[int]) -> np.ndarray:
+    """All 256 lane streams decoded in lock step (vectorised over lanes)."""
+    g = n // 8
+    lut = decode_table(lens)
+    buf = np.concatenate([streams, np.zeros(4, dtype=np.uint8)]).astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(lane_bytes.astype(np.int64))[:-1]])
+    bitpos = starts * 8
+    ends = (starts + lane_bytes.astype(np.int64)) * 8
+    codes = np.zeros(n, dtype=np.uint8)
+    lanes = np.arange(LANES)
+    for s in range((g + LANES - 1) // LANES):
+        grp = s * LANES + lanes
+        live = grp < g
+        for e in range(8):
+            p = np.minimum(bitpos, buf.size * 8 - 24)
+            byte = p >> 3
+            word = buf[byte] | (buf[byte + 1] << 8) | (buf[byte + 2] << 16)
+            ent = lut[(word >> (p & 7)) & ((1 << HUFF_MAX_LEN) - 1)]
+            ln = (ent >> 8).astype(np.int64)
+            if np.any(live & ((ln == 0) | (bitpos + ln > ends))):
+                raise ValueError("corrupt HSZ1 huffman stream")
+            codes[grp[live] * 8 + e] = (ent[live] & 15).astype(np.uint8)
+            bitpos = np.where(live, bitpos + ln, bitpos)
+    return codes
+
+
 def decode_frame_reference(frame, length: int, w: int) -> bytes:
     mv = memoryview(frame).cast("B")
-    mode, n_esc, d = struct.unpack_from("<B3xI16s8x", mv, 0)
+    mode, n_esc, d, lens_b = struct.unpack_from("<B3xI16s8s", mv, 0)
     body = np.frombuffer(mv[FRAME_HEADER_BYTES:], dtype=np.uint8)
     if mode == 0:
         return body[:length].tobytes()
     n = length // w
+    dic = np.frombuffer(d, dtype=np.uint8)
+    if mode == 2:
+        lens = [(lens_b[j // 2] >> (4 * (j % 2))) & 15 for j in range(16)]
+        lo = body[:n]
+        lane_bytes = body[n: n + LANE_TABLE_BYTES].view("<u2")
+        c_bytes = int(lane_bytes.astype(np.int64).sum())
+        s0 = n + LANE_TABLE_BYTES
+        codes = _decode_huffman_streams(body[s0: s0 + c_bytes], lane_bytes, n, lens)
+        esc = body[s0 + c_bytes: s0 + c_bytes + n_esc]
+        hi = dic[np.minimum(codes, 14)].copy()
+        hi[codes == ESC] = esc
+        out = np.stack([lo, hi], 1).reshape(-1)
+        tail = body[s0 + c_bytes + n_esc: s0 + c_bytes + n_esc + (length - 2 * n)]
+        return out.tobytes() + tail.tobytes()
     nb = (n + 1) // 2
     nib = body[:nb]
     codes = np.empty(nb * 2, dtype=np.uint8)
@@ -193,7 +390,6 @@ def decode_frame_reference(frame, length: int, w: int) -> bytes:
     codes = codes[:n]
     lo = body[nb: nb + (w - 1) * n].reshape(n, w - 1)
     esc = body[nb + (w - 1) * n: nb + (w - 1) * n + n_esc]
-    dic = np.frombuffer(d, dtype=np.uint8)
     hi = dic[np.minimum(codes, 14)].copy()
     hi[codes == ESC] = esc
     out = np.empty((n, w), dtype=np.uint8)
@@ -212,6 +408,13 @@ def decode_reference(blob) -> bytes:
         out.append(decode_frame_reference(mv[h.offsets[i]: h.offsets[i + 1]], hi - lo,
                                           h.elem_width))
     return b"".join(out)
+
+
+def frame_modes(blob) -> List[int]:
+    """Mode byte of every frame (diagnostics / tests)."""
+    mv = memoryview(blob).cast("B")
+    h = parse_header(mv)
+    return [mv[h.offsets[i]] for i in range(h.n_frames)]
 
 
 # ---------------------------------------------------------------------------
@@ -239,7 +442,7 @@ def decode_cpu_into(blob, out_addr: int, first: int = 0, count: int = None,
     h = header or parse_header(mv)
     count = h.n_frames - first if count is None else count
     arr = np.frombuffer(mv, dtype=np.uint8)
-    offs = np.asarray(h.offsets[first: first + count], dtype=np.uint64)
+    offs = np.asarray(h.offsets[first: first + count + 1], dtype=np.uint64)
     validate_offsets(h, len(mv))
     native.hsz_decode_cpu(arr.ctypes.data, offs.ctypes.data, first, count, h.logical_size,
                           h.elem_width, h.frame_bytes, out_addr, nthreads)
@@ -268,7 +471,7 @@ def encode_device(src, elem_width: int, stream_handle: int,
                   frame_bytes: int = DEFAULT_FRAME_BYTES, launch: bool = True):
     """Encode a contiguous CUDA uint8 tensor on the GPU.
 
-    Returns ``(blob_tensor, nbytes_device)`` where ``blob_tensor`` has the
+    Returns ``(blob_tensor, nbytes_device, meta)``: ``blob_tensor`` has the
     worst-case capacity and ``nbytes_device`` is a 1-element uint64-as-int64
     CUDA tensor with the encoded size; everything is enqueued on
     ``stream_handle`` (the caller reads the size after synchronising).
@@ -277,7 +480,6 @@ def encode_device(src, elem_width: int, stream_handle: int,
 
     from . import native
 
-    dev = src.device.index if src.device.index is not None else torch.cuda.current_device()
     logical = src.numel()
     nf = n_frames_for(logical, frame_bytes)
     out = torch.empty(max_encoded_bytes(logical, frame_bytes), dtype=torch.uint8,
@@ -316,8 +518,8 @@ def decode_device_into(blob_dev, header: Header, out_dev, stream_handle: int,
     count = header.n_frames - first if count is None else count
     if count <= 0:
         return
-    offs = [o - blob_base for o in header.offsets[first: first + count]]
-    if min(offs) < 0 or header.offsets[first + count] - blob_base > blob_dev.numel():
+    offs = [o - blob_base for o in header.offsets[first: first + count + 1]]
+    if min(offs) < 0 or offs[-1] > blob_dev.numel():
         raise ValueError("HSZ1 frames outside the device buffer")
     dev = blob_dev.device.index if blob_dev.device.index is not None else \
         torch.cuda.current_device()

@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU call: gpu test suite, smoke, headline bench (+ optional rocprof pass).
+# Every GPU step has its own time limit and the chain stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
+mkdir -p $HIPSNAPSHOT_BENCH_DIR
+if [ "${TESTS:-1}" = "1" ]; then
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread \
+    > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+    || { echo SMOKE_FAIL; tail -30 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 600 python bench.py --steps ${STEPS:-5} --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err \
+    || { echo BENCH_FAIL; tail -30 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json; grep -E "step|async|restore" gpurun_out/bench.err
+if [ "${PROF:-0}" = "1" ]; then
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+    -d gpurun_out/prof_bench -o bench -- python3 bench.py --steps 2 --warmup 1 --async-iters 1 \
+    > gpurun_out/prof_bench.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof_bench.log; exit 1; }
+find gpurun_out/prof_bench -name "*stats*"
+fi

@@ -29,7 +29,13 @@ def test_compression_ratio_on_weight_like_data():
     raw = _bytes(x)
     blob = codec.encode_reference(raw, 2)
     ratio = len(blob) / len(raw)
-    assert 0.74 < ratio < 0.77, ratio  # 12 bits per bf16 + escapes + headers
+    # mode 2: 8 raw bits + ~2.7 Huffman bits per bf16, within 1 % of the entropy bound
+    assert 0.66 < ratio < 0.68, ratio
+    assert set(codec.frame_modes(blob)) == {2}
+    hi = np.frombuffer(raw, dtype=np.uint8)[1::2]
+    p = np.bincount(hi, minlength=256) / hi.size
+    ent = -(p[p > 0] * np.log2(p[p > 0])).sum()
+    assert ratio < (8 + ent) / 16 * 1.012
     y = torch.randn(1_000_000) * 1e-3
     blob = codec.encode_reference(_bytes(y), 4)
     assert len(blob) / (4 * y.numel()) < 0.88
@@ -62,6 +68,60 @@ def test_escape_heavy_frame_falls_back():
     blob = codec.encode_reference(el.tobytes(), 2, frame_bytes=len(el))
     h = codec.parse_header(blob)
     assert blob[h.offsets[0]] == 0 and codec.decode_reference(blob) == el.tobytes()
+
+
+def test_huffman_lengths_rules():
+    # prefix-free and complete for ordinary histograms
+    lens = codec.huffman_lengths([50, 30, 10, 10] + [0] * 12)
+    assert lens[:4] == [1, 2, 3, 3] and sum(2.0 ** -x for x in lens if x) == 1.0
+    # ties go to the lower index (deterministic across implementations)
+    assert codec.huffman_lengths([5, 5, 5, 5] + [0] * 12)[:4] == [2, 2, 2, 2]
+    # one used index -> 1 bit; nothing used -> nothing
+    assert codec.huffman_lengths([0, 7] + [0] * 14)[1] == 1
+    assert codec.huffman_lengths([0] * 16) == [0] * 16
+    # Fibonacci-like counts would need 15 bits: limited to HUFF_MAX_LEN, Kraft <= 1
+    fib = [1, 1]
+    for _ in range(14):
+        fib.append(fib[-1] + fib[-2])
+    lens = codec.huffman_lengths(fib)
+    assert max(lens) == codec.HUFF_MAX_LEN
+    assert sum(2.0 ** -x for x in lens) <= 1.0
+    # canonical codes are prefix-free and the LUT inverts them
+    lut = codec.decode_table(lens)
+    codes = codec.canonical_codes(lens)
+    for c in range(16):
+        assert lut[codes[c]] == c | (lens[c] << 8)
+
+
+def test_mode2_frames_and_skewed_histograms():
+    # a near-constant high byte (1 dominant index, long codes for the rest)
+    g = np.random.default_rng(3)
+    hi = np.full(65536, 0x3C, dtype=np.uint8)
+    hi[g.integers(0, hi.size, 300)] = g.integers(0x30, 0x40, 300)
+    el = np.stack([g.integers(0, 256, hi.size, dtype=np.uint8), hi], 1).reshape(-1)
+    raw = el.tobytes() + b"\x07"  # odd tail byte
+    blob = codec.encode_reference(raw, 2, frame_bytes=len(raw) - 1)
+    assert codec.frame_modes(blob)[0] == 2
+    assert codec.decode_reference(blob) == raw
+    assert codec.decode_cpu(blob).tobytes() == raw
+    assert codec.encode_cpu(raw, 2, len(raw) - 1).tobytes() == blob
+    # fewer groups than lanes (most lane streams empty) still round-trips
+    small = _bytes((torch.randn(4096) * 0.02).to(torch.bfloat16))
+    b2 = codec.encode_reference(small, 2, frame_bytes=len(small))
+    assert codec.decode_reference(b2) == small and codec.decode_cpu(b2).tobytes() == small
+
+
+def test_version1_blobs_still_decode():
+    import struct
+
+    raw = _bytes((torch.randn(50_000) * 0.02).to(torch.bfloat16))
+    blob = bytearray(codec.encode_reference(raw, 2, frame_bytes=16 * 1024))
+    if set(codec.frame_modes(bytes(blob))) <= {0, 1}:
+        struct.pack_into("<I", blob, 4, 1)
+        assert codec.decode_reference(bytes(blob)) == raw
+    v1 = bytearray(codec.encode_reference(raw, 4, frame_bytes=16 * 1024))  # w=4: modes 0/1
+    struct.pack_into("<I", v1, 4, 1)
+    assert codec.decode_reference(bytes(v1)) == raw and codec.decode_cpu(bytes(v1)).tobytes() == raw
 
 
 def test_frames_covering():

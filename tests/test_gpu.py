@@ -385,7 +385,7 @@ def test_hsz_gpu_large_blob_ratio(gpu):
     out, total, _ = codec.encode_device(x.view(torch.uint8), 2, int(s.cuda_stream))
     s.synchronize()
     nb = int(total.item())
-    assert 0.74 < nb / (x.numel() * 2) < 0.77
+    assert 0.66 < nb / (x.numel() * 2) < 0.68  # mode-2 (Huffman) frames
     nf = codec.n_frames_for(x.numel() * 2, codec.DEFAULT_FRAME_BYTES)
     hdr = codec.parse_header(out[:codec.payload_start(nf)].cpu().numpy().tobytes())
     back = torch.empty_like(x)
