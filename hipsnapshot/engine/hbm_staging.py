@@ -16,8 +16,11 @@ copy bandwidth, so instead:
 3. the stagers are re-pointed at arena views and wait on an event recorded
    after the launch; the background commit thread drains the arena to storage.
 
-Falls back (per device) to the host-staging path when the arena does not fit
-in free HBM minus ``HBM_STAGING_RESERVE_BYTES``.
+When the whole state does not fit in free HBM minus
+``HBM_STAGING_RESERVE_BYTES`` (or ``HBM_STAGING_MAX_BYTES``), write requests are
+frozen greedily in plan order until the arena is full and the rest takes the
+host-staging path before ``async_take`` returns: the time-to-unblock then
+scales with the bytes that did NOT fit, instead of falling back wholesale.
 """
 
 from __future__ import annotations
@@ -37,77 +40,95 @@ logger = logging.getLogger(__name__)
 _ALIGN = 256
 
 
-def _collect(write_reqs: List[WriteReq]):
-    """(stager-like object with .tensor/.producer) for every CUDA source."""
+def _cuda_sources(wr: WriteReq):
+    """The stagers whose CUDA tensors a write request reads (empty if none)."""
     from ..io.batcher import GPUBatchedBufferStager
     from ..io.tensor import TensorBufferStager
 
-    out = []
-    for wr in write_reqs:
-        st = wr.buffer_stager
-        if isinstance(st, TensorBufferStager) and st.tensor.is_cuda \
-                and st._tensor_prepare_func is None:
-            out.append(st)
-        elif isinstance(st, GPUBatchedBufferStager):
-            out.extend(m for _, m in st.members)
-    return out
+    st = wr.buffer_stager
+    if isinstance(st, TensorBufferStager) and st.tensor.is_cuda \
+            and st._tensor_prepare_func is None:
+        return [st]
+    if isinstance(st, GPUBatchedBufferStager):
+        return [m for _, m in st.members]
+    return []
+
+
+def _nbytes(st) -> int:
+    nb = st.tensor.numel() * st.tensor.element_size()
+    return (nb + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
 def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
-    """Returns {device: arena_bytes} for the devices that were frozen."""
+    """Returns {device: arena_bytes} for the devices that were (partly) frozen."""
     if not native.gpu_available():
         return {}
-    stagers = _collect(write_reqs)
-    if not stagers:
-        return {}
-    by_dev = defaultdict(list)
-    for st in stagers:
-        by_dev[st.tensor.device.index if st.tensor.device.index is not None
-               else torch.cuda.current_device()].append(st)
-    frozen = {}
-    for dev, sts in by_dev.items():
-        offs, total = [], 0
-        for st in sts:
-            offs.append(total)
-            nb = st.tensor.numel() * st.tensor.element_size()
-            total += (nb + _ALIGN - 1) // _ALIGN * _ALIGN
-        free, _ = torch.cuda.mem_get_info(dev)
-        if total + knobs.hbm_staging_reserve_bytes() > free:
-            logger.info(f"HBM staging skipped on cuda:{dev}: need {total} B, free {free} B")
+    by_dev = defaultdict(list)  # device -> [(request bytes, stagers)]
+    for wr in write_reqs:
+        sts = _cuda_sources(wr)
+        if not sts:
             continue
-        stream = torch.cuda.current_stream(dev)
-        with torch.cuda.device(dev):
-            arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
-            batch = native.CopyBatch()
-            views = []
-            for st, off in zip(sts, offs):
-                t = st.tensor.detach()
-                view = arena[off: off + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
-                if t.numel():
-                    batch.add(t.data_ptr(), t.dtype, t.stride(), view.data_ptr(), t.dtype,
-                              view.stride(), list(t.shape), t.element_size())
-                views.append(view)
-            # producers may differ from the current stream: order after them
-            for p in {st.producer for st in sts if st.producer is not None}:
-                if p != stream.cuda_stream:
-                    ev = torch.cuda.Event()
-                    ev.record(torch.cuda.default_stream(dev) if p == 0
-                              else torch.cuda.ExternalStream(p))
-                    stream.wait_event(ev)
-            keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
-            done = torch.cuda.Event()
-            done.record(stream)
-        for st, view in zip(sts, views):
-            st.tensor = view
-            st.producer = None  # ordering is carried by wait_event
-            st.frozen = True
-            st.wait_event = done
-        # keep the descriptor tables alive until the copy ran
-        done_keep = (keep, done)
+        t = sts[0].tensor
+        dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
+        by_dev[dev].append((sum(_nbytes(st) for st in sts), sts))
+    frozen = {}
+    cap = knobs.hbm_staging_max_bytes()
+    for dev, reqs in by_dev.items():
+        free, _ = torch.cuda.mem_get_info(dev)
+        room = min(free - knobs.hbm_staging_reserve_bytes(), cap)
+        want = sum(nb for nb, _ in reqs)
+        sts, total = [], 0
+        for nb, req_sts in reqs:
+            if total + nb <= room:
+                sts.extend(req_sts)
+                total += nb
+        if not sts:
+            logger.info(f"HBM staging skipped on cuda:{dev}: need {want} B, room {room} B")
+            continue
+        if total < want:
+            logger.info(f"HBM staging on cuda:{dev}: {total} of {want} B frozen, the rest "
+                        "is staged to host before async_take returns")
+        offs, off = [], 0
         for st in sts:
-            st.arena_keepalive = done_keep
+            offs.append(off)
+            off += _nbytes(st)
+        _freeze(dev, sts, offs, total)
         frozen[dev] = total
     return frozen
+
+
+def _freeze(dev: int, sts, offs, total: int) -> None:
+    stream = torch.cuda.current_stream(dev)
+    with torch.cuda.device(dev):
+        arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
+        batch = native.CopyBatch()
+        views = []
+        for st, off in zip(sts, offs):
+            t = st.tensor.detach()
+            view = arena[off: off + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
+            if t.numel():
+                batch.add(t.data_ptr(), t.dtype, t.stride(), view.data_ptr(), t.dtype,
+                          view.stride(), list(t.shape), t.element_size())
+            views.append(view)
+        # producers may differ from the current stream: order after them
+        for p in {st.producer for st in sts if st.producer is not None}:
+            if p != stream.cuda_stream:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.default_stream(dev) if p == 0
+                          else torch.cuda.ExternalStream(p))
+                stream.wait_event(ev)
+        keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
+        done = torch.cuda.Event()
+        done.record(stream)
+    for st, view in zip(sts, views):
+        st.tensor = view
+        st.producer = None  # ordering is carried by wait_event
+        st.frozen = True
+        st.wait_event = done
+    # keep the descriptor tables alive until the copy ran
+    done_keep = (keep, done)
+    for st in sts:
+        st.arena_keepalive = done_keep
 
 
 def is_deferrable(wr: WriteReq) -> bool:

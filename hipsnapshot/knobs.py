@@ -20,6 +20,8 @@ MI355X-specific knobs:
 * ``HIPSNAPSHOT_ASYNC_HBM_STAGING`` (1) -- async_take snapshots device state into
   spare HBM with one gather-kernel launch and drains it in the background.
 * ``HIPSNAPSHOT_HBM_STAGING_RESERVE_BYTES`` (8 GiB) -- HBM left free for training.
+* ``HIPSNAPSHOT_HBM_STAGING_MAX_BYTES`` (unlimited) -- cap on the async-take HBM
+  arena; requests beyond it are host-staged before ``async_take`` returns.
 * ``HIPSNAPSHOT_SLAB_ALIGN`` (256) -- byte alignment of slab members.
 * ``HIPSNAPSHOT_TRUST_OBJECTS`` (0) -- allow full unpickling of ``object``
   entries written by OTHER tools (our own writes are trusted by the reader).
@@ -124,6 +126,10 @@ def async_hbm_staging_enabled() -> bool:
 
 def hbm_staging_reserve_bytes() -> int:
     return _get_int("HBM_STAGING_RESERVE_BYTES", 8 * 1024 ** 3)
+
+
+def hbm_staging_max_bytes() -> int:
+    return _get_int("HBM_STAGING_MAX_BYTES", 1 << 62)
 
 
 def slab_align() -> int:

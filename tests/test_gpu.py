@@ -233,6 +233,47 @@ def test_async_take_host_fallback_when_hbm_short(gpu, tmp_path):
     assert torch.equal(Snapshot(str(tmp_path / "s")).read_object("0/sd/w"), ref.cpu())
 
 
+def test_async_take_partial_hbm_freeze(gpu, tmp_path):
+    """Arena smaller than the state: the requests that fit are frozen in HBM,
+    the rest is host-staged before async_take returns -- both consistent."""
+    from hipsnapshot.io.batcher import GPUBatchedBufferStager
+    from hipsnapshot.engine import hbm_staging
+
+    big = torch.randn(2048, 1024, device=gpu)            # 8 MiB: its own blob
+    small = [torch.randn(1000 + i, device=gpu) for i in range(8)]  # one slab
+    refs = [big.clone()] + [t.clone() for t in small]
+    seen = {}
+    orig = hbm_staging.freeze_device_state
+
+    def spy(write_reqs):
+        out = orig(write_reqs)
+        seen["frozen"] = out
+        seen["kinds"] = [(type(wr.buffer_stager).__name__, hbm_staging.is_deferrable(wr))
+                         for wr in write_reqs]
+        return out
+
+    with override_knob("HBM_STAGING_MAX_BYTES", str(1 << 20)), \
+            override_slab_size_threshold_bytes(4 << 20):
+        hbm_staging.freeze_device_state = spy
+        try:
+            pending = Snapshot.async_take(str(tmp_path / "s"),
+                                          {"sd": StateDict(big=big, small=small)})
+        finally:
+            hbm_staging.freeze_device_state = orig
+    big.add_(1.0)
+    for t in small:
+        t.mul_(0)
+    pending.wait()
+    assert 0 < seen["frozen"][0] <= 1 << 20
+    assert (GPUBatchedBufferStager.__name__, True) in seen["kinds"]   # slab frozen
+    assert ("TensorBufferStager", False) in seen["kinds"]             # big: host path
+    out = StateDict(big=torch.zeros_like(big), small=[torch.zeros_like(t) for t in small])
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    assert torch.equal(out["big"], refs[0])
+    for got, ref in zip(out["small"], refs[1:]):
+        assert torch.equal(got, ref)
+
+
 def test_fp8_quantized_save_gpu(gpu, tmp_path):
     from hipsnapshot.ops.quant import dequantize_reference, quantize_reference
 
