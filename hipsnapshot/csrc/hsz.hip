@@ -788,13 +788,28 @@ hsz_decode(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offs
   for (uint64_t j = threadIdx.x; j < len - n * W; j += kThreads) o[n * W + j] = tail[j];
 }
 
+// Branch-free bit-buffer refill to 56..63 valid bits: the 8 stream bytes at
+// byte `pos` come from two aligned 8-B LDS reads and a funnel shift.  Bits of
+// a byte that only partly fits are OR-ed in again (same values) next time.
+__device__ __forceinline__ void refill(const uint64_t* coded64, uint32_t& pos, uint64_t& acc,
+                                       int& nb) {
+  const uint32_t q = pos >> 3, sh = (pos & 7) * 8;
+  const uint64_t a = coded64[q], b = coded64[q + 1];
+  const uint64_t bits = sh ? (a >> sh) | (b << (64 - sh)) : a;
+  acc |= bits << nb;
+  const int k = (63 - nb) >> 3;
+  pos += k;
+  nb += 8 * k;
+}
+
 // Mode-2 decoder (2-byte elements).  A frame whose fields do not fit its
 // stored extent is left undecoded (the host validated the frame table).
 __global__ void __launch_bounds__(kThreads)
 hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
             uint32_t first_frame, uint64_t logical, uint32_t frame_bytes,
             uint8_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t coded[kMaxCoded + 1 + 8];
+  // streams + 16 B of slack for the 8-B refill reads past the last stream
+  __shared__ uint64_t coded64[(kMaxCoded + 1 + 16 + 7) / 8];
   __shared__ uint16_t lut[kLut];
   __shared__ uint16_t hcode[16];
   __shared__ uint8_t hlen[16];
@@ -848,6 +863,7 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
       kFrameHeader + n + kLaneTable + c_bytes + n_esc + tail_len > extent)
     return;  // uniform across the workgroup (ctotal is shared)
   const uint8_t* streams = body + n + kLaneTable;
+  uint8_t* coded = reinterpret_cast<uint8_t*>(coded64);
   if ((reinterpret_cast<uintptr_t>(streams) & 3) == 0) {
     const uint32_t nw = c_bytes / 4;
     const uint32_t* sw = reinterpret_cast<const uint32_t*>(streams);
@@ -857,10 +873,10 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   } else {
     for (uint32_t j = threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
   }
+  if (threadIdx.x < 16) coded[c_bytes + threadIdx.x] = 0;
   __syncthreads();
   const uint64_t groups = n / 8;
   const bool vec = ((reinterpret_cast<uintptr_t>(o) & 15) | (reinterpret_cast<uintptr_t>(lo) & 7)) == 0;
-  const uint32_t end = loff + lb;
   uint32_t pos = loff;
   uint64_t acc = 0;
   int nb = 0;
@@ -876,13 +892,9 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
     uint32_t wd[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      if (nb < kMaxLen) {
-        while (nb <= 56) {
-          acc |= uint64_t(pos < end ? coded[pos] : 0) << nb;
-          ++pos;
-          nb += 8;
-        }
-      }
+      // every lane refills at the same points (no divergence): >= 56 bits
+      // cover the next 4 codes of <= kMaxLen bits
+      if ((e & 3) == 0) refill(coded64, pos, acc, nb);
       const uint32_t ent = lut[acc & (kLut - 1)];
       uint32_t l = ent >> 8;
       uint32_t c = ent & 15;
