@@ -22,7 +22,6 @@ read (elastic)
 
 from __future__ import annotations
 
-import copy
 import logging
 import math
 from collections import OrderedDict
@@ -78,40 +77,46 @@ class LocalBox:
         self.sharding_dim = sharding_dim
 
 
-# (global shape, mesh, coordinate, placements) -> (local shape, global offset);
-# the same layouts recur every snapshot of a training job
+# DTensorSpec (hashable, hash cached by torch) -> (skip, local shape, global
+# offset, sharding dim): the same layouts recur every snapshot of a training
+# job, and FSDP2 state dicts share one spec object per parameter.
 _LAYOUT_CACHE: dict = {}
 
 
-def _dtensor_boxes(dt, for_write: bool) -> List[LocalBox]:
+def _dtensor_layout(dt, for_write: bool):
     from torch.distributed.tensor._utils import compute_local_shape_and_global_offset
 
+    key = (dt._spec, for_write)
+    hit = _LAYOUT_CACHE.get(key)
+    if hit is not None:
+        return hit
     placements = list(dt.placements)
+    mesh = dt.device_mesh
+    coord = mesh.get_coordinate()
+    skip = coord is None or (for_write and any(
+        isinstance(p, Replicate) and coord[mdim] != 0 for mdim, p in enumerate(placements)))
+    shape, offset = ((), ()) if coord is None else \
+        compute_local_shape_and_global_offset(dt.shape, mesh, placements)
+    sdim = next((p.dim for p in placements if isinstance(p, DShard)), 0)
+    hit = (skip, [int(x) for x in shape], [int(x) for x in offset], sdim)
+    if len(_LAYOUT_CACHE) > 65536:
+        _LAYOUT_CACHE.clear()
+    _LAYOUT_CACHE[key] = hit
+    return hit
+
+
+def _dtensor_boxes(dt, for_write: bool) -> List[LocalBox]:
+    placements = dt.placements
     for p in placements:
         if type(p).__name__ == "_StridedShard":
             raise NotImplementedError("DTensor _StridedShard placements are not supported yet")
     if any(isinstance(p, Partial) for p in placements):
         dt = dt.redistribute(dt.device_mesh,
                              [Replicate() if isinstance(p, Partial) else p for p in placements])
-        placements = list(dt.placements)
-    mesh = dt.device_mesh
-    coord = mesh.get_coordinate()
-    if coord is None:
+    skip, shape, offset, sdim = _dtensor_layout(dt, for_write)
+    if skip:
         return []
-    if for_write:
-        for mdim, p in enumerate(placements):
-            if isinstance(p, Replicate) and coord[mdim] != 0:
-                return []
-    key = (tuple(dt.shape), id(mesh), tuple(coord), tuple(placements))
-    hit = _LAYOUT_CACHE.get(key)
-    if hit is None:
-        hit = compute_local_shape_and_global_offset(dt.shape, mesh, placements)
-        if len(_LAYOUT_CACHE) > 65536:
-            _LAYOUT_CACHE.clear()
-        _LAYOUT_CACHE[key] = hit
-    shape, offset = hit
     local = dt._local_tensor
-    sdim = next((p.dim for p in placements if isinstance(p, DShard)), 0)
     if local.dim() == 0 and len(shape) == 0:
         return [LocalBox([], [], local, 0)]
     if any(s == 0 for s in shape):
@@ -171,13 +176,15 @@ class ShardedTensorIOPreparer:
         chunk_len = max(math.floor(max_shard_sz_bytes / slice_sz), 1) if slice_sz else sizes[dim]
         chunk_len = max(chunk_len, 1)
         n_chunks = max(1, math.ceil(sizes[dim] / chunk_len))
+        if n_chunks == 1:
+            return [(shard, list(offsets), list(sizes))]
         out = []
         for i in range(n_chunks):
             start = i * chunk_len
             length = min((i + 1) * chunk_len, sizes[dim]) - start
-            so = copy.deepcopy(list(offsets))
+            so = list(offsets)
             so[dim] += start
-            sz = copy.deepcopy(list(sizes))
+            sz = list(sizes)
             sz[dim] = length
             out.append((torch.narrow(shard, dim, start, length), so, sz))
         return out
@@ -188,9 +195,10 @@ class ShardedTensorIOPreparer:
                       serializer: Optional[str] = None
                       ) -> Tuple[ShardedTensorEntry, List[WriteReq]]:
         shards, reqs = [], []
+        max_shard = get_max_shard_size_bytes()
         for box in local_boxes(obj, for_write=True):
             pieces = cls.subdivide_shard(box.tensor, box.offsets, box.sizes, box.sharding_dim,
-                                         get_max_shard_size_bytes())
+                                         max_shard)
             for t, offs, sizes in pieces:
                 suffix = "_".join(str(i) for i in offs)
                 entry, wrs = TensorIOPreparer.prepare_write(

@@ -280,8 +280,10 @@ class Snapshot:
                 object_entries[logical] = entry
                 path_reqs[logical] = wrs
         timeline.add("prepare_write", "phase", t_prep, time.perf_counter(), n=len(flattened))
-        with timeline.span("partition"):
-            object_entries, path_reqs = partition_write_reqs(object_entries, path_reqs, comm)
+        if rep_paths:  # identical on every rank (result of a collective)
+            with timeline.span("partition"):
+                object_entries, path_reqs = partition_write_reqs(object_entries, path_reqs,
+                                                                 comm)
         write_reqs = [wr for wrs in path_reqs.values() for wr in wrs]
         if not knobs.is_batching_disabled():
             with timeline.span("batch"):
@@ -294,8 +296,12 @@ class Snapshot:
                 plan_compression(write_reqs)
         manifest.update(primitives)
         manifest.update(object_entries)
-        with timeline.span("gather_manifest"):
-            metadata = cls._gather_metadata(manifest, comm)
+        metadata = None
+        if is_async:
+            # async: every rank has the metadata before any staging can fail,
+            # so a failing rank reports through the commit barrier, not a hang
+            with timeline.span("gather_manifest"):
+                metadata = cls._gather_metadata(manifest, comm)
 
         budget = get_process_memory_budget_bytes(comm)
         deferred: List[WriteReq] = []
@@ -312,6 +318,12 @@ class Snapshot:
             from .engine.scheduler import DeferredIOWork
 
             pending = DeferredIOWork(pending, deferred, storage, budget, rank)
+        if metadata is None:
+            # sync take: entries are final since planning; gathering them only
+            # now takes the metadata collective off the path to the first D2H
+            # and overlaps it with the writes still draining in the I/O engine
+            with timeline.span("gather_manifest"):
+                metadata = cls._gather_metadata(manifest, comm)
         return pending, metadata
 
     # --------------------------------------------------------------- restore
@@ -507,7 +519,9 @@ class Snapshot:
         mine = sorted(p for p, v in flattened.items()
                       if not is_sharded(v) and any(fnmatch.fnmatch(p, g) for g in replicated))
         ws = comm.get_world_size()
-        if ws == 1:
+        if ws == 1 or not replicated:
+            # ``replicated`` is the cross-rank intersection from _coalesce, so
+            # every rank takes this early exit together (no collective needed)
             return set(mine)
         gathered: List[Any] = [None] * ws
         comm.all_gather_object(gathered, mine)
