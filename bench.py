@@ -64,6 +64,8 @@ def main() -> None:
     ap.add_argument("--fsync", action="store_true")
     ap.add_argument("--direct-io", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="do not restrict the rank to the CPUs of its GPU's NUMA node")
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"],
                     help="hsz1 (default) = lossless GPU-side exponent-nibble compression of "
                          "the bf16 blobs, restore verified bitwise; none = raw blobs "
@@ -89,6 +91,13 @@ def main() -> None:
     gpu_index = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(gpu_index)
     dev = torch.device("cuda", gpu_index)
+    if not args.no_numa_bind:
+        # before any I/O-engine / staging thread exists: they inherit it
+        from hipsnapshot.utils.affinity import bind_to_gpu_numa
+
+        rep = bind_to_gpu_numa(gpu_index)
+        if local_rank == 0:
+            print(f"numa: {rep}", file=sys.stderr, flush=True)
     if args.backend == "nccl":
         dist.init_process_group("nccl", device_id=dev)
     else:

@@ -109,3 +109,27 @@ def test_timeline_trace(tmp_path, monkeypatch):
     assert sum(e["args"].get("bytes", 0) for e in take if e["name"] == "write") > 0
     rest = json.load(open(tmp_path / "tl.rank0.restore0.json"))["traceEvents"]
     assert {"load_stateful", "read"} <= {e["name"] for e in rest}
+
+
+def test_numa_affinity_helpers(monkeypatch):
+    from hipsnapshot.utils import affinity
+
+    assert affinity._parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert affinity._parse_cpulist("") == set()
+    # unknown topology (no GPU here): nothing is bound, the reason is reported
+    monkeypatch.setattr(affinity, "gpu_numa_node", lambda d: None)
+    rep = affinity.bind_to_gpu_numa(0)
+    assert rep["bound"] is False and "unknown" in rep["reason"]
+    # too few usable CPUs on the GPU's node -> no binding
+    monkeypatch.setattr(affinity, "gpu_numa_node", lambda d: 7)
+    monkeypatch.setattr(affinity, "node_cpus", lambda n: set())
+    rep = affinity.bind_to_gpu_numa(0)
+    assert rep["bound"] is False and rep["local"] == 0
+    # node covering every allowed CPU -> already local, affinity untouched
+    import os
+
+    allowed = os.sched_getaffinity(0)
+    monkeypatch.setattr(affinity, "node_cpus", lambda n: set(allowed) | {10 ** 6})
+    rep = affinity.bind_to_gpu_numa(0, min_cpus=1)
+    assert rep["bound"] is False and rep["reason"] == "already local"
+    assert os.sched_getaffinity(0) == allowed
