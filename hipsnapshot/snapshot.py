@@ -137,6 +137,7 @@ class Snapshot:
     def _take(cls, path, app_state, pg, replicated, storage_options,
               _custom_tensor_prepare_func, quantize, compression) -> "Snapshot":
         cls._validate_app_state(app_state)
+        _numa_bind_once()
         loop = asyncio.new_event_loop()
         comm = Comm(pg)
         t0 = time.monotonic()
@@ -189,6 +190,7 @@ class Snapshot:
     def _async_take(cls, path, app_state, pg, replicated, storage_options,
                     _custom_tensor_prepare_func, quantize, compression) -> "PendingSnapshot":
         cls._validate_app_state(app_state)
+        _numa_bind_once()
         loop = asyncio.new_event_loop()
         comm = Comm(pg)
         t0 = time.monotonic()
@@ -336,6 +338,7 @@ class Snapshot:
 
     def _restore(self, app_state: AppState) -> None:
         self._validate_app_state(app_state)
+        _numa_bind_once()
         loop = asyncio.new_event_loop()
         comm = Comm(self.pg)
         storage = url_to_storage_plugin_in_event_loop(self.path, loop, self._storage_options)
@@ -578,6 +581,23 @@ class Snapshot:
         rio = ReadIO(path=SNAPSHOT_METADATA_FNAME)
         storage.sync_read(rio, loop)
         return SnapshotMetadata.from_json(bytes(rio.data()).decode("utf-8"))
+
+
+_numa_done = [False]
+
+
+def _numa_bind_once() -> None:
+    """``HIPSNAPSHOT_NUMA_BIND=1``: bind this process to the CPUs of its
+    current GPU's NUMA node before the first I/O threads start (once)."""
+    if _numa_done[0]:
+        return
+    _numa_done[0] = True
+    if os.environ.get("HIPSNAPSHOT_NUMA_BIND") and torch.cuda.is_available():
+        from .utils.affinity import maybe_bind_from_env
+
+        rep = maybe_bind_from_env(torch.cuda.current_device())
+        if rep is not None:
+            logger.info(f"NUMA binding: {rep}")
 
 
 def flat_prefix(key: str) -> str:
