@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Checkpointing a TRAINING job: Llama-3 FSDP2 model + AdamW state, taken with
+``async_take`` while training continues (BASELINE config 5's "train-step
+overlap", on local storage or the in-process fake S3).
+
+Reported (max over ranks):
+
+* baseline step time (fwd + bwd + AdamW, synthetic tokens);
+* ``Snapshot.take`` (blocking) time of model + optimizer state;
+* ``async_take`` time-to-unblock, background drain time, the number of
+  training steps that ran while the snapshot drained, and their mean / max
+  step time (the slowdown the checkpoint costs the trainer);
+* a bitwise restore check of every model and optimizer shard.
+
+The reference publishes no such number (time-to-unblock is printed but not
+reported by `/root/reference/benchmarks/torchrec/main.py:133-151`).
+
+    python benchmarks/train_overlap/main.py --layers 32 --seq 2048
+    torchrun --nproc-per-node 8 benchmarks/train_overlap/main.py
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from common import emit, init_dist, log, max_over_ranks, sync  # noqa: E402
+from hipsnapshot import Snapshot  # noqa: E402
+from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama  # noqa: E402
+
+
+def _local(t):
+    return t._local_tensor if hasattr(t, "_local_tensor") else t
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3_8b", choices=["llama3_8b", "llama3_70b", "tiny"])
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--baseline-steps", type=int, default=5)
+    ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
+    ap.add_argument("--storage", default="fs", choices=["fs", "s3"])
+    ap.add_argument("--path", default=None)
+    args = ap.parse_args()
+
+    rank, ws, dev = init_dist()
+    if dev.type == "cuda":
+        from hipsnapshot.utils.affinity import bind_to_gpu_numa
+
+        bind_to_gpu_numa(dev.index)
+    from torch.distributed.device_mesh import init_device_mesh
+
+    cfg = getattr(LlamaConfig, args.model)()
+    if args.layers:
+        cfg.n_layers = args.layers
+    mesh = init_device_mesh(dev.type, (ws,))
+    model = build_fsdp_llama(cfg, dev, torch.bfloat16, mesh=mesh)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-5, foreach=True)
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+
+    def step() -> float:
+        t0 = time.perf_counter()
+        tok = torch.randint(0, cfg.vocab_size, (args.batch, args.seq + 1), device=dev,
+                            generator=gen)
+        logits = model(tok[:, :-1])
+        loss = F.cross_entropy(logits.float().flatten(0, 1), tok[:, 1:].flatten())
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    for _ in range(2):  # creates the AdamW state
+        step()
+    sync(dev)
+    base = [step() for _ in range(args.baseline_steps)]
+    base_ms = max_over_ranks(statistics.median(base), dev) * 1e3
+    ckpt_bytes = sum(_local(p).numel() * _local(p).element_size() for p in model.parameters())
+    for st in opt.state.values():
+        for v in st.values():
+            if torch.is_tensor(v):
+                ckpt_bytes += _local(v).numel() * _local(v).element_size()
+    t = torch.tensor([ckpt_bytes], dtype=torch.int64, device=dev)
+    dist.all_reduce(t)
+    ckpt_bytes = int(t.item())
+    log(f"baseline step {base_ms:.1f} ms; checkpoint {ckpt_bytes / 1e9:.2f} GB (model + AdamW)")
+
+    srv = None
+    opts = None
+    if args.storage == "s3":
+        from hipsnapshot.storage.fake_servers import FakeS3Server
+
+        srv = FakeS3Server() if rank == 0 else None
+        url = [srv.url if srv else None]
+        dist.broadcast_object_list(url, src=0)
+        opts = {"aws_access_key_id": "AKIDFAKE", "aws_secret_access_key": "fake-secret",
+                "endpoint_url": url[0], "multipart_threshold": 64 << 20, "part_size": 64 << 20}
+        root = "s3://ckpt/train_overlap"
+    else:
+        root = args.path or os.path.join(os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"),
+                                         "train_overlap")
+        if rank == 0:
+            shutil.rmtree(root, ignore_errors=True)
+    app = {"model": model, "optim": opt}
+
+    # blocking take (reference semantics) for comparison
+    log("phase: sync take")
+    sync(dev)
+    t0 = time.perf_counter()
+    Snapshot.take(f"{root}/sync", app, storage_options=opts, compression=args.compression)
+    sync_s = max_over_ranks(time.perf_counter() - t0, dev)
+    if args.storage == "fs" and rank == 0:
+        shutil.rmtree(f"{root}/sync", ignore_errors=True)  # keep the disk footprint to one copy
+
+    # async take while training continues
+    log(f"phase: async take (sync take {sync_s:.3f} s)")
+    sync(dev)
+    ref = {n: _local(p).detach().clone() for n, p in model.named_parameters()}
+    t0 = time.perf_counter()
+    pending = Snapshot.async_take(f"{root}/async", app, storage_options=opts,
+                                  compression=args.compression)
+    unblock = time.perf_counter() - t0
+    during = []
+    while not pending.done():
+        during.append(step())
+    pending.wait()
+    drain = time.perf_counter() - t0
+    # every rank must finish its loop before collectives resume
+    unblock = max_over_ranks(unblock, dev)
+    drain = max_over_ranks(drain, dev)
+    n_during = int(max_over_ranks(float(len(during)), dev))
+    mean_ms = max_over_ranks(statistics.mean(during) if during else 0.0, dev) * 1e3
+    max_ms = max_over_ranks(max(during) if during else 0.0, dev) * 1e3
+
+    log(f"phase: restore (unblock {unblock * 1e3:.1f} ms, {len(during)} steps during drain)")
+    # restore the async snapshot: parameters must equal the values at the
+    # async_take call, not the ones the overlapped steps produced
+    Snapshot(f"{root}/async", storage_options=opts).restore(app)
+    ok = all(torch.equal(_local(p), ref[n]) for n, p in model.named_parameters())
+    okt = torch.tensor([int(ok)], device=dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+
+    emit({"bench": "train_overlap_async_take", "model": args.model, "layers": cfg.n_layers,
+          "world_size": ws, "seq": args.seq, "batch": args.batch, "storage": args.storage,
+          "compression": args.compression, "checkpoint_bytes": ckpt_bytes,
+          "baseline_step_ms": round(base_ms, 2), "sync_take_s": round(sync_s, 3),
+          "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),
+          "async_unblock_ms": round(unblock * 1e3, 2), "async_drain_s": round(drain, 3),
+          "steps_during_drain": n_during, "step_ms_during_drain_mean": round(mean_ms, 2),
+          "step_ms_during_drain_max": round(max_ms, 2),
+          "slowdown_during_drain": round(mean_ms / base_ms - 1.0, 4) if during else None,
+          "restore_bitwise_ok": bool(okt.item()), "data": "synthetic tokens, random init"})
+    sync(dev)
+    if srv:
+        srv.stop()
+    elif rank == 0:
+        shutil.rmtree(root, ignore_errors=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

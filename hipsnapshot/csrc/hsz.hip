@@ -557,8 +557,11 @@ __global__ void __launch_bounds__(kThreads)
 hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
             const FrameMeta* __restrict__ meta, const uint16_t* __restrict__ lane_bytes_all,
             uint8_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t coded[kMaxCoded + 1];
+  // lane streams as 32-bit words; a word shared by two lanes' streams is
+  // assembled with LDS atomic ORs (the buffer starts zeroed)
+  __shared__ uint32_t coded32[(kMaxCoded + 1 + 8 + 3) / 4];
   __shared__ uint8_t code_of[256];
+  __shared__ uint32_t enc_tab[256];  // high byte -> codeword | len << 16 | escape << 31
   __shared__ uint16_t hcode[16];
   __shared__ uint8_t hlen[16];
   __shared__ uint32_t eidx[kMaxEsc];
@@ -576,6 +579,8 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   uint8_t* fr = out + m.offset;
   write_frame_header(m, fr);
   for (int v = threadIdx.x; v < 256; v += kThreads) code_of[v] = kEsc;
+  const uint32_t c_words = (m.coded + 3) / 4;
+  for (uint32_t i = threadIdx.x; i < c_words; i += kThreads) coded32[i] = 0;
   if (threadIdx.x == 0) {
     ecount = 0;
     for (int c = 0; c < 16; ++c) hlen[c] = m.lens[c];
@@ -583,8 +588,14 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   }
   __syncthreads();
   if (threadIdx.x < m.nsel) code_of[m.dict[threadIdx.x]] = uint8_t(threadIdx.x);
+  __syncthreads();
+  {  // one LDS lookup per element instead of three
+    const uint32_t c = code_of[threadIdx.x];
+    enc_tab[threadIdx.x] = uint32_t(hcode[c]) | (uint32_t(hlen[c]) << 16) |
+                           (c == kEsc ? 0x80000000u : 0u);
+  }
   const uint32_t lb = lane_bytes_all[f * kLanes + threadIdx.x];
-  const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);  // syncs: code_of is ready
+  const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);  // syncs: enc_tab is ready
   uint8_t* body = fr + kFrameHeader;
   uint8_t* lo = body;
   uint16_t* table = reinterpret_cast<uint16_t*>(body + n);  // n % 8 == 0: aligned
@@ -593,8 +604,11 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   const uint64_t groups = n / 8;
   const bool aligned = (reinterpret_cast<uintptr_t>(s) & 15) == 0;
   const bool lo_aligned = (reinterpret_cast<uintptr_t>(lo) & 7) == 0;
-  uint32_t pos = loff, acc = 0;
-  int nb = 0;
+  // bit cursor: word wpos, nb pending bits in acc; the stream starts at byte
+  // loff, i.e. (loff & 3) * 8 zero bits into word loff / 4
+  uint32_t wpos = loff >> 2;
+  uint64_t acc = 0;
+  int nb = int(loff & 3) * 8;
   for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
     uint32_t wd[4];
     load_group(s, g, aligned, wd);
@@ -606,18 +620,21 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
         const int e = q * 2 + h;
         const uint32_t hi = (wd[q] >> (16 * h + 8)) & 255;
         lob |= uint64_t((wd[q] >> (16 * h)) & 255) << (8 * e);
-        const uint32_t c = code_of[hi];
-        if (c == kEsc) {
+        const uint32_t ent = enc_tab[hi];
+        if (ent >> 31) {
           const int k = atomicAdd(&ecount, 1);
           if (k < kMaxEsc) { eidx[k] = uint32_t(g * 8 + e); evals[k] = uint8_t(hi); }
         }
-        acc |= uint32_t(hcode[c]) << nb;
-        nb += hlen[c];
-        while (nb >= 8) {
-          coded[pos++] = uint8_t(acc);
-          acc >>= 8;
-          nb -= 8;
-        }
+        acc |= uint64_t(ent & 0xffffu) << nb;
+        nb += (ent >> 16) & 31;
+      }
+      // after 2 codes acc holds <= 31 + 22 = 53 bits: emit a full 32-bit
+      // word when there is one (predicated per lane, no divergent loop)
+      if (nb >= 32) {
+        atomicOr(&coded32[wpos], uint32_t(acc));
+        ++wpos;
+        acc >>= 32;
+        nb -= 32;
       }
     }
     if (lo_aligned) {
@@ -627,8 +644,9 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
       for (int e = 0; e < 8; ++e) lo[8 * g + e] = uint8_t(lob >> (8 * e));
     }
   }
-  if (nb > 0) coded[pos] = uint8_t(acc);
+  if (nb > 0) atomicOr(&coded32[wpos], uint32_t(acc));  // < 32 bits left
   __syncthreads();
+  const uint8_t* coded = reinterpret_cast<const uint8_t*>(coded32);
   const uint32_t c_bytes = m.coded;
   if ((reinterpret_cast<uintptr_t>(streams) & 3) == 0) {
     const uint32_t nw = c_bytes / 4;

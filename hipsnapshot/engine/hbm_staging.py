@@ -75,7 +75,11 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
     cap = knobs.hbm_staging_max_bytes()
     for dev, reqs in by_dev.items():
         free, _ = torch.cuda.mem_get_info(dev)
-        room = min(free - knobs.hbm_staging_reserve_bytes(), cap)
+        # blocks torch's caching allocator holds but does not use are free
+        # for the arena too (the allocator releases them and retries when a
+        # fresh allocation does not fit) -- a trainer's cache is often tens of GB
+        cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        room = min(free + max(cached, 0) - knobs.hbm_staging_reserve_bytes(), cap)
         want = sum(nb for nb, _ in reqs)
         sts, total = [], 0
         for nb, req_sts in reqs:
@@ -92,7 +96,12 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
         for st in sts:
             offs.append(off)
             off += _nbytes(st)
-        _freeze(dev, sts, offs, total)
+        try:
+            _freeze(dev, sts, offs, total)
+        except torch.cuda.OutOfMemoryError:
+            # fragmentation: the estimate above was optimistic -> host path
+            logger.info(f"HBM staging on cuda:{dev}: arena of {total} B not allocatable")
+            continue
         frozen[dev] = total
     return frozen
 
@@ -103,12 +112,12 @@ def _freeze(dev: int, sts, offs, total: int) -> None:
         arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
         batch = native.CopyBatch()
         views = []
+        base = arena.data_ptr()
         for st, off in zip(sts, offs):
             t = st.tensor.detach()
             view = arena[off: off + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
             if t.numel():
-                batch.add(t.data_ptr(), t.dtype, t.stride(), view.data_ptr(), t.dtype,
-                          view.stride(), list(t.shape), t.element_size())
+                batch.add_tensor(t, base + off)
             views.append(view)
         # producers may differ from the current stream: order after them
         for p in {st.producer for st in sts if st.producer is not None}:

@@ -138,6 +138,8 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     async def _write(wr: WriteReq, buf: StagedBuffer, cost: int) -> None:
         try:
             async with io_sem:
+                if failure:  # the snapshot is failing: do not start more writes
+                    return
                 t_w = time.perf_counter()
                 await storage.write(WriteIO(path=wr.path, buf=buf.view, addr=buf.addr))
                 timeline.add("write", "io", t_w, time.perf_counter(), path=wr.path,
@@ -188,8 +190,9 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
         if failure:
             for t in staging:
                 t.cancel()
-            for t in io_tasks:
-                t.cancel()
+            # writes already handed to the I/O engine are NOT cancelled: their
+            # pinned buffers may only go back to the pool once the engine is
+            # done reading them (queued ones return without writing)
             await asyncio.gather(*staging, *io_tasks, return_exceptions=True)
             executor.shutdown(wait=True)
             raise failure[0]

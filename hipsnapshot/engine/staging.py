@@ -275,8 +275,7 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
         base = slab.data_ptr() if slab is not None else pb.ptr
         batch = native.CopyBatch()
         for t, off in members:
-            batch.add(t.data_ptr(), t.dtype, t.stride(), base + off, t.dtype,
-                      _contig_strides(t.shape), list(t.shape), t.element_size())
+            batch.add_tensor(t, base + off)
         keep = batch.launch(dev, stream, sync=False)
         if slab is not None:
             native.memcpy(dev, slot, pb.ptr, slab.data_ptr(), total_bytes, native.D2H, None,
@@ -314,8 +313,7 @@ def _gather_encoded(members, total_bytes: int, producers, codec: dict) -> Staged
     _join_current_stream(dev, slot)
     batch = native.CopyBatch()
     for t, off in members:
-        batch.add(t.data_ptr(), t.dtype, t.stride(), slab.data_ptr() + off, t.dtype,
-                  _contig_strides(t.shape), list(t.shape), t.element_size())
+        batch.add_tensor(t, slab.data_ptr() + off)
     keep = batch.launch(dev, stream, sync=False)
     try:
         return _encode_device_to_host(dev, slot, slab, codec)

@@ -473,19 +473,43 @@ class CopyBatch:
                 flags, z, a, b = mode
         self.rows.append((src_ptr, dst_ptr, numel, len(z), sc, dc, flags, z, a, b))
 
+    def add_bytes(self, src_ptr: int, dst_ptr: int, nbytes: int) -> None:
+        """Contiguous byte copy (the common case: no stride analysis needed)."""
+        if nbytes > 0:
+            self.rows.append((src_ptr, dst_ptr, nbytes, 1, 0, 0, 1, (nbytes,), (1,), (1,)))
+
+    def add_tensor(self, t: torch.Tensor, dst_ptr: int) -> None:
+        """Copy ``t`` (any strides) into C-order bytes at ``dst_ptr``."""
+        if t.is_contiguous():
+            self.add_bytes(t.data_ptr(), dst_ptr, t.numel() * t.element_size())
+            return
+        st = [1] * t.dim()
+        for i in range(t.dim() - 2, -1, -1):
+            st[i] = st[i + 1] * max(int(t.shape[i + 1]), 1)
+        self.add(t.data_ptr(), t.dtype, t.stride(), dst_ptr, t.dtype, st, list(t.shape),
+                 t.element_size())
+
     def pack(self) -> np.ndarray:
-        arr = np.zeros(len(self.rows), dtype=COPY_DESC_DTYPE)
-        for i, (sp, dp, numel, nd, sc, dc, fl, z, a, b) in enumerate(self.rows):
-            arr[i]["src"] = sp
-            arr[i]["dst"] = dp
-            arr[i]["numel"] = numel
-            arr[i]["ndim"] = nd
-            arr[i]["src_dtype"] = sc
-            arr[i]["dst_dtype"] = dc
-            arr[i]["flags"] = fl
-            arr[i]["sizes"][:nd] = z
-            arr[i]["src_strides"][:nd] = a
-            arr[i]["dst_strides"][:nd] = b
+        """Descriptor table, filled column-wise (per-row structured-array
+        assignment costs ~10 us a row: milliseconds for a model's state)."""
+        n = len(self.rows)
+        arr = np.zeros(n, dtype=COPY_DESC_DTYPE)
+        if not n:
+            return arr
+        cols = list(zip(*self.rows))
+        arr["src"] = np.asarray(cols[0], dtype=np.uint64)
+        arr["dst"] = np.asarray(cols[1], dtype=np.uint64)
+        arr["numel"] = cols[2]
+        arr["ndim"] = cols[3]
+        arr["src_dtype"] = cols[4]
+        arr["dst_dtype"] = cols[5]
+        arr["flags"] = cols[6]
+        for field, col in (("sizes", cols[7]), ("src_strides", cols[8]),
+                           ("dst_strides", cols[9])):
+            mat = np.zeros((n, MAX_DIMS), dtype=np.int64)
+            for i, v in enumerate(col):
+                mat[i, :len(v)] = v
+            arr[field] = mat
         return arr
 
     def launch(self, dev: int, stream_handle: int, sync: bool = True) -> None:
@@ -503,6 +527,15 @@ class CopyBatch:
         ws_bytes = int(lib.hsg_copy_workspace_bytes(arr.ctypes.data, len(arr)))
         stage = PinnedBuffer(ws_bytes)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+        cur = torch.cuda.current_stream(dev)
+        if int(cur.cuda_stream) != int(stream_handle):
+            # ``ws`` comes from torch's caching allocator in the CURRENT
+            # stream's order: its block may have been freed a moment ago by
+            # another thread (the trainer) with kernels still queued on that
+            # stream.  The launch stream must not write it before they ran.
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            torch.cuda.ExternalStream(int(stream_handle), device=f"cuda:{dev}").wait_event(ev)
         rc = lib.hsg_copy_nd(dev, arr.ctypes.data, len(arr), ws.data_ptr(), ws_bytes,
                              stage.ptr, stream_handle, 1 if sync else 0)
         _check(rc, "hsg_copy_nd")
