@@ -559,3 +559,51 @@ def test_take_orders_after_pending_default_stream_work(gpu, tmp_path, compressio
         s.mul_(0)
     Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(big=out_big, small=out_small)})
     assert torch.equal(out_big, big) and all(torch.equal(x, small[0]) for x in out_small)
+
+
+def test_copy_workspace_ordered_after_busy_default_stream(gpu):
+    """A staging thread gathers slabs (copy-kernel workspaces come from torch's
+    caching allocator on the default stream) while the main thread keeps that
+    stream busy, frees small tensors with kernels still queued and reuses the
+    memory: no queued kernel may see its inputs overwritten."""
+    import threading
+
+    from hipsnapshot.engine import staging
+
+    stop = threading.Event()
+    errors = []
+
+    def worker():
+        try:
+            ts = [torch.randn(1000 + i, device=gpu) for i in range(8)]
+            refs = torch.cat([t.cpu() for t in ts])
+            offs = [sum((1000 + j) * 4 for j in range(i)) for i in range(8)]
+            total = offs[-1] + (1007) * 4
+            while not stop.is_set():
+                st = staging.gather_to_host(list(zip(ts, offs)), total, [])
+                got = torch.frombuffer(bytearray(st.view), dtype=torch.float32)
+                st.release()
+                if not torch.equal(got, refs):
+                    errors.append("slab bytes differ")
+                    return
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = threading.Thread(target=worker)
+    th.start()
+    a = torch.randn(2048, 2048, device=gpu)
+    results = []
+    try:
+        for i in range(300):
+            a = torch.tanh(a @ a)  # keeps the default stream backed up
+            x = torch.full((65536,), float(i), device=gpu)
+            y = x * 2
+            del x  # freed while `x * 2` may still be queued
+            results.append((i, y))
+        torch.cuda.synchronize()
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors
+    for i, y in results:
+        assert torch.all(y == 2.0 * i), i
