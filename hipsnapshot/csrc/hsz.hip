@@ -65,6 +65,12 @@ struct FrameMeta {
 
 __device__ __forceinline__ uint64_t align16(uint64_t n) { return (n + 15) & ~uint64_t(15); }
 
+// bf16/fp16 high bytes come in +/- pairs 128 apart (sign bit), which land on
+// the same LDS bank; the lookup tables shift the upper half by one dword so
+// that v and v ^ 0x80 are served in the same cycle (PMC: SQ_LDS_BANK_CONFLICT).
+__device__ __forceinline__ uint32_t cslot(uint32_t v) { return v + ((v >> 7) << 2); }  // u8 tables
+__device__ __forceinline__ uint32_t eslot(uint32_t v) { return v + (v >> 7); }         // u32 tables
+
 __device__ __forceinline__ int block_sum(int v, int* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -126,9 +132,9 @@ __device__ void build_dict(const uint32_t* hist, uint8_t* dict, uint8_t* code_of
     for (int j = k + lane; j < 16; j += 64) dict[j] = 0;
   }
   __syncthreads();
-  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[v] = kEsc;
+  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[cslot(v)] = kEsc;
   __syncthreads();
-  if (threadIdx.x < *nsel) code_of[dict[threadIdx.x]] = uint8_t(threadIdx.x);
+  if (threadIdx.x < *nsel) code_of[cslot(dict[threadIdx.x])] = uint8_t(threadIdx.x);
   __syncthreads();
 }
 
@@ -227,7 +233,7 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
             FrameMeta* __restrict__ meta, uint16_t* __restrict__ lane_bytes_all) {
   __shared__ uint32_t hist[256];
   __shared__ uint8_t dict[16];
-  __shared__ uint8_t code_of[256];
+  __shared__ uint8_t code_of[260];  // indexed through cslot()
   __shared__ int nsel;
   __shared__ int red[4];
   const uint64_t f = blockIdx.x;
@@ -266,7 +272,7 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
         for (int q = 0; q < 4; ++q) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const uint32_t c = code_of[(wd[q] >> (16 * h + 8)) & 255];
+            const uint32_t c = code_of[cslot((wd[q] >> (16 * h + 8)) & 255)];
             lcnt[c * kLanes + threadIdx.x] += 1;
           }
         }
@@ -318,12 +324,12 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
       const uint4 v = sv[i];
       const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int p = W - 1; p < 16; p += W) esc += code_of[(wd[p >> 2] >> (8 * (p & 3))) & 255] == kEsc;
+      for (int p = W - 1; p < 16; p += W) esc += code_of[cslot((wd[p >> 2] >> (8 * (p & 3))) & 255)] == kEsc;
     }
     for (uint64_t e = nv * 16 / W + threadIdx.x; e < n; e += kThreads)
-      esc += code_of[s[e * W + W - 1]] == kEsc;
+      esc += code_of[cslot(s[e * W + W - 1])] == kEsc;
   } else {
-    for (uint64_t e = threadIdx.x; e < n; e += kThreads) esc += code_of[s[e * W + W - 1]] == kEsc;
+    for (uint64_t e = threadIdx.x; e < n; e += kThreads) esc += code_of[cslot(s[e * W + W - 1])] == kEsc;
   }
   const int total = block_sum(esc, red);
   if (threadIdx.x == 0) {
@@ -416,7 +422,7 @@ template <int W>
 __global__ void __launch_bounds__(kThreads)
 hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
            const FrameMeta* __restrict__ meta, uint8_t* __restrict__ out) {
-  __shared__ uint8_t code_of[256];
+  __shared__ uint8_t code_of[260];  // indexed through cslot()
   __shared__ uint32_t eidx[kMaxEsc];
   __shared__ uint8_t evals[kMaxEsc];
   __shared__ int ecount;
@@ -444,10 +450,10 @@ hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_byt
     }
     return;
   }
-  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[v] = kEsc;
+  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[cslot(v)] = kEsc;
   if (threadIdx.x == 0) ecount = 0;
   __syncthreads();
-  if (threadIdx.x < m.nsel) code_of[m.dict[threadIdx.x]] = uint8_t(threadIdx.x);
+  if (threadIdx.x < m.nsel) code_of[cslot(m.dict[threadIdx.x])] = uint8_t(threadIdx.x);
   __syncthreads();
   uint8_t* nib = body;
   const uint64_t nb = (n + 1) / 2;
@@ -474,7 +480,7 @@ hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_byt
         for (int h = 0; h < 2; ++h) {
           const int e = q * 2 + h;
           const uint32_t hi = (wd[q] >> (16 * h + 8)) & 255;
-          const uint32_t c = code_of[hi];
+          const uint32_t c = code_of[cslot(hi)];
           codes |= c << (4 * e);
           lob |= uint64_t((wd[q] >> (16 * h)) & 255) << (8 * e);
           if (c == kEsc) {
@@ -499,7 +505,7 @@ hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_byt
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const uint32_t hi = wd[e] >> 24;
-        const uint32_t c = code_of[hi];
+        const uint32_t c = code_of[cslot(hi)];
         codes |= c << (4 * e);
         lob[3 * e] = wd[e] & 255;
         lob[3 * e + 1] = (wd[e] >> 8) & 255;
@@ -531,7 +537,7 @@ hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_byt
         if (e >= n) break;
         const uint8_t* el = s + e * W;
         const uint32_t hi = el[W - 1];
-        const uint32_t c = code_of[hi];
+        const uint32_t c = code_of[cslot(hi)];
         byte |= uint8_t(c << (4 * h));
         for (int b = 0; b < W - 1; ++b) lo[e * (W - 1) + b] = el[b];
         if (c == kEsc) {
@@ -560,8 +566,8 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   // lane streams as 32-bit words; a word shared by two lanes' streams is
   // assembled with LDS atomic ORs (the buffer starts zeroed)
   __shared__ uint32_t coded32[(kMaxCoded + 1 + 8 + 3) / 4];
-  __shared__ uint8_t code_of[256];
-  __shared__ uint32_t enc_tab[256];  // high byte -> codeword | len << 16 | escape << 31
+  __shared__ uint8_t code_of[260];  // indexed through cslot()
+  __shared__ uint32_t enc_tab[257];  // eslot(high byte) -> codeword | len << 16 | escape << 31
   __shared__ uint16_t hcode[16];
   __shared__ uint8_t hlen[16];
   __shared__ uint32_t eidx[kMaxEsc];
@@ -578,7 +584,7 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   const uint8_t* s = src + base;
   uint8_t* fr = out + m.offset;
   write_frame_header(m, fr);
-  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[v] = kEsc;
+  for (int v = threadIdx.x; v < 256; v += kThreads) code_of[cslot(v)] = kEsc;
   const uint32_t c_words = (m.coded + 3) / 4;
   for (uint32_t i = threadIdx.x; i < c_words; i += kThreads) coded32[i] = 0;
   if (threadIdx.x == 0) {
@@ -587,11 +593,11 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
     canonical_codes(hlen, hcode);
   }
   __syncthreads();
-  if (threadIdx.x < m.nsel) code_of[m.dict[threadIdx.x]] = uint8_t(threadIdx.x);
+  if (threadIdx.x < m.nsel) code_of[cslot(m.dict[threadIdx.x])] = uint8_t(threadIdx.x);
   __syncthreads();
   {  // one LDS lookup per element instead of three
-    const uint32_t c = code_of[threadIdx.x];
-    enc_tab[threadIdx.x] = uint32_t(hcode[c]) | (uint32_t(hlen[c]) << 16) |
+    const uint32_t c = code_of[cslot(threadIdx.x)];
+    enc_tab[eslot(threadIdx.x)] = uint32_t(hcode[c]) | (uint32_t(hlen[c]) << 16) |
                            (c == kEsc ? 0x80000000u : 0u);
   }
   const uint32_t lb = lane_bytes_all[f * kLanes + threadIdx.x];
@@ -620,7 +626,7 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
         const int e = q * 2 + h;
         const uint32_t hi = (wd[q] >> (16 * h + 8)) & 255;
         lob |= uint64_t((wd[q] >> (16 * h)) & 255) << (8 * e);
-        const uint32_t ent = enc_tab[hi];
+        const uint32_t ent = enc_tab[eslot(hi)];
         if (ent >> 31) {
           const int k = atomicAdd(&ecount, 1);
           if (k < kMaxEsc) { eidx[k] = uint32_t(g * 8 + e); evals[k] = uint8_t(hi); }
