@@ -469,8 +469,11 @@ class LazySnapshotMetadata(SnapshotMetadata):
         return SnapshotMetadata.to_json(self)
 
 
+_COMPACT = json.JSONEncoder(separators=(",", ":"))  # one encoder, not one per entry
+
+
 def entry_json(entry: Entry) -> str:
-    return json.dumps(entry.to_dict(), sort_keys=False, separators=(",", ":"))
+    return _COMPACT.encode(entry.to_dict())
 
 
 def metadata_json_from_parts(version: str, world_size: int, parts: List[str]) -> str:

@@ -151,23 +151,23 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
     # less than 2 slabs' worth of batchable bytes remain on a device, close
     # slabs at a quarter of the threshold.
     remaining: Dict[Optional[torch.device], int] = defaultdict(int)
+    info = []  # (batchable below threshold?, nbytes, device) once per request
     for wr in write_reqs:
         st = wr.buffer_stager
         if is_batchable(st):
-            nb = st.tensor.numel() * st.tensor.element_size()
+            t = st.tensor
+            nb = t.numel() * t.element_size()
             if nb < threshold:
-                remaining[st.tensor.device if st.tensor.is_cuda else None] += nb
-    for wr in write_reqs:
+                dev = t.device if t.is_cuda else None
+                remaining[dev] += nb
+                info.append((True, nb, dev))
+                continue
+        info.append((False, 0, None))
+    for wr, (small, nbytes, dev) in zip(write_reqs, info):
+        if not small:
+            out.append(wr)
+            continue
         st = wr.buffer_stager
-        if not is_batchable(st):
-            out.append(wr)
-            continue
-        t = st.tensor
-        nbytes = t.numel() * t.element_size()
-        if nbytes >= threshold:
-            out.append(wr)
-            continue
-        dev = t.device if t.is_cuda else None
         remaining[dev] -= nbytes
         cap = threshold if remaining[dev] + nbytes > 2 * threshold else \
             max(threshold // 4, min(threshold, 16 << 20))
@@ -178,7 +178,9 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
             tag = f"cuda{dev.index}" if dev is not None else "cpu"
             return Slab(dev, f"{name_prefix}_{tag}_{k}")
 
-        lst = slabs.setdefault(dev, [_new_slab(0)])
+        lst = slabs.get(dev)
+        if lst is None:
+            lst = slabs[dev] = [_new_slab(0)]
         if lst[-1].members and _align(lst[-1].sz_bytes, align) + nbytes >= cap:
             lst.append(_new_slab(len(lst)))
         lo, hi = lst[-1].add(nbytes, st, align)

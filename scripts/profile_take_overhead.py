@@ -25,6 +25,7 @@ def main() -> None:
     ap.add_argument("--takes", type=int, default=20)
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--compression", default="none")
+    ap.add_argument("--optim", action="store_true", help="include AdamW state (3x the leaves)")
     args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
@@ -43,17 +44,25 @@ def main() -> None:
     print("params:", len(list(model.parameters())))
     root = tempfile.mkdtemp()
     app = {"model": model}
+    if args.optim:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-4)
+        model(torch.randint(0, cfg.vocab_size, (1, 8))).sum().backward()
+        opt.step()
+        app["optim"] = opt
     Snapshot.take(os.path.join(root, "warm"), app, compression=args.compression)
     prof = cProfile.Profile() if args.profile else None
-    t0 = time.perf_counter()
+    times = []
     for i in range(args.takes):
         if prof:
             prof.enable()
+        t0 = time.perf_counter()
         Snapshot.take(os.path.join(root, "s"), app, compression=args.compression)
+        times.append(time.perf_counter() - t0)
         if prof:
             prof.disable()
-    dt = (time.perf_counter() - t0) / args.takes
-    print(f"mean take: {dt * 1e3:.2f} ms")
+    times.sort()
+    print(f"mean take: {sum(times) / len(times) * 1e3:.2f} ms, median "
+          f"{times[len(times) // 2] * 1e3:.2f} ms, min {times[0] * 1e3:.2f} ms")
     if prof:
         pstats.Stats(prof).sort_stats("cumulative").print_stats(35)
     shutil.rmtree(root, ignore_errors=True)
