@@ -12,7 +12,10 @@ import torch
 import torch.distributed as dist
 
 
-def init_dist(backend: str = None):
+def init_dist(backend: str = None, gpu: bool = None):
+    """Process group + this rank's device.  ``backend="gloo"`` with ``gpu``
+    (default: a GPU is visible) rehearses several ranks sharing one GPU --
+    correctness and planning cost, not scaling (RCCL refuses shared GPUs)."""
     if "RANK" not in os.environ:
         s = socket.socket()
         s.bind(("127.0.0.1", 0))
@@ -29,7 +32,14 @@ def init_dist(backend: str = None):
         dev = torch.device("cuda", local_rank)
     else:
         dist.init_process_group(backend)
-        dev = torch.device("cpu")
+        if gpu is None:
+            gpu = torch.cuda.is_available()
+        if gpu:
+            idx = local_rank % torch.cuda.device_count()
+            torch.cuda.set_device(idx)
+            dev = torch.device("cuda", idx)
+        else:
+            dev = torch.device("cpu")
     return dist.get_rank(), dist.get_world_size(), dev
 
 

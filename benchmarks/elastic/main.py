@@ -25,11 +25,24 @@ from hipsnapshot.models.llama import Llama, LlamaConfig, build_fsdp_llama  # noq
 
 
 def checksums(model):
+    """sha256 of a few full tensors, assembled on rank 0 from every rank's
+    shard through CPU object collectives (works with gloo ranks that share a
+    GPU, where DTensor.full_tensor() would need RCCL)."""
+    from torch.distributed.tensor._utils import compute_local_shape_and_global_offset
+
     out = {}
     for k, v in model.state_dict().items():
-        if k.startswith("layers.0.") or k in ("norm.weight",):
-            full = v.full_tensor().detach().cpu().contiguous()
-            out[k] = hashlib.sha256(full.view(torch.uint8).numpy().tobytes()).hexdigest()
+        if not (k.startswith("layers.0.") or k in ("norm.weight",)):
+            continue
+        _, off = compute_local_shape_and_global_offset(v.shape, v.device_mesh, v.placements)
+        pieces = [None] * dist.get_world_size()
+        dist.all_gather_object(pieces, (list(off), v.to_local().detach().cpu()))
+        if dist.get_rank() == 0:
+            full = torch.empty(v.shape, dtype=v.dtype)
+            for o, t in pieces:
+                if t.numel():
+                    full[tuple(slice(a, a + n) for a, n in zip(o, t.shape))] = t
+            out[k] = hashlib.sha256(full.contiguous().view(torch.uint8).numpy().tobytes()).hexdigest()
     return out
 
 
@@ -40,8 +53,10 @@ def main():
                                                    "hs_elastic"))
     ap.add_argument("--model", default="llama3_8b")
     ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
+                    help="gloo: several ranks may share one GPU (correctness rehearsal)")
     args = ap.parse_args()
-    rank, ws, dev = init_dist()
+    rank, ws, dev = init_dist(args.backend)
     from torch.distributed.device_mesh import init_device_mesh
     from torch.distributed.fsdp import fully_shard
 
@@ -76,12 +91,18 @@ def main():
         sync(dev)
         s = max_over_ranks(time.perf_counter() - t0, dev)
         cs = checksums(model)
-        with open(args.path + ".checksums.json") as f:
-            ref = json.load(f)
-        bad = [k for k in ref if cs[k] != ref[k]]
-        ok = not bad
-        if bad:
-            log(f"mismatch: {bad[:5]} {[(cs[k], ref[k]) for k in bad[:3]]}")
+        ok = True
+        if rank == 0:
+            with open(args.path + ".checksums.json") as f:
+                ref = json.load(f)
+            bad = [k for k in ref if cs[k] != ref[k]]
+            ok = not bad
+        flag = [ok]
+        dist.broadcast_object_list(flag, src=0)
+        ok = flag[0]
+        bad = [] if ok else ["(see rank 0)"]
+        if not ok and rank == 0:
+            log(f"checksum mismatch: {[k for k in ref if cs[k] != ref[k]][:5]}")
         saved_ws = Snapshot(args.path).metadata.world_size
         nbytes = sum(p._local_tensor.numel() * 2 for p in model.parameters()) * ws
         emit({"bench": "elastic_restore", "saved_world_size": saved_ws, "world_size": ws,

@@ -22,7 +22,7 @@ from hipsnapshot.models.resnet import resnet18  # noqa: E402
 
 
 def main():
-    rank, ws, dev = init_dist("gloo")
+    rank, ws, dev = init_dist("gloo", gpu=False)
     torch.manual_seed(0)
     model = DDP(resnet18(100))
     opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9)
