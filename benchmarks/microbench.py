@@ -116,6 +116,59 @@ def main():
     best, med = timeit(torch_gather, 3)
     emit(test="gather_hbm_torch_copy_loop", GBps=total / best / 1e9, median_GBps=total / med / 1e9)
 
+    # GPU time of the copy kernel alone (descriptor tables pre-built): one
+    # 1 GiB contiguous copy, and a Llama-3-8B-like freeze (291 tensors, 16 GB
+    # -> arena) as the async_take HBM freeze issues it
+    def gpu_ms(batch, dst_keep):
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        best = None
+        for _ in range(4):
+            keep = batch.launch(dev, int(st.cuda_stream), sync=False)
+            st.synchronize()
+            del keep
+        for _ in range(5):
+            e0.record(st)
+            keep = batch.launch(dev, int(st.cuda_stream), sync=False)
+            e1.record(st)
+            st.synchronize()
+            del keep
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        return best
+
+    big = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:0")
+    big2 = torch.empty_like(big)
+    b1 = native.CopyBatch()
+    b1.add_bytes(big.data_ptr(), big2.data_ptr(), big.numel())
+    ms = gpu_ms(b1, big2)
+    emit(test="copy_nd_contig_1GiB_gpu_time", GBps=big.numel() / ms / 1e6, ms=ms,
+         note="payload bytes/s; HBM traffic 2x")
+    del big, big2
+    shapes = [(128256, 4096), (128256, 4096)] + [(4096, 4096), (1024, 4096), (1024, 4096),
+                                                 (4096, 4096), (14336, 4096), (4096, 14336),
+                                                 (14336, 4096), (4096,), (4096,)] * 32 + [(4096,)]
+    ws_ = [torch.empty(sh, dtype=torch.bfloat16, device="cuda:0") for sh in shapes]
+    tot = sum(w.numel() * 2 for w in ws_)
+    arena = torch.empty(tot + 256 * len(ws_), dtype=torch.uint8, device="cuda:0")
+    bf = native.CopyBatch()
+    off = 0
+    for w in ws_:
+        bf.add_tensor(w, arena.data_ptr() + off)
+        off += (w.numel() * 2 + 255) // 256 * 256
+    ms = gpu_ms(bf, arena)
+    emit(test="freeze_llama3_8b_291_tensors_gpu_time", GBps=tot / ms / 1e6, ms=ms, bytes=tot,
+         note="payload bytes/s; the trainer's stream waits this long after async_take")
+    tt = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tt[0].record()
+    for w in ws_:
+        arena[:w.numel() * 2].view(torch.bfloat16).view(w.shape).copy_(w)
+    tt[1].record()
+    torch.cuda.synchronize()
+    emit(test="freeze_llama3_8b_torch_copy_loop_gpu_time", ms=tt[0].elapsed_time(tt[1]),
+         GBps=tot / tt[0].elapsed_time(tt[1]) / 1e6)
+    del ws_, arena
+
     # strided pack: transpose view of 8192x8192 bf16
     a = torch.empty(8192, 8192, dtype=torch.bfloat16, device="cuda:0").normal_()
     at = a.t()
