@@ -147,6 +147,10 @@ def main() -> None:
     max_ms = max_over_ranks(max(during) if during else 0.0, dev) * 1e3
 
     log(f"phase: restore (unblock {unblock * 1e3:.1f} ms, {len(during)} steps during drain)")
+    stored = None
+    if args.storage == "fs" and rank == 0:
+        stored = sum(os.path.getsize(os.path.join(r, f))
+                     for r, _, fs in os.walk(f"{root}/async") for f in fs)
     # restore the async snapshot: parameters must equal the values at the
     # async_take call, not the ones the overlapped steps produced
     Snapshot(f"{root}/async", storage_options=opts).restore(app)
@@ -163,7 +167,8 @@ def main() -> None:
           "steps_during_drain": n_during, "step_ms_during_drain_mean": round(mean_ms, 2),
           "step_ms_during_drain_max": round(max_ms, 2),
           "slowdown_during_drain": round(mean_ms / base_ms - 1.0, 4) if during else None,
-          "restore_bitwise_ok": bool(okt.item()), "data": "synthetic tokens, random init"})
+          "restore_bitwise_ok": bool(okt.item()), "stored_bytes": stored,
+          "data": "synthetic tokens, random init"})
     sync(dev)
     if srv:
         srv.stop()

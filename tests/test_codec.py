@@ -259,3 +259,26 @@ def _dtensor_worker(path: str, mode: str) -> None:
         d = distribute_tensor(torch.zeros_like(full), mesh, [Shard(1)])
         Snapshot(path).restore({"sd": StateDict(w=d)})
         assert torch.equal(d.full_tensor(), full)
+
+
+def test_ratio_holds_for_trained_weights_and_adam_state():
+    """The high-byte entropy of TRAINED weights and AdamW moments is as low as
+    at init (the ratio is not an artefact of random-init data)."""
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(128, 512), torch.nn.GELU(), torch.nn.Linear(512, 128))
+    opt = torch.optim.AdamW(m.parameters(), lr=3e-3)
+    x_all = torch.randn(2048, 128)
+    w_t = torch.randn(128, 128) / 12
+    for _ in range(150):
+        x = x_all[torch.randint(0, 2048, (128,))]
+        loss = ((m(x) - torch.tanh(x @ w_t)) ** 2).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    st = opt.state[m[0].weight]
+    for name, t, bound in [("weight", m[0].weight, 0.70), ("exp_avg", st["exp_avg"], 0.70),
+                           ("exp_avg_sq", st["exp_avg_sq"], 0.62)]:
+        raw = _bytes(t.detach().to(torch.bfloat16))
+        blob = codec.encode_cpu(raw, 2, 16 * 1024)
+        assert len(blob) / len(raw) < bound, (name, len(blob) / len(raw))
+        assert codec.decode_cpu(blob.tobytes()).tobytes() == raw
