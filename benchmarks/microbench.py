@@ -241,37 +241,38 @@ def main():
         del blob, back
     del w
 
-    # HSZ1 lossless codec: encode (4 launches) and decode of 1 GiB bf16 in HBM
+    # HSZ1 lossless codec: encode (4 launches) and decode of 1 GiB bf16 / fp32 in HBM
     from hipsnapshot.ops import codec
 
-    x = (torch.randn(512 << 20, device="cuda:0") / 64).to(torch.bfloat16).view(torch.uint8)
-    st = torch.cuda.current_stream()
-    out, total, meta = codec.encode_device(x, 2, int(st.cuda_stream))
-    st.synchronize()
-    nb = int(total.item())
-    nf = codec.n_frames_for(x.numel(), codec.DEFAULT_FRAME_BYTES)
-    hdr = codec.parse_header(out[:codec.payload_start(nf)].cpu().numpy().tobytes())
-    offs = torch.tensor(hdr.offsets, dtype=torch.int64, device="cuda:0")
-    back = torch.empty_like(x)
+    for name, dt, w in (("bf16", torch.bfloat16, 2), ("fp32", torch.float32, 4)):
+        x = (torch.randn((1 << 30) // w, device="cuda:0") / 64).to(dt).view(torch.uint8)
+        st = torch.cuda.current_stream()
+        out, total, meta = codec.encode_device(x, w, int(st.cuda_stream))
+        st.synchronize()
+        nb = int(total.item())
+        nf = codec.n_frames_for(x.numel(), codec.DEFAULT_FRAME_BYTES)
+        hdr = codec.parse_header(out[:codec.payload_start(nf)].cpu().numpy().tobytes())
+        offs = torch.tensor(hdr.offsets, dtype=torch.int64, device="cuda:0")
+        back = torch.empty_like(x)
 
-    def enc():
-        codec.launch_encode(x, 2, int(st.cuda_stream), codec.DEFAULT_FRAME_BYTES, out, total,
-                            meta)
+        def enc():
+            codec.launch_encode(x, w, int(st.cuda_stream), codec.DEFAULT_FRAME_BYTES, out, total,
+                                meta)
 
-    def dec():
-        native.hsz_decode_gpu(dev, out.data_ptr(), offs.data_ptr(), 0, hdr.n_frames,
-                              hdr.logical_size, 2, hdr.frame_bytes, back.data_ptr(),
-                              int(st.cuda_stream))
+        def dec():
+            native.hsz_decode_gpu(dev, out.data_ptr(), offs.data_ptr(), 0, hdr.n_frames,
+                                  hdr.logical_size, w, hdr.frame_bytes, back.data_ptr(),
+                                  int(st.cuda_stream))
 
-    best, med = timeit(enc)
-    emit(test="hsz_encode_1GiB_bf16", GBps=x.numel() / best / 1e9,
-         median_GBps=x.numel() / med / 1e9, ms=best * 1e3, ratio=nb / x.numel(),
-         note="logical bytes/s; HBM traffic = 2 reads + ~0.67 write")
-    best, med = timeit(dec)
-    emit(test="hsz_decode_1GiB_bf16", GBps=x.numel() / best / 1e9,
-         median_GBps=x.numel() / med / 1e9, ms=best * 1e3)
-    assert torch.equal(back, x)
-    del x, out, back
+        best, med = timeit(enc)
+        emit(test=f"hsz_encode_1GiB_{name}", GBps=x.numel() / best / 1e9,
+             median_GBps=x.numel() / med / 1e9, ms=best * 1e3, ratio=nb / x.numel(),
+             note="logical bytes/s; HBM traffic = 2 reads + ratio write")
+        best, med = timeit(dec)
+        emit(test=f"hsz_decode_1GiB_{name}", GBps=x.numel() / best / 1e9,
+             median_GBps=x.numel() / med / 1e9, ms=best * 1e3)
+        assert torch.equal(back, x)
+        del x, out, back, meta, offs
 
     if not args.skip_fs:
         os.makedirs(args.dir, exist_ok=True)

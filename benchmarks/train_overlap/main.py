@@ -16,6 +16,7 @@ The reference publishes no such number (time-to-unblock is printed but not
 reported by `/root/reference/benchmarks/torchrec/main.py:133-151`).
 
     python benchmarks/train_overlap/main.py --layers 32 --seq 2048
+    python benchmarks/train_overlap/main.py --layers 16 --master-dtype fp32
     torchrun --nproc-per-node 8 benchmarks/train_overlap/main.py
 """
 
@@ -54,6 +55,9 @@ def main() -> None:
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
     ap.add_argument("--storage", default="fs", choices=["fs", "s3"])
     ap.add_argument("--path", default=None)
+    ap.add_argument("--master-dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="stored parameter (and AdamW state) dtype; fp32 = mixed precision "
+                         "with bf16 compute")
     args = ap.parse_args()
 
     rank, ws, dev = init_dist()
@@ -67,7 +71,8 @@ def main() -> None:
     if args.layers:
         cfg.n_layers = args.layers
     mesh = init_device_mesh(dev.type, (ws,))
-    model = build_fsdp_llama(cfg, dev, torch.bfloat16, mesh=mesh)
+    master = torch.float32 if args.master_dtype == "fp32" else torch.bfloat16
+    model = build_fsdp_llama(cfg, dev, master, mesh=mesh, compute_dtype=torch.bfloat16)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-5, foreach=True)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
 
@@ -160,7 +165,8 @@ def main() -> None:
 
     emit({"bench": "train_overlap_async_take", "model": args.model, "layers": cfg.n_layers,
           "world_size": ws, "seq": args.seq, "batch": args.batch, "storage": args.storage,
-          "compression": args.compression, "checkpoint_bytes": ckpt_bytes,
+          "compression": args.compression, "master_dtype": args.master_dtype,
+          "checkpoint_bytes": ckpt_bytes,
           "baseline_step_ms": round(base_ms, 2), "sync_take_s": round(sync_s, 3),
           "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 2), "async_drain_s": round(drain, 3),

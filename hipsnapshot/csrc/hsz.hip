@@ -3,7 +3,7 @@
 // Encode (before D2H) = 4 launches on the caller's stream:
 //   hsz_analyze<W>  one workgroup per 256 KiB frame: 2048-sample LDS histogram
 //                   -> 15-entry dictionary (wave-wide argmax), then a full pass
-//                   over the frame.  For 2-byte elements that pass keeps one
+//                   over the frame.  For 2-/4-byte elements that pass keeps one
 //                   16-bin index histogram per lane in LDS; thread 0 builds the
 //                   length-limited Huffman code and every lane sizes its own
 //                   stream, so the frame mode (raw / nibble / huffman) and the
@@ -14,7 +14,7 @@
 //                   step, coalesced 16-B loads, nibble codes via an LDS code
 //                   table, low-byte plane stores; the rare escapes go to an LDS
 //                   list and are written in element order by rank
-//   hsz_encode2     mode 2: lane t packs the codes of element groups t, t+256,
+//   hsz_encode2<W>  mode 2: lane t packs the codes of element groups t, t+256,
 //                   ... into its own bit stream in LDS (stream offsets from a
 //                   block scan of the analyze pass's lane sizes) while the
 //                   low-byte plane streams out with 8-B stores; the finished
@@ -22,7 +22,7 @@
 // Decode (after H2D) = 2 launches, one workgroup per frame each:
 //   hsz_decode<W>   modes 0/1 (escape positions are collected from the nibble
 //                   plane first, then every element is rebuilt)
-//   hsz_decode2     mode 2: the frame's streams are staged in LDS, lane t
+//   hsz_decode2<W>  mode 2: the frame's streams are staged in LDS, lane t
 //                   decodes its stream through a 2048-entry LDS lookup table
 //                   and stores its groups as 16-B vectors (adjacent lanes ->
 //                   adjacent groups, so the stores coalesce); escapes are
@@ -212,19 +212,52 @@ __device__ void canonical_codes(const uint8_t* lens, uint16_t* codes) {
     }
 }
 
-// The 8 high bytes of element group g (elements 8g..8g+7, 2-byte elements).
+// Element group g (elements 8g..8g+7, W = 2 or 4 bytes each) as 2W
+// little-endian words: W / 2 coalesced 16-B loads per lane.
+template <int W>
 __device__ __forceinline__ void load_group(const uint8_t* s, uint64_t g, bool aligned,
-                                           uint32_t wd[4]) {
+                                           uint32_t wd[2 * W]) {
   if (aligned) {
-    const uint4 v = reinterpret_cast<const uint4*>(s)[g];
-    wd[0] = v.x; wd[1] = v.y; wd[2] = v.z; wd[3] = v.w;
-  } else {
-    const uint8_t* p = s + 16 * g;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int k = 0; k < W / 2; ++k) {
+      const uint4 v = reinterpret_cast<const uint4*>(s)[g * (W / 2) + k];
+      wd[4 * k] = v.x; wd[4 * k + 1] = v.y; wd[4 * k + 2] = v.z; wd[4 * k + 3] = v.w;
+    }
+  } else {
+    const uint8_t* p = s + 8 * W * g;
+#pragma unroll
+    for (int q = 0; q < 2 * W; ++q)
       wd[q] = uint32_t(p[4 * q]) | (uint32_t(p[4 * q + 1]) << 8) | (uint32_t(p[4 * q + 2]) << 16) |
               (uint32_t(p[4 * q + 3]) << 24);
   }
+}
+
+// Element e of a loaded group (e must be a compile-time constant after unrolling).
+template <int W>
+__device__ __forceinline__ uint32_t group_elem(const uint32_t* wd, int e) {
+  if constexpr (W == 2) return (wd[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+  else return wd[e];
+}
+
+// The low (W-1) bytes of the 8 elements of a group form 8(W-1) contiguous
+// bytes of the low-byte plane, held as W-1 u64 words.  put_lo takes the
+// whole element and keeps its low bytes.
+template <int W>
+__device__ __forceinline__ void put_lo(uint64_t* lw, int e, uint32_t v) {
+  constexpr int L = 8 * (W - 1);
+  const int bp = L * e;
+  const uint64_t x = v & ((1u << L) - 1);  // drop the high byte
+  lw[bp >> 6] |= x << (bp & 63);
+  if ((bp & 63) + L > 64) lw[(bp >> 6) + 1] |= x >> (64 - (bp & 63));
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t get_lo(const uint64_t* lw, int e) {
+  constexpr int L = 8 * (W - 1);
+  const int bp = L * e;
+  uint64_t x = lw[bp >> 6] >> (bp & 63);
+  if ((bp & 63) + L > 64) x |= lw[(bp >> 6) + 1] << (64 - (bp & 63));
+  return uint32_t(x) & ((1u << L) - 1);
 }
 
 template <int W>
@@ -253,7 +286,7 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   const uint64_t tail = len - n * W;
   const uint64_t coded1 = kFrameHeader + (n + 1) / 2 + uint64_t(W - 1) * n + tail;  // + escapes
   const uint64_t raw = kFrameHeader + len;
-  if constexpr (W == 2) {
+  if constexpr (W == 2 || W == 4) {
     if (n > 0 && n % 8 == 0) {
       // mode-2 sizing: one 16-bin histogram per lane (lane t owns groups t, t+256, ...)
       __shared__ uint32_t lcnt[16 * kLanes];
@@ -266,15 +299,12 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
       const uint64_t groups = n / 8;
       const bool aligned = (reinterpret_cast<uintptr_t>(s) & 15) == 0;
       for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
-        uint32_t wd[4];
-        load_group(s, g, aligned, wd);
+        uint32_t wd[2 * W];
+        load_group<W>(s, g, aligned, wd);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const uint32_t c = code_of[cslot((wd[q] >> (16 * h + 8)) & 255)];
-            lcnt[c * kLanes + threadIdx.x] += 1;
-          }
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t c = code_of[cslot(group_elem<W>(wd, e) >> (8 * (W - 1)))];
+          lcnt[c * kLanes + threadIdx.x] += 1;
         }
       }
       __syncthreads();
@@ -295,7 +325,7 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
       if (threadIdx.x == 0) {
         const uint32_t esc = fcnt[kEsc];
         const uint64_t size1 = coded1 + esc;
-        const uint64_t size2 = kFrameHeader + n + kLaneTable + uint64_t(c_bytes) + esc + tail;
+        const uint64_t size2 = kFrameHeader + uint64_t(W - 1) * n + kLaneTable + uint64_t(c_bytes) + esc + tail;
         FrameMeta m;
         m.mode = 0;
         if (esc <= uint32_t(kMaxEsc)) {
@@ -558,7 +588,8 @@ hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_byt
     tail[j] = j < tail_len ? s[n * W + j] : 0;
 }
 
-// Mode-2 encoder (2-byte elements).  LDS: 64 KiB stream buffer + escapes.
+// Mode-2 encoder (W = 2 or 4).  LDS: 64 KiB stream buffer + escapes.
+template <int W>
 __global__ void __launch_bounds__(kThreads)
 hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
             const FrameMeta* __restrict__ meta, const uint16_t* __restrict__ lane_bytes_all,
@@ -580,7 +611,7 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   if (m.mode != 2) return;
   const uint64_t base = f * frame_bytes;
   const uint64_t len = min(uint64_t(frame_bytes), logical - base);
-  const uint64_t n = len / 2;
+  const uint64_t n = len / W;
   const uint8_t* s = src + base;
   uint8_t* fr = out + m.offset;
   write_frame_header(m, fr);
@@ -604,9 +635,10 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);  // syncs: enc_tab is ready
   uint8_t* body = fr + kFrameHeader;
   uint8_t* lo = body;
-  uint16_t* table = reinterpret_cast<uint16_t*>(body + n);  // n % 8 == 0: aligned
+  const uint64_t nlo = uint64_t(W - 1) * n;
+  uint16_t* table = reinterpret_cast<uint16_t*>(body + nlo);  // n % 8 == 0: aligned
   table[threadIdx.x] = uint16_t(lb);
-  uint8_t* streams = body + n + kLaneTable;
+  uint8_t* streams = body + nlo + kLaneTable;
   const uint64_t groups = n / 8;
   const bool aligned = (reinterpret_cast<uintptr_t>(s) & 15) == 0;
   const bool lo_aligned = (reinterpret_cast<uintptr_t>(lo) & 7) == 0;
@@ -616,16 +648,19 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   uint64_t acc = 0;
   int nb = int(loff & 3) * 8;
   for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
-    uint32_t wd[4];
-    load_group(s, g, aligned, wd);
-    uint64_t lob = 0;
+    uint32_t wd[2 * W];
+    load_group<W>(s, g, aligned, wd);
+    uint64_t lw[W - 1];
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k) lw[k] = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int e = q * 2 + h;
-        const uint32_t hi = (wd[q] >> (16 * h + 8)) & 255;
-        lob |= uint64_t((wd[q] >> (16 * h)) & 255) << (8 * e);
+        const uint32_t v = group_elem<W>(wd, e);
+        const uint32_t hi = v >> (8 * (W - 1));
+        put_lo<W>(lw, e, v);
         const uint32_t ent = enc_tab[eslot(hi)];
         if (ent >> 31) {
           const int k = atomicAdd(&ecount, 1);
@@ -643,11 +678,14 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
         nb -= 32;
       }
     }
-    if (lo_aligned) {
-      reinterpret_cast<uint64_t*>(lo)[g] = lob;
-    } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) lo[8 * g + e] = uint8_t(lob >> (8 * e));
+    for (int k = 0; k < W - 1; ++k) {
+      if (lo_aligned) {
+        reinterpret_cast<uint64_t*>(lo)[g * (W - 1) + k] = lw[k];
+      } else {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) lo[8 * ((W - 1) * g + k) + b] = uint8_t(lw[k] >> (8 * b));
+      }
     }
   }
   if (nb > 0) atomicOr(&coded32[wpos], uint32_t(acc));  // < 32 bits left
@@ -666,11 +704,11 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   uint8_t* escp = streams + c_bytes;
   write_escapes(eidx, evals, min(ecount, kMaxEsc), escp);
   uint8_t* tail = escp + m.n_esc;
-  const uint64_t tail_len = len - 2 * n;
+  const uint64_t tail_len = len - W * n;
   const uint64_t used = uint64_t(tail - body);
   const uint64_t padded_end = m.size - kFrameHeader;
   for (uint64_t j = threadIdx.x; used + j < padded_end; j += kThreads)
-    tail[j] = j < tail_len ? s[2 * n + j] : 0;
+    tail[j] = j < tail_len ? s[W * n + j] : 0;
 }
 
 template <int W>
@@ -826,8 +864,9 @@ __device__ __forceinline__ void refill(const uint64_t* coded64, uint32_t& pos, u
   nb += 8 * k;
 }
 
-// Mode-2 decoder (2-byte elements).  A frame whose fields do not fit its
-// stored extent is left undecoded (the host validated the frame table).
+// Mode-2 decoder (W = 2 or 4).  A frame whose fields do not fit its stored
+// extent is left undecoded (the host validated the frame table).
+template <int W>
 __global__ void __launch_bounds__(kThreads)
 hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
             uint32_t first_frame, uint64_t logical, uint32_t frame_bytes,
@@ -848,7 +887,8 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   const uint64_t f = first_frame + fl;
   const uint64_t base = f * frame_bytes;
   const uint64_t len = min(uint64_t(frame_bytes), logical - base);
-  const uint64_t n = len / 2;
+  const uint64_t n = len / W;
+  const uint64_t nlo = uint64_t(W - 1) * n;
   const uint8_t* fr = frames + offsets[fl];
   const uint64_t extent = offsets[fl + 1] - offsets[fl];
   if (fr[0] != 2) return;
@@ -861,7 +901,7 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   if (threadIdx.x == 0) ecount = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
-    int ok = n % 8 == 0 && n_esc <= uint32_t(kMaxEsc) && kFrameHeader + n + kLaneTable <= extent;
+    int ok = n % 8 == 0 && n_esc <= uint32_t(kMaxEsc) && kFrameHeader + nlo + kLaneTable <= extent;
     for (int c = 0; c < 16; ++c) ok &= hlen[c] <= kMaxLen;
     valid = ok;
     canonical_codes(hlen, hcode);
@@ -879,14 +919,14 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   }
   const uint8_t* body = fr + kFrameHeader;
   const uint8_t* lo = body;
-  const uint32_t lb = reinterpret_cast<const uint16_t*>(body + n)[threadIdx.x];
+  const uint32_t lb = reinterpret_cast<const uint16_t*>(body + nlo)[threadIdx.x];
   const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);
   const uint32_t c_bytes = ctotal;
-  const uint64_t tail_len = len - 2 * n;
+  const uint64_t tail_len = len - W * n;
   if (c_bytes > kMaxCoded ||
-      kFrameHeader + n + kLaneTable + c_bytes + n_esc + tail_len > extent)
+      kFrameHeader + nlo + kLaneTable + c_bytes + n_esc + tail_len > extent)
     return;  // uniform across the workgroup (ctotal is shared)
-  const uint8_t* streams = body + n + kLaneTable;
+  const uint8_t* streams = body + nlo + kLaneTable;
   uint8_t* coded = reinterpret_cast<uint8_t*>(coded64);
   if ((reinterpret_cast<uintptr_t>(streams) & 3) == 0) {
     const uint32_t nw = c_bytes / 4;
@@ -905,15 +945,20 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   uint64_t acc = 0;
   int nb = 0;
   for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
-    uint64_t lob;
-    if (vec) {
-      lob = reinterpret_cast<const uint64_t*>(lo)[g];
-    } else {
-      lob = 0;
+    uint64_t lw[W - 1];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) lob |= uint64_t(lo[8 * g + e]) << (8 * e);
+    for (int k = 0; k < W - 1; ++k) {
+      if (vec) {
+        lw[k] = reinterpret_cast<const uint64_t*>(lo)[g * (W - 1) + k];
+      } else {
+        lw[k] = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) lw[k] |= uint64_t(lo[8 * ((W - 1) * g + k) + b]) << (8 * b);
+      }
     }
-    uint32_t wd[4] = {0, 0, 0, 0};
+    uint32_t wd[2 * W];
+#pragma unroll
+    for (int q = 0; q < 2 * W; ++q) wd[q] = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       // every lane refills at the same points (no divergence): >= 56 bits
@@ -931,15 +976,20 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
         if (k < kMaxEsc) eidx[k] = uint32_t(g * 8 + e);
         hi = 0;
       }
-      wd[e >> 1] |= (uint32_t((lob >> (8 * e)) & 255) | (hi << 8)) << (16 * (e & 1));
+      const uint32_t v = get_lo<W>(lw, e) | (hi << (8 * (W - 1)));
+      if constexpr (W == 2) wd[e >> 1] |= v << (16 * (e & 1));
+      else wd[e] = v;
     }
     if (vec) {
-      reinterpret_cast<uint4*>(o)[g] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+#pragma unroll
+      for (int k = 0; k < W / 2; ++k)
+        reinterpret_cast<uint4*>(o)[g * (W / 2) + k] =
+            make_uint4(wd[4 * k], wd[4 * k + 1], wd[4 * k + 2], wd[4 * k + 3]);
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 2 * W; ++q)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) o[16 * g + 4 * q + b] = uint8_t(wd[q] >> (8 * b));
+        for (int b = 0; b < 4; ++b) o[8 * W * g + 4 * q + b] = uint8_t(wd[q] >> (8 * b));
     }
   }
   // the barrier orders every wave's element stores before the escape patches
@@ -953,8 +1003,8 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
     sorted[rank] = me;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < ne; i += kThreads) o[2 * uint64_t(sorted[i]) + 1] = escv[i];
-  if (tail_len && threadIdx.x == 0) o[2 * n] = escv[n_esc];
+  for (int i = threadIdx.x; i < ne; i += kThreads) o[W * uint64_t(sorted[i]) + W - 1] = escv[i];
+  if (threadIdx.x < tail_len) o[W * n + threadIdx.x] = escv[n_esc + threadIdx.x];
 }
 
 thread_local char g_hsz_err[256];
@@ -1005,8 +1055,11 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
     default: hipLaunchKernelGGL(hsz_encode<8>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
   }
   if (w == 2)
-    hipLaunchKernelGGL(hsz_encode2, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m,
-                       lanes, o);
+    hipLaunchKernelGGL(hsz_encode2<2>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes,
+                       m, lanes, o);
+  else if (w == 4)
+    hipLaunchKernelGGL(hsz_encode2<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes,
+                       m, lanes, o);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("hsz encode launch", e);
 }
@@ -1032,7 +1085,10 @@ int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t fi
     default: return -1001;
   }
   if (w == 2)
-    hipLaunchKernelGGL(hsz_decode2, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical,
+    hipLaunchKernelGGL(hsz_decode2<2>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical,
+                       frame_bytes, o);
+  else if (w == 4)
+    hipLaunchKernelGGL(hsz_decode2<4>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical,
                        frame_bytes, o);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("hsz decode launch", e);

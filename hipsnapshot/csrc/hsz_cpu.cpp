@@ -132,14 +132,14 @@ void plan_frame(const uint8_t* s, uint64_t len, int w, Plan* p) {
   p->nsel = k;
   std::memset(p->code_of, kEsc, 256);
   for (int j = 0; j < k; ++j) p->code_of[p->dict[j]] = uint8_t(j);
-  const bool m2 = w == 2 && n > 0 && n % 8 == 0;
+  const bool m2 = (w == 2 || w == 4) && n > 0 && n % 8 == 0;
   uint64_t esc = 0;
   std::vector<uint32_t> lane_cnt;  // [lane][16]
   uint64_t cnt[16] = {0};
   if (m2) {
     lane_cnt.assign(size_t(kLanes) * 16, 0);
     for (uint64_t e = 0; e < n; ++e) {
-      const uint8_t c = p->code_of[s[2 * e + 1]];
+      const uint8_t c = p->code_of[s[e * w + w - 1]];
       ++lane_cnt[((e >> 3) & (kLanes - 1)) * 16 + c];
     }
     for (int l = 0; l < kLanes; ++l)
@@ -163,7 +163,7 @@ void plan_frame(const uint8_t* s, uint64_t len, int w, Plan* p) {
         p->lane_bytes[l] = uint16_t(std::min<uint64_t>(b, 65535));
         c_bytes += b;
       }
-      const uint64_t size2 = kFrameHeader + n + kLaneTable + c_bytes + esc + tail;
+      const uint64_t size2 = kFrameHeader + uint64_t(w - 1) * n + kLaneTable + c_bytes + esc + tail;
       if (c_bytes <= kMaxCoded && size2 < coded1 && size2 < raw) {
         p->mode = 2;
         p->coded = c_bytes;
@@ -206,8 +206,12 @@ void encode_frame(const uint8_t* s, uint64_t len, int w, const Plan& p, uint8_t*
     uint16_t codes[16];
     canonical_codes(p.lens, codes);
     uint8_t* lo = body;
-    for (uint64_t e = 0; e < n; ++e) lo[e] = s[2 * e];
-    uint8_t* table = body + n;
+    if (w == 2) {
+      for (uint64_t e = 0; e < n; ++e) lo[e] = s[2 * e];
+    } else {
+      for (uint64_t e = 0; e < n; ++e) std::memcpy(lo + e * (w - 1), s + e * w, w - 1);
+    }
+    uint8_t* table = body + uint64_t(w - 1) * n;
     std::memcpy(table, p.lane_bytes, kLaneTable);  // little-endian host
     uint8_t* streams = table + kLaneTable;
     const uint64_t groups = n / 8;
@@ -217,7 +221,7 @@ void encode_frame(const uint8_t* s, uint64_t len, int w, const Plan& p, uint8_t*
       int nb = 0;
       for (uint64_t g = uint64_t(l); g < groups; g += kLanes)
         for (int e = 0; e < 8; ++e) {
-          const uint8_t c = p.code_of[s[2 * (8 * g + e) + 1]];
+          const uint8_t c = p.code_of[s[(8 * g + e) * w + w - 1]];
           acc |= uint32_t(codes[c]) << nb;
           nb += p.lens[c];
           while (nb >= 8) {
@@ -230,7 +234,7 @@ void encode_frame(const uint8_t* s, uint64_t len, int w, const Plan& p, uint8_t*
     }
     esc = streams + p.coded;
     for (uint64_t e = 0; e < n; ++e)
-      if (p.code_of[s[2 * e + 1]] == kEsc) esc[ne++] = s[2 * e + 1];
+      if (p.code_of[s[e * w + w - 1]] == kEsc) esc[ne++] = s[e * w + w - 1];
   } else {
     const uint64_t nb = (n + 1) / 2;
     uint8_t* nib = body;
@@ -262,7 +266,7 @@ void encode_frame(const uint8_t* s, uint64_t len, int w, const Plan& p, uint8_t*
 }
 
 // Mode-2 frame body -> logical bytes.  `extent` = the frame's stored size.
-int decode_frame2(const uint8_t* fr, uint64_t extent, uint64_t len, uint8_t* o) {
+int decode_frame2(const uint8_t* fr, uint64_t extent, uint64_t len, int w, uint8_t* o) {
   uint32_t n_esc;
   std::memcpy(&n_esc, fr + 4, 4);
   const uint8_t* dict = fr + 8;
@@ -270,18 +274,19 @@ int decode_frame2(const uint8_t* fr, uint64_t extent, uint64_t len, uint8_t* o) 
   for (int c = 0; c < 16; ++c) lens[c] = (fr[24 + c / 2] >> (4 * (c & 1))) & 15;
   for (int c = 0; c < 16; ++c)
     if (lens[c] > kMaxLen) return -74;
-  const uint64_t n = len / 2;
+  const uint64_t n = len / w;
+  const uint64_t nlo = uint64_t(w - 1) * n;
   if (n % 8 || n_esc > kMaxEsc) return -74;
   const uint8_t* body = fr + kFrameHeader;
-  if (kFrameHeader + n + kLaneTable > extent) return -74;
+  if (kFrameHeader + nlo + kLaneTable > extent) return -74;
   const uint8_t* lo = body;
   uint16_t lane_bytes[kLanes];
-  std::memcpy(lane_bytes, body + n, kLaneTable);
+  std::memcpy(lane_bytes, body + nlo, kLaneTable);
   uint64_t c_bytes = 0;
   for (int l = 0; l < kLanes; ++l) c_bytes += lane_bytes[l];
-  const uint64_t tail = len - 2 * n;
-  if (kFrameHeader + n + kLaneTable + c_bytes + n_esc + tail > extent) return -74;
-  const uint8_t* streams = body + n + kLaneTable;
+  const uint64_t tail = len - n * w;
+  if (kFrameHeader + nlo + kLaneTable + c_bytes + n_esc + tail > extent) return -74;
+  const uint8_t* streams = body + nlo + kLaneTable;
   const uint8_t* escv = streams + c_bytes;
   uint16_t codes[16];
   canonical_codes(lens, codes);
@@ -317,10 +322,15 @@ int decode_frame2(const uint8_t* fr, uint64_t extent, uint64_t len, uint8_t* o) 
   uint32_t ne = 0;
   for (uint64_t e = 0; e < n; ++e) {
     const uint8_t c = idx[e];
-    o[2 * e] = lo[e];
-    o[2 * e + 1] = c == kEsc ? (ne < n_esc ? escv[ne++] : 0) : dict[c];
+    uint8_t* d = o + e * w;
+    if (w == 2) {
+      d[0] = lo[e];
+    } else {
+      std::memcpy(d, lo + e * (w - 1), w - 1);
+    }
+    d[w - 1] = c == kEsc ? (ne < n_esc ? escv[ne++] : 0) : dict[c];
   }
-  if (tail) std::memcpy(o + 2 * n, escv + n_esc, tail);
+  if (tail) std::memcpy(o + n * w, escv + n_esc, tail);
   return 0;
 }
 
@@ -331,7 +341,7 @@ int decode_frame(const uint8_t* fr, uint64_t extent, uint64_t len, int w, uint8_
     std::memcpy(o, body, len);
     return 0;
   }
-  if (fr[0] == 2) return w == 2 ? decode_frame2(fr, extent, len, o) : -74;
+  if (fr[0] == 2) return w == 2 || w == 4 ? decode_frame2(fr, extent, len, w, o) : -74;
   if (fr[0] != 1) return -74;
   uint32_t n_esc;
   std::memcpy(&n_esc, fr + 4, 4);

@@ -168,13 +168,24 @@ def init_weights_(model: nn.Module, std: float = 0.02, seed: Optional[int] = 0) 
 
 
 def build_fsdp_llama(cfg: LlamaConfig, device: torch.device,
-                     dtype: torch.dtype = torch.bfloat16, mesh=None) -> nn.Module:
-    """Llama sharded with FSDP2 (DTensor params, Shard(0)) on ``mesh``."""
+                     dtype: torch.dtype = torch.bfloat16, mesh=None,
+                     compute_dtype: Optional[torch.dtype] = None) -> nn.Module:
+    """Llama sharded with FSDP2 (DTensor params, Shard(0)) on ``mesh``.
+
+    ``dtype`` is the stored (master) parameter dtype; a different
+    ``compute_dtype`` (e.g. fp32 master weights, bf16 compute) installs an
+    FSDP2 mixed-precision policy with fp32 gradient reduction.
+    """
     from torch.distributed.fsdp import fully_shard
 
     with torch.device("meta"):
         model = Llama(cfg).to(dtype)
     kw = {"mesh": mesh} if mesh is not None else {}
+    if compute_dtype is not None and compute_dtype != dtype:
+        from torch.distributed.fsdp import MixedPrecisionPolicy
+
+        kw["mp_policy"] = MixedPrecisionPolicy(param_dtype=compute_dtype,
+                                               reduce_dtype=torch.float32)
     for layer in model.layers:
         fully_shard(layer, **kw)
     fully_shard(model, **kw)

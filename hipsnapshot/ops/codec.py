@@ -7,9 +7,9 @@ of information for trained or initialised weights (measured in
 ``tests/test_codec.py``), the other bytes are near-random.  HSZ1 keeps the
 low bytes verbatim and codes each high byte as a 4-bit index into a per-frame
 15-entry dictionary (index 15 = escape, value stored separately): bf16 blobs
-shrink to ~75 %, fp32 to ~87.5 %, bit-exactly.  For 2-byte elements a frame
-may instead Huffman-code those 16 indices (mode 2, ~2.7 bits per element), so
-bf16 blobs shrink to ~67 %.  Frames that do not compress are stored raw, so
+shrink to ~75 %, fp32 to ~87.5 %, bit-exactly.  For 2- and 4-byte elements a
+frame may instead Huffman-code those 16 indices (mode 2, ~2.7 bits per
+element), so bf16 blobs shrink to ~67 % and fp32 to ~83 %.  Frames that do not compress are stored raw, so
 any byte stream is accepted.
 
 Encoding and decoding run on the GPU (``csrc/hsz.hip``) before D2H / after
@@ -32,15 +32,15 @@ Blob layout (little endian)::
                      low bytes (w-1)*n B   (each element without its high byte)
                      escapes   n_escapes B (high bytes of code-15 elements, in order)
                      tail      (len - n*w) B raw
-             mode 2 (w == 2 and n % 8 == 0 only):
-                     low bytes n B
+             mode 2 (w in (2, 4) and n % 8 == 0 only):
+                     low bytes (w-1)*n B (each element without its high byte)
                      lane table 256 x u16: byte length of each lane's stream
                      streams   the 256 lane streams back to back; lane t codes
                                the indices of element groups t, t+256, t+512, ...
                                (group g = elements 8g..8g+7) with canonical
                                Huffman codes packed LSB-first (bit-reversed
                                codewords), each stream zero-padded to a byte
-                     escapes   n_escapes B (element order), tail (len - 2n) B
+                     escapes   n_escapes B (element order), tail (len - n*w) B
              padded to 16 B
     where n = len // w elements of the frame's len logical bytes.
 
@@ -293,15 +293,16 @@ def _encode_frame(data: np.ndarray, w: int) -> bytes:
     if n_esc > MAX_ESCAPES:
         return _raw_frame(data)
     esc = hi[esc_mask]
-    if w == 2 and n % 8 == 0:
+    if w in (2, 4) and n % 8 == 0:
         lens = huffman_lengths(np.bincount(codes, minlength=16))
         c_bytes = int(_lane_layout(codes, lens)[3].sum())
-        size2 = FRAME_HEADER_BYTES + n + LANE_TABLE_BYTES + c_bytes + n_esc + tail
+        size2 = FRAME_HEADER_BYTES + (w - 1) * n + LANE_TABLE_BYTES + c_bytes + n_esc + tail
         if c_bytes <= HUFF_MAX_CODED and size2 < coded and size2 < raw:
             streams, lane_bytes = _huffman_streams(codes, lens)
             lens_b = bytes(lens[2 * j] | (lens[2 * j + 1] << 4) for j in range(8))
+            lo = np.ascontiguousarray(el[:, : w - 1]).reshape(-1)
             return (struct.pack("<B3xI16s8s", 2, n_esc, d.tobytes(), lens_b)
-                    + el[:, 0].tobytes() + lane_bytes.astype("<u2").tobytes() + streams
+                    + lo.tobytes() + lane_bytes.astype("<u2").tobytes() + streams
                     + esc.tobytes() + data[n * w:].tobytes())
     if coded >= raw:
         return _raw_frame(data)
@@ -371,16 +372,19 @@ def decode_frame_reference(frame, length: int, w: int) -> bytes:
     dic = np.frombuffer(d, dtype=np.uint8)
     if mode == 2:
         lens = [(lens_b[j // 2] >> (4 * (j % 2))) & 15 for j in range(16)]
-        lo = body[:n]
-        lane_bytes = body[n: n + LANE_TABLE_BYTES].view("<u2")
+        nlo = (w - 1) * n
+        lo = body[:nlo].reshape(n, w - 1)
+        lane_bytes = body[nlo: nlo + LANE_TABLE_BYTES].view("<u2")
         c_bytes = int(lane_bytes.astype(np.int64).sum())
-        s0 = n + LANE_TABLE_BYTES
+        s0 = nlo + LANE_TABLE_BYTES
         codes = _decode_huffman_streams(body[s0: s0 + c_bytes], lane_bytes, n, lens)
         esc = body[s0 + c_bytes: s0 + c_bytes + n_esc]
         hi = dic[np.minimum(codes, 14)].copy()
         hi[codes == ESC] = esc
-        out = np.stack([lo, hi], 1).reshape(-1)
-        tail = body[s0 + c_bytes + n_esc: s0 + c_bytes + n_esc + (length - 2 * n)]
+        out = np.empty((n, w), dtype=np.uint8)
+        out[:, : w - 1] = lo
+        out[:, w - 1] = hi
+        tail = body[s0 + c_bytes + n_esc: s0 + c_bytes + n_esc + (length - w * n)]
         return out.tobytes() + tail.tobytes()
     nb = (n + 1) // 2
     nib = body[:nb]

@@ -38,7 +38,27 @@ def test_compression_ratio_on_weight_like_data():
     assert ratio < (8 + ent) / 16 * 1.012
     y = torch.randn(1_000_000) * 1e-3
     blob = codec.encode_reference(_bytes(y), 4)
-    assert len(blob) / (4 * y.numel()) < 0.88
+    # fp32: 24 raw bits + ~2.7 Huffman bits per element (mode 1 would be 0.876)
+    assert 0.83 < len(blob) / (4 * y.numel()) < 0.845
+    assert set(codec.frame_modes(blob)) == {2}
+
+
+def test_fp32_mode2_with_tail_native_matches_reference():
+    y = torch.randn(8000) * 0.02
+    raw = _bytes(y) + b"\x01\x02\x03"  # 3-byte tail after 8000 elements
+    fb = 32016  # one frame holding the whole 32003-byte blob
+    blob = codec.encode_reference(raw, 4, frame_bytes=fb)
+    assert codec.frame_modes(blob) == [2]
+    assert codec.decode_reference(blob) == raw
+    assert codec.encode_cpu(raw, 4, fb).tobytes() == blob
+    assert codec.decode_cpu(blob).tobytes() == raw
+    # a corrupt lane table that points past the frame is rejected, not read
+    h = codec.parse_header(blob)
+    bad = bytearray(blob)
+    tab = h.offsets[0] + codec.FRAME_HEADER_BYTES + 3 * 8000
+    bad[tab: tab + 2] = (0xFFFF).to_bytes(2, "little")
+    with pytest.raises(RuntimeError):
+        codec.decode_cpu(bytes(bad))
 
 
 def test_incompressible_frames_stored_raw():
@@ -119,9 +139,11 @@ def test_version1_blobs_still_decode():
     if set(codec.frame_modes(bytes(blob))) <= {0, 1}:
         struct.pack_into("<I", blob, 4, 1)
         assert codec.decode_reference(bytes(blob)) == raw
-    v1 = bytearray(codec.encode_reference(raw, 4, frame_bytes=16 * 1024))  # w=4: modes 0/1
+    raw8 = _bytes(torch.randn(20_000, dtype=torch.float64) * 0.02)
+    v1 = bytearray(codec.encode_reference(raw8, 8, frame_bytes=16 * 1024))  # w=8: modes 0/1
+    assert 1 in codec.frame_modes(bytes(v1)) and 2 not in codec.frame_modes(bytes(v1))
     struct.pack_into("<I", v1, 4, 1)
-    assert codec.decode_reference(bytes(v1)) == raw and codec.decode_cpu(bytes(v1)).tobytes() == raw
+    assert codec.decode_reference(bytes(v1)) == raw8 and codec.decode_cpu(bytes(v1)).tobytes() == raw8
 
 
 def test_frames_covering():

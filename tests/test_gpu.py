@@ -7,6 +7,7 @@ missing.
 
 import os
 
+import numpy as np
 import pytest
 import torch
 
@@ -393,7 +394,9 @@ def test_hsz_encode_gpu_bit_exact_vs_reference(gpu, w, kind):
     from hipsnapshot.ops import codec
 
     host = _codec_inputs()[kind]
-    for n in (host.numel(), host.numel() - 7, 4096 * 16 + 3):
+    # 2 * 65536 + 32003: the last frame holds 8000 fp32 elements and a 3-byte
+    # tail (a mode-2 frame with a tail when w == 4)
+    for n in (host.numel(), host.numel() - 7, 4096 * 16 + 3, 2 * 65536 + 32003):
         h = host[:n].contiguous()
         ref = codec.encode_reference(h.numpy().tobytes(), w, 64 * 1024)
         d = h.to(gpu)
@@ -402,7 +405,9 @@ def test_hsz_encode_gpu_bit_exact_vs_reference(gpu, w, kind):
         s.synchronize()
         nb = int(total.item())
         assert nb == len(ref), (kind, w, n)
-        assert out[:nb].cpu().numpy().tobytes() == ref, (kind, w, n)
+        got = out[:nb].cpu().numpy()
+        diff = np.flatnonzero(got != np.frombuffer(ref, dtype=np.uint8))
+        assert diff.size == 0, (kind, w, n, "first differing byte", int(diff[0]))
         # GPU decode of the whole blob and of a middle frame range
         hdr = codec.parse_header(ref)
         back = torch.empty(n, dtype=torch.uint8, device=gpu)
@@ -432,6 +437,22 @@ def test_hsz_gpu_large_blob_ratio(gpu):
     back = torch.empty_like(x)
     codec.decode_device_into(out[:nb], hdr, back.view(torch.uint8), int(s.cuda_stream))
     assert torch.equal(back.view(torch.int16), x.view(torch.int16))
+
+
+def test_hsz_gpu_fp32_blob_ratio(gpu):
+    from hipsnapshot.ops import codec
+
+    x = torch.randn(32 << 20, device=gpu) / 64  # 128 MiB fp32
+    s = torch.cuda.current_stream()
+    out, total, _ = codec.encode_device(x.view(torch.uint8), 4, int(s.cuda_stream))
+    s.synchronize()
+    nb = int(total.item())
+    assert 0.83 < nb / (x.numel() * 4) < 0.845  # mode-2 frames (mode 1 would be 0.876)
+    nf = codec.n_frames_for(x.numel() * 4, codec.DEFAULT_FRAME_BYTES)
+    hdr = codec.parse_header(out[:codec.payload_start(nf)].cpu().numpy().tobytes())
+    back = torch.empty_like(x)
+    codec.decode_device_into(out[:nb], hdr, back.view(torch.uint8), int(s.cuda_stream))
+    assert torch.equal(back.view(torch.int32), x.view(torch.int32))
 
 
 # ---- HSZ1 compressed snapshots on the GPU path ---------------------------------
