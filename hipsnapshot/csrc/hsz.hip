@@ -1,11 +1,13 @@
 // hsz: HSZ1 lossless exponent-entropy codec on gfx950 (format: hipsnapshot/ops/codec.py).
 //
 // Encode (before D2H) = 4 launches on the caller's stream:
-//   hsz_analyze<W>  one workgroup per 256 KiB frame: 2048-sample LDS histogram
-//                   -> 15-entry dictionary (wave-wide argmax), then a full pass
-//                   over the frame.  For 2-/4-byte elements that pass keeps one
-//                   16-bin index histogram per lane in LDS; thread 0 builds the
-//                   length-limited Huffman code and every lane sizes its own
+//   hsz_analyze<W>  one workgroup per 256 KiB frame: LDS histogram of a 2048-
+//                   element sample (64 coalesced runs of 32) -> 15-entry
+//                   dictionary (wave-wide argmax), then a full pass over the
+//                   frame.  For 2-/4-byte elements that pass keeps one 16-bin
+//                   index histogram per lane in LDS; wave 0 builds the
+//                   length-limited Huffman code in registers (one node per
+//                   lane, shuffle argmins) and every lane sizes its own
 //                   stream, so the frame mode (raw / nibble / huffman) and the
 //                   exact coded size are known before anything is written
 //   hsz_layout      one workgroup: exclusive scan of frame sizes, blob header +
@@ -42,6 +44,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kLanes = 256;  // mode-2 lane streams per frame == threads per workgroup
 constexpr int kSample = 2048;
+constexpr int kRun = 32;  // dictionary sample = kSample / kRun runs (codec.sample_indices)
 constexpr int kMaxEsc = 1024;
 constexpr int kHeader = 64;
 constexpr int kFrameHeader = 32;
@@ -138,78 +141,87 @@ __device__ void build_dict(const uint32_t* hist, uint8_t* dict, uint8_t* code_of
   __syncthreads();
 }
 
-// Huffman code lengths of the 16 indices (mirror of codec.huffman_lengths).
-// One thread; the node arrays live in LDS (runtime-indexed register arrays
-// would go to scratch).  Leaves are nodes 0..15, merged nodes 16..30.
-__device__ void huffman_lengths(const uint32_t* cnt, uint8_t* lens, uint32_t* w, int* par) {
-  int k = 0;
-  for (int c = 0; c < 16; ++c) {
-    w[c] = cnt[c];
-    par[c] = cnt[c] ? -1 : -2;
-    lens[c] = 0;
-    k += cnt[c] != 0;
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t x = __shfl_xor(v, o, 64);
+    v = x < v ? x : v;
   }
-  if (k == 0) return;
-  if (k == 1) {
-    for (int c = 0; c < 16; ++c)
-      if (cnt[c]) lens[c] = 1;
-    return;
-  }
-  int m = 16;
-  for (int step = 0; step < k - 1; ++step) {
-    int a = -1, b = -1;
-    for (int i = 0; i < m; ++i)
-      if (par[i] == -1 && (a < 0 || w[i] < w[a])) a = i;
-    par[a] = -3;
-    for (int i = 0; i < m; ++i)
-      if (par[i] == -1 && (b < 0 || w[i] < w[b])) b = i;
-    w[m] = w[a] + w[b];
-    par[m] = -1;
-    par[a] = m;
-    par[b] = m;
-    ++m;
-  }
-  int maxl = 0;
-  for (int c = 0; c < 16; ++c) {
-    if (!cnt[c]) continue;
-    int d = 0;
-    for (int j = c; par[j] >= 0; j = par[j]) ++d;
-    lens[c] = uint8_t(d);
-    maxl = d > maxl ? d : maxl;
-  }
-  if (maxl <= kMaxLen) return;
-  for (int c = 0; c < 16; ++c)
-    if (lens[c] > kMaxLen) lens[c] = kMaxLen;
-  for (;;) {
-    uint32_t kraft = 0;
-    for (int c = 0; c < 16; ++c)
-      if (cnt[c]) kraft += 1u << (kMaxLen - lens[c]);
-    if (kraft <= (1u << kMaxLen)) break;
-    int s = -1;
-    for (int c = 0; c < 16; ++c) {
-      if (!cnt[c] || lens[c] >= kMaxLen) continue;
-      if (s < 0 || lens[c] > lens[s] || (lens[c] == lens[s] && cnt[c] <= cnt[s])) s = c;
-    }
-    ++lens[s];
-  }
+  return v;
 }
 
-// Bit-reversed canonical codewords (mirror of codec.canonical_codes); one thread.
-__device__ void canonical_codes(const uint8_t* lens, uint16_t* codes) {
-  for (int c = 0; c < 16; ++c) codes[c] = 0;
-  uint32_t code = 0;
-  int prev = 0;
-  bool first = true;
-  for (int l = 1; l <= kMaxLen; ++l)
-    for (int c = 0; c < 16; ++c) {
-      if (lens[c] != l) continue;
-      if (!first) code = (code + 1) << (l - prev);
-      first = false;
-      prev = l;
-      uint32_t rev = 0;
-      for (int b = 0; b < l; ++b) rev |= ((code >> b) & 1u) << (l - 1 - b);
-      codes[c] = uint16_t(rev);
-    }
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t x = __shfl_xor(v, o, 64);
+    v = x > v ? x : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Huffman code length of index `lane` (mirror of codec.huffman_lengths), built
+// by one whole wave: lane i holds node i (leaves 0..15 = index values, merged
+// nodes 16.. in creation order), each merge is two wave-wide argmins over
+// (weight, node) -- the same tie-break as the reference -- and depths are
+// found by chasing parent links with lane shuffles.  `cnt` is the index's
+// count in lanes 0..15 (ignored elsewhere); returns its length (0 = unused).
+// Everything stays in registers: no LDS round trips on a serial path.
+__device__ uint32_t wave_huffman_len(uint32_t cnt) {
+  const int lane = threadIdx.x & 63;
+  const bool used = lane < 16 && cnt != 0;
+  const int k = __popcll(__ballot(used));
+  if (k <= 1) return used ? 1u : 0u;
+  uint64_t w = used ? cnt : 0;
+  bool alive = used;
+  int par = -1;
+  for (int step = 0; step < k - 1; ++step) {
+    const int m = 16 + step;
+    const uint64_t a = wave_min_u64(alive ? (w << 8) | uint64_t(lane) : ~0ull);
+    if (lane == int(a & 255)) { alive = false; par = m; }
+    const uint64_t b = wave_min_u64(alive ? (w << 8) | uint64_t(lane) : ~0ull);
+    if (lane == int(b & 255)) { alive = false; par = m; }
+    if (lane == m) { w = (a >> 8) + (b >> 8); alive = true; }
+  }
+  int j = lane;
+  uint32_t d = 0;
+  for (int it = 0; it < k - 1; ++it) {  // depth <= k - 1
+    const int p = __shfl(par, j, 64);
+    if (p >= 0) { j = p; ++d; }
+  }
+  uint32_t len = used ? d : 0;
+  if (wave_max_u64(len) <= uint64_t(kMaxLen)) return len;
+  if (len > uint32_t(kMaxLen)) len = kMaxLen;
+  for (;;) {  // Kraft fix: lengthen the longest code below the limit (rarer, then larger index)
+    const uint32_t kraft = wave_sum_u32(used ? 1u << (kMaxLen - len) : 0u);
+    if (kraft <= (1u << kMaxLen)) break;
+    const uint64_t key = (used && len < uint32_t(kMaxLen))
+                             ? (uint64_t(len) << 56) | (uint64_t(0xffffffffu - cnt) << 8) | uint64_t(lane)
+                             : 0;
+    if (lane == int(wave_max_u64(key) & 255)) ++len;
+  }
+  return len;
+}
+
+// Bit-reversed canonical codeword of index `lane` (mirror of
+// codec.canonical_codes), one wave: the code of a symbol is the Kraft sum of
+// the symbols before it in (length, index) order, scaled to its length.
+// `len` = the index's code length in lanes 0..15 (<= kMaxLen).
+__device__ uint32_t wave_canonical_code(uint32_t len) {
+  const int lane = threadIdx.x & 63;
+  uint32_t kr = 0;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const uint32_t ls = __shfl(len, s, 64);
+    if (ls && (ls < len || (ls == len && s < lane))) kr += 1u << (kMaxLen - ls);
+  }
+  if (lane >= 16 || len == 0) return 0;
+  return __builtin_bitreverse32(kr >> (kMaxLen - len)) >> (32 - len);
 }
 
 // Element group g (elements 8g..8g+7, W = 2 or 4 bytes each) as 2W
@@ -251,6 +263,22 @@ __device__ __forceinline__ void put_lo(uint64_t* lw, int e, uint32_t v) {
   if ((bp & 63) + L > 64) lw[(bp >> 6) + 1] |= x >> (64 - (bp & 63));
 }
 
+// The W-1 low-byte words of group g from the low-byte plane.
+template <int W>
+__device__ __forceinline__ void load_lo(const uint8_t* lo, uint64_t g, bool aligned,
+                                        uint64_t lw[W - 1]) {
+#pragma unroll
+  for (int k = 0; k < W - 1; ++k) {
+    if (aligned) {
+      lw[k] = reinterpret_cast<const uint64_t*>(lo)[g * (W - 1) + k];
+    } else {
+      lw[k] = 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) lw[k] |= uint64_t(lo[8 * ((W - 1) * g + k) + b]) << (8 * b);
+    }
+  }
+}
+
 template <int W>
 __device__ __forceinline__ uint32_t get_lo(const uint64_t* lw, int e) {
   constexpr int L = 8 * (W - 1);
@@ -276,9 +304,10 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   const uint8_t* s = src + base;
   for (int v = threadIdx.x; v < 256; v += kThreads) hist[v] = 0;
   __syncthreads();
-  const uint64_t stride = n / kSample > 0 ? n / kSample : 1;
+  // half a wave reads one run of kRun consecutive elements (coalesced)
+  const uint64_t step = n / (kSample / kRun);
   for (int i = threadIdx.x; i < kSample; i += kThreads) {
-    const uint64_t idx = uint64_t(i) * stride;
+    const uint64_t idx = n <= uint64_t(kSample) ? uint64_t(i) : uint64_t(i / kRun) * step + i % kRun;
     if (idx < n) atomicAdd(&hist[s[idx * W + W - 1]], 1u);
   }
   __syncthreads();
@@ -292,8 +321,6 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
       __shared__ uint32_t lcnt[16 * kLanes];
       __shared__ uint32_t fcnt[16];
       __shared__ uint8_t hlen[16];
-      __shared__ uint32_t hw[32];
-      __shared__ int hpar[32];
       for (int i = threadIdx.x; i < 16 * kLanes; i += kThreads) lcnt[i] = 0;
       __syncthreads();
       const uint64_t groups = n / 8;
@@ -308,13 +335,22 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
         }
       }
       __syncthreads();
-      if (threadIdx.x < 16) {
-        uint32_t sum = 0;
-        for (int l = 0; l < kLanes; ++l) sum += lcnt[threadIdx.x * kLanes + l];
-        fcnt[threadIdx.x] = sum;
+      {  // frame histogram: wave q sums the lane columns of indices 4q..4q+3
+        const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+#pragma unroll
+        for (int c = 4 * q; c < 4 * q + 4; ++c) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int r = 0; r < kLanes; r += 64) v += lcnt[c * kLanes + r + lane];
+          v = wave_sum_u32(v);
+          if (lane == 0) fcnt[c] = v;
+        }
       }
       __syncthreads();
-      if (threadIdx.x == 0) huffman_lengths(fcnt, hlen, hw, hpar);
+      if (threadIdx.x < 64) {
+        const uint32_t len = wave_huffman_len(threadIdx.x < 16 ? fcnt[threadIdx.x] : 0u);
+        if (threadIdx.x < 16) hlen[threadIdx.x] = uint8_t(len);
+      }
       __syncthreads();
       uint32_t bits = 0;
 #pragma unroll
@@ -618,10 +654,14 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   for (int v = threadIdx.x; v < 256; v += kThreads) code_of[cslot(v)] = kEsc;
   const uint32_t c_words = (m.coded + 3) / 4;
   for (uint32_t i = threadIdx.x; i < c_words; i += kThreads) coded32[i] = 0;
-  if (threadIdx.x == 0) {
-    ecount = 0;
-    for (int c = 0; c < 16; ++c) hlen[c] = m.lens[c];
-    canonical_codes(hlen, hcode);
+  if (threadIdx.x < 64) {
+    const uint32_t l = threadIdx.x < 16 ? m.lens[threadIdx.x] : 0u;
+    const uint32_t code = wave_canonical_code(l);
+    if (threadIdx.x < 16) {
+      hlen[threadIdx.x] = uint8_t(l);
+      hcode[threadIdx.x] = uint16_t(code);
+    }
+    if (threadIdx.x == 0) ecount = 0;
   }
   __syncthreads();
   if (threadIdx.x < m.nsel) code_of[cslot(m.dict[threadIdx.x])] = uint8_t(threadIdx.x);
@@ -647,9 +687,15 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   uint32_t wpos = loff >> 2;
   uint64_t acc = 0;
   int nb = int(loff & 3) * 8;
+  // software-pipelined: the next group's load is in flight while this one is
+  // coded (2 waves/SIMD at this LDS size cannot hide HBM latency otherwise)
+  uint32_t nx[2 * W];
+  if (threadIdx.x < groups) load_group<W>(s, threadIdx.x, aligned, nx);
   for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
     uint32_t wd[2 * W];
-    load_group<W>(s, g, aligned, wd);
+#pragma unroll
+    for (int q = 0; q < 2 * W; ++q) wd[q] = nx[q];
+    if (g + kThreads < groups) load_group<W>(s, g + kThreads, aligned, nx);
     uint64_t lw[W - 1];
 #pragma unroll
     for (int k = 0; k < W - 1; ++k) lw[k] = 0;
@@ -900,11 +946,14 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   }
   if (threadIdx.x == 0) ecount = 0;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int ok = n % 8 == 0 && n_esc <= uint32_t(kMaxEsc) && kFrameHeader + nlo + kLaneTable <= extent;
-    for (int c = 0; c < 16; ++c) ok &= hlen[c] <= kMaxLen;
-    valid = ok;
-    canonical_codes(hlen, hcode);
+  if (threadIdx.x < 64) {
+    const uint32_t l = threadIdx.x < 16 ? hlen[threadIdx.x] : 0u;
+    const bool long_code = __ballot(l > uint32_t(kMaxLen)) != 0;
+    const uint32_t code = wave_canonical_code(l < uint32_t(kMaxLen) ? l : uint32_t(kMaxLen));
+    if (threadIdx.x < 16) hcode[threadIdx.x] = uint16_t(code);
+    if (threadIdx.x == 0)
+      valid = !long_code && n % 8 == 0 && n_esc <= uint32_t(kMaxEsc) &&
+              kFrameHeader + nlo + kLaneTable <= extent;
   }
   __syncthreads();
   if (!valid) return;
@@ -945,17 +994,10 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   uint64_t acc = 0;
   int nb = 0;
   for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+    // (loading the next group's low bytes one iteration ahead measured slower
+    // here: this loop is bound by its LDS stream and LUT reads)
     uint64_t lw[W - 1];
-#pragma unroll
-    for (int k = 0; k < W - 1; ++k) {
-      if (vec) {
-        lw[k] = reinterpret_cast<const uint64_t*>(lo)[g * (W - 1) + k];
-      } else {
-        lw[k] = 0;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) lw[k] |= uint64_t(lo[8 * ((W - 1) * g + k) + b]) << (8 * b);
-      }
-    }
+    load_lo<W>(lo, g, vec, lw);
     uint32_t wd[2 * W];
 #pragma unroll
     for (int q = 0; q < 2 * W; ++q) wd[q] = 0;

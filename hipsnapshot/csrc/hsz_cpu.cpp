@@ -16,6 +16,7 @@
 namespace {
 
 constexpr int kSample = 2048;
+constexpr int kRun = 32;
 constexpr uint32_t kMaxEsc = 1024;
 constexpr uint64_t kHeader = 64;
 constexpr uint64_t kFrameHeader = 32;
@@ -118,11 +119,16 @@ struct Plan {
 void plan_frame(const uint8_t* s, uint64_t len, int w, Plan* p) {
   const uint64_t n = len / w;
   uint32_t hist[256] = {0};
-  const uint64_t stride = n / kSample > 0 ? n / kSample : 1;
-  for (uint64_t i = 0; i < kSample; ++i) {
-    const uint64_t idx = i * stride;
-    if (idx >= n) break;
-    ++hist[s[idx * w + w - 1]];
+  // sample: every element up to kSample, else kSample / kRun runs of kRun
+  // consecutive elements evenly spread over the frame (codec.sample_indices)
+  if (n <= uint64_t(kSample)) {
+    for (uint64_t i = 0; i < n; ++i) ++hist[s[i * w + w - 1]];
+  } else {
+    const uint64_t step = n / (kSample / kRun);
+    for (uint64_t i = 0; i < uint64_t(kSample); ++i) {
+      const uint64_t idx = (i / kRun) * step + i % kRun;
+      ++hist[s[idx * w + w - 1]];
+    }
   }
   int order[256];
   for (int v = 0; v < 256; ++v) order[v] = v;

@@ -45,7 +45,8 @@ Blob layout (little endian)::
     where n = len // w elements of the frame's len logical bytes.
 
 Dictionary: the 15 most frequent high bytes of a deterministic 2048-element
-sample of the frame (count descending, value ascending); a frame is coded
+sample of the frame (64 evenly spaced runs of 32 elements, ``sample_indices``;
+count descending, value ascending); a frame is coded
 only if it has at most ``MAX_ESCAPES`` escapes and the coded size is smaller.
 Mode 2 code lengths come from the frame's exact index histogram (Huffman with
 deterministic tie-breaks, limited to ``HUFF_MAX_LEN`` bits: ``huffman_lengths``).
@@ -72,6 +73,7 @@ HEADER_BYTES = 64
 FRAME_HEADER_BYTES = 32
 DEFAULT_FRAME_BYTES = 256 * 1024
 SAMPLE = 2048
+SAMPLE_RUN = 32  # the sample is SAMPLE // SAMPLE_RUN evenly spaced runs
 MAX_ESCAPES = 1024
 ESC = 15
 CODEC_NAME = "hsz1"
@@ -225,10 +227,20 @@ def decode_table(lens) -> np.ndarray:
 # NumPy reference (the GPU and C++ implementations must match it bit for bit)
 # ---------------------------------------------------------------------------
 
+def sample_indices(n: int) -> np.ndarray:
+    """Elements of an n-element frame that choose its dictionary: all of them
+    up to ``SAMPLE``, else ``SAMPLE // SAMPLE_RUN`` runs of ``SAMPLE_RUN``
+    consecutive elements, run r starting at r * (n // runs).  Runs instead of
+    single strided elements: the GPU reads ~2 % of the frame for the sample,
+    not every 128-B line of it."""
+    if n <= SAMPLE:
+        return np.arange(n)
+    i = np.arange(SAMPLE)
+    return (i // SAMPLE_RUN) * (n // (SAMPLE // SAMPLE_RUN)) + i % SAMPLE_RUN
+
+
 def _frame_dict(hi: np.ndarray) -> np.ndarray:
-    n = hi.size
-    stride = max(1, n // SAMPLE)
-    sample = hi[: stride * SAMPLE: stride][:SAMPLE]
+    sample = hi[sample_indices(hi.size)]
     counts = np.bincount(sample, minlength=256)
     order = sorted(range(256), key=lambda v: (-int(counts[v]), v))
     chosen = [v for v in order[:15] if counts[v] > 0]

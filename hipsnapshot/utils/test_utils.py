@@ -229,3 +229,28 @@ def all_dtypes() -> List[torch.dtype]:
     return [d for d in ALL_SUPPORTED_DTYPES
             if d not in (getattr(torch, "uint16", None), getattr(torch, "uint32", None),
                          getattr(torch, "uint64", None))]
+
+
+def hsz_deep_tree_frame(n: int = 65536) -> bytes:
+    """One bf16-shaped HSZ1 frame (``2 * n`` bytes) whose index histogram needs
+    a length-limited Huffman code: 14 rare high bytes with Fibonacci counts
+    (1, 1, 2, ... 377) placed exactly on the dictionary's sample positions, so
+    all of them enter the dictionary, plus one dominant high byte.  The
+    unlimited tree is deeper than ``codec.HUFF_MAX_LEN``, so encoders must run
+    the Kraft fix-up (``codec.huffman_lengths``)."""
+    import numpy as np
+
+    from ..ops import codec
+
+    at = codec.sample_indices(n)
+    hi = np.full(n, 0x3C, dtype=np.uint8)
+    fib = [1, 1]
+    while len(fib) < 14:
+        fib.append(fib[-1] + fib[-2])
+    vals = [v for v in range(0x30, 0x50) if v != 0x3C][:14]
+    pos = 0
+    for v, c in zip(vals, fib):
+        hi[at[pos:pos + c]] = v
+        pos += c
+    lo = np.random.default_rng(5).integers(0, 256, n, dtype=np.uint8)
+    return np.stack([lo, hi], 1).reshape(-1).tobytes()

@@ -131,6 +131,19 @@ def test_mode2_frames_and_skewed_histograms():
     assert codec.decode_reference(b2) == small and codec.decode_cpu(b2).tobytes() == small
 
 
+def test_length_limited_huffman_frame_native_matches_reference():
+    from hipsnapshot.utils.test_utils import hsz_deep_tree_frame
+
+    raw = hsz_deep_tree_frame()
+    blob = codec.encode_reference(raw, 2, frame_bytes=len(raw))
+    o = codec.parse_header(blob).offsets[0]
+    lens = [(blob[o + 24 + j // 2] >> (4 * (j % 2))) & 15 for j in range(16)]
+    assert codec.frame_modes(blob) == [2] and max(lens) == codec.HUFF_MAX_LEN
+    assert codec.decode_reference(blob) == raw
+    assert codec.encode_cpu(raw, 2, len(raw)).tobytes() == blob
+    assert codec.decode_cpu(blob).tobytes() == raw
+
+
 def test_version1_blobs_still_decode():
     import struct
 

@@ -423,6 +423,28 @@ def test_hsz_encode_gpu_bit_exact_vs_reference(gpu, w, kind):
             assert torch.equal(part.cpu(), h[lo:hi_])
 
 
+def test_hsz_gpu_length_limited_huffman_frame(gpu):
+    # the GPU's wave-parallel Huffman construction must apply the same
+    # length limit (Kraft fix-up) as the reference, byte for byte
+    from hipsnapshot.ops import codec
+    from hipsnapshot.utils.test_utils import hsz_deep_tree_frame
+
+    raw = hsz_deep_tree_frame()
+    ref = codec.encode_reference(raw, 2, frame_bytes=len(raw))
+    d = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(gpu)
+    s = torch.cuda.current_stream()
+    out, total, _ = codec.encode_device(d, 2, int(s.cuda_stream), len(raw))
+    s.synchronize()
+    nb = int(total.item())
+    assert nb == len(ref)
+    got = out[:nb].cpu().numpy()
+    diff = np.flatnonzero(got != np.frombuffer(ref, dtype=np.uint8))
+    assert diff.size == 0, ("first differing byte", int(diff[0]))
+    back = torch.empty_like(d)
+    codec.decode_device_into(out[:nb], codec.parse_header(ref), back, int(s.cuda_stream))
+    assert torch.equal(back, d)
+
+
 def test_hsz_gpu_large_blob_ratio(gpu):
     from hipsnapshot.ops import codec
 
