@@ -1,4 +1,7 @@
-"""DeepSpeed trick (duck-typed fake engine), RSS profiler, knobs."""
+"""DeepSpeed trick (duck-typed fake engine), RSS profiler, knobs, NUMA helpers,
+equality helpers, UVM adapter."""
+
+import os
 
 import torch
 
@@ -133,3 +136,64 @@ def test_numa_affinity_helpers(monkeypatch):
     rep = affinity.bind_to_gpu_numa(0, min_cpus=1)
     assert rep["bound"] is False and rep["reason"] == "already local"
     assert os.sched_getaffinity(0) == allowed
+
+
+def test_equality_helpers():
+    # reference: tests/test_test_utils.py (tensor / sharded-tensor equality
+    # used by every round-trip test)
+    import pytest as _pytest
+    import torch.distributed as dist
+
+    from hipsnapshot.utils.test_utils import (assert_state_dict_eq, free_port,
+                                              sharded_tensor_eq, tensor_eq)
+
+    a = torch.arange(6.0).view(2, 3)
+    assert tensor_eq(a, a.clone()) and not tensor_eq(a, a + 1)
+    assert not tensor_eq(a, a.double()) and not tensor_eq(a, a.view(3, 2))
+    q = torch.quantize_per_tensor(a, 0.5, 2, torch.qint8)
+    assert tensor_eq(q, q.clone()) and not tensor_eq(q, a)
+    assert not tensor_eq(q, torch.quantize_per_tensor(a, 0.25, 2, torch.qint8))
+    f8 = a.to(torch.float8_e4m3fn)
+    assert tensor_eq(f8, f8.clone())
+    assert_state_dict_eq({"x": [a, 1, "s"], "y": {"z": a}}, {"x": [a.clone(), 1, "s"], "y": {"z": a}})
+    with _pytest.raises(AssertionError):
+        assert_state_dict_eq({"x": a}, {"x": a + 1})
+    with _pytest.raises(AssertionError):
+        assert_state_dict_eq({"x": a, "y": 1}, {"y": 1, "x": a})  # key order is part of equality
+    with _pytest.raises(AssertionError):
+        assert_state_dict_eq([1, 2], (1, 2))
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    own_pg = not dist.is_initialized()
+    if own_pg:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0,
+                                world_size=1)
+    try:
+        from torch.distributed._shard.sharded_tensor import empty as st_empty
+        from torch.distributed._shard.sharding_spec import ChunkShardingSpec
+
+        spec = ChunkShardingSpec(dim=0, placements=["rank:0/cpu", "rank:0/cpu"])
+        s1, s2, s3 = (st_empty(spec, 4, 3) for _ in range(3))
+        for s, v in ((s1, 1.0), (s2, 1.0), (s3, 2.0)):
+            for sh in s.local_shards():
+                sh.tensor.fill_(v)
+        assert sharded_tensor_eq(s1, s2) and tensor_eq(s1, s2)
+        assert not sharded_tensor_eq(s1, s3) and not sharded_tensor_eq(s1, a)
+        other = st_empty(ChunkShardingSpec(dim=1, placements=["rank:0/cpu", "rank:0/cpu"]), 4, 3)
+        for sh in other.local_shards():
+            sh.tensor.fill_(1.0)
+        assert not sharded_tensor_eq(s1, other)  # same values, different shard layout
+    finally:
+        if own_pg:
+            dist.destroy_process_group()
+
+
+def test_uvm_adapter_without_managed_memory():
+    # reference: tests/test_uvm_tensor.py -- the adapter must be importable
+    # and inert for ordinary tensors (managed allocation itself: test_gpu.py)
+    from hipsnapshot.ops.uvm import is_uvm_tensor, uvm_to_cpu
+
+    t = torch.randn(5, 3)
+    assert not is_uvm_tensor(t)
+    assert torch.equal(uvm_to_cpu(t), t)
+    assert not is_uvm_tensor(t.t())
