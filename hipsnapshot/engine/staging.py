@@ -23,7 +23,8 @@ from __future__ import annotations
 
 import threading
 import time
-from typing import List, Optional, Sequence, Tuple
+from contextlib import contextmanager
+from typing import Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -55,6 +56,22 @@ def device_of(t: torch.Tensor) -> int:
     return torch.cuda.current_device() if idx is None else idx
 
 
+_plan = threading.local()
+
+
+@contextmanager
+def plan_scope() -> Iterator[None]:
+    """One take's planning on the calling thread: a device's current stream
+    cannot change inside it, so ``producer_stream_handle`` looks it up once
+    per device instead of once per tensor."""
+    prev = getattr(_plan, "streams", None)
+    _plan.streams = {}
+    try:
+        yield
+    finally:
+        _plan.streams = prev
+
+
 def producer_stream_handle(t: torch.Tensor) -> Optional[int]:
     """The stream that produces ``t`` (current stream of its device, captured
     on the calling thread -- call at plan time on the training thread).
@@ -62,7 +79,13 @@ def producer_stream_handle(t: torch.Tensor) -> Optional[int]:
     non-blocking copy streams must be ordered after; None = host tensor."""
     if not t.is_cuda:
         return None
-    return int(torch.cuda.current_stream(t.device).cuda_stream)
+    cache = getattr(_plan, "streams", None)
+    if cache is None:
+        return int(torch.cuda.current_stream(t.device).cuda_stream)
+    h = cache.get(t.device.index)
+    if h is None:
+        h = cache[t.device.index] = int(torch.cuda.current_stream(t.device).cuda_stream)
+    return h
 
 
 def _pinned_staged(nbytes: int) -> Tuple[native.PinnedBuffer, StagedBuffer]:

@@ -70,7 +70,12 @@ class PrimitivePreparer:
 def prepare_write(obj: Any, logical_path: str, rank: int, replicated: bool,
                   is_async_snapshot: bool = False,
                   _tensor_prepare_func: Optional[PrepareFunc] = None,
-                  serializer: Optional[str] = None) -> Tuple[Entry, List[WriteReq]]:
+                  serializer: Optional[str] = None,
+                  max_chunk_size_bytes: Optional[int] = None,
+                  max_shard_size_bytes: Optional[int] = None) -> Tuple[Entry, List[WriteReq]]:
+    """The size knobs default to their current values; a take reads them once
+    and passes them to every call (an env lookup per leaf adds up at ~300
+    leaves per Llama-3-8B state dict)."""
     if PrimitivePreparer.should_inline(obj):
         entry = PrimitivePreparer.prepare_write(obj)
         entry.replicated = replicated
@@ -79,9 +84,10 @@ def prepare_write(obj: Any, logical_path: str, rank: int, replicated: bool,
     if is_sharded(obj):
         return ShardedTensorIOPreparer.prepare_write(
             storage_path=storage_path, obj=obj, is_async_snapshot=is_async_snapshot,
-            _tensor_prepare_func=_tensor_prepare_func, serializer=serializer)
+            _tensor_prepare_func=_tensor_prepare_func, serializer=serializer,
+            max_shard_size_bytes=max_shard_size_bytes)
     if isinstance(obj, torch.Tensor):
-        if obj.numel() * obj.element_size() > get_max_chunk_size_bytes():
+        if obj.numel() * obj.element_size() > (max_chunk_size_bytes or get_max_chunk_size_bytes()):
             entry, wrs = ChunkedTensorIOPreparer.prepare_write(
                 storage_path=storage_path, tensor=obj,
                 chunking_instruction=ChunkedTensorIOPreparer.chunk_tensor(obj),

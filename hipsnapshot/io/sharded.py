@@ -192,10 +192,11 @@ class ShardedTensorIOPreparer:
     @classmethod
     def prepare_write(cls, storage_path: str, obj: Any, is_async_snapshot: bool = False,
                       _tensor_prepare_func: Optional[PrepareFunc] = None,
-                      serializer: Optional[str] = None
+                      serializer: Optional[str] = None,
+                      max_shard_size_bytes: Optional[int] = None
                       ) -> Tuple[ShardedTensorEntry, List[WriteReq]]:
         shards, reqs = [], []
-        max_shard = get_max_shard_size_bytes()
+        max_shard = max_shard_size_bytes or get_max_shard_size_bytes()
         for box in local_boxes(obj, for_write=True):
             pieces = cls.subdivide_shard(box.tensor, box.offsets, box.sizes, box.sharding_dim,
                                          max_shard)

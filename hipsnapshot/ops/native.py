@@ -19,7 +19,7 @@ import ctypes
 import logging
 import os
 import threading
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -154,6 +154,34 @@ def io_engine(nthreads: int = 16) -> IOEngine:
                 eng = IOEngine(nthreads)
                 _engines[key] = eng
     return eng
+
+
+_idle_engines: Dict[Tuple[int, int], List[IOEngine]] = {}
+_MAX_IDLE_ENGINES = 4
+
+
+def acquire_io_engine(nthreads: int) -> IOEngine:
+    """An engine for one storage plugin's exclusive use: an idle one left by a
+    closed plugin, else a new one.  A take opens one plugin, so reusing the
+    engine saves starting and joining ``nthreads`` threads per take."""
+    with _lock:
+        lst = _idle_engines.get((os.getpid(), nthreads))
+        if lst:
+            return lst.pop()
+    return IOEngine(nthreads)
+
+
+def release_io_engine(eng: IOEngine, reusable: bool) -> None:
+    """Return an engine from ``acquire_io_engine``.  Only an engine with no
+    job in flight may be reused (``reusable``): a later owner must never see a
+    completion it did not submit."""
+    if reusable and eng.handle and os.getpid() == eng.pid:
+        with _lock:
+            lst = _idle_engines.setdefault((eng.pid, eng.nthreads), [])
+            if len(lst) < _MAX_IDLE_ENGINES:
+                lst.append(eng)
+                return
+    eng.close()
 
 
 def file_size(path: str) -> int:

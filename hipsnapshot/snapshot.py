@@ -41,6 +41,7 @@ import torch.distributed as dist
 from torch.nn.parallel import DistributedDataParallel as DDP
 
 from . import knobs
+from .engine import staging
 from .engine.scheduler import (
     PendingIOWork,
     get_process_memory_budget_bytes,
@@ -85,6 +86,30 @@ class TakeStats:
 
     last: Dict[str, float] = {}
 
+
+
+def _state_dict_for_save(stateful: Any) -> Any:
+    """``stateful.state_dict()`` for a take.
+
+    For an ``nn.Module`` whose class keeps ``nn.Module.state_dict`` (FSDP2
+    modules included) this is ``state_dict(keep_vars=True)`` with plain
+    tensors detached afterwards: DTensor parameters are kept as they are (the
+    snapshot only reads their local tensors, which do not require grad), which
+    skips one DTensor-dispatched ``detach`` per parameter -- ~25 us each, 291
+    of them for Llama-3-8B, on every take.  Restore keeps calling
+    ``state_dict()`` (it copies into the returned tensors in place).
+    """
+    import torch.nn as nn
+
+    if not (isinstance(stateful, nn.Module) and type(stateful).state_dict is nn.Module.state_dict):
+        return stateful.state_dict()
+    from torch.distributed.tensor import DTensor
+
+    sd = stateful.state_dict(keep_vars=True)
+    for k, v in sd.items():
+        if isinstance(v, torch.Tensor) and v.requires_grad and not isinstance(v, DTensor):
+            sd[k] = v.detach()
+    return sd
 
 class Snapshot:
     """A persisted program state at one point in time.
@@ -246,7 +271,7 @@ class Snapshot:
         for key in global_keys:
             if key in app_state:
                 with timeline.span("state_dict", key=key):
-                    m, f = flatten(app_state[key].state_dict(), prefix=key)
+                    m, f = flatten(_state_dict_for_save(app_state[key]), prefix=key)
                 manifest.update(m)
                 flattened.update(f)
             # user state_dict() implementations may run collectives: keep them
@@ -265,22 +290,25 @@ class Snapshot:
         path_reqs: Dict[str, List[WriteReq]] = {}
         primitives: Dict[str, PrimitiveEntry] = {}
         rank = comm.get_rank()
-        for logical, obj in flattened.items():
-            ser = None
-            if quantize and any(fnmatch.fnmatch(logical, p) for p in quantize):
-                ser = Serializer.FP8_BLOCK.value
-            entry, wrs = prepare_write(
-                obj=obj, logical_path=logical, rank=rank, replicated=logical in rep_paths,
-                is_async_snapshot=is_async,
-                _tensor_prepare_func=(
-                    (lambda t, tracing, _p=logical: prepare_func(_p, t, tracing))
-                    if prepare_func is not None else None),
-                serializer=ser)
-            if isinstance(entry, PrimitiveEntry):
-                primitives[logical] = entry
-            else:
-                object_entries[logical] = entry
-                path_reqs[logical] = wrs
+        max_chunk, max_shard = knobs.get_max_chunk_size_bytes(), knobs.get_max_shard_size_bytes()
+        with staging.plan_scope():
+            for logical, obj in flattened.items():
+                ser = None
+                if quantize and any(fnmatch.fnmatch(logical, p) for p in quantize):
+                    ser = Serializer.FP8_BLOCK.value
+                entry, wrs = prepare_write(
+                    obj=obj, logical_path=logical, rank=rank, replicated=logical in rep_paths,
+                    is_async_snapshot=is_async,
+                    _tensor_prepare_func=(
+                        (lambda t, tracing, _p=logical: prepare_func(_p, t, tracing))
+                        if prepare_func is not None else None),
+                    serializer=ser, max_chunk_size_bytes=max_chunk,
+                    max_shard_size_bytes=max_shard)
+                if isinstance(entry, PrimitiveEntry):
+                    primitives[logical] = entry
+                else:
+                    object_entries[logical] = entry
+                    path_reqs[logical] = wrs
         timeline.add("prepare_write", "phase", t_prep, time.perf_counter(), n=len(flattened))
         if rep_paths:  # identical on every rank (result of a collective)
             with timeline.span("partition"):

@@ -52,7 +52,7 @@ class FSStoragePlugin(StoragePlugin):
             return None
         if self._engine is None:
             try:
-                self._engine = _native.IOEngine(self.io_threads)
+                self._engine = _native.acquire_io_engine(self.io_threads)
             except Exception:  # pragma: no cover - compiler missing
                 self._native_ok = False
                 return None
@@ -166,7 +166,7 @@ class FSStoragePlugin(StoragePlugin):
                     self._loop.remove_reader(self._engine.efd)
                 except Exception:
                     pass
-            self._engine.close()
+            _native.release_io_engine(self._engine, reusable=not self._pending)
             self._engine = None
             self._loop = None
 
