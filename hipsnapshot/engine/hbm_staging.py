@@ -34,6 +34,7 @@ import torch
 from .. import knobs
 from ..io_types import WriteReq
 from ..ops import native
+from ..utils.tracing import timeline
 
 logger = logging.getLogger(__name__)
 
@@ -109,7 +110,8 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
 def _freeze(dev: int, sts, offs, total: int) -> None:
     stream = torch.cuda.current_stream(dev)
     with torch.cuda.device(dev):
-        arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
+        with timeline.span("freeze_alloc", bytes=total):
+            arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
         batch = native.CopyBatch()
         views = []
         base = arena.data_ptr()
@@ -126,7 +128,8 @@ def _freeze(dev: int, sts, offs, total: int) -> None:
                 ev.record(torch.cuda.default_stream(dev) if p == 0
                           else torch.cuda.ExternalStream(p))
                 stream.wait_event(ev)
-        keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
+        with timeline.span("freeze_launch", n=len(sts)):
+            keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
         done = torch.cuda.Event()
         done.record(stream)
     for st, view in zip(sts, views):

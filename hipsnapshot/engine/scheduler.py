@@ -24,6 +24,7 @@ import asyncio
 import logging
 import os
 import socket
+import threading
 import time
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
@@ -38,6 +39,37 @@ from ..utils.tracing import timeline
 logger = logging.getLogger(__name__)
 
 _budget_cache: Dict[tuple, int] = {}
+
+# Worker pools outlive a take: a pipeline that finished cleanly hands its
+# pool back instead of joining its threads, and the next take reuses them.
+_idle_pools: Dict[tuple, List[ThreadPoolExecutor]] = {}
+_pool_lock = threading.Lock()
+_MAX_IDLE_POOLS = 2
+
+
+def _acquire_pool(kind: str, n: int, rank: int) -> ThreadPoolExecutor:
+    key = (os.getpid(), kind, n)
+    with _pool_lock:
+        lst = _idle_pools.get(key)
+        if lst:
+            return lst.pop()
+    ex = ThreadPoolExecutor(max_workers=n, thread_name_prefix=f"hipsnapshot-{kind}-{rank}")
+    ex._hs_key = key  # type: ignore[attr-defined]
+    return ex
+
+
+def _release_pool(ex: ThreadPoolExecutor, reusable: bool) -> None:
+    """Give back a pool from ``_acquire_pool``.  ``reusable`` only when every
+    task submitted to it has finished (a clean pipeline end); otherwise the
+    pool is shut down as before."""
+    key = getattr(ex, "_hs_key", None)
+    if reusable and key is not None and key[0] == os.getpid():
+        with _pool_lock:
+            lst = _idle_pools.setdefault(key, [])
+            if len(lst) < _MAX_IDLE_POOLS:
+                lst.append(ex)
+                return
+    ex.shutdown(wait=reusable)
 
 
 def get_local_world_size(pg) -> int:
@@ -98,11 +130,16 @@ class PendingIOWork:
         self._failure = failure
 
     async def complete(self) -> None:
+        done = False
         try:
             if self.io_tasks:
                 await asyncio.gather(*self.io_tasks, return_exceptions=True)
+            done = True
         finally:
-            self.executor.shutdown(wait=True)
+            if done:
+                _release_pool(self.executor, reusable=True)
+            else:  # cancelled while waiting: tasks may still run
+                self.executor.shutdown(wait=True)
             self.stats.t_done = time.monotonic()
         if self._failure:
             raise self._failure[0]
@@ -120,8 +157,7 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                              io_concurrency: Optional[int] = None) -> PendingIOWork:
     stage_threads = stage_threads or knobs.get_stage_threads()
     io_concurrency = io_concurrency or knobs.get_io_threads()
-    executor = ThreadPoolExecutor(max_workers=stage_threads,
-                                  thread_name_prefix=f"hipsnapshot-stage-{rank}")
+    executor = _acquire_pool("stage", stage_threads, rank)
     stats = PipelineStats()
     stats.n_reqs = len(write_reqs)
     failure: List[BaseException] = []
@@ -270,8 +306,7 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
     # reads are split across all I/O workers by the native engine, so a few
     # whole-blob reads in flight saturate it; more would only pin more memory
     max_inflight = knobs.get_read_inflight()
-    executor = ThreadPoolExecutor(max_workers=consume_threads,
-                                  thread_name_prefix=f"hipsnapshot-consume-{rank}")
+    executor = _acquire_pool("consume", consume_threads, rank)
     stats = PipelineStats()
     stats.n_reqs = len(read_reqs)
     pending = deque(read_reqs)
@@ -343,6 +378,7 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                 dest.release()
             in_use[0] -= cost
 
+    clean = False
     try:
         while pending or inflight:
             while pending and len(inflight) < max_inflight:
@@ -360,8 +396,12 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                         o.cancel()
                     await asyncio.gather(*inflight, return_exceptions=True)
                     raise t.exception()
+        clean = True
     finally:
-        executor.shutdown(wait=True)
+        if clean:
+            _release_pool(executor, reusable=True)
+        else:
+            executor.shutdown(wait=True)
     stats.t_done = time.monotonic()
     logger.debug(f"Rank {rank} read {stats.bytes_written / 1e9:.3f} GB in "
                  f"{stats.t_done - stats.t_start:.3f}s")

@@ -550,10 +550,14 @@ class CopyBatch:
         """
         if not self.rows:
             return None
+        from ..utils.tracing import timeline
+
         lib = require_gpu_lib()
-        arr = self.pack()
-        ws_bytes = int(lib.hsg_copy_workspace_bytes(arr.ctypes.data, len(arr)))
-        stage = PinnedBuffer(ws_bytes)
+        with timeline.span("copy_pack", n=len(self.rows)):
+            arr = self.pack()
+            ws_bytes = int(lib.hsg_copy_workspace_bytes(arr.ctypes.data, len(arr)))
+        with timeline.span("copy_stage_alloc", bytes=ws_bytes):
+            stage = PinnedBuffer(ws_bytes)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
         cur = torch.cuda.current_stream(dev)
         if int(cur.cuda_stream) != int(stream_handle):
