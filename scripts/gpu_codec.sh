@@ -1,13 +1,21 @@
 #!/bin/bash
-# Compression path on the GPU: tests, then the headline bench raw vs hsz1.
+# codec kernels only: bit-exact / round-trip tests, then the microbench with kernel stats
 set -o pipefail
-mkdir -p gpurun_out/timeline
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
-timeout -k 10 600 python -m pytest tests/test_gpu.py -q -x -k "hsz or compressed" > gpurun_out/codec_tests.log 2>&1 || { echo CODEC_TEST_FAIL; tail -40 gpurun_out/codec_tests.log; exit 1; }
-tail -1 gpurun_out/codec_tests.log
-for c in none hsz1; do
-  HIPSNAPSHOT_TIMELINE=$PWD/gpurun_out/timeline/$c timeout -k 10 400 python bench.py --steps 5 --warmup 2 --async-iters 2 --compression $c > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || { echo BENCH_FAIL $c; tail -30 gpurun_out/bench_$c.err; exit 1; }
-  cat gpurun_out/bench_$c.json; grep -E "^step|^async|^restore" gpurun_out/bench_$c.err
-  python scripts/timeline_summary.py gpurun_out/timeline/$c.rank0.take6.json gpurun_out/timeline/$c.rank0.restore0.json > gpurun_out/timeline_$c.txt 2>&1; cat gpurun_out/timeline_$c.txt
-done
+OUT=gpurun_out/${CODEC_OUT:-codec}
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH
+timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -v -m gpu -k "hsz or compressed" \
+    --timeout 120 --timeout-method thread > $OUT/pytest_hsz.log 2>&1 \
+    || { echo PYTEST_FAIL; grep -E "FAILED|Error|assert" $OUT/pytest_hsz.log | head -20; exit 1; }
+tail -1 $OUT/pytest_hsz.log
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_micro -o micro \
+    -- python3 benchmarks/microbench.py --skip-fs > $OUT/micro.jsonl 2> $OUT/micro.err \
+    || { echo MICRO_FAIL; tail -30 $OUT/micro.err; exit 1; }
+grep hsz $OUT/micro.jsonl
+python3 - "$OUT/prof_micro/micro_kernel_stats.csv" <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if "hsz" in r["Name"]:
+        print(r["Name"].split("::")[1][:24], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
+PY
