@@ -231,8 +231,9 @@ def sample_indices(n: int) -> np.ndarray:
     """Elements of an n-element frame that choose its dictionary: all of them
     up to ``SAMPLE``, else ``SAMPLE // SAMPLE_RUN`` runs of ``SAMPLE_RUN``
     consecutive elements, run r starting at r * (n // runs).  Runs instead of
-    single strided elements: the GPU reads ~2 % of the frame for the sample,
-    not every 128-B line of it."""
+    single strided elements: the GPU's sample loads are coalesced (2 lines
+    per run) instead of 2048 separate lines, which made the sample phase
+    latency-bound."""
     if n <= SAMPLE:
         return np.arange(n)
     i = np.arange(SAMPLE)
