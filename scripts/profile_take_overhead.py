@@ -26,6 +26,7 @@ def main() -> None:
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--compression", default="none")
     ap.add_argument("--optim", action="store_true", help="include AdamW state (3x the leaves)")
+    ap.add_argument("--restore", action="store_true", help="time Snapshot.restore instead")
     args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
@@ -52,16 +53,20 @@ def main() -> None:
     Snapshot.take(os.path.join(root, "warm"), app, compression=args.compression)
     prof = cProfile.Profile() if args.profile else None
     times = []
+    snap = Snapshot(os.path.join(root, "warm"))
     for i in range(args.takes):
         if prof:
             prof.enable()
         t0 = time.perf_counter()
-        Snapshot.take(os.path.join(root, "s"), app, compression=args.compression)
+        if args.restore:
+            snap.restore(app)
+        else:
+            Snapshot.take(os.path.join(root, "s"), app, compression=args.compression)
         times.append(time.perf_counter() - t0)
         if prof:
             prof.disable()
     times.sort()
-    print(f"mean take: {sum(times) / len(times) * 1e3:.2f} ms, median "
+    print(f"mean {'restore' if args.restore else 'take'}: {sum(times) / len(times) * 1e3:.2f} ms, median "
           f"{times[len(times) // 2] * 1e3:.2f} ms, min {times[0] * 1e3:.2f} ms")
     if prof:
         pstats.Stats(prof).sort_stats("cumulative").print_stats(35)
