@@ -36,3 +36,23 @@ def test_hsio_under_sanitizer(tmp_path, san):
                          timeout=300)
     assert run.returncode == 0, run.stderr[-3000:]
     assert "ok" in run.stdout
+
+
+def test_hsz_decoder_fuzz_under_asan(tmp_path):
+    """The CPU HSZ1 decoder reads 8 bytes at a time and past lane boundaries;
+    corrupted frames must never make it read outside the frame."""
+    cxx = shutil.which("g++") or shutil.which("clang++")
+    if cxx is None:
+        pytest.skip("no C++ compiler")
+    exe = str(tmp_path / "fuzz")
+    cmd = [cxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+           "-fno-omit-frame-pointer", "-pthread", "-o", exe,
+           os.path.join(ROOT, "tests", "native", "hsz_fuzz.cpp")]
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        pytest.skip(f"sanitizer toolchain unavailable: {proc.stderr[-300:]}")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    run = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert run.returncode == 0, run.stdout[-500:] + run.stderr[-3000:]
+    assert "ok" in run.stdout
