@@ -254,3 +254,22 @@ def ddp_infer_replication(path: str, ignore: bool):
         assert man["0/ddp/module.0.weight"].replicated
     else:
         assert all(e.replicated for k, e in man.items() if hasattr(e, "location"))
+
+
+def committed_on_return(path):
+    """take() returns on every rank only once .snapshot_metadata exists."""
+    import os
+
+    import torch
+
+    from hipsnapshot import Snapshot, StateDict
+
+    rank = torch.distributed.get_rank()
+    for i in range(5):
+        p = f"{path}_{i}"
+        sd = StateDict(t=torch.full((1000,), float(rank + i)), step=i)
+        Snapshot.take(p, {"sd": sd})
+        assert os.path.exists(os.path.join(p, ".snapshot_metadata")), (rank, i)
+        out = StateDict(t=torch.zeros(1000), step=-1)
+        Snapshot(p).restore({"sd": out})
+        assert out["step"] == i and torch.equal(out["t"], torch.full((1000,), float(rank + i)))

@@ -64,3 +64,9 @@ def test_replication_glob_semantics(tmp_path):
 @pytest.mark.parametrize("ignore", [False, True])
 def test_ddp_replication_inference(tmp_path, ignore):
     run_distributed(W.ddp_infer_replication, 2, str(tmp_path / f"d{ignore}"), ignore)
+
+
+def test_take_returns_after_commit_on_every_rank(tmp_path):
+    # reference quirk: take() returned before rank 0 wrote the metadata, so a
+    # rank that read the snapshot at once could find nothing
+    run_distributed(W.committed_on_return, 3, str(tmp_path / "c"))
