@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -599,6 +600,8 @@ int get_stream(int dev, int slot, hipStream_t* out, hipEvent_t* ev) {
   auto it = g_streams.find(k);
   if (it == g_streams.end()) {
     HS_CHECK(hipSetDevice(dev));
+    // default priority: lowest-priority copy streams made a concurrent
+    // training step 45 % slower instead of 18 % (profiles/overlap/priority.md)
     hipStream_t s;
     HS_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     hipEvent_t e;
