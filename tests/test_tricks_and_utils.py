@@ -197,3 +197,88 @@ def test_uvm_adapter_without_managed_memory():
     assert not is_uvm_tensor(t)
     assert torch.equal(uvm_to_cpu(t), t)
     assert not is_uvm_tensor(t.t())
+
+
+def test_state_dict_for_save_skips_dtensor_detach():
+    # take() reads FSDP2 DTensor parameters as they are (no per-parameter
+    # DTensor detach), detaches plain grad-requiring tensors, and leaves
+    # classes with their own state_dict() alone
+    import torch.distributed as dist
+    import torch.nn as nn
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import DTensor
+
+    from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+    from hipsnapshot.snapshot import _state_dict_for_save
+    from hipsnapshot.utils.test_utils import free_port
+
+    lin = nn.Linear(4, 3)
+    sd = _state_dict_for_save(lin)
+    assert list(sd) == ["weight", "bias"] and not sd["weight"].requires_grad
+    assert sd["weight"].data_ptr() == lin.weight.data_ptr()
+
+    class Custom(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.p = nn.Parameter(torch.ones(2))
+
+        def state_dict(self, *a, **k):
+            return {"custom": 1}
+
+    assert _state_dict_for_save(Custom()) == {"custom": 1}
+
+    own_pg = not dist.is_initialized()
+    if own_pg:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0,
+                                world_size=1)
+    try:
+        m = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cpu"), torch.float32,
+                             mesh=init_device_mesh("cpu", (1,)))
+        sd = _state_dict_for_save(m)
+        ref = m.state_dict()
+        assert list(sd) == list(ref)
+        params = dict(m.named_parameters())
+        for k, v in sd.items():
+            assert isinstance(v, DTensor) and v is params[k]  # the parameter itself
+            assert not v._local_tensor.requires_grad
+            assert torch.equal(v._local_tensor, ref[k]._local_tensor)
+    finally:
+        if own_pg:
+            dist.destroy_process_group()
+
+
+def test_worker_pools_are_reused_only_when_clean():
+    from hipsnapshot.engine import scheduler
+    from hipsnapshot.ops import native
+
+    a = scheduler._acquire_pool("t", 2, 0)
+    a.submit(lambda: None).result()
+    scheduler._release_pool(a, reusable=True)
+    b = scheduler._acquire_pool("t", 2, 0)
+    assert b is a  # an idle pool comes back
+    scheduler._release_pool(b, reusable=False)  # shut down, not pooled
+    c = scheduler._acquire_pool("t", 2, 0)
+    assert c is not a
+    scheduler._release_pool(c, reusable=True)
+
+    e1 = native.acquire_io_engine(2)
+    native.release_io_engine(e1, reusable=True)
+    e2 = native.acquire_io_engine(2)
+    assert e2 is e1
+    native.release_io_engine(e2, reusable=False)  # jobs in flight: closed
+    assert e2.handle is None
+    e3 = native.acquire_io_engine(2)
+    assert e3 is not e1 and e3.handle
+    native.release_io_engine(e3, reusable=True)
+
+
+def test_plan_scope_caches_per_device_and_restores():
+    from hipsnapshot.engine import staging
+
+    assert staging.producer_stream_handle(torch.zeros(2)) is None  # host tensor
+    with staging.plan_scope():
+        assert staging._plan.streams == {}
+        with staging.plan_scope():  # nested scopes restore the outer cache
+            staging._plan.streams[0] = 123
+        assert staging._plan.streams == {}
+    assert getattr(staging._plan, "streams", None) is None
