@@ -55,11 +55,16 @@ def main() -> None:
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
     ap.add_argument("--storage", default="fs", choices=["fs", "s3"])
     ap.add_argument("--path", default=None)
+    ap.add_argument("--switch-interval-ms", type=float, default=None,
+                    help="sys.setswitchinterval for this process (GIL hand-over period; "
+                         "Python's default is 5 ms)")
     ap.add_argument("--master-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="stored parameter (and AdamW state) dtype; fp32 = mixed precision "
                          "with bf16 compute")
     args = ap.parse_args()
 
+    if args.switch_interval_ms is not None:
+        sys.setswitchinterval(args.switch_interval_ms / 1e3)
     rank, ws, dev = init_dist()
     if dev.type == "cuda":
         from hipsnapshot.utils.affinity import bind_to_gpu_numa
@@ -166,6 +171,7 @@ def main() -> None:
     emit({"bench": "train_overlap_async_take", "model": args.model, "layers": cfg.n_layers,
           "world_size": ws, "seq": args.seq, "batch": args.batch, "storage": args.storage,
           "compression": args.compression, "master_dtype": args.master_dtype,
+          "switch_interval_ms": sys.getswitchinterval() * 1e3,
           "checkpoint_bytes": ckpt_bytes,
           "baseline_step_ms": round(base_ms, 2), "sync_take_s": round(sync_s, 3),
           "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),
