@@ -89,16 +89,19 @@ class TakeStats:
     last: Dict[str, float] = {}
 
 
-def _state_dict_for_save(stateful: Any) -> Any:
-    """``stateful.state_dict()`` for a take.
+def _state_dict_view(stateful: Any) -> Any:
+    """``stateful.state_dict()`` for a take or a restore.
 
     For an ``nn.Module`` whose class keeps ``nn.Module.state_dict`` (FSDP2
     modules included) this is ``state_dict(keep_vars=True)`` with plain
     tensors detached afterwards: DTensor parameters are kept as they are (the
-    snapshot only reads their local tensors, which do not require grad), which
-    skips one DTensor-dispatched ``detach`` per parameter -- ~25 us each, 291
-    of them for Llama-3-8B, on every take.  Restore keeps calling
-    ``state_dict()`` (it copies into the returned tensors in place).
+    snapshot only reads and writes their local tensors, which do not require
+    grad), which skips one DTensor-dispatched ``detach`` per parameter --
+    ~25 us each, 291 of them for Llama-3-8B, on every take and restore.  On
+    restore the read consumers fill ``_local_tensor`` in place, and the final
+    ``load_state_dict`` copies each DTensor parameter onto itself, which
+    ``copy_`` skips (same tensor); plain tensors are detached views, so the
+    worker threads can write into them without ``no_grad``.
     """
     import torch.nn as nn
 
@@ -279,7 +282,7 @@ class Snapshot:
         for key in global_keys:
             if key in app_state:
                 with timeline.span("state_dict", key=key):
-                    m, f = flatten(_state_dict_for_save(app_state[key]), prefix=key)
+                    m, f = flatten(_state_dict_view(app_state[key]), prefix=key)
                 manifest.update(m)
                 flattened.update(f)
             # user state_dict() implementations may run collectives: keep them
@@ -399,8 +402,9 @@ class Snapshot:
                        comm: Comm, loop: asyncio.AbstractEventLoop) -> None:
         if stateful is None:
             return
-        manifest, merged = get_manifest_for_rank(self.metadata, comm.get_rank())
-        _, flat = flatten(stateful.state_dict(), prefix=key)
+        with timeline.span("restore_plan_view"):
+            manifest, merged = get_manifest_for_rank(self.metadata, comm.get_rank())
+            _, flat = flatten(_state_dict_view(stateful), prefix=key)
         flat = {k: v for k, v in flat.items() if isinstance(v, torch.Tensor) or is_sharded(v)}
         prefix = flat_prefix(key)
         manifest = {k: v for k, v in manifest.items()
@@ -424,8 +428,9 @@ class Snapshot:
         budget = get_process_memory_budget_bytes(comm)
         with timeline.span("read_pipeline", n=len(reads)):
             sync_execute_read_reqs(reads, storage, budget, comm.get_rank(), loop)
-        state_dict = inflate(containers, {k: f.obj for k, f in futs.items()}, prefix=key)
-        stateful.load_state_dict(state_dict)
+        with timeline.span("load_state_dict", n=len(futs)):
+            state_dict = inflate(containers, {k: f.obj for k, f in futs.items()}, prefix=key)
+            stateful.load_state_dict(state_dict)
 
     # ---------------------------------------------------------- inspection
 

@@ -199,7 +199,7 @@ def test_uvm_adapter_without_managed_memory():
     assert not is_uvm_tensor(t.t())
 
 
-def test_state_dict_for_save_skips_dtensor_detach():
+def test_state_dict_view_skips_dtensor_detach():
     # take() reads FSDP2 DTensor parameters as they are (no per-parameter
     # DTensor detach), detaches plain grad-requiring tensors, and leaves
     # classes with their own state_dict() alone
@@ -209,11 +209,11 @@ def test_state_dict_for_save_skips_dtensor_detach():
     from torch.distributed.tensor import DTensor
 
     from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
-    from hipsnapshot.snapshot import _state_dict_for_save
+    from hipsnapshot.snapshot import _state_dict_view
     from hipsnapshot.utils.test_utils import free_port
 
     lin = nn.Linear(4, 3)
-    sd = _state_dict_for_save(lin)
+    sd = _state_dict_view(lin)
     assert list(sd) == ["weight", "bias"] and not sd["weight"].requires_grad
     assert sd["weight"].data_ptr() == lin.weight.data_ptr()
 
@@ -225,7 +225,7 @@ def test_state_dict_for_save_skips_dtensor_detach():
         def state_dict(self, *a, **k):
             return {"custom": 1}
 
-    assert _state_dict_for_save(Custom()) == {"custom": 1}
+    assert _state_dict_view(Custom()) == {"custom": 1}
 
     own_pg = not dist.is_initialized()
     if own_pg:
@@ -234,7 +234,7 @@ def test_state_dict_for_save_skips_dtensor_detach():
     try:
         m = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cpu"), torch.float32,
                              mesh=init_device_mesh("cpu", (1,)))
-        sd = _state_dict_for_save(m)
+        sd = _state_dict_view(m)
         ref = m.state_dict()
         assert list(sd) == list(ref)
         params = dict(m.named_parameters())
@@ -242,6 +242,21 @@ def test_state_dict_for_save_skips_dtensor_detach():
             assert isinstance(v, DTensor) and v is params[k]  # the parameter itself
             assert not v._local_tensor.requires_grad
             assert torch.equal(v._local_tensor, ref[k]._local_tensor)
+        # restore fills the parameters' local tensors in place through the same view
+        import tempfile
+
+        from hipsnapshot import Snapshot
+
+        with tempfile.TemporaryDirectory() as d:
+            Snapshot.take(d, {"m": m})
+            want = {k: v._local_tensor.clone() for k, v in sd.items()}
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.zero_()
+            Snapshot(d).restore({"m": m})
+            for k, p in m.named_parameters():
+                assert torch.equal(p._local_tensor, want[k]), k
+                assert p.requires_grad and not p._local_tensor.requires_grad
     finally:
         if own_pg:
             dist.destroy_process_group()
