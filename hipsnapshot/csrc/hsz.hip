@@ -757,11 +757,19 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
     tail[j] = j < tail_len ? s[W * n + j] : 0;
 }
 
+// A rejected (corrupt / truncated) frame is reported through `err` (host-
+// mapped pinned word, may be null): one plain store of 1 -- every writer
+// stores the same value -- read by the host after the stream sync, so a bad
+// blob raises like the host decoder's -74 instead of restoring stale bytes.
+__device__ __forceinline__ void flag_corrupt(uint32_t* err) {
+  if (err != nullptr) *reinterpret_cast<volatile uint32_t*>(err) = 1u;
+}
+
 template <int W>
 __global__ void __launch_bounds__(kThreads)
 hsz_decode(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
            uint32_t first_frame, uint64_t logical, uint32_t frame_bytes,
-           uint8_t* __restrict__ out) {
+           uint8_t* __restrict__ out, uint32_t* err) {
   __shared__ uint32_t eidx[kMaxEsc];
   __shared__ uint32_t sorted[kMaxEsc];
   __shared__ int ecount;
@@ -772,10 +780,23 @@ hsz_decode(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offs
   const uint64_t len = min(uint64_t(frame_bytes), logical - base);
   const uint64_t n = len / W;
   const uint8_t* fr = frames + offsets[fl];
+  const uint64_t extent = offsets[fl + 1] - offsets[fl];
+  // every early return below depends only on the frame: uniform per block
+  if (offsets[fl + 1] < offsets[fl] + kFrameHeader) {
+    if (threadIdx.x == 0) flag_corrupt(err);
+    return;
+  }
   uint8_t* o = out + fl * uint64_t(frame_bytes);
   const int mode = fr[0];
   const uint8_t* body = fr + kFrameHeader;
-  if (mode == 2) return;  // hsz_decode2
+  if (mode == 2) {  // hsz_decode2 (element widths 2 and 4 only)
+    if (W != 2 && W != 4 && threadIdx.x == 0) flag_corrupt(err);
+    return;
+  }
+  if (mode == 0 && kFrameHeader + len > extent) {
+    if (threadIdx.x == 0) flag_corrupt(err);
+    return;
+  }
   if (mode == 0) {
     if ((((reinterpret_cast<uintptr_t>(o)) | reinterpret_cast<uintptr_t>(body)) & 15) == 0) {
       const uint64_t nv = len / 16;
@@ -789,10 +810,15 @@ hsz_decode(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offs
     return;
   }
   const uint32_t n_esc = *reinterpret_cast<const uint32_t*>(fr + 4);
+  const uint64_t nb = (n + 1) / 2;
+  if (mode != 1 || n_esc > uint32_t(kMaxEsc) ||
+      kFrameHeader + nb + uint64_t(W - 1) * n + n_esc + (len - n * W) > extent) {
+    if (threadIdx.x == 0) flag_corrupt(err);
+    return;
+  }
   if (threadIdx.x < 16) dict[threadIdx.x] = fr[8 + threadIdx.x];
   if (threadIdx.x == 0) ecount = 0;
   __syncthreads();
-  const uint64_t nb = (n + 1) / 2;
   const uint8_t* nib = body;
   const uint8_t* lo = body + nb;
   const uint8_t* escv = lo + uint64_t(W - 1) * n;
@@ -911,12 +937,13 @@ __device__ __forceinline__ void refill(const uint64_t* coded64, uint32_t& pos, u
 }
 
 // Mode-2 decoder (W = 2 or 4).  A frame whose fields do not fit its stored
-// extent is left undecoded (the host validated the frame table).
+// extent, or whose lane streams decode invalid codes or overrun, is flagged
+// through `err` (the host validated the frame table itself).
 template <int W>
 __global__ void __launch_bounds__(kThreads)
 hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
             uint32_t first_frame, uint64_t logical, uint32_t frame_bytes,
-            uint8_t* __restrict__ out) {
+            uint8_t* __restrict__ out, uint32_t* err) {
   // streams + 16 B of slack for the 8-B refill reads past the last stream
   __shared__ uint64_t coded64[(kMaxCoded + 1 + 16 + 7) / 8];
   __shared__ uint16_t lut[kLut];
@@ -937,7 +964,8 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   const uint64_t nlo = uint64_t(W - 1) * n;
   const uint8_t* fr = frames + offsets[fl];
   const uint64_t extent = offsets[fl + 1] - offsets[fl];
-  if (fr[0] != 2) return;
+  // too-short frames are reported by hsz_decode
+  if (offsets[fl + 1] < offsets[fl] + kFrameHeader || fr[0] != 2) return;
   uint8_t* o = out + fl * uint64_t(frame_bytes);
   const uint32_t n_esc = *reinterpret_cast<const uint32_t*>(fr + 4);
   if (threadIdx.x < 16) {
@@ -956,7 +984,10 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
               kFrameHeader + nlo + kLaneTable <= extent;
   }
   __syncthreads();
-  if (!valid) return;
+  if (!valid) {
+    if (threadIdx.x == 0) flag_corrupt(err);
+    return;
+  }
   for (int x = threadIdx.x; x < kLut; x += kThreads) {
     uint16_t ent = 0;
 #pragma unroll
@@ -973,8 +1004,10 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   const uint32_t c_bytes = ctotal;
   const uint64_t tail_len = len - W * n;
   if (c_bytes > kMaxCoded ||
-      kFrameHeader + nlo + kLaneTable + c_bytes + n_esc + tail_len > extent)
+      kFrameHeader + nlo + kLaneTable + c_bytes + n_esc + tail_len > extent) {
+    if (threadIdx.x == 0) flag_corrupt(err);
     return;  // uniform across the workgroup (ctotal is shared)
+  }
   const uint8_t* streams = body + nlo + kLaneTable;
   uint8_t* coded = reinterpret_cast<uint8_t*>(coded64);
   if ((reinterpret_cast<uintptr_t>(streams) & 3) == 0) {
@@ -993,6 +1026,7 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   uint32_t pos = loff;
   uint64_t acc = 0;
   int nb = 0;
+  bool bad = false;
   for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
     // (loading the next group's low bytes one iteration ahead measured slower
     // here: this loop is bound by its LDS stream and LUT reads)
@@ -1009,7 +1043,11 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
       const uint32_t ent = lut[acc & (kLut - 1)];
       uint32_t l = ent >> 8;
       uint32_t c = ent & 15;
-      if (l == 0) { l = kMaxLen; c = 0; }  // corrupt stream: keep going, bounded
+      if (l == 0) {  // corrupt stream: flag it, keep going (bounded)
+        l = kMaxLen;
+        c = 0;
+        bad = true;
+      }
       acc >>= l;
       nb -= int(l);
       uint32_t hi = dict[c];
@@ -1034,6 +1072,8 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
         for (int b = 0; b < 4; ++b) o[8 * W * g + 4 * q + b] = uint8_t(wd[q] >> (8 * b));
     }
   }
+  // a lane may not read past its own stream (host decoder: same check)
+  if (bad || uint64_t(pos - loff) * 8 - uint64_t(nb) > uint64_t(lb) * 8) flag_corrupt(err);
   // the barrier orders every wave's element stores before the escape patches
   __syncthreads();
   const uint8_t* escv = streams + c_bytes;
@@ -1109,9 +1149,11 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
 // Decode `count` frames starting at global frame `first` into `out` (logical
 // bytes of those frames).  `offsets` (device, count + 1 entries) are byte
 // offsets of each frame relative to `frames`, then the end of the last one.
+// `err` (nullable): host-mapped pinned uint32 set to 1 when any frame is
+// rejected; read it after synchronising `stream`.
 int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t first,
                    uint32_t count, uint64_t logical, int w, uint32_t frame_bytes, void* out,
-                   void* stream) {
+                   void* stream, void* err) {
   hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return fail("hipSetDevice", e);
   if (count == 0) return 0;
@@ -1119,19 +1161,20 @@ int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t fi
   auto* fr = static_cast<const uint8_t*>(frames);
   auto* off = static_cast<const uint64_t*>(offsets);
   auto* o = static_cast<uint8_t*>(out);
+  auto* ew = static_cast<uint32_t*>(err);
   switch (w) {
-    case 1: hipLaunchKernelGGL(hsz_decode<1>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
-    case 2: hipLaunchKernelGGL(hsz_decode<2>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
-    case 4: hipLaunchKernelGGL(hsz_decode<4>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
-    case 8: hipLaunchKernelGGL(hsz_decode<8>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o); break;
+    case 1: hipLaunchKernelGGL(hsz_decode<1>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o, ew); break;
+    case 2: hipLaunchKernelGGL(hsz_decode<2>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o, ew); break;
+    case 4: hipLaunchKernelGGL(hsz_decode<4>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o, ew); break;
+    case 8: hipLaunchKernelGGL(hsz_decode<8>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o, ew); break;
     default: return -1001;
   }
   if (w == 2)
     hipLaunchKernelGGL(hsz_decode2<2>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical,
-                       frame_bytes, o);
+                       frame_bytes, o, ew);
   else if (w == 4)
     hipLaunchKernelGGL(hsz_decode2<4>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical,
-                       frame_bytes, o);
+                       frame_bytes, o, ew);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("hsz decode launch", e);
 }

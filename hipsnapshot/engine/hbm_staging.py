@@ -40,6 +40,16 @@ logger = logging.getLogger(__name__)
 
 _ALIGN = 256
 
+# (descriptor keepalive, completion event) of freeze launches that may still
+# be queued on the trainer's stream.  The pinned descriptor block must not go
+# back to the pool before the kernel has read it -- not even when the take
+# fails and drops its stagers -- so it is held here until its event completes.
+_live_launches: List[tuple] = []
+
+
+def _retire_launches() -> None:
+    _live_launches[:] = [kd for kd in _live_launches if not kd[1].query()]
+
 
 def _cuda_sources(wr: WriteReq):
     """The stagers whose CUDA tensors a write request reads (empty if none)."""
@@ -108,6 +118,7 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
 
 
 def _freeze(dev: int, sts, offs, total: int) -> None:
+    _retire_launches()
     stream = torch.cuda.current_stream(dev)
     with torch.cuda.device(dev):
         with timeline.span("freeze_alloc", bytes=total):
@@ -132,6 +143,7 @@ def _freeze(dev: int, sts, offs, total: int) -> None:
             keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
         done = torch.cuda.Event()
         done.record(stream)
+    _live_launches.append((keep, done))
     for st, view in zip(sts, views):
         st.tensor = view
         st.producer = None  # ordering is carried by wait_event

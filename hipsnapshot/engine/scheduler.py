@@ -119,15 +119,48 @@ class PipelineStats:
         return d
 
 
+class MemoryGate:
+    """Host-memory budget of one take, shared by every pipeline it runs.
+
+    A request is admitted when its cost fits, or when nothing at all is held
+    (so one oversized request still makes progress).  Releases wake every
+    pipeline waiting on the gate, so an async take's deferred pipeline (see
+    ``DeferredIOWork``) only stages what the first pipeline's in-flight
+    writes have left of the budget."""
+
+    def __init__(self, limit: int) -> None:
+        self.limit = limit
+        self.in_use = 0
+        self._wakes: set = set()
+
+    def try_admit(self, cost: int) -> bool:
+        if self.in_use + cost > self.limit and self.in_use > 0:
+            return False
+        self.in_use += cost
+        return True
+
+    def release(self, cost: int) -> None:
+        self.in_use -= cost
+        for ev in self._wakes:
+            ev.set()
+
+    def subscribe(self, ev: asyncio.Event) -> None:
+        self._wakes.add(ev)
+
+    def unsubscribe(self, ev: asyncio.Event) -> None:
+        self._wakes.discard(ev)
+
+
 class PendingIOWork:
     """Storage writes still in flight after staging completed."""
 
     def __init__(self, io_tasks: set, executor: ThreadPoolExecutor, stats: PipelineStats,
-                 failure: List[BaseException]) -> None:
+                 failure: List[BaseException], gate: Optional[MemoryGate] = None) -> None:
         self.io_tasks = io_tasks
         self.executor = executor
         self.stats = stats
         self._failure = failure
+        self.gate = gate
 
     async def complete(self) -> None:
         done = False
@@ -154,7 +187,8 @@ class PendingIOWork:
 async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                              memory_budget_bytes: int, rank: int,
                              stage_threads: Optional[int] = None,
-                             io_concurrency: Optional[int] = None) -> PendingIOWork:
+                             io_concurrency: Optional[int] = None,
+                             gate: Optional[MemoryGate] = None) -> PendingIOWork:
     stage_threads = stage_threads or knobs.get_stage_threads()
     io_concurrency = io_concurrency or knobs.get_io_threads()
     executor = _acquire_pool("stage", stage_threads, rank)
@@ -162,11 +196,12 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     stats.n_reqs = len(write_reqs)
     failure: List[BaseException] = []
     pending = deque(write_reqs)
-    in_use = [0]
+    gate = gate if gate is not None else MemoryGate(memory_budget_bytes)
     staging: Dict[asyncio.Task, tuple] = {}
     io_tasks: set = set()
     io_sem = asyncio.Semaphore(io_concurrency)
     wake = asyncio.Event()
+    gate.subscribe(wake)
     from ..utils.tracing import WriteReporter
 
     reporter = WriteReporter(rank, memory_budget_bytes)
@@ -186,17 +221,16 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             raise
         finally:
             buf.release()
-            in_use[0] -= cost
+            gate.release(cost)
             wake.set()
 
     try:
         while pending or staging:
             while pending and len(staging) < stage_threads and not failure:
                 cost = pending[0].buffer_stager.get_staging_cost_bytes()
-                if in_use[0] + cost > memory_budget_bytes and (staging or in_use[0] > 0):
+                if not gate.try_admit(cost):
                     break
                 wr = pending.popleft()
-                in_use[0] += cost
                 task = asyncio.ensure_future(wr.buffer_stager.stage_buffer(executor))
                 staging[task] = (wr, cost, time.perf_counter())
             if failure:
@@ -207,7 +241,7 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             done, _ = await asyncio.wait(waiters | {waiter}, return_when=asyncio.FIRST_COMPLETED)
             if not waiter.done():
                 waiter.cancel()
-            reporter.maybe_report(len(pending), len(staging), len(io_tasks), in_use[0],
+            reporter.maybe_report(len(pending), len(staging), len(io_tasks), gate.in_use,
                                   stats.bytes_written)
             for task in done:
                 if task is waiter:
@@ -215,7 +249,7 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                 wr, cost, t_s = staging.pop(task)
                 exc = task.exception()
                 if exc is not None:
-                    in_use[0] -= cost
+                    gate.release(cost)
                     failure.append(exc)
                     continue
                 buf = as_staged(task.result())
@@ -235,16 +269,21 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     except BaseException:
         executor.shutdown(wait=False)
         raise
+    finally:
+        # staging is over: later wake-ups (write completions) are not needed
+        gate.unsubscribe(wake)
     stats.t_staged = time.monotonic()
     logger.debug(f"Rank {rank} completed staging in {stats.t_staged - stats.t_start:.3f}s")
-    return PendingIOWork(io_tasks, executor, stats, failure)
+    return PendingIOWork(io_tasks, executor, stats, failure, gate)
 
 
 class DeferredIOWork:
     """``PendingIOWork`` for an async take whose device state was frozen in
     HBM: the immediate part (host tensors, already copied) is staged before
     ``async_take`` returns; the deferred part (HBM arena -> pinned -> storage)
-    runs its whole pipeline in the background commit thread."""
+    runs its whole pipeline in the background commit thread.  Both pipelines
+    draw on ONE ``MemoryGate``, so host memory stays within the per-rank
+    budget while the first pipeline's staged buffers are still being written."""
 
     def __init__(self, first: PendingIOWork, deferred: List[WriteReq], storage: StoragePlugin,
                  memory_budget_bytes: int, rank: int) -> None:
@@ -258,7 +297,8 @@ class DeferredIOWork:
 
     async def complete(self) -> None:
         async def run_deferred() -> None:
-            p = await execute_write_reqs(self.deferred, self.storage, self.budget, self.rank)
+            p = await execute_write_reqs(self.deferred, self.storage, self.budget, self.rank,
+                                         gate=self.first.gate)
             self._second = p
             await p.complete()
 
@@ -313,6 +353,11 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
     in_use = [0]
     inflight: set = set()
     io_sem = asyncio.Semaphore(io_concurrency)
+    # set on the first failed read: queued reads then return without reading.
+    # Reads already handed to storage are NOT cancelled -- the plugin (e.g.
+    # the native engine) may still be writing into their pinned destination,
+    # which must not go back to the pool before that write has finished.
+    failing: List[BaseException] = []
 
     async def _one_compressed(rr: ReadReq) -> None:
         from ..ops import codec as hsz
@@ -320,23 +365,31 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
 
         info = rr.codec
         nf = hsz.n_frames_for(int(info["blob_bytes"]), int(info["frame_bytes"]))
-        async with io_sem:
-            t_r = time.perf_counter()
-            head_io = ReadIO(path=rr.path, byte_range=(0, hsz.payload_start(nf)))
-            await storage.read(head_io)
-            header = hsz.parse_header(head_io.data())
-            lo, hi = rr.byte_range if rr.byte_range is not None else (0, header.logical_size)
-            first, last = header.frames_covering(lo, hi)
-            c_lo, c_hi = header.offsets[first], header.offsets[last]
-            hsz.validate_offsets(header, header.offsets[-1])
-            dest = await asyncio.get_running_loop().run_in_executor(
-                None, rr.buffer_consumer.get_compressed_read_dest, c_hi - c_lo)
-            if dest is None:
-                dest = as_staged(bytearray(max(c_hi - c_lo, 1)))
-            body_io = ReadIO(path=rr.path, byte_range=(c_lo, c_hi), dest=dest)
-            if c_hi > c_lo:
-                await storage.read(body_io)
-            t_c = time.perf_counter()
+        dest = None
+        try:
+            async with io_sem:
+                if failing:
+                    return
+                t_r = time.perf_counter()
+                head_io = ReadIO(path=rr.path, byte_range=(0, hsz.payload_start(nf)))
+                await storage.read(head_io)
+                header = hsz.parse_header(head_io.data())
+                lo, hi = rr.byte_range if rr.byte_range is not None else (0, header.logical_size)
+                first, last = header.frames_covering(lo, hi)
+                c_lo, c_hi = header.offsets[first], header.offsets[last]
+                hsz.validate_offsets(header, header.offsets[-1])
+                dest = await asyncio.get_running_loop().run_in_executor(
+                    None, rr.buffer_consumer.get_compressed_read_dest, c_hi - c_lo)
+                if dest is None:
+                    dest = as_staged(bytearray(max(c_hi - c_lo, 1)))
+                body_io = ReadIO(path=rr.path, byte_range=(c_lo, c_hi), dest=dest)
+                if c_hi > c_lo:
+                    await storage.read(body_io)
+                t_c = time.perf_counter()
+        except BaseException:
+            if dest is not None:
+                dest.release()
+            raise
         span = CompressedSpan(dest, header, first, last, lo, hi)
         timeline.add("read", "io", t_r, t_c, path=rr.path, bytes=c_hi - c_lo, logical=hi - lo)
         stats.bytes_written += hi - lo
@@ -355,6 +408,8 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
             return
         dest = None
         try:
+            if failing:
+                return
             nbytes = _expected_read_bytes(rr)
             if nbytes is not None:
                 # pinned-pool misses cost a hipHostMalloc: keep them off the
@@ -363,6 +418,8 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                     None, rr.buffer_consumer.get_read_dest, nbytes)
             read_io = ReadIO(path=rr.path, byte_range=rr.byte_range, dest=dest)
             async with io_sem:
+                if failing:
+                    return
                 t_r = time.perf_counter()
                 await storage.read(read_io)
                 t_c = time.perf_counter()
@@ -392,8 +449,8 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
             inflight = set(inflight)
             for t in done:
                 if t.exception() is not None:
-                    for o in inflight:
-                        o.cancel()
+                    failing.append(t.exception())
+                    # drain, do not cancel: see ``failing`` above
                     await asyncio.gather(*inflight, return_exceptions=True)
                     raise t.exception()
         clean = True

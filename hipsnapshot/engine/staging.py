@@ -474,14 +474,20 @@ def _scatter_compressed(span, regions, dev: int, producer: Optional[int] = None)
     native.memcpy(dev, slot, offs_dev.data_ptr(), offs.data_ptr(), offs.numel() * 8,
                   native.H2D, None, sync=False)
     stream = native.copy_stream(dev, slot)
+    err = native.DecodeErrorWord()
     native.hsz_decode_gpu(dev, enc.data_ptr(), offs_dev.data_ptr(), first, last - first,
                           h.logical_size, h.elem_width, h.frame_bytes,
-                          (direct if direct is not None else out).data_ptr(), stream)
+                          (direct if direct is not None else out).data_ptr(), stream,
+                          err.addr)
     if direct is not None:
         native.stream_sync(dev, slot)
+        err.check(f"frames [{first}, {last})")
         return
     shift = span.lo - log_lo
+    # one stream sync for decode + copy (a failed restore leaves its targets
+    # undefined either way, as on the host path)
     _copy_regions(out[shift:], regions, dev, slot)
+    err.check(f"frames [{first}, {last})")
 
 
 def _contiguous_src_range(src_dtype: torch.dtype, src_shape: Sequence[int], off: int, narrows):

@@ -541,9 +541,11 @@ def decode_device_into(blob_dev, header: Header, out_dev, stream_handle: int,
     dev = blob_dev.device.index if blob_dev.device.index is not None else \
         torch.cuda.current_device()
     offs_t = torch.tensor(offs, dtype=torch.int64).to(blob_dev.device, non_blocking=False)
+    err = native.DecodeErrorWord()
     native.hsz_decode_gpu(dev, blob_dev.data_ptr(), offs_t.data_ptr(), first, count,
                           header.logical_size, header.elem_width, header.frame_bytes,
-                          out_dev.data_ptr(), stream_handle)
+                          out_dev.data_ptr(), stream_handle, err.addr)
     # keep the offsets alive until the kernel ran
     torch.cuda.ExternalStream(stream_handle).synchronize() if stream_handle else \
         torch.cuda.synchronize(dev)
+    err.check(f"frames [{first}, {first + count})")

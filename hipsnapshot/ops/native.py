@@ -263,7 +263,7 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                   c_void_p, c_void_p])
         _declare(lib, "hsg_hsz_decode", c_int,
                  [c_int, c_void_p, c_void_p, ctypes.c_uint32, ctypes.c_uint32, c_uint64, c_int,
-                  ctypes.c_uint32, c_void_p, c_void_p])
+                  ctypes.c_uint32, c_void_p, c_void_p, c_void_p])
         if lib.hsg_desc_size() != COPY_DESC_DTYPE.itemsize:
             _hsgpu_error = (f"CopyDesc layout mismatch: native {lib.hsg_desc_size()} "
                             f"vs python {COPY_DESC_DTYPE.itemsize}")
@@ -650,6 +650,8 @@ def hsz_decode_cpu(frames_addr: int, offsets_addr: int, first: int, count: int, 
                    w: int, frame_bytes: int, out_addr: int, nthreads: int = 8) -> None:
     r = hsio().hsz_decode_cpu(frames_addr, offsets_addr, first, count, logical, w, frame_bytes,
                               out_addr, nthreads)
+    if r == -74:  # EBADMSG: a frame failed validation
+        raise CorruptBlobError("corrupt HSZ1 blob: the host decoder rejected a frame")
     if r != 0:
         raise RuntimeError(f"hsz_decode_cpu failed ({r})")
 
@@ -679,7 +681,32 @@ def hsz_encode_gpu(dev: int, src_addr: int, logical: int, w: int, frame_bytes: i
 
 def hsz_decode_gpu(dev: int, frames_addr: int, offsets_addr: int, first: int, count: int,
                    logical: int, w: int, frame_bytes: int, out_addr: int,
-                   stream_handle: int) -> None:
+                   stream_handle: int, err_addr: int = 0) -> None:
+    """Enqueue the decode of frames [first, first+count) on ``stream_handle``.
+    ``err_addr``: a zeroed host-mapped pinned uint32 (``DecodeErrorWord``) the
+    kernels set to 1 for a rejected frame; check it after the stream sync."""
     _hsz_check(require_gpu_lib().hsg_hsz_decode(dev, frames_addr, offsets_addr, first, count,
                                                 logical, w, frame_bytes, out_addr,
-                                                stream_handle), "hsg_hsz_decode")
+                                                stream_handle, err_addr or None),
+               "hsg_hsz_decode")
+
+
+class CorruptBlobError(ValueError, RuntimeError):
+    """An HSZ1 blob failed validation in the host or GPU decoder."""
+
+
+class DecodeErrorWord:
+    """Pinned host word the GPU decoders flag corrupt HSZ1 frames in (the
+    device writes it through the host mapping; no extra copy or sync)."""
+
+    def __init__(self) -> None:
+        import torch
+
+        self._t = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.addr = self._t.data_ptr()
+
+    def check(self, what: str) -> None:
+        """Call after the decode's stream was synchronised."""
+        if int(self._t[0]) != 0:
+            raise CorruptBlobError(
+                f"corrupt HSZ1 blob: the GPU decoder rejected a frame of {what}")

@@ -28,18 +28,23 @@ DEFAULT_TCP_STORE_TIMEOUT = timedelta(seconds=600)
 _pg_to_store: Dict[object, dist.Store] = {}
 
 
-def get_or_create_store(comm: Comm) -> dist.Store:
-    store = None
+def existing_store(comm: Comm) -> Optional[dist.Store]:
+    """The default c10d store, or one ``create_store`` made earlier for this
+    group; None if neither exists.  Never issues a collective."""
     if dist.is_initialized():
         try:
             store = dist.distributed_c10d._get_default_store()
         except Exception:  # pragma: no cover - MPI backend
             store = None
+        if store is not None:
+            return store
+    return _pg_to_store.get(comm.pg)
+
+
+def get_or_create_store(comm: Comm) -> dist.Store:
+    store = existing_store(comm)
     if store is not None:
         return store
-    key = comm.pg
-    if key in _pg_to_store:
-        return _pg_to_store[key]
     return create_store(comm)
 
 

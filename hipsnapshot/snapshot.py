@@ -70,7 +70,7 @@ from .io_types import ReadIO, ReadReq, StoragePlugin, WriteIO, WriteReq
 from .parallel.comm import Comm
 from .parallel.elasticity import get_manifest_for_rank, handle_sharded_tensor_elasticity
 from .parallel.partitioner import consolidate_replicated_entries, partition_write_reqs
-from .parallel.store import LinearBarrier, get_or_create_store
+from .parallel.store import LinearBarrier, existing_store, get_or_create_store
 from .stateful import AppState, RNGState, Stateful
 from .storage.registry import url_to_storage_plugin_in_event_loop
 from .utils.tracing import paused_gc, roctx_range, timeline
@@ -232,11 +232,17 @@ class Snapshot:
         t0 = time.monotonic()
         path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
         storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
+        progress: Dict[str, bool] = {}
         try:
             pending, metadata = cls._take_impl(path, app_state, rep, keys, comm, storage, loop,
                                                True, _custom_tensor_prepare_func, quantize,
-                                               compression)
-        except BaseException:
+                                               compression, progress=progress)
+        except BaseException as e:
+            if progress.get("metadata_gathered"):
+                # peers that staged successfully are already in (or about to
+                # start) their commit threads: fail their barrier now instead
+                # of letting them wait DEFAULT_BARRIER_TIMEOUT
+                _report_async_failure(comm, path, nonce, e)
             storage.sync_close(loop)
             loop.close()
             raise
@@ -262,7 +268,8 @@ class Snapshot:
                    global_keys: List[str], comm: Comm, storage: StoragePlugin,
                    loop: asyncio.AbstractEventLoop, is_async: bool,
                    prepare_func: Optional[PrepareFunc], quantize: Optional[List[str]],
-                   compression: Optional[str] = None
+                   compression: Optional[str] = None,
+                   progress: Optional[Dict[str, bool]] = None,
                    ) -> Tuple[PendingIOWork, SnapshotMetadata]:
         if comm.get_rank() == 0:
             with timeline.span("uncommit"):
@@ -339,10 +346,14 @@ class Snapshot:
         manifest.update(object_entries)
         metadata = None
         if is_async:
-            # async: every rank has the metadata before any staging can fail,
-            # so a failing rank reports through the commit barrier, not a hang
+            # async: every rank has the metadata before any staging can fail;
+            # a rank whose staging fails after this point reports the error
+            # through the commit barrier (``_report_async_failure``), so its
+            # peers' commit threads fail at once instead of timing out
             with timeline.span("gather_manifest"):
                 metadata = cls._gather_metadata(manifest, comm)
+            if progress is not None:
+                progress["metadata_gathered"] = True
 
         budget = get_process_memory_budget_bytes(comm)
         deferred: List[WriteReq] = []
@@ -647,6 +658,30 @@ def flat_prefix(key: str) -> str:
     return encode_key(key)
 
 
+def _commit_barrier(store, path: str, nonce: str, rank: int, world_size: int) -> LinearBarrier:
+    return LinearBarrier(prefix=f"hipsnapshot_{nonce}_{path}", store=store, rank=rank,
+                         world_size=world_size, leader_rank=0)
+
+
+def _report_async_failure(comm: Comm, path: str, nonce: str, exc: BaseException) -> None:
+    """A rank failed between the metadata gather and its commit thread:
+    publish the error on the async commit barrier so the leader fails in
+    ``arrive`` and every peer in ``depart``.  Only an EXISTING store is used
+    (creating one is collective and the peers are not in a collective)."""
+    if comm.get_world_size() <= 1:
+        return
+    store = existing_store(comm)
+    if store is None:
+        logger.warning("async_take failed on this rank and no store exists to report it; "
+                       "peers will wait for the commit barrier timeout")
+        return
+    try:
+        _commit_barrier(store, path, nonce, comm.get_rank(),
+                        comm.get_world_size()).report_error(repr(exc))
+    except Exception as e:  # noqa: BLE001 - never mask the original error
+        logger.warning(f"could not report async_take failure to peers: {e}")
+
+
 class PendingSnapshot:
     """Handle of an in-flight ``async_take``; the commit happens in a thread
     that never issues collectives (store-based two-phase barrier)."""
@@ -678,8 +713,7 @@ class PendingSnapshot:
         # WARNING: no collectives in this thread
         barrier = None
         if store is not None:
-            barrier = LinearBarrier(prefix=f"hipsnapshot_{nonce}_{path}", store=store, rank=rank,
-                                    world_size=world_size, leader_rank=0)
+            barrier = _commit_barrier(store, path, nonce, rank, world_size)
         try:
             pending_io_work.sync_complete(event_loop)
             if barrier is not None:

@@ -78,7 +78,7 @@ class FSStoragePlugin(StoragePlugin):
         self._pending[job_id] = (fut, keepalive)
         # the completion may already be queued
         self._on_ready()
-        return await fut
+        return await _uncancellable(fut)
 
     def _flags(self, mkdirs: bool = False) -> int:
         f = 0
@@ -102,7 +102,8 @@ class FSStoragePlugin(StoragePlugin):
         addr = write_io.addr if write_io.addr is not None else buffer_address(mv)
         eng = self._get_engine()
         if eng is None:
-            await asyncio.get_running_loop().run_in_executor(None, _py_write, path, mv)
+            await _uncancellable(asyncio.get_running_loop().run_in_executor(
+                None, _py_write, path, mv))
         else:
             job = eng.submit_write(path, addr, n, 0, self._flags(mkdirs=True))
             res = await self._await_job(job, mv)
@@ -129,8 +130,8 @@ class FSStoragePlugin(StoragePlugin):
             read_io.buf = dest_view
             return
         if eng is None:
-            got = await asyncio.get_running_loop().run_in_executor(
-                None, _py_read, path, dest_view, offset)
+            got = await _uncancellable(asyncio.get_running_loop().run_in_executor(
+                None, _py_read, path, dest_view, offset))
         else:
             job = eng.submit_read(path, addr, n, offset, self._flags())
             got = await self._await_job(job, dest_view)
@@ -169,6 +170,27 @@ class FSStoragePlugin(StoragePlugin):
             _native.release_io_engine(self._engine, reusable=not self._pending)
             self._engine = None
             self._loop = None
+
+
+async def _uncancellable(fut: "asyncio.Future[Any]") -> Any:
+    """Await a job that reads or writes a caller-owned buffer.
+
+    Cancelling the awaiting task does not stop the engine worker (or executor
+    thread) behind ``fut``: it keeps pread()ing into / pwrite()ing from the
+    buffer.  Callers release that buffer (back to the pinned pool, or to
+    hipHostFree) as soon as this coroutine ends, so a cancellation must not
+    end it early: wait for the job, then re-raise the cancellation."""
+    cancelled = False
+    while not fut.done():
+        try:
+            await asyncio.shield(fut)
+        except asyncio.CancelledError:
+            if fut.cancelled():
+                raise
+            cancelled = True
+    if cancelled:
+        raise asyncio.CancelledError()
+    return fut.result()
 
 
 def _py_write(path: str, mv: memoryview) -> None:

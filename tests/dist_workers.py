@@ -177,6 +177,42 @@ def async_take_faulty(path: str):
     assert not os.path.exists(os.path.join(path, ".snapshot_metadata"))
 
 
+def async_take_staging_fault(path: str):
+    """Rank 1 fails while staging, after the metadata gather: rank 0's commit
+    thread must fail promptly through the barrier, not after its timeout."""
+    import time
+    from datetime import timedelta
+    from unittest import mock
+
+    from hipsnapshot.snapshot import PendingSnapshot
+
+    rank = dist.get_rank()
+
+    def boom(*a, **k):
+        raise OSError("injected staging failure")
+
+    PendingSnapshot.DEFAULT_BARRIER_TIMEOUT = timedelta(seconds=120)
+    sd = {"sd": StateDict(t=torch.ones(100) * rank)}
+    t0 = time.monotonic()
+    if rank == 1:
+        with mock.patch("hipsnapshot.snapshot.sync_execute_write_reqs", boom):
+            try:
+                Snapshot.async_take(path, sd)
+                raise AssertionError("async_take should have raised")
+            except OSError as e:
+                assert "injected staging failure" in str(e)
+    else:
+        pending = Snapshot.async_take(path, sd)
+        try:
+            pending.wait()
+            raise AssertionError("rank 0 must observe rank 1's failure")
+        except RuntimeError as e:
+            assert "injected staging failure" in str(e), str(e)
+        assert time.monotonic() - t0 < 60, "failure was not propagated through the barrier"
+    dist.barrier()
+    assert not os.path.exists(os.path.join(path, ".snapshot_metadata"))
+
+
 def linear_barrier(prefix: str, skip_arrive_rank: int = -1, error_rank: int = -1):
     from hipsnapshot.parallel.store import LinearBarrier, get_or_create_store
 

@@ -45,6 +45,10 @@ def test_async_take_fault_injection(tmp_path):
     run_distributed(W.async_take_faulty, 2, str(tmp_path / "f"))
 
 
+def test_async_take_staging_fault_fails_peers_promptly(tmp_path):
+    run_distributed(W.async_take_staging_fault, 2, str(tmp_path / "sf"))
+
+
 def test_linear_barrier():
     run_distributed(W.linear_barrier, 3, "lb_ok")
 

@@ -477,6 +477,79 @@ def test_hsz_gpu_fp32_blob_ratio(gpu):
     assert torch.equal(back.view(torch.int32), x.view(torch.int32))
 
 
+def _corruptions(blob: bytes, w: int):
+    """(name, corrupted blob) pairs that the host decoder rejects."""
+    from hipsnapshot.ops import codec
+
+    h = codec.parse_header(blob)
+    f1 = h.offsets[1]
+    n = h.frame_bytes // w
+    lane_tab = f1 + 32 + (w - 1) * n   # mode-2 body: low bytes, then the lane table
+
+    def patch(off, val):
+        b = bytearray(blob)
+        b[off:off + len(val)] = val
+        return bytes(b)
+
+    out = [("mode byte", patch(f1, b"\x09")),
+           ("code length > max", patch(f1 + 24, b"\xff")),
+           ("lane table overflow", patch(lane_tab, b"\xff\xff"))]
+    if codec.frame_modes(blob)[1] == 2:
+        # every lane claims 0 stream bytes: lanes read past their own streams
+        out.append(("lane overrun", patch(lane_tab, bytes(2 * 256))))
+    return out
+
+
+@pytest.mark.parametrize("w", [2, 4])
+def test_hsz_gpu_decode_rejects_corrupt_frames(gpu, w):
+    """Every frame the host decoder rejects (-74) makes the GPU decode raise
+    too, instead of leaving the output unwritten."""
+    from hipsnapshot.ops import codec
+
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(3 * 65536 // w, generator=g) * 0.02)
+    x = x.to(torch.bfloat16) if w == 2 else x
+    raw = x.view(torch.uint8).numpy().tobytes()
+    blob = codec.encode_reference(raw, w, 64 * 1024)
+    assert codec.frame_modes(blob)[1] == 2
+    s = torch.cuda.current_stream()
+    for name, bad in _corruptions(blob, w):
+        with pytest.raises(Exception):
+            codec.decode_cpu(bad)
+        d = torch.frombuffer(bytearray(bad), dtype=torch.uint8).to(gpu)
+        out = torch.empty(len(raw), dtype=torch.uint8, device=gpu)
+        with pytest.raises(ValueError, match="corrupt HSZ1"):
+            codec.decode_device_into(d, codec.parse_header(bad), out, int(s.cuda_stream))
+    # the intact blob still decodes (no sticky error state)
+    d = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(gpu)
+    out = torch.empty(len(raw), dtype=torch.uint8, device=gpu)
+    codec.decode_device_into(d, codec.parse_header(blob), out, int(s.cuda_stream))
+    assert out.cpu().numpy().tobytes() == raw
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_gpu_restore_of_corrupt_compressed_blob_raises(gpu, tmp_path, direct):
+    from hipsnapshot.knobs import override_is_batching_disabled
+    from hipsnapshot.ops import codec
+
+    big = (torch.randn(3000, 1024, device=gpu) * 0.02).to(torch.bfloat16)
+    path = str(tmp_path / "c")
+    with override_is_batching_disabled(True):
+        Snapshot.take(path, {"sd": StateDict(big=big)}, compression="hsz1")
+    f = os.path.join(path, "0", "sd", "big")
+    blob = open(f, "rb").read()
+    h = codec.parse_header(blob)
+    with open(f, "r+b") as fh:  # frame 2's mode byte
+        fh.seek(h.offsets[2])
+        fh.write(b"\x09")
+    # direct: decoded straight into the target; else via scratch + cast copy
+    out = StateDict(big=torch.zeros(3000, 1024, device=gpu,
+                                    dtype=torch.bfloat16 if direct else torch.float32))
+    with override_is_batching_disabled(True), pytest.raises(Exception, match="corrupt HSZ1"):
+        Snapshot(path).restore({"sd": out})
+    torch.cuda.synchronize()
+
+
 # ---- HSZ1 compressed snapshots on the GPU path ---------------------------------
 
 def _compressible_state(gpu):
