@@ -51,14 +51,15 @@ def build_hsio(force: bool = False) -> str:
 
 
 def build_hsgpu(force: bool = False) -> str:
-    srcs = [os.path.join(CSRC, "hsgpu.hip"), os.path.join(CSRC, "hsz.hip")]
+    srcs = [os.path.join(CSRC, "hsgpu.hip"), os.path.join(CSRC, "hsz.hip"),
+            os.path.join(CSRC, "hsdma.hip")]
     if force or _stale(HSGPU_SO, srcs):
         hipcc = os.path.join(ROCM, "bin", "hipcc")
         if not os.path.exists(hipcc):
             hipcc = shutil.which("hipcc") or hipcc
         _atomic_build(HSGPU_SO, lambda out: [hipcc, f"--offload-arch={GPU_ARCH}", "-O3",
                                              "-std=c++17", "-fPIC", "-shared", "-Wall",
-                                             "-o", out] + srcs)
+                                             "-o", out] + srcs + ["-ldl"])
     return HSGPU_SO
 
 

@@ -2,8 +2,9 @@
 
 Every GPU byte that leaves or enters HBM goes through here:
 
-* D2H of one tensor: pinned pool block + ``hipMemcpyAsync`` on a per-thread
-  copy stream ordered after the producer stream (SDMA, no pageable bounce) --
+* D2H of one tensor: pinned pool block + one bulk copy (``bulk_d2h``:
+  hipMemcpyAsync on a per-thread copy stream ordered after the producer
+  stream, or the SDMA engines through ROCr; no pageable bounce) --
   replaces the reference's pageable ``tensor.to("cpu")`` in a 4-thread pool
   (`/root/reference/torchsnapshot/io_preparers/tensor.py:247-254`).
 * non-contiguous views are packed by the ``hs_copy_nd`` kernel straight into
@@ -93,6 +94,34 @@ def _pinned_staged(nbytes: int) -> Tuple[native.PinnedBuffer, StagedBuffer]:
     return pb, StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
 
 
+_sdma_ok: dict = {}
+
+
+def _use_sdma(dev: int) -> bool:
+    from .. import knobs
+
+    if knobs.get_d2h_engine() != "sdma":
+        return False
+    ok = _sdma_ok.get(dev)
+    if ok is None:
+        ok = _sdma_ok[dev] = native.sdma_engines(dev) > 0
+    return ok
+
+
+def bulk_d2h(dev: int, slot: int, dst: int, src: int, nbytes: int,
+             producer: Optional[int] = None) -> None:
+    """Blocking device -> pinned-host copy of ``nbytes``, ordered after the
+    copy stream (dev, slot) and, if given, after ``producer``.  Runs on the
+    SDMA engines when ``HIPSNAPSHOT_D2H_ENGINE=sdma`` (no CU time taken from
+    a concurrent training step), else as hipMemcpyAsync."""
+    if nbytes and _use_sdma(dev):
+        if producer is not None:
+            native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
+        native.sdma_d2h(dev, dst, src, nbytes, native.copy_stream(dev, slot))
+        return
+    native.memcpy(dev, slot, dst, src, nbytes, native.D2H, producer, sync=True)
+
+
 def _elem_strides_ok(t: torch.Tensor) -> bool:
     return t.dim() <= native.MAX_DIMS
 
@@ -115,7 +144,7 @@ def d2h_tensor(t: torch.Tensor, producer: Optional[int],
     t_s = time.perf_counter()
     try:
         if t.is_contiguous():
-            native.memcpy(dev, slot, pb.ptr, t.data_ptr(), nbytes, native.D2H, producer, sync=True)
+            bulk_d2h(dev, slot, pb.ptr, t.data_ptr(), nbytes, producer)
         else:
             # pack-to-host: kernel stores the packed view over PCIe into the
             # host-mapped pinned block, ordered after the producer stream.
@@ -168,7 +197,7 @@ def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dic
     nbytes = _read_u64_device(dev, slot, total.data_ptr())
     pb, staged = _pinned_staged(nbytes)
     try:
-        native.memcpy(dev, slot, pb.ptr, out.data_ptr(), nbytes, native.D2H, None, sync=True)
+        bulk_d2h(dev, slot, pb.ptr, out.data_ptr(), nbytes)
     except BaseException:
         staged.release()
         raise
@@ -186,8 +215,7 @@ def _encode_on_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dict) -> S
     raw_pb = native.PinnedBuffer(max(n, 1))
     try:
         if n:
-            native.memcpy(dev, slot, raw_pb.ptr, src_u8.data_ptr(), n, native.D2H, None,
-                          sync=True)
+            bulk_d2h(dev, slot, raw_pb.ptr, src_u8.data_ptr(), n)
         return _encode_host_bytes(raw_pb.ptr, n, codec)
     finally:
         raw_pb.release()
@@ -301,8 +329,7 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
             batch.add_tensor(t, base + off)
         keep = batch.launch(dev, stream, sync=False)
         if slab is not None:
-            native.memcpy(dev, slot, pb.ptr, slab.data_ptr(), total_bytes, native.D2H, None,
-                          sync=False)
+            bulk_d2h(dev, slot, pb.ptr, slab.data_ptr(), total_bytes)
         native.stream_sync(dev, slot)
         if keep is not None:
             keep[0].release()

@@ -108,6 +108,17 @@ def get_io_read_split_bytes() -> int:
     return _get_int("IO_READ_SPLIT_BYTES", 8 * 1024 * 1024)
 
 
+def get_d2h_engine() -> str:
+    """Engine for bulk device -> pinned-host copies: ``blit`` = hipMemcpyAsync
+    (the HIP runtime's copy kernel on the CUs), ``sdma`` = the GPU's DMA
+    engines through ROCr (``csrc/hsdma.hip``; falls back to blit when ROCr
+    reports no engine)."""
+    v = str(_get("D2H_ENGINE") or "blit").strip().lower()
+    if v not in ("blit", "sdma"):
+        raise ValueError(f"HIPSNAPSHOT_D2H_ENGINE must be blit or sdma, not {v!r}")
+    return v
+
+
 def get_stage_threads() -> int:
     return _get_int("STAGE_THREADS", 4)
 

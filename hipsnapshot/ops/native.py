@@ -257,6 +257,10 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
         _declare(lib, "hsg_hsz_last_error", c_char_p, [])
+        _declare(lib, "hsg_sdma_last_error", c_char_p, [])
+        _declare(lib, "hsg_sdma_engines", c_int, [c_int])
+        _declare(lib, "hsg_sdma_d2h", c_int,
+                 [c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p])
         _declare(lib, "hsg_hsz_meta_bytes", c_uint64, [ctypes.c_uint32])
         _declare(lib, "hsg_hsz_encode", c_int,
                  [c_int, c_void_p, c_uint64, c_int, ctypes.c_uint32, c_void_p, c_void_p,
@@ -376,6 +380,24 @@ def memcpy(dev: int, slot: int, dst: int, src: int, nbytes: int, kind: int,
     _check(lib.hsg_memcpy(dev, slot, dst, src, nbytes, kind, _stream_handle(producer),
                           int(producer is not None),
                           1 if sync else 0), "hsg_memcpy")
+
+
+def sdma_engines(dev: int) -> int:
+    """SDMA engines usable for device -> host copies of ``dev`` (0 = none:
+    the SDMA path is unavailable and hipMemcpyAsync is used)."""
+    return int(require_gpu_lib().hsg_sdma_engines(dev))
+
+
+def sdma_d2h(dev: int, dst: int, src: int, nbytes: int, stream=None,
+             max_engines: int = 0) -> None:
+    """Blocking device -> pinned-host copy on the SDMA engines, ordered after
+    the work queued on ``stream`` (handle or torch stream; None/0 = the null
+    stream).  ``max_engines`` 0 = every free engine."""
+    lib = require_gpu_lib()
+    r = lib.hsg_sdma_d2h(dev, dst, src, nbytes, max_engines, _stream_handle(stream) or None)
+    if r != 0:
+        msg = lib.hsg_sdma_last_error()
+        raise HipError(f"hsg_sdma_d2h failed ({r}): {msg.decode() if msg else ''}")
 
 
 def copy_stream(dev: int, slot: int) -> int:

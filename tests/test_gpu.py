@@ -723,3 +723,55 @@ def test_copy_workspace_ordered_after_busy_default_stream(gpu):
     assert not errors, errors
     for i, y in results:
         assert torch.all(y == 2.0 * i), i
+
+
+# ---- SDMA device -> host engine (csrc/hsdma.hip) ----------------------------
+
+def test_sdma_d2h_sees_kernel_writes_just_made(gpu):
+    """The SDMA engine reads HBM behind the L2: bytes a kernel wrote on the
+    producer stream right before the copy must arrive (system-scope release)."""
+    if native.sdma_engines(0) == 0:
+        pytest.skip("ROCr reports no SDMA engine")
+    n = (96 << 20) + 4096 + 17
+    pb = native.PinnedBuffer(n)
+    host = torch.frombuffer(pb.view, dtype=torch.uint8)[:n]
+    s = torch.cuda.Stream()
+    src = torch.empty(n, dtype=torch.uint8, device=gpu)
+    try:
+        for val in (3, 250, 77):
+            with torch.cuda.stream(s):
+                src.fill_(val)
+                src[12345:99999].random_(0, 255)
+            # no host sync: the copy must order itself after the stream
+            native.sdma_d2h(0, pb.ptr, src.data_ptr(), n, s)
+            assert torch.equal(host, src.cpu()), val
+        for k in (1, 2, 3):  # split over several engines
+            with torch.cuda.stream(s):
+                src.random_(0, 255)
+            native.sdma_d2h(0, pb.ptr, src.data_ptr(), n, s, max_engines=k)
+            assert torch.equal(host, src.cpu()), k
+    finally:
+        pb.release()
+
+
+@pytest.mark.parametrize("compression", ["none", "hsz1"])
+def test_snapshot_with_sdma_d2h(gpu, tmp_path, compression):
+    if native.sdma_engines(0) == 0:
+        pytest.skip("ROCr reports no SDMA engine")
+    sd = _compressible_state(gpu)
+    ref = _clone_state(sd)
+    with override_knob("D2H_ENGINE", "sdma"):
+        Snapshot.take(str(tmp_path / "s"), {"sd": sd}, compression=compression)
+        pending = Snapshot.async_take(str(tmp_path / "a"), {"sd": sd}, compression=compression)
+        for k, v in sd.items():  # mutate after unblock: must not leak
+            if isinstance(v, torch.Tensor):
+                v.zero_()
+        pending.wait()
+    for p in ("s", "a"):
+        out = {k: (torch.zeros_like(v) if isinstance(v, torch.Tensor) else
+                   [torch.zeros_like(x) for x in v] if isinstance(v, list) else v)
+               for k, v in ref.items()}
+        out = StateDict(**out)
+        Snapshot(str(tmp_path / p)).restore({"sd": out})
+        torch.cuda.synchronize()
+        assert_state_dict_eq({k: out[k] for k in ref}, ref)
