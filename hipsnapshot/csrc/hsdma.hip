@@ -17,9 +17,10 @@
 // provided: the host -> device direction would need a system-scope acquire in
 // every consumer, which HIP cannot be told about.
 //
-// A copy is split into pieces over the engines ROCr reports as free for the
-// GPU -> CPU direction, each piece on its own completion signal; the call
-// returns when all pieces are done (or reports the first failure).
+// By default a copy is one request on the engine ROCr assigns; optionally it
+// is split into pieces over the engines ROCr reports as free for the GPU ->
+// CPU direction, each piece on its own completion signal.  The call returns
+// when all pieces are done (or reports the first failure).
 
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -180,9 +181,10 @@ int hsg_sdma_engines(int dev) {
   return __builtin_popcount(d->engines);
 }
 
-// Blocking device -> pinned-host copy of n bytes on up to `max_engines` SDMA
-// engines.  `stream` = the HIP stream whose queued work produced `src` (the
-// copy is ordered after it).  Returns 0, or < 0 on failure (nothing is left
+// Blocking device -> pinned-host copy of n bytes on the SDMA engines
+// (`max_engines` 0 = one request on the engine ROCr assigns).  `stream` =
+// the HIP stream whose queued work produced `src` (the copy is ordered
+// after it).  Returns 0, or < 0 on failure (nothing is left
 // in flight on failure: every issued piece is waited for).
 int hsg_sdma_d2h(int dev, void* dst, const void* src, uint64_t n, int max_engines, void* stream) {
   DevInfo* d = dev_info(dev);
@@ -204,11 +206,16 @@ int hsg_sdma_d2h(int dev, void* dst, const void* src, uint64_t n, int max_engine
       return -4;
     }
   }
+  // max_engines 0: one request, ROCr picks the engine (it spreads concurrent
+  // requests from several staging threads over its engines and never
+  // conflicts with copies the HIP runtime issues itself); > 0: split over
+  // that many explicitly chosen free engines
   std::vector<int> engines;
-  for (int b = 0; b < 32; ++b)
-    if (d->engines & (1u << b)) engines.push_back(b);
+  if (max_engines > 0)
+    for (int b = 0; b < 32; ++b)
+      if (d->engines & (1u << b)) engines.push_back(b);
   int k = int(engines.size());
-  if (max_engines > 0 && k > max_engines) k = max_engines;
+  if (k > max_engines) k = max_engines;
   // pieces >= 64 MiB: fewer, larger DMA requests per engine
   const uint64_t min_piece = 64ull << 20;
   if (k > 1 && n / uint64_t(k) < min_piece) k = int(std::max<uint64_t>(1, n / min_piece));

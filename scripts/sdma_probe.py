@@ -38,6 +38,8 @@ def blit(n):
 for n in (16 << 20, 256 << 20, N):
     row = {"MiB": n >> 20}
     row["blit_GBps"], row["blit_ok"] = run(blit, n)
+    g, ok = run(lambda m: native.sdma_d2h(0, pb.ptr, src.data_ptr(), m, s), n)
+    row["sdma_auto_GBps"], row["sdma_auto_ok"] = round(g, 1), ok
     for k in sorted({1, 2, 4, n_eng} - {0}):
         if k > n_eng:
             continue
