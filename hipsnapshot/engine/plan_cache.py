@@ -1,0 +1,229 @@
+"""Reuse of a take's plan across takes of the same device-resident state.
+
+A training job snapshots the same tensors every N steps.  Planning them --
+``state_dict`` flattening aside -- is pure CPU work whose result only depends
+on WHICH tensors are saved (address, shape, strides, dtype, device, sharding)
+and on the take's settings: the manifest entries, the write requests with
+their stagers, the slab layout, the compression plan and each entry's JSON
+fragment.  For Llama-3-8B FSDP that is ~5-7 ms per take on one MI355X
+(``prepare_write`` 2 ms, batching 0.7 ms, compression planning 0.6 ms,
+metadata JSON 2 ms; ``profiles/timeline_r2/``), i.e. the bulk of an
+``async_take``'s time-to-unblock and a fixed cost per take that grows in
+relative terms with the number of ranks (each rank plans its own shards).
+
+Only DEVICE-RESIDENT tensor leaves (CUDA tensors, DTensor / ShardedTensor
+with CUDA local shards) are cached.  Primitives, objects and host tensors --
+the RNG state is a fresh host tensor on every call -- are planned on every
+take and batched separately, into slabs with their own name prefix
+(``r<rank>v_...``), so they never collide with the plan's slabs.
+
+Soundness:
+
+* a plan is reused only if every resident leaf has the same signature
+  (data_ptr, shape, strides, dtype, device; DTensor placements + mesh +
+  global shape; ShardedTensor shard boxes) in the same logical order, and
+  the settings key (rank, world size, sync/async, quantize globs,
+  compression, every ``HIPSNAPSHOT_*``/``TORCHSNAPSHOT_*`` variable, the
+  app-state objects) matches;
+* the plan holds the leaves it was built from, so no address it matched can
+  be recycled by the caching allocator while the plan exists -- equal
+  data_ptr means the same memory.  The plan is dropped when any of the
+  app-state objects is garbage collected (``weakref.finalize``), on the next
+  mismatch, or by ``clear()``;
+* a plan is used by one take at a time (``busy`` until its I/O completed --
+  an ``async_take`` still draining owns its stagers); a take that finds the
+  plan busy plans from scratch;
+* stagers are reset before reuse (``TensorBufferStager.reset_for_reuse``:
+  the async HBM freeze re-points them at arena views) and pick up the
+  caller's CURRENT stream as producer.
+
+Replicated state (DDP) is not cached: partitioning its writes is a
+collective, and ranks must not disagree about running it.
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+import weakref
+from typing import Any, Dict, Iterator, List, Optional
+
+import torch
+
+from .. import knobs
+from ..format.manifest import Entry, iter_tensor_entries
+from ..io_types import WriteReq
+
+try:
+    from torch.distributed.tensor import DTensor
+except Exception:  # pragma: no cover
+    DTensor = None  # type: ignore[assignment]
+
+try:
+    from torch.distributed._shard.sharded_tensor import ShardedTensor
+except Exception:  # pragma: no cover
+    ShardedTensor = None  # type: ignore[assignment]
+
+_lock = threading.Lock()
+_plans: Dict[tuple, "TakePlan"] = {}
+stats = {"hits": 0, "misses": 0, "stores": 0}
+
+
+def enabled() -> bool:
+    return knobs.plan_cache_enabled()
+
+
+def _local(obj: Any) -> Optional[torch.Tensor]:
+    if DTensor is not None and isinstance(obj, DTensor):
+        return obj._local_tensor
+    if ShardedTensor is not None and isinstance(obj, ShardedTensor):
+        shards = obj.local_shards()
+        return shards[0].tensor if shards else None
+    return obj if isinstance(obj, torch.Tensor) else None
+
+
+def is_resident(obj: Any) -> bool:
+    """Leaves whose plan can be reused: tensors in device memory (tests
+    monkeypatch this to exercise the cache on the CPU)."""
+    t = _local(obj)
+    return t is not None and t.is_cuda
+
+
+def _tsig(t: torch.Tensor) -> tuple:
+    return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype, t.device)
+
+
+def leaf_sig(obj: Any) -> tuple:
+    if DTensor is not None and isinstance(obj, DTensor):
+        return ("d", _tsig(obj._local_tensor), tuple(obj.placements), id(obj.device_mesh),
+                tuple(obj.shape))
+    if ShardedTensor is not None and isinstance(obj, ShardedTensor):
+        return ("s", tuple((_tsig(s.tensor), tuple(s.metadata.shard_offsets),
+                            tuple(s.metadata.shard_sizes)) for s in obj.local_shards()),
+                tuple(obj.size()))
+    return ("t",) + _tsig(obj)
+
+
+def signatures(resident: Dict[str, Any]) -> tuple:
+    return tuple((k, leaf_sig(v)) for k, v in resident.items())
+
+
+def settings_key(app_state: Dict[str, Any], rank: int, world_size: int, is_async: bool,
+                 quantize, compression: str) -> tuple:
+    env = tuple(sorted((k, v) for k, v in os.environ.items()
+                       if k.startswith(("HIPSNAPSHOT_", "TORCHSNAPSHOT_"))))
+    objs = tuple(sorted((k, id(v)) for k, v in app_state.items()))
+    return (objs, rank, world_size, bool(is_async), tuple(quantize or ()), compression, env)
+
+
+def _tensor_stagers(write_reqs: List[WriteReq]) -> Iterator[Any]:
+    from ..io.batcher import BatchedBufferStager, GPUBatchedBufferStager
+    from ..io.tensor import TensorBufferStager
+
+    for wr in write_reqs:
+        st = wr.buffer_stager
+        if isinstance(st, TensorBufferStager):
+            yield st
+        elif isinstance(st, (GPUBatchedBufferStager, BatchedBufferStager)):
+            for _, m in st.members:
+                yield m
+
+
+class TakePlan:
+    def __init__(self, key: tuple, sigs: tuple, keep: List[Any], entries: Dict[str, Entry],
+                 write_reqs: List[WriteReq]) -> None:
+        self.key = key
+        self.sigs = sigs
+        self.keep = keep          # the leaves: their addresses stay reserved
+        self.entries = entries    # logical path -> final Entry (batched / compressed)
+        self.write_reqs = write_reqs
+        self.json: Dict[str, str] = {}  # logical path -> entry JSON (metadata gather)
+        self.busy = True
+
+    def reset(self) -> None:
+        """Stagers back to their planned state, producer = current stream."""
+        from . import staging
+
+        with staging.plan_scope():
+            for st in _tensor_stagers(self.write_reqs):
+                st.reset_for_reuse()
+
+
+def lookup(key: tuple, sigs: tuple) -> Optional[TakePlan]:
+    with _lock:
+        p = _plans.get(key)
+        if p is None or p.busy or p.sigs != sigs:
+            stats["misses"] += 1
+            return None
+        p.busy = True
+        stats["hits"] += 1
+    p.reset()
+    return p
+
+
+def store(key: tuple, sigs: tuple, resident: Dict[str, Any], object_entries: Dict[str, Entry],
+          write_reqs: List[WriteReq], app_state: Dict[str, Any]) -> Optional[TakePlan]:
+    """Keep the resident part of a fresh plan; returns it marked busy (the
+    caller's take is using it), or None when it cannot be cached."""
+    entries = {k: object_entries[k] for k in resident if k in object_entries}
+    if len(entries) != len(resident):
+        return None
+    ids = {id(te) for e in entries.values() for te in iter_tensor_entries(e)}
+    mine: List[WriteReq] = []
+    covered = set()
+    for wr in write_reqs:
+        sts = list(_tensor_stagers([wr]))
+        if sts and all(id(st.entry) in ids for st in sts):
+            mine.append(wr)
+            covered.update(id(st.entry) for st in sts)
+    if covered != ids:
+        # some resident blob is shared with a per-take leaf (e.g. a slab that
+        # also holds a host tensor): the resident part cannot be replayed alone
+        return None
+    keep = list(resident.values())
+    for v in resident.values():
+        if DTensor is not None and isinstance(v, DTensor):
+            keep.append(v.device_mesh)
+    plan = TakePlan(key, sigs, keep, entries, mine)
+    with _lock:
+        old = _plans.get(key)
+        if old is not None and old.busy:
+            return None  # an async take still drains with it: keep that one
+        _plans[key] = plan
+        stats["stores"] += 1
+    for v in app_state.values():
+        if id(v) in _watched:
+            continue
+        try:
+            weakref.finalize(v, _drop_object, id(v))
+        except TypeError:  # not weak-referenceable: never cached
+            with _lock:
+                if _plans.get(key) is plan:
+                    del _plans[key]
+            return None
+        _watched.add(id(v))
+    return plan
+
+
+_watched: set = set()  # ids of app-state objects with a finalizer
+
+
+def _drop_object(obj_id: int) -> None:
+    """An app-state object was garbage collected: drop every plan keyed on
+    it (their tensors are released with them)."""
+    with _lock:
+        _watched.discard(obj_id)
+        for key in [k for k in _plans if any(i == obj_id for _, i in k[0])]:
+            del _plans[key]
+
+
+def release(plan: Optional[TakePlan]) -> None:
+    if plan is not None:
+        with _lock:
+            plan.busy = False
+
+
+def clear() -> None:
+    """Forget every cached plan (and release the tensors they hold)."""
+    with _lock:
+        _plans.clear()

@@ -180,6 +180,7 @@ class TensorBufferStager(BufferStager):
     def __init__(self, tensor: torch.Tensor, entry: TensorEntry, is_async_snapshot: bool,
                  _tensor_prepare_func: Optional[PrepareFunc] = None) -> None:
         self.tensor = tensor
+        self._plan_tensor = tensor  # what the plan saves (``tensor`` may be re-pointed)
         self.entry = entry
         self.is_async_snapshot = is_async_snapshot
         self._tensor_prepare_func = _tensor_prepare_func
@@ -189,6 +190,15 @@ class TensorBufferStager(BufferStager):
         self.frozen = False
         self.wait_event = None  # torch.cuda.Event guarding a frozen HBM copy
         self.codec: Optional[dict] = None  # HSZ1 info when the blob is compressed
+
+    def reset_for_reuse(self) -> None:
+        """Back to the planned state for a later take (engine/plan_cache.py):
+        undo an async HBM freeze and order after the caller's current stream."""
+        self.tensor = self._plan_tensor
+        self.frozen = False
+        self.wait_event = None
+        self.__dict__.pop("arena_keepalive", None)
+        self.producer = staging.producer_stream_handle(self.tensor)
 
     def _source(self) -> torch.Tensor:
         t = self.tensor

@@ -120,6 +120,12 @@ def get_d2h_engine() -> str:
     return v
 
 
+def plan_cache_enabled() -> bool:
+    """Reuse a take's plan for the next take of the same device-resident
+    tensors (``engine/plan_cache.py``)."""
+    return _get_bool("PLAN_CACHE", True)
+
+
 def get_stage_threads() -> int:
     return _get_int("STAGE_THREADS", 4)
 

@@ -174,11 +174,12 @@ class Snapshot:
         with timeline.span("coalesce"):
             path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
         storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
+        progress: Dict[str, Any] = {}
         try:
             with roctx_range("hipsnapshot.take.plan_and_stage"):
                 pending, metadata = cls._take_impl(path, app_state, rep, keys, comm, storage,
                                                    loop, False, _custom_tensor_prepare_func,
-                                                   quantize, compression)
+                                                   quantize, compression, progress=progress)
             t_staged = time.monotonic()
             with roctx_range("hipsnapshot.take.drain_io"), timeline.span("drain_io"):
                 pending.sync_complete(loop)
@@ -195,6 +196,7 @@ class Snapshot:
                     with timeline.span("committed_barrier", "commit"):
                         comm.barrier()
         finally:
+            _release_plan(progress)
             storage.sync_close(loop)
             loop.close()
         timeline.dump("take", comm.get_rank())
@@ -232,12 +234,13 @@ class Snapshot:
         t0 = time.monotonic()
         path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
         storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
-        progress: Dict[str, bool] = {}
+        progress: Dict[str, Any] = {}
         try:
             pending, metadata = cls._take_impl(path, app_state, rep, keys, comm, storage, loop,
                                                True, _custom_tensor_prepare_func, quantize,
                                                compression, progress=progress)
         except BaseException as e:
+            _release_plan(progress)
             if progress.get("metadata_gathered"):
                 # peers that staged successfully are already in (or about to
                 # start) their commit threads: fail their barrier now instead
@@ -250,7 +253,7 @@ class Snapshot:
         timeline.dump("async_take", comm.get_rank())
         return PendingSnapshot(path=path, pending_io_work=pending, comm=comm, metadata=metadata,
                                storage=storage, event_loop=loop, storage_options=storage_options,
-                               nonce=nonce)
+                               nonce=nonce, plan=progress.get("plan"))
 
     @staticmethod
     def _uncommit(storage: StoragePlugin, loop: asyncio.AbstractEventLoop) -> None:
@@ -269,7 +272,7 @@ class Snapshot:
                    loop: asyncio.AbstractEventLoop, is_async: bool,
                    prepare_func: Optional[PrepareFunc], quantize: Optional[List[str]],
                    compression: Optional[str] = None,
-                   progress: Optional[Dict[str, bool]] = None,
+                   progress: Optional[Dict[str, Any]] = None,
                    ) -> Tuple[PendingIOWork, SnapshotMetadata]:
         if comm.get_rank() == 0:
             with timeline.span("uncommit"):
@@ -301,16 +304,36 @@ class Snapshot:
 
         with timeline.span("replicated_entries"):
             rep_paths = cls._calculate_replicated_entries(flattened, replicated, comm)
-        t_prep = time.perf_counter()
+        from .engine import plan_cache
         from .format.serialization import Serializer
+        from .io.compression import plan_compression, resolve
 
+        comp = resolve(compression)
+        rank = comm.get_rank()
+        # plan reuse (engine/plan_cache.py): device-resident leaves whose plan
+        # from an earlier take still holds are not planned again
+        plan = cache_key = sigs = None
+        resident: Dict[str, Any] = {}
+        if not rep_paths and prepare_func is None and plan_cache.enabled():
+            with timeline.span("plan_lookup"):
+                resident = {k: v for k, v in flattened.items() if plan_cache.is_resident(v)}
+                if resident:
+                    everything = dict(app_state)
+                    if rng_item is not None:
+                        everything[rng_item[0]] = rng_item[1]
+                    cache_key = plan_cache.settings_key(everything, rank, comm.get_world_size(),
+                                                        is_async, quantize, comp)
+                    sigs = plan_cache.signatures(resident)
+                    plan = plan_cache.lookup(cache_key, sigs)
+        to_plan = flattened if plan is None else \
+            {k: v for k, v in flattened.items() if k not in resident}
+        t_prep = time.perf_counter()
         object_entries: Dict[str, Entry] = {}
         path_reqs: Dict[str, List[WriteReq]] = {}
         primitives: Dict[str, PrimitiveEntry] = {}
-        rank = comm.get_rank()
         max_chunk, max_shard = knobs.get_max_chunk_size_bytes(), knobs.get_max_shard_size_bytes()
         with staging.plan_scope():
-            for logical, obj in flattened.items():
+            for logical, obj in to_plan.items():
                 ser = None
                 if quantize and any(fnmatch.fnmatch(logical, p) for p in quantize):
                     ser = Serializer.FP8_BLOCK.value
@@ -327,7 +350,7 @@ class Snapshot:
                 else:
                     object_entries[logical] = entry
                     path_reqs[logical] = wrs
-        timeline.add("prepare_write", "phase", t_prep, time.perf_counter(), n=len(flattened))
+        timeline.add("prepare_write", "phase", t_prep, time.perf_counter(), n=len(to_plan))
         if rep_paths:  # identical on every rank (result of a collective)
             with timeline.span("partition"):
                 object_entries, path_reqs = partition_write_reqs(object_entries, path_reqs,
@@ -335,13 +358,24 @@ class Snapshot:
         write_reqs = [wr for wrs in path_reqs.values() for wr in wrs]
         if not knobs.is_batching_disabled():
             with timeline.span("batch"):
-                _, write_reqs = batch_write_requests(list(object_entries.values()), write_reqs,
-                                                     name_prefix=f"r{rank}")
-        from .io.compression import plan_compression, resolve
-
-        if resolve(compression) == "hsz1":
+                # with a reused plan, this take's own slabs get their own
+                # prefix: they can never collide with the plan's slabs
+                _, write_reqs = batch_write_requests(
+                    list(object_entries.values()), write_reqs,
+                    name_prefix=f"r{rank}" if plan is None else f"r{rank}v")
+        if comp == "hsz1":
             with timeline.span("plan_compression"):
                 plan_compression(write_reqs)
+        if plan is not None:
+            object_entries = {k: plan.entries[k] if k in plan.entries else object_entries[k]
+                              for k in flattened
+                              if k in plan.entries or k in object_entries}
+            write_reqs = plan.write_reqs + write_reqs
+        elif cache_key is not None:
+            plan = plan_cache.store(cache_key, sigs, resident, object_entries, write_reqs,
+                                    everything)
+        if progress is not None:
+            progress["plan"] = plan
         manifest.update(primitives)
         manifest.update(object_entries)
         metadata = None
@@ -351,7 +385,7 @@ class Snapshot:
             # through the commit barrier (``_report_async_failure``), so its
             # peers' commit threads fail at once instead of timing out
             with timeline.span("gather_manifest"):
-                metadata = cls._gather_metadata(manifest, comm)
+                metadata = cls._gather_metadata(manifest, comm, plan)
             if progress is not None:
                 progress["metadata_gathered"] = True
 
@@ -364,18 +398,29 @@ class Snapshot:
                 freeze_device_state(write_reqs)
             deferred = [wr for wr in write_reqs if is_deferrable(wr)]
             write_reqs = [wr for wr in write_reqs if not is_deferrable(wr)]
-        with timeline.span("stage", n=len(write_reqs)):
-            pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop)
+        # largest first: the writes still running after the last D2H -- the
+        # take's tail -- are then the small ones (slabs), not a 100 MB chunk
+        write_reqs.sort(key=lambda wr: wr.buffer_stager.get_staging_cost_bytes(), reverse=True)
+        gather = None
+        if metadata is None:
+            # sync take: entries are final since planning, so the metadata
+            # gather (JSON encoding + one collective) runs on a helper thread
+            # while the main thread stages: it leaves the path to the first
+            # D2H and the post-staging tail alike
+            gather = _BackgroundGather(cls._gather_metadata, manifest, comm, plan)
+        try:
+            with timeline.span("stage", n=len(write_reqs)):
+                pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop)
+        except BaseException:
+            if gather is not None:
+                gather.join_quietly()  # the staging error is the one to report
+            raise
+        if gather is not None:
+            metadata = gather.result()
         if deferred:
             from .engine.scheduler import DeferredIOWork
 
             pending = DeferredIOWork(pending, deferred, storage, budget, rank)
-        if metadata is None:
-            # sync take: entries are final since planning; gathering them only
-            # now takes the metadata collective off the path to the first D2H
-            # and overlaps it with the writes still draining in the I/O engine
-            with timeline.span("gather_manifest"):
-                metadata = cls._gather_metadata(manifest, comm)
         return pending, metadata
 
     # --------------------------------------------------------------- restore
@@ -583,14 +628,29 @@ class Snapshot:
         return set.intersection(*[set(g) for g in gathered])
 
     @staticmethod
-    def _gather_metadata(manifest: Dict[str, Entry], comm: Comm) -> SnapshotMetadata:
+    def _gather_metadata(manifest: Dict[str, Entry], comm: Comm,
+                         plan=None) -> SnapshotMetadata:
         """ONE all-gather of (replicated entries, pre-encoded JSON fragments of
         every other entry).  Each rank JSON-encodes its own entries in
         parallel; the committing rank only consolidates the replicated ones
         and joins strings (reference: all-gather of entry objects, then rank 0
-        encodes the whole manifest, `snapshot.py:842-853`)."""
+        encodes the whole manifest, `snapshot.py:842-853`).  Entries of a
+        reused take plan keep the JSON encoded by the first take."""
         rep = {k: e for k, e in manifest.items() if is_replicated(e)}
-        frags = [(k, entry_json(e)) for k, e in manifest.items() if k not in rep]
+        if plan is None:
+            frags = [(k, entry_json(e)) for k, e in manifest.items() if k not in rep]
+        else:
+            cached, planned = plan.json, plan.entries
+            frags = []
+            for k, e in manifest.items():
+                if k in rep:
+                    continue
+                js = cached.get(k)
+                if js is None:
+                    js = entry_json(e)
+                    if k in planned:
+                        cached[k] = js
+                frags.append((k, js))
         ws = comm.get_world_size()
         gathered: List[Any] = [None] * ws
         comm.all_gather_object(gathered, (rep, frags))
@@ -658,6 +718,47 @@ def flat_prefix(key: str) -> str:
     return encode_key(key)
 
 
+def _release_plan(progress: Dict[str, Any]) -> None:
+    """The take that used a cached plan is over (its I/O completed or it
+    failed): the plan may serve the next take."""
+    from .engine import plan_cache
+
+    plan_cache.release(progress.pop("plan", None))
+
+
+class _BackgroundGather:
+    """Runs ``fn(manifest, comm)`` (the metadata gather) on a helper thread.
+    Every rank starts it at the same point of the take, so its collective
+    pairs up across ranks whatever the main threads do meanwhile; the helper
+    adopts the caller's HIP device (current device is per thread and RCCL
+    object collectives stage their bytes on it)."""
+
+    def __init__(self, fn, manifest, comm: Comm, plan) -> None:
+        self._out: Dict[str, Any] = {}
+        dev = torch.cuda.current_device() if torch.cuda.is_initialized() else None
+
+        def run() -> None:
+            try:
+                if dev is not None:
+                    torch.cuda.set_device(dev)
+                with timeline.span("gather_manifest"):
+                    self._out["v"] = fn(manifest, comm, plan)
+            except BaseException as e:  # noqa: BLE001 - re-raised in result()
+                self._out["e"] = e
+
+        self._th = threading.Thread(target=run, name="hipsnapshot-manifest", daemon=True)
+        self._th.start()
+
+    def join_quietly(self) -> None:
+        self._th.join()
+
+    def result(self):
+        self._th.join()
+        if "e" in self._out:
+            raise self._out["e"]
+        return self._out["v"]
+
+
 def _commit_barrier(store, path: str, nonce: str, rank: int, world_size: int) -> LinearBarrier:
     return LinearBarrier(prefix=f"hipsnapshot_{nonce}_{path}", store=store, rank=rank,
                          world_size=world_size, leader_rank=0)
@@ -691,7 +792,8 @@ class PendingSnapshot:
     def __init__(self, path: str, pending_io_work: PendingIOWork, comm: Comm,
                  metadata: SnapshotMetadata, storage: StoragePlugin,
                  event_loop: asyncio.AbstractEventLoop,
-                 storage_options: Optional[Dict[str, Any]] = None, nonce: str = "") -> None:
+                 storage_options: Optional[Dict[str, Any]] = None, nonce: str = "",
+                 plan=None) -> None:
         self.path = path
         self.pg = comm.pg
         self.exc_info = None
@@ -703,13 +805,13 @@ class PendingSnapshot:
             target=self._complete_snapshot, name="hipsnapshot-commit",
             kwargs=dict(path=path, rank=comm.get_rank(), world_size=comm.get_world_size(),
                         pending_io_work=pending_io_work, metadata=metadata, storage=storage,
-                        event_loop=event_loop, store=store, nonce=nonce))
+                        event_loop=event_loop, store=store, nonce=nonce, plan=plan))
         self.thread.start()
 
     def _complete_snapshot(self, path: str, rank: int, world_size: int,
                            pending_io_work: PendingIOWork, metadata: SnapshotMetadata,
                            storage: StoragePlugin, event_loop: asyncio.AbstractEventLoop,
-                           store, nonce: str) -> None:
+                           store, nonce: str, plan=None) -> None:
         # WARNING: no collectives in this thread
         barrier = None
         if store is not None:
@@ -732,6 +834,7 @@ class PendingSnapshot:
             self.exc_info = sys.exc_info()
             logger.warning(f"Encountered exception while taking snapshot asynchronously:\n{e}")
         finally:
+            _release_plan({"plan": plan})  # its stagers are idle again
             try:
                 storage.sync_close(event_loop)
             finally:

@@ -775,3 +775,46 @@ def test_snapshot_with_sdma_d2h(gpu, tmp_path, compression):
         Snapshot(str(tmp_path / p)).restore({"sd": out})
         torch.cuda.synchronize()
         assert_state_dict_eq({k: out[k] for k in ref}, ref)
+
+
+# ---- take-plan reuse on device-resident state (engine/plan_cache.py) ---------
+
+def test_plan_reuse_gpu_sync_and_async(gpu, tmp_path):
+    from hipsnapshot.engine import plan_cache
+
+    plan_cache.clear()
+    h0 = plan_cache.stats["hits"]
+    sd = _compressible_state(gpu)
+    sd["host"] = torch.randn(3000)           # per-take host leaf next to cached ones
+    refs = []
+    for i, mode in enumerate(["sync", "sync", "async", "async", "sync"]):
+        for k, v in sd.items():
+            if isinstance(v, torch.Tensor):
+                v.add_(1)
+            elif isinstance(v, list):
+                for x in v:
+                    x.add_(1)
+        sd["step"] = i
+        refs.append(_clone_state(sd))
+        path = str(tmp_path / f"p{i}")
+        if mode == "sync":
+            Snapshot.take(path, {"sd": sd}, compression="hsz1")
+        else:
+            p = Snapshot.async_take(path, {"sd": sd}, compression="hsz1")
+            for k, v in sd.items():  # after unblock: must not leak
+                if isinstance(v, torch.Tensor):
+                    v.mul_(-3)
+            p.wait()
+            for k, v in refs[-1].items():
+                if isinstance(v, torch.Tensor):
+                    sd[k].copy_(v)
+    # sync plan reused by takes 1 and 4, async plan by take 3
+    assert plan_cache.stats["hits"] - h0 == 3
+    for i, ref in enumerate(refs):
+        out = StateDict(**{k: (torch.zeros_like(v) if isinstance(v, torch.Tensor) else
+                               [torch.zeros_like(x) for x in v] if isinstance(v, list) else v)
+                           for k, v in ref.items()})
+        Snapshot(str(tmp_path / f"p{i}")).restore({"sd": out})
+        torch.cuda.synchronize()
+        assert_state_dict_eq({k: out[k] for k in ref}, ref)
+    plan_cache.clear()
