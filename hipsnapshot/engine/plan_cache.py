@@ -108,6 +108,24 @@ def signatures(resident: Dict[str, Any]) -> tuple:
     return tuple((k, leaf_sig(v)) for k, v in resident.items())
 
 
+def fast_signatures(resident: Dict[str, Any]) -> Optional[tuple]:
+    """Identity-based signatures: the leaf OBJECT (plans keep theirs alive,
+    so ids cannot be recycled) plus what can change under a live object --
+    the local tensor's address / shape / strides and the DTensor spec
+    object.  ~1 us per leaf instead of ~4 us for ``signatures``; None when a
+    leaf needs the full comparison (ShardedTensor)."""
+    out = []
+    for k, v in resident.items():
+        lt = getattr(v, "_local_tensor", None)
+        if lt is not None:
+            out.append((id(v), lt.data_ptr(), lt.shape, lt.stride(), id(v._spec)))
+        elif ShardedTensor is not None and isinstance(v, ShardedTensor):
+            return None
+        else:
+            out.append((id(v), v.data_ptr(), v.shape, v.stride()))
+    return tuple(out)
+
+
 def settings_key(app_state: Dict[str, Any], rank: int, world_size: int, is_async: bool,
                  quantize, compression: str) -> tuple:
     env = tuple(sorted((k, v) for k, v in os.environ.items()
@@ -131,9 +149,10 @@ def _tensor_stagers(write_reqs: List[WriteReq]) -> Iterator[Any]:
 
 class TakePlan:
     def __init__(self, key: tuple, sigs: tuple, keep: List[Any], entries: Dict[str, Entry],
-                 write_reqs: List[WriteReq]) -> None:
+                 write_reqs: List[WriteReq], fast: Optional[tuple] = None) -> None:
         self.key = key
         self.sigs = sigs
+        self.fast = fast
         self.keep = keep          # the leaves: their addresses stay reserved
         self.entries = entries    # logical path -> final Entry (batched / compressed)
         self.write_reqs = write_reqs
@@ -149,10 +168,23 @@ class TakePlan:
                 st.reset_for_reuse()
 
 
-def lookup(key: tuple, sigs: tuple) -> Optional[TakePlan]:
+def lookup(key: tuple, resident: Dict[str, Any]) -> Optional[TakePlan]:
+    """The cached plan for ``key`` if every resident leaf still matches it
+    (marked busy for the caller's take), else None."""
     with _lock:
         p = _plans.get(key)
-        if p is None or p.busy or p.sigs != sigs:
+        if p is None or p.busy:
+            stats["misses"] += 1
+            return None
+    fast = fast_signatures(resident)
+    if fast is None or fast != p.fast:
+        # new leaf objects (e.g. views a state_dict creates on every call):
+        # compare what they point at
+        if signatures(resident) != p.sigs:
+            stats["misses"] += 1
+            return None
+    with _lock:
+        if p.busy or _plans.get(key) is not p:
             stats["misses"] += 1
             return None
         p.busy = True
@@ -161,10 +193,12 @@ def lookup(key: tuple, sigs: tuple) -> Optional[TakePlan]:
     return p
 
 
-def store(key: tuple, sigs: tuple, resident: Dict[str, Any], object_entries: Dict[str, Entry],
+def store(key: tuple, resident: Dict[str, Any], object_entries: Dict[str, Entry],
           write_reqs: List[WriteReq], app_state: Dict[str, Any]) -> Optional[TakePlan]:
     """Keep the resident part of a fresh plan; returns it marked busy (the
     caller's take is using it), or None when it cannot be cached."""
+    sigs = signatures(resident)
+    fast = fast_signatures(resident)
     entries = {k: object_entries[k] for k in resident if k in object_entries}
     if len(entries) != len(resident):
         return None
@@ -184,7 +218,7 @@ def store(key: tuple, sigs: tuple, resident: Dict[str, Any], object_entries: Dic
     for v in resident.values():
         if DTensor is not None and isinstance(v, DTensor):
             keep.append(v.device_mesh)
-    plan = TakePlan(key, sigs, keep, entries, mine)
+    plan = TakePlan(key, sigs, keep, entries, mine, fast)
     with _lock:
         old = _plans.get(key)
         if old is not None and old.busy:

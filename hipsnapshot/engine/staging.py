@@ -117,8 +117,18 @@ def bulk_d2h(dev: int, slot: int, dst: int, src: int, nbytes: int,
     if nbytes and _use_sdma(dev):
         if producer is not None:
             native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
-        native.sdma_d2h(dev, dst, src, nbytes, native.copy_stream(dev, slot))
-        return
+            producer = None  # the copy stream is ordered after it now
+        try:
+            native.sdma_d2h(dev, dst, src, nbytes, native.copy_stream(dev, slot))
+            return
+        except native.HipError as e:
+            # nothing is left in flight after a failed SDMA copy (every issued
+            # piece was waited for): redo it as a blit, and stop using SDMA
+            import logging
+
+            logging.getLogger(__name__).warning(
+                f"SDMA device->host copy failed on cuda:{dev} ({e}); using hipMemcpyAsync")
+            _sdma_ok[dev] = False
     native.memcpy(dev, slot, dst, src, nbytes, native.D2H, producer, sync=True)
 
 

@@ -312,7 +312,7 @@ class Snapshot:
         rank = comm.get_rank()
         # plan reuse (engine/plan_cache.py): device-resident leaves whose plan
         # from an earlier take still holds are not planned again
-        plan = cache_key = sigs = None
+        plan = cache_key = None
         resident: Dict[str, Any] = {}
         if not rep_paths and prepare_func is None and plan_cache.enabled():
             with timeline.span("plan_lookup"):
@@ -323,8 +323,7 @@ class Snapshot:
                         everything[rng_item[0]] = rng_item[1]
                     cache_key = plan_cache.settings_key(everything, rank, comm.get_world_size(),
                                                         is_async, quantize, comp)
-                    sigs = plan_cache.signatures(resident)
-                    plan = plan_cache.lookup(cache_key, sigs)
+                    plan = plan_cache.lookup(cache_key, resident)
         to_plan = flattened if plan is None else \
             {k: v for k, v in flattened.items() if k not in resident}
         t_prep = time.perf_counter()
@@ -372,8 +371,7 @@ class Snapshot:
                               if k in plan.entries or k in object_entries}
             write_reqs = plan.write_reqs + write_reqs
         elif cache_key is not None:
-            plan = plan_cache.store(cache_key, sigs, resident, object_entries, write_reqs,
-                                    everything)
+            plan = plan_cache.store(cache_key, resident, object_entries, write_reqs, everything)
         if progress is not None:
             progress["plan"] = plan
         manifest.update(primitives)

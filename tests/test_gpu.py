@@ -818,3 +818,22 @@ def test_plan_reuse_gpu_sync_and_async(gpu, tmp_path):
         torch.cuda.synchronize()
         assert_state_dict_eq({k: out[k] for k in ref}, ref)
     plan_cache.clear()
+
+
+def test_sdma_failure_falls_back_to_blit(gpu, tmp_path, monkeypatch):
+    from hipsnapshot.engine import staging
+
+    def broken(*a, **k):
+        raise native.HipError("injected SDMA failure")
+
+    monkeypatch.setattr(native, "sdma_d2h", broken)
+    monkeypatch.setattr(staging, "_sdma_ok", {0: True})
+    sd = StateDict(w=torch.randn(3000, 1000, device=gpu), b=torch.randn(77, device=gpu))
+    ref = {k: v.clone() for k, v in sd.items()}
+    with override_knob("D2H_ENGINE", "sdma"):
+        Snapshot.take(str(tmp_path / "s"), {"sd": sd})
+    assert staging._sdma_ok[0] is False
+    out = StateDict(w=torch.zeros_like(ref["w"]), b=torch.zeros_like(ref["b"]))
+    Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    torch.cuda.synchronize()
+    assert torch.equal(out["w"], ref["w"]) and torch.equal(out["b"], ref["b"])

@@ -177,3 +177,35 @@ def test_plan_dropped_when_state_is_collected(tmp_path, resident):
     del sd
     gc.collect()
     assert len(plan_cache._plans) == 0
+
+
+def test_new_view_objects_each_take_still_reuse(tmp_path, resident, monkeypatch):
+    """A state_dict that returns fresh views of the same memory on every call
+    misses the identity fast path but matches the full signatures."""
+    monkeypatch.setattr(plan_cache, "is_resident",
+                        lambda obj: isinstance(obj, torch.Tensor) and obj.numel() >= 1000)
+
+    class Holder:
+        def __init__(self):
+            self.w = torch.randn(4000)
+            self.b = torch.randn(2000, 3)
+
+        def state_dict(self):
+            return {"w": self.w.detach(), "b": self.b[:, :]}
+
+        def load_state_dict(self, sd):
+            self.w.copy_(sd["w"])
+            self.b.copy_(sd["b"])
+
+    h = Holder()
+    refs = []
+    for i in range(3):
+        h.w.add_(1)
+        h.b.mul_(2)
+        Snapshot.take(str(tmp_path / f"v{i}"), {"h": h})
+        refs.append((h.w.clone(), h.b.clone()))
+    assert plan_cache.stats["hits"] == 2
+    for i, (w, b) in enumerate(refs):
+        out = Holder()
+        Snapshot(str(tmp_path / f"v{i}")).restore({"h": out})
+        assert torch.equal(out.w, w) and torch.equal(out.b, b)
