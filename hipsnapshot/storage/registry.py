@@ -15,6 +15,13 @@ import asyncio
 from typing import Any, Callable, Dict, Optional
 
 from ..io_types import StoragePlugin
+from . import fs as _fs
+from .fs import FSStoragePlugin
+
+# the reference's tests swap the FS plugin with
+# mock.patch("torchsnapshot.storage_plugin.FSStoragePlugin", ...); ours patch
+# hipsnapshot.storage.fs.FSStoragePlugin -- either replacement is honoured
+_FS_PLUGIN = FSStoragePlugin
 
 Factory = Callable[[str, Optional[Dict[str, Any]]], StoragePlugin]
 _REGISTRY: Dict[str, Factory] = {}
@@ -26,9 +33,8 @@ def register_storage_plugin(protocol: str, factory: Factory) -> None:
 
 def _builtin(protocol: str, path: str, storage_options) -> Optional[StoragePlugin]:
     if protocol == "fs":
-        from .fs import FSStoragePlugin
-
-        return FSStoragePlugin(root=path, storage_options=storage_options)
+        cls = FSStoragePlugin if FSStoragePlugin is not _FS_PLUGIN else _fs.FSStoragePlugin
+        return cls(root=path, storage_options=storage_options)
     if protocol == "s3":
         from .s3 import S3StoragePlugin
 
