@@ -63,6 +63,8 @@ def main() -> None:
     ap.add_argument("--path", default=None)
     ap.add_argument("--async-iters", type=int, default=3)
     ap.add_argument("--no-restore-check", action="store_true")
+    ap.add_argument("--restore-iters", type=int, default=1,
+                    help="restores to time (median reported); each is checked bitwise")
     ap.add_argument("--fsync", action="store_true")
     ap.add_argument("--direct-io", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
@@ -189,17 +191,21 @@ def main() -> None:
         # bitwise restore check of EVERY local shard (HBM holds the copies)
         named = list(model.named_parameters())
         refs = [p._local_tensor.clone() for _, p in named]
-        for _, p in named:
-            p._local_tensor.zero_()
-        barrier_sync()
-        tr = time.perf_counter()
-        Snapshot(path).restore(app_state)
-        barrier_sync()
-        restore_s = time.perf_counter() - tr
-        # compare against the parameters as they are NOW (load_state_dict may
-        # re-point a module's parameter)
-        bad = [(n, r, p._local_tensor) for (n, p), r in zip(named, refs)
-               if not torch.equal(r, p._local_tensor)]
+        times, bad = [], []
+        for _ in range(max(1, args.restore_iters)):
+            for _, p in named:
+                p._local_tensor.zero_()
+            barrier_sync()
+            tr = time.perf_counter()
+            Snapshot(path).restore(app_state)
+            barrier_sync()
+            times.append(time.perf_counter() - tr)
+            # compare against the parameters as they are NOW (load_state_dict
+            # may re-point a module's parameter)
+            named = list(model.named_parameters())
+            bad += [(n, r, p._local_tensor) for (n, p), r in zip(named, refs)
+                    if not torch.equal(r, p._local_tensor)]
+        restore_s = statistics.median(times)
         for n, r, cur in bad[:5]:
             nz = int((cur != 0).sum().item())
             print(f"rank {rank}: restore mismatch in {n}: shape {tuple(cur.shape)}, "

@@ -364,27 +364,48 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
         from ..io_types import CompressedSpan
 
         info = rr.codec
-        nf = hsz.n_frames_for(int(info["blob_bytes"]), int(info["frame_bytes"]))
+        logical = int(info["blob_bytes"])
+        nf = hsz.n_frames_for(logical, int(info["frame_bytes"]))
         dest = None
         try:
             async with io_sem:
                 if failing:
                     return
                 t_r = time.perf_counter()
-                head_io = ReadIO(path=rr.path, byte_range=(0, hsz.payload_start(nf)))
-                await storage.read(head_io)
-                header = hsz.parse_header(head_io.data())
-                lo, hi = rr.byte_range if rr.byte_range is not None else (0, header.logical_size)
-                first, last = header.frames_covering(lo, hi)
-                c_lo, c_hi = header.offsets[first], header.offsets[last]
-                hsz.validate_offsets(header, header.offsets[-1])
-                dest = await asyncio.get_running_loop().run_in_executor(
-                    None, rr.buffer_consumer.get_compressed_read_dest, c_hi - c_lo)
-                if dest is None:
-                    dest = as_staged(bytearray(max(c_hi - c_lo, 1)))
-                body_io = ReadIO(path=rr.path, byte_range=(c_lo, c_hi), dest=dest)
-                if c_hi > c_lo:
-                    await storage.read(body_io)
+                whole = rr.byte_range is None or tuple(rr.byte_range) == (0, logical)
+                stored = await storage.size(rr.path) if whole else None
+                if stored is not None:
+                    # whole blob: ONE read of header + frames (no header round
+                    # trip; the read enters the engine queue in request order)
+                    full = await asyncio.get_running_loop().run_in_executor(
+                        None, rr.buffer_consumer.get_compressed_read_dest, stored)
+                    if full is None:
+                        full = as_staged(bytearray(max(stored, 1)))
+                    dest = full
+                    await storage.read(ReadIO(path=rr.path, byte_range=(0, stored), dest=full))
+                    header = hsz.parse_header(full.view[:hsz.payload_start(nf)])
+                    hsz.validate_offsets(header, stored)
+                    lo, hi = 0, header.logical_size
+                    first, last = 0, header.n_frames
+                    c_lo, c_hi = header.offsets[0], header.offsets[-1]
+                    dest = StagedBuffer(full.view[c_lo:c_hi], full.addr + c_lo,
+                                        release=full.release, keepalive=full)
+                else:
+                    head_io = ReadIO(path=rr.path, byte_range=(0, hsz.payload_start(nf)))
+                    await storage.read(head_io)
+                    header = hsz.parse_header(head_io.data())
+                    lo, hi = rr.byte_range if rr.byte_range is not None \
+                        else (0, header.logical_size)
+                    first, last = header.frames_covering(lo, hi)
+                    c_lo, c_hi = header.offsets[first], header.offsets[last]
+                    hsz.validate_offsets(header, header.offsets[-1])
+                    dest = await asyncio.get_running_loop().run_in_executor(
+                        None, rr.buffer_consumer.get_compressed_read_dest, c_hi - c_lo)
+                    if dest is None:
+                        dest = as_staged(bytearray(max(c_hi - c_lo, 1)))
+                    body_io = ReadIO(path=rr.path, byte_range=(c_lo, c_hi), dest=dest)
+                    if c_hi > c_lo:
+                        await storage.read(body_io)
                 t_c = time.perf_counter()
         except BaseException:
             if dest is not None:
@@ -463,6 +484,21 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
     logger.debug(f"Rank {rank} read {stats.bytes_written / 1e9:.3f} GB in "
                  f"{stats.t_done - stats.t_start:.3f}s")
     return stats
+
+
+def order_reads_for_pipeline(read_reqs: List[ReadReq], lead_min_bytes: int = 1 << 20
+                             ) -> List[ReadReq]:
+    """With ``HIPSNAPSHOT_READ_ORDER=pipeline``: largest reads first, led by
+    the smallest read of at least ``lead_min_bytes`` (the first H2D starts
+    5 ms earlier).  Off by default: the whole restore measured 4-8 % slower
+    than manifest order (knobs.get_read_order)."""
+    if len(read_reqs) < 3 or knobs.get_read_order() == "plan":
+        return list(read_reqs)
+    sized = [(rr.buffer_consumer.get_consuming_cost_bytes(), i, rr)
+             for i, rr in enumerate(read_reqs)]
+    lead = min((t for t in sized if t[0] >= lead_min_bytes), default=None)
+    rest = sorted((t for t in sized if t is not lead), key=lambda t: (-t[0], t[1]))
+    return ([lead[2]] if lead is not None else []) + [t[2] for t in rest]
 
 
 def sync_execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,

@@ -204,6 +204,11 @@ class StoragePlugin(ABC):
     async def delete_dir(self, path: str) -> None:
         raise NotImplementedError(f"{type(self).__name__} does not implement delete_dir")
 
+    async def size(self, path: str) -> Optional[int]:
+        """Stored size of a blob, or None when the backend cannot tell
+        cheaply (then compressed blobs are read header-first)."""
+        return None
+
     @abstractmethod
     async def close(self) -> None:
         ...

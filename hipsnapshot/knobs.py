@@ -120,6 +120,14 @@ def get_d2h_engine() -> str:
     return v
 
 
+def get_read_order() -> str:
+    """Restore read order: ``plan`` (manifest order, default) or ``pipeline``
+    (a small lead read, then largest first).  Measured A/B on one MI355X,
+    Llama-3-8B restore, median of 5: plan 70.7 / 72.8 GB/s, pipeline 65.1 /
+    68.2 GB/s (profiles/timeline_r2/read_order.txt)."""
+    return str(_get("READ_ORDER") or "plan")
+
+
 def plan_cache_enabled() -> bool:
     """Reuse a take's plan for the next take of the same device-resident
     tensors (``engine/plan_cache.py``)."""

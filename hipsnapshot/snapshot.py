@@ -47,6 +47,7 @@ from .engine import staging
 from .engine.scheduler import (
     PendingIOWork,
     get_process_memory_budget_bytes,
+    order_reads_for_pipeline,
     _budget_cache,
     sync_execute_read_reqs,
     sync_execute_write_reqs,
@@ -479,6 +480,7 @@ class Snapshot:
             flat.pop(logical, None)
         if not knobs.is_batching_disabled():
             reads = batch_read_requests(reads)
+        reads = order_reads_for_pipeline(reads)
         budget = get_process_memory_budget_bytes(comm)
         with timeline.span("read_pipeline", n=len(reads)):
             sync_execute_read_reqs(reads, storage, budget, comm.get_rank(), loop)

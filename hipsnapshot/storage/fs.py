@@ -142,6 +142,9 @@ class FSStoragePlugin(StoragePlugin):
         read_io.buf = dest_view
         self.bytes_read += n
 
+    async def size(self, path: str) -> Optional[int]:
+        return os.path.getsize(self._abs(path))
+
     async def commit_metadata(self, path: str, buf: bytes) -> None:
         """Atomic commit: write a temp file then rename it into place."""
         final = self._abs(path)

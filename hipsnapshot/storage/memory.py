@@ -49,6 +49,11 @@ class MemoryStoragePlugin(StoragePlugin):
         else:
             read_io.buf = memoryview(data)
 
+    async def size(self, path: str) -> Optional[int]:
+        with _LOCK:
+            data = _STORE.get(self._key(path))
+        return None if data is None else len(data)
+
     async def delete(self, path: str) -> None:
         with _LOCK:
             _STORE.pop(self._key(path), None)
