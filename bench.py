@@ -14,10 +14,11 @@ time-to-unblock (max over ranks, median over the iterations) is reported in
 every local shard is zeroed, restored, and compared bitwise to a copy.
 
 Blobs are written with the lossless HSZ1 codec by default (``--compression``):
-the GPU codes each bf16's sign+exponent byte as a 4-bit dictionary index
-before the D2H, so ~75 % of the bytes cross PCIe and hit storage.  ``value``
-is always LOGICAL model bytes / step time; ``stored_bytes`` reports what was
-written.  ``--compression none`` writes raw, reference-format blobs.
+the GPU Huffman-codes each bf16's sign+exponent byte before the D2H, so ~67 %
+of the bytes cross PCIe and hit storage.  ``value`` is always LOGICAL model
+bytes / step time; ``stored_bytes`` reports what was written.  The same save
+with raw, reference-format blobs is timed afterwards (``--raw-steps``) and
+reported as ``raw_GBps``; ``--compression none`` makes raw blobs the headline.
 
 Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
@@ -63,7 +64,10 @@ def main() -> None:
     ap.add_argument("--path", default=None)
     ap.add_argument("--async-iters", type=int, default=3)
     ap.add_argument("--no-restore-check", action="store_true")
-    ap.add_argument("--restore-iters", type=int, default=1,
+    ap.add_argument("--raw-steps", type=int, default=3,
+                    help="after the headline, also time this many takes with raw "
+                         "(reference-format, uncompressed) blobs -> raw_GBps (0 = skip)")
+    ap.add_argument("--restore-iters", type=int, default=3,
                     help="restores to time (median reported); each is checked bitwise")
     ap.add_argument("--fsync", action="store_true")
     ap.add_argument("--direct-io", action="store_true")
@@ -187,6 +191,7 @@ def main() -> None:
 
     restore_ok = None
     restore_gbps = None
+    restore_each = None
     if not args.no_restore_check:
         # bitwise restore check of EVERY local shard (HBM holds the copies)
         named = list(model.named_parameters())
@@ -216,7 +221,28 @@ def main() -> None:
         restore_ok = bool(ok.item())
         restore_gbps = total_bytes / restore_s / 1e9
         del refs
-        log(f"restore: {restore_s:.3f}s ({restore_gbps:.2f} GB/s) ok={restore_ok}")
+        restore_each = [round(total_bytes / t / 1e9, 2) for t in times]
+        log(f"restore: {restore_s:.3f}s ({restore_gbps:.2f} GB/s) ok={restore_ok} "
+            f"each {restore_each} GB/s")
+
+    # the same save with raw, reference-format blobs (no HSZ1): what the
+    # headline would be without the codec, measured in the same process
+    raw_gbps = None
+    if args.raw_steps > 0 and args.compression != "none":
+        if rank == 0:
+            shutil.rmtree(path + "_async", ignore_errors=True)
+        dist.barrier()
+        raw_path = path + "_raw"
+        Snapshot.take(raw_path, app_state, storage_options=opts, compression="none")
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(args.raw_steps):
+            Snapshot.take(raw_path, app_state, storage_options=opts, compression="none")
+        barrier_sync()
+        e = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        raw_gbps = total_bytes / (float(e.item()) / args.raw_steps) / 1e9
+        log(f"raw (uncompressed) save: {raw_gbps:.2f} GB/s")
 
     base = BASELINE_GBPS.get(world)
     if rank == 0:
@@ -246,8 +272,12 @@ def main() -> None:
             "async_total_ms": round(statistics.median(drain), 2) if drain else None,
             "restore_bitwise_ok": restore_ok,
             "restore_GBps": round(restore_gbps, 2) if restore_gbps else None,
+            "restore_GBps_each": restore_each,
             "compression": args.compression,
             "stored_bytes": stored,
+            "raw_GBps": round(raw_gbps, 3) if raw_gbps else None,
+            "raw_note": "same save with uncompressed reference-format blobs "
+                        f"({args.raw_steps} timed takes after 1 warmup)",
             "baseline_note": "reference DDP 20GB save, p4d: 1 GPU 1.44 GB/s, 8 GPU 5.92 GB/s; "
                              "no published number for 2/4 GPUs",
         }
