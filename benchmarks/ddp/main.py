@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
     ap.add_argument("--torch-save", action="store_true")
     ap.add_argument("--repeats", type=int, default=2)
+    ap.add_argument("--compression", default="none", choices=["none", "hsz1"],
+                    help="none = reference-format blobs (the published comparison)")
     ap.add_argument("--model", default="many_params", choices=["many_params", "llama3_8b"],
                     help="llama3_8b = BASELINE config 2 (Llama-3-8B DDP bf16, partitioned save)")
     args = ap.parse_args()
@@ -56,13 +58,16 @@ def main():
     for i in range(args.repeats):
         sync(dev)
         with Timer() as t:
-            Snapshot.take(os.path.join(root, "snap"), {"model": model}, replicated=["**"])
+            Snapshot.take(os.path.join(root, "snap"), {"model": model}, replicated=["**"],
+                          compression=args.compression)
             sync(dev)
         s = max_over_ranks(t.s, dev)
         log(f"hipsnapshot take {i}: {s:.2f}s ({nbytes / s / 1e9:.2f} GB/s)")
         best = s if best is None else min(best, s)
     ref = {1: 13.91, 8: 3.38}.get(ws) if args.model == "many_params" else None
-    out = {"bench": "ddp_20gb_save" if args.model == "many_params" else "llama3_8b_ddp_save", "world_size": ws, "bytes": nbytes, "seconds": round(best, 3),
+    out = {"bench": "ddp_20gb_save" if args.model == "many_params" else "llama3_8b_ddp_save",
+           "world_size": ws, "compression": args.compression, "bytes": nbytes,
+           "seconds": round(best, 3),
            "GBps": round(nbytes / best / 1e9, 3),
            "reference_seconds": ref, "speedup_vs_reference": round(ref / best, 2) if ref else None}
     if args.torch_save and rank == 0:

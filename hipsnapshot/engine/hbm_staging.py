@@ -13,8 +13,9 @@ copy bandwidth, so instead:
    freshly allocated HBM arena (stream order makes the copy consistent with
    everything the trainer already enqueued and everything it enqueues later,
    without any host synchronisation);
-3. the stagers are re-pointed at arena views and wait on an event recorded
-   after the launch; the background commit thread drains the arena to storage.
+3. the stagers are re-pointed at the arena (``frozen_at``; the views are
+   built lazily by the drain) and wait on an event recorded after the launch;
+   the background commit thread drains the arena to storage.
 
 When the whole state does not fit in free HBM minus
 ``HBM_STAGING_RESERVE_BYTES`` (or ``HBM_STAGING_MAX_BYTES``), write requests are
@@ -124,14 +125,11 @@ def _freeze(dev: int, sts, offs, total: int) -> None:
         with timeline.span("freeze_alloc", bytes=total):
             arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
         batch = native.CopyBatch()
-        views = []
         base = arena.data_ptr()
         for st, off in zip(sts, offs):
             t = st.tensor.detach()
-            view = arena[off: off + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
             if t.numel():
                 batch.add_tensor(t, base + off)
-            views.append(view)
         # producers may differ from the current stream: order after them
         for p in {st.producer for st in sts if st.producer is not None}:
             if p != stream.cuda_stream:
@@ -144,8 +142,8 @@ def _freeze(dev: int, sts, offs, total: int) -> None:
         done = torch.cuda.Event()
         done.record(stream)
     _live_launches.append((keep, done))
-    for st, view in zip(sts, views):
-        st.tensor = view
+    for st, off in zip(sts, offs):
+        st.frozen_at = (arena, off)  # _source() views the arena from now on
         st.producer = None  # ordering is carried by wait_event
         st.frozen = True
         st.wait_event = done

@@ -189,6 +189,9 @@ class TensorBufferStager(BufferStager):
         # arena that nobody else mutates -> no extra host copy needed
         self.frozen = False
         self.wait_event = None  # torch.cuda.Event guarding a frozen HBM copy
+        # (arena, byte offset) of the frozen copy; the view is built lazily
+        # in the drain so async_take does not pay ~4 us per tensor for it
+        self.frozen_at: Optional[Tuple[torch.Tensor, int]] = None
         self.codec: Optional[dict] = None  # HSZ1 info when the blob is compressed
 
     def reset_for_reuse(self) -> None:
@@ -197,10 +200,15 @@ class TensorBufferStager(BufferStager):
         self.tensor = self._plan_tensor
         self.frozen = False
         self.wait_event = None
+        self.frozen_at = None
         self.__dict__.pop("arena_keepalive", None)
         self.producer = staging.producer_stream_handle(self.tensor)
 
     def _source(self) -> torch.Tensor:
+        if self.frozen_at is not None:
+            arena, off = self.frozen_at
+            t = self.tensor
+            return arena[off: off + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
         t = self.tensor
         if self._tensor_prepare_func is not None:
             t = self._tensor_prepare_func(t, False)
