@@ -58,6 +58,11 @@ def main() -> None:
     ap.add_argument("--switch-interval-ms", type=float, default=None,
                     help="sys.setswitchinterval for this process (GIL hand-over period; "
                          "Python's default is 5 ms)")
+    ap.add_argument("--step-sync", default="stream", choices=["stream", "device"],
+                    help="how a training step waits for its GPU work: the trainer's stream "
+                         "(what loss.item() does) or the whole device (torch.cuda."
+                         "synchronize(), which also waits for the snapshot drain's copy "
+                         "streams and so charges their work to the step)")
     ap.add_argument("--master-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="stored parameter (and AdamW state) dtype; fp32 = mixed precision "
                          "with bf16 compute")
@@ -91,7 +96,10 @@ def main() -> None:
         opt.step()
         opt.zero_grad(set_to_none=True)
         if dev.type == "cuda":
-            torch.cuda.synchronize()
+            if args.step_sync == "device":
+                torch.cuda.synchronize()
+            else:
+                torch.cuda.current_stream(dev).synchronize()
         return time.perf_counter() - t0
 
     for _ in range(2):  # creates the AdamW state
@@ -171,7 +179,7 @@ def main() -> None:
     emit({"bench": "train_overlap_async_take", "model": args.model, "layers": cfg.n_layers,
           "world_size": ws, "seq": args.seq, "batch": args.batch, "storage": args.storage,
           "compression": args.compression, "master_dtype": args.master_dtype,
-          "switch_interval_ms": sys.getswitchinterval() * 1e3,
+          "switch_interval_ms": sys.getswitchinterval() * 1e3, "step_sync": args.step_sync,
           "checkpoint_bytes": ckpt_bytes,
           "baseline_step_ms": round(base_ms, 2), "sync_take_s": round(sync_s, 3),
           "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),

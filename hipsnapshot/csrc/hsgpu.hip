@@ -808,6 +808,21 @@ int hsg_stream_sync(int dev, int slot) {
   return 0;
 }
 
+// Grid cap for the calling thread's launches (0 = none).  The async-take
+// drain runs its staging threads with a cap so its kernels (HSZ1 encode,
+// slab gathers) occupy only that many CUs while training continues: at full
+// width the encoder made a concurrent Llama-3-8B training step ~30 % slower
+// (profiles/overlap_iso/), and the drain is PCIe-bound anyway.
+thread_local int t_grid_cap = 0;
+
+int hsg_set_thread_grid_cap(int cap) {
+  const int old = t_grid_cap;
+  t_grid_cap = cap < 0 ? 0 : cap;
+  return old;
+}
+
+int hsg_thread_grid_cap() { return t_grid_cap; }
+
 void* hsg_copy_stream(int dev, int slot) {
   hipStream_t s;
   hipEvent_t ev;
@@ -857,7 +872,8 @@ int hsg_copy_nd(int dev, const void* descs, int n, void* workspace, uint64_t ws_
   char* ws = static_cast<char*>(workspace);
   HS_CHECK(hipMemcpyAsync(ws, stage, toff + tbytes, hipMemcpyHostToDevice, s));
   const int64_t ntiles = static_cast<int64_t>(tiles.size());
-  const int grid = static_cast<int>(std::min<int64_t>(ntiles, 256 * 8));
+  int grid = static_cast<int>(std::min<int64_t>(ntiles, 256 * 8));
+  if (t_grid_cap > 0) grid = std::min(grid, t_grid_cap);
   // dynamic LDS only when a transpose descriptor is present (64x65 words)
   size_t lds = 0;
   for (int i = 0; i < n; ++i) {

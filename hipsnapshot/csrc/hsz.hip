@@ -39,6 +39,8 @@
 #include <cstdint>
 #include <cstdio>
 
+extern "C" int hsg_thread_grid_cap();  // hsgpu.hip
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -289,15 +291,14 @@ __device__ __forceinline__ uint32_t get_lo(const uint64_t* lw, int e) {
 }
 
 template <int W>
-__global__ void __launch_bounds__(kThreads)
-hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+__device__ inline void
+hsz_analyze_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
             FrameMeta* __restrict__ meta, uint16_t* __restrict__ lane_bytes_all) {
   __shared__ uint32_t hist[256];
   __shared__ uint8_t dict[16];
   __shared__ uint8_t code_of[260];  // indexed through cslot()
   __shared__ int nsel;
   __shared__ int red[4];
-  const uint64_t f = blockIdx.x;
   const uint64_t base = f * frame_bytes;
   const uint64_t len = min(uint64_t(frame_bytes), logical - base);
   const uint64_t n = len / W;
@@ -415,6 +416,19 @@ hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   }
 }
 
+// One workgroup per frame; with a grid smaller than the frame count (a
+// background drain caps it, hsg_set_thread_grid_cap) each workgroup walks
+// several frames, so the encoder occupies only that many CUs.
+template <int W>
+__global__ void __launch_bounds__(kThreads)
+hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+            FrameMeta* __restrict__ meta, uint16_t* __restrict__ lane_bytes_all, uint32_t nf) {
+  for (uint64_t f = blockIdx.x; f < nf; f += gridDim.x) {
+    hsz_analyze_frame<W>(f, src, logical, frame_bytes, meta, lane_bytes_all);
+    __syncthreads();  // the next frame reuses this workgroup's LDS
+  }
+}
+
 __global__ void __launch_bounds__(1024)
 hsz_layout(FrameMeta* __restrict__ meta, uint32_t n_frames, uint8_t* __restrict__ out,
            uint64_t logical, uint32_t w, uint32_t frame_bytes, uint64_t* __restrict__ total) {
@@ -485,14 +499,13 @@ __device__ __forceinline__ void write_frame_header(const FrameMeta& m, uint8_t* 
 }
 
 template <int W>
-__global__ void __launch_bounds__(kThreads)
-hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+__device__ inline void
+hsz_encode_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
            const FrameMeta* __restrict__ meta, uint8_t* __restrict__ out) {
   __shared__ uint8_t code_of[260];  // indexed through cslot()
   __shared__ uint32_t eidx[kMaxEsc];
   __shared__ uint8_t evals[kMaxEsc];
   __shared__ int ecount;
-  const uint64_t f = blockIdx.x;
   const FrameMeta& m = meta[f];  // arrays indexed at run time: read from memory
   if (m.mode == 2) return;  // hsz_encode2
   const uint64_t base = f * frame_bytes;
@@ -624,10 +637,23 @@ hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_byt
     tail[j] = j < tail_len ? s[n * W + j] : 0;
 }
 
-// Mode-2 encoder (W = 2 or 4).  LDS: 64 KiB stream buffer + escapes.
+// One workgroup per frame; with a grid smaller than the frame count (a
+// background drain caps it, hsg_set_thread_grid_cap) each workgroup walks
+// several frames, so the encoder occupies only that many CUs.
 template <int W>
 __global__ void __launch_bounds__(kThreads)
-hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+hsz_encode(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+           const FrameMeta* __restrict__ meta, uint8_t* __restrict__ out, uint32_t nf) {
+  for (uint64_t f = blockIdx.x; f < nf; f += gridDim.x) {
+    hsz_encode_frame<W>(f, src, logical, frame_bytes, meta, out);
+    __syncthreads();  // the next frame reuses this workgroup's LDS
+  }
+}
+
+// Mode-2 encoder (W = 2 or 4).  LDS: 64 KiB stream buffer + escapes.
+template <int W>
+__device__ inline void
+hsz_encode2_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
             const FrameMeta* __restrict__ meta, const uint16_t* __restrict__ lane_bytes_all,
             uint8_t* __restrict__ out) {
   // lane streams as 32-bit words; a word shared by two lanes' streams is
@@ -642,7 +668,6 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t ctotal;
   __shared__ int ecount;
-  const uint64_t f = blockIdx.x;
   const FrameMeta& m = meta[f];  // arrays indexed at run time: read from memory
   if (m.mode != 2) return;
   const uint64_t base = f * frame_bytes;
@@ -755,6 +780,20 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
   const uint64_t padded_end = m.size - kFrameHeader;
   for (uint64_t j = threadIdx.x; used + j < padded_end; j += kThreads)
     tail[j] = j < tail_len ? s[W * n + j] : 0;
+}
+
+// One workgroup per frame; with a grid smaller than the frame count (a
+// background drain caps it, hsg_set_thread_grid_cap) each workgroup walks
+// several frames, so the encoder occupies only that many CUs.
+template <int W>
+__global__ void __launch_bounds__(kThreads)
+hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+            const FrameMeta* __restrict__ meta, const uint16_t* __restrict__ lane_bytes_all,
+            uint8_t* __restrict__ out, uint32_t nf) {
+  for (uint64_t f = blockIdx.x; f < nf; f += gridDim.x) {
+    hsz_encode2_frame<W>(f, src, logical, frame_bytes, meta, lane_bytes_all, out);
+    __syncthreads();  // the next frame reuses this workgroup's LDS
+  }
 }
 
 // A rejected (corrupt / truncated) frame is reported through `err` (host-
@@ -1121,27 +1160,29 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
   auto* m = static_cast<FrameMeta*>(meta);
   auto* lanes = reinterpret_cast<uint16_t*>(m + nf);
   auto* o = static_cast<uint8_t*>(out);
+  const int cap = hsg_thread_grid_cap();
+  const uint32_t g = cap > 0 ? std::min<uint32_t>(nf, uint32_t(cap)) : nf;
   switch (w) {
-    case 1: hipLaunchKernelGGL(hsz_analyze<1>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes); break;
-    case 2: hipLaunchKernelGGL(hsz_analyze<2>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes); break;
-    case 4: hipLaunchKernelGGL(hsz_analyze<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes); break;
-    case 8: hipLaunchKernelGGL(hsz_analyze<8>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes); break;
+    case 1: hipLaunchKernelGGL(hsz_analyze<1>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, nf); break;
+    case 2: hipLaunchKernelGGL(hsz_analyze<2>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, nf); break;
+    case 4: hipLaunchKernelGGL(hsz_analyze<4>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, nf); break;
+    case 8: hipLaunchKernelGGL(hsz_analyze<8>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, nf); break;
     default: return -1001;
   }
   hipLaunchKernelGGL(hsz_layout, dim3(1), dim3(1024), 0, s, m, nf, o, logical, uint32_t(w),
                      frame_bytes, static_cast<uint64_t*>(total));
   switch (w) {
-    case 1: hipLaunchKernelGGL(hsz_encode<1>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
-    case 2: hipLaunchKernelGGL(hsz_encode<2>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
-    case 4: hipLaunchKernelGGL(hsz_encode<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
-    default: hipLaunchKernelGGL(hsz_encode<8>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o); break;
+    case 1: hipLaunchKernelGGL(hsz_encode<1>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o, nf); break;
+    case 2: hipLaunchKernelGGL(hsz_encode<2>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o, nf); break;
+    case 4: hipLaunchKernelGGL(hsz_encode<4>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o, nf); break;
+    default: hipLaunchKernelGGL(hsz_encode<8>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o, nf); break;
   }
   if (w == 2)
-    hipLaunchKernelGGL(hsz_encode2<2>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes,
-                       m, lanes, o);
+    hipLaunchKernelGGL(hsz_encode2<2>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes,
+                       m, lanes, o, nf);
   else if (w == 4)
-    hipLaunchKernelGGL(hsz_encode2<4>, dim3(nf), dim3(kThreads), 0, s, src8, logical, frame_bytes,
-                       m, lanes, o);
+    hipLaunchKernelGGL(hsz_encode2<4>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes,
+                       m, lanes, o, nf);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("hsz encode launch", e);
 }

@@ -53,7 +53,13 @@ def _acquire_pool(kind: str, n: int, rank: int) -> ThreadPoolExecutor:
         lst = _idle_pools.get(key)
         if lst:
             return lst.pop()
-    ex = ThreadPoolExecutor(max_workers=n, thread_name_prefix=f"hipsnapshot-{kind}-{rank}")
+    init = None
+    if kind == "stage_bg":  # async-take drain: kernels on a slice of the GPU
+        from .staging import mark_background_thread
+
+        init = mark_background_thread
+    ex = ThreadPoolExecutor(max_workers=n, thread_name_prefix=f"hipsnapshot-{kind}-{rank}",
+                            initializer=init)
     ex._hs_key = key  # type: ignore[attr-defined]
     return ex
 
@@ -188,10 +194,13 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                              memory_budget_bytes: int, rank: int,
                              stage_threads: Optional[int] = None,
                              io_concurrency: Optional[int] = None,
-                             gate: Optional[MemoryGate] = None) -> PendingIOWork:
+                             gate: Optional[MemoryGate] = None,
+                             background: bool = False) -> PendingIOWork:
+    """``background``: the pipeline runs while the caller keeps using the GPU
+    (async-take drain); its staging kernels get a capped grid."""
     stage_threads = stage_threads or knobs.get_stage_threads()
     io_concurrency = io_concurrency or knobs.get_io_threads()
-    executor = _acquire_pool("stage", stage_threads, rank)
+    executor = _acquire_pool("stage_bg" if background else "stage", stage_threads, rank)
     stats = PipelineStats()
     stats.n_reqs = len(write_reqs)
     failure: List[BaseException] = []
@@ -298,7 +307,7 @@ class DeferredIOWork:
     async def complete(self) -> None:
         async def run_deferred() -> None:
             p = await execute_write_reqs(self.deferred, self.storage, self.budget, self.rank,
-                                         gate=self.first.gate)
+                                         gate=self.first.gate, background=True)
             self._second = p
             await p.complete()
 

@@ -41,6 +41,16 @@ _next_slot = [0]
 NUM_COPY_SLOTS = 4
 
 
+def mark_background_thread() -> None:
+    """Executor-thread initializer of an async-take drain: this thread's
+    kernels (encode, slab gathers) are capped at ``HIPSNAPSHOT_DRAIN_CUS``
+    workgroups so a concurrent training step keeps the rest of the GPU."""
+    from .. import knobs
+
+    if native.hsgpu_loaded() and native.gpu_available():
+        native.set_thread_grid_cap(knobs.get_drain_cus())
+
+
 def copy_slot() -> int:
     """A copy-stream slot per OS thread (concurrent DMAs from executor threads)."""
     s = getattr(_tls, "slot", None)

@@ -120,6 +120,15 @@ def get_d2h_engine() -> str:
     return v
 
 
+def get_drain_cus() -> int:
+    """Grid cap (workgroups, ~CUs) for the kernels of an async-take drain
+    while training continues; 0 (default) = uncapped.  Measured on Llama-3-8B
+    + AdamW (profiles/overlap_iso/README.md): caps of 16-128 stretch the drain
+    (the encoder runs at 1.8 GB/s per workgroup) without lowering the total
+    training time a checkpoint costs (250-400 ms either way), so no cap."""
+    return max(0, _get_int("DRAIN_CUS", 0))
+
+
 def get_read_order() -> str:
     """Restore read order: ``plan`` (manifest order, default) or ``pipeline``
     (a small lead read, then largest first).  Measured A/B on one MI355X,

@@ -257,6 +257,7 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
         _declare(lib, "hsg_hsz_last_error", c_char_p, [])
+        _declare(lib, "hsg_set_thread_grid_cap", c_int, [c_int])
         _declare(lib, "hsg_sdma_last_error", c_char_p, [])
         _declare(lib, "hsg_sdma_engines", c_int, [c_int])
         _declare(lib, "hsg_sdma_d2h", c_int,
@@ -380,6 +381,13 @@ def memcpy(dev: int, slot: int, dst: int, src: int, nbytes: int, kind: int,
     _check(lib.hsg_memcpy(dev, slot, dst, src, nbytes, kind, _stream_handle(producer),
                           int(producer is not None),
                           1 if sync else 0), "hsg_memcpy")
+
+
+def set_thread_grid_cap(cap: int) -> int:
+    """Cap the grid of this thread's data-plane launches (copy gathers, HSZ1
+    encode) at ``cap`` workgroups, i.e. about that many CUs; 0 = no cap.
+    Returns the previous cap."""
+    return int(require_gpu_lib().hsg_set_thread_grid_cap(int(cap)))
 
 
 def sdma_engines(dev: int) -> int:

@@ -390,7 +390,20 @@ def _codec_inputs():
 
 @pytest.mark.parametrize("w", [1, 2, 4, 8])
 @pytest.mark.parametrize("kind", ["bf16", "random", "escapes", "fp32"])
-def test_hsz_encode_gpu_bit_exact_vs_reference(gpu, w, kind):
+@pytest.mark.parametrize("grid_cap", [0, 3])
+def test_hsz_encode_gpu_bit_exact_vs_reference(gpu, w, kind, grid_cap, monkeypatch):
+    """``grid_cap`` 3: each workgroup walks several frames (async-take drains
+    cap the encoder's grid) -- same bytes."""
+    from hipsnapshot.ops import codec
+
+    prev = native.set_thread_grid_cap(grid_cap)
+    try:
+        _hsz_encode_bit_exact(gpu, w, kind)
+    finally:
+        native.set_thread_grid_cap(prev)
+
+
+def _hsz_encode_bit_exact(gpu, w, kind):
     from hipsnapshot.ops import codec
 
     host = _codec_inputs()[kind]
