@@ -24,12 +24,12 @@ Soundness:
   global shape; ShardedTensor shard boxes) in the same logical order, and
   the settings key (rank, world size, sync/async, quantize globs,
   compression, every ``HIPSNAPSHOT_*``/``TORCHSNAPSHOT_*`` variable, the
-  app-state objects) matches;
+  app-state keys) matches;
 * the plan holds the leaves it was built from, so no address it matched can
   be recycled by the caching allocator while the plan exists -- equal
-  data_ptr means the same memory.  The plan is dropped when any of the
-  app-state objects is garbage collected (``weakref.finalize``), on the next
-  mismatch, or by ``clear()``;
+  data_ptr means the same memory.  The plan is dropped when an app-state
+  object that owns a cached leaf is garbage collected (``weakref.finalize``),
+  on the next mismatch, or by ``clear()``;
 * a plan is used by one take at a time (``busy`` until its I/O completed --
   an ``async_take`` still draining owns its stagers); a take that finds the
   plan busy plans from scratch;
@@ -128,10 +128,14 @@ def fast_signatures(resident: Dict[str, Any]) -> Optional[tuple]:
 
 def settings_key(app_state: Dict[str, Any], rank: int, world_size: int, is_async: bool,
                  quantize, compression: str) -> tuple:
+    """Everything besides the leaves that shapes a plan.  The app-state KEYS
+    are part of it, not the objects: ``{"model": m, "progress": StateDict(
+    step=i)}`` rebuilt for every take must still reuse the model's plan (the
+    leaf signatures establish that the model's tensors are the same)."""
     env = tuple(sorted((k, v) for k, v in os.environ.items()
                        if k.startswith(("HIPSNAPSHOT_", "TORCHSNAPSHOT_"))))
-    objs = tuple(sorted((k, id(v)) for k, v in app_state.items()))
-    return (objs, rank, world_size, bool(is_async), tuple(quantize or ()), compression, env)
+    return (tuple(sorted(app_state)), rank, world_size, bool(is_async),
+            tuple(quantize or ()), compression, env)
 
 
 def _tensor_stagers(write_reqs: List[WriteReq]) -> Iterator[Any]:
@@ -157,6 +161,7 @@ class TakePlan:
         self.entries = entries    # logical path -> final Entry (batched / compressed)
         self.write_reqs = write_reqs
         self.json: Dict[str, str] = {}  # logical path -> entry JSON (metadata gather)
+        self.owner_ids: set = set()  # ids of the app-state objects behind the leaves
         self.busy = True
 
     def reset(self) -> None:
@@ -194,9 +199,11 @@ def lookup(key: tuple, resident: Dict[str, Any]) -> Optional[TakePlan]:
 
 
 def store(key: tuple, resident: Dict[str, Any], object_entries: Dict[str, Entry],
-          write_reqs: List[WriteReq], app_state: Dict[str, Any]) -> Optional[TakePlan]:
+          write_reqs: List[WriteReq], owners: List[Any]) -> Optional[TakePlan]:
     """Keep the resident part of a fresh plan; returns it marked busy (the
-    caller's take is using it), or None when it cannot be cached."""
+    caller's take is using it), or None when it cannot be cached.  ``owners``:
+    the app-state objects the resident leaves come from -- the plan is
+    dropped (and its tensors released) when any of them is collected."""
     sigs = signatures(resident)
     fast = fast_signatures(resident)
     entries = {k: object_entries[k] for k in resident if k in object_entries}
@@ -219,23 +226,21 @@ def store(key: tuple, resident: Dict[str, Any], object_entries: Dict[str, Entry]
         if DTensor is not None and isinstance(v, DTensor):
             keep.append(v.device_mesh)
     plan = TakePlan(key, sigs, keep, entries, mine, fast)
+    plan.owner_ids = {id(v) for v in owners}
+    for v in owners:
+        if id(v) in _watched:
+            continue
+        try:
+            weakref.finalize(v, _drop_object, id(v))
+        except TypeError:  # not weak-referenceable: never cached
+            return None
+        _watched.add(id(v))
     with _lock:
         old = _plans.get(key)
         if old is not None and old.busy:
             return None  # an async take still drains with it: keep that one
         _plans[key] = plan
         stats["stores"] += 1
-    for v in app_state.values():
-        if id(v) in _watched:
-            continue
-        try:
-            weakref.finalize(v, _drop_object, id(v))
-        except TypeError:  # not weak-referenceable: never cached
-            with _lock:
-                if _plans.get(key) is plan:
-                    del _plans[key]
-            return None
-        _watched.add(id(v))
     return plan
 
 
@@ -247,7 +252,7 @@ def _drop_object(obj_id: int) -> None:
     it (their tensors are released with them)."""
     with _lock:
         _watched.discard(obj_id)
-        for key in [k for k in _plans if any(i == obj_id for _, i in k[0])]:
+        for key in [k for k, p in _plans.items() if obj_id in p.owner_ids]:
             del _plans[key]
 
 

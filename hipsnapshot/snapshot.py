@@ -372,7 +372,10 @@ class Snapshot:
                               if k in plan.entries or k in object_entries}
             write_reqs = plan.write_reqs + write_reqs
         elif cache_key is not None:
-            plan = plan_cache.store(cache_key, resident, object_entries, write_reqs, everything)
+            prefixes = {k: flat_prefix(k) for k in everything}
+            owners = [everything[k] for k, pre in prefixes.items()
+                      if any(r == pre or r.startswith(pre + "/") for r in resident)]
+            plan = plan_cache.store(cache_key, resident, object_entries, write_reqs, owners)
         if progress is not None:
             progress["plan"] = plan
         manifest.update(primitives)

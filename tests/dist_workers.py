@@ -107,6 +107,37 @@ def fsdp_take(path: str):
         torch.save(full, path + "_ref.pt")
 
 
+def fsdp_take_reusing_plan(path: str):
+    """Several takes of FSDP2 (DTensor) state with the plan cache active on
+    every rank (host tensors marked resident): later takes reuse the plan,
+    each snapshot restores to the values it was taken with."""
+    from torch.distributed.device_mesh import init_device_mesh
+
+    from hipsnapshot.engine import plan_cache
+    from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+
+    plan_cache.is_resident = lambda obj: hasattr(obj, "_local_tensor")
+    plan_cache.clear()
+    mesh = init_device_mesh("cpu", (dist.get_world_size(),))
+    model = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cpu"), torch.float32, mesh=mesh)
+    refs = []
+    for i in range(3):
+        with torch.no_grad():
+            for p in model.parameters():
+                p._local_tensor.add_(1.0)
+        Snapshot.take(f"{path}_{i}", {"model": model, "progress": StateDict(step=i)})
+        refs.append({k: v.full_tensor().clone() for k, v in model.state_dict().items()})
+    assert plan_cache.stats["hits"] == 2, plan_cache.stats
+    for i in range(3):
+        for p in model.parameters():
+            p._local_tensor.zero_()
+        prog = StateDict(step=-1)
+        Snapshot(f"{path}_{i}").restore({"model": model, "progress": prog})
+        assert prog["step"] == i
+        for k, v in model.state_dict().items():
+            assert torch.equal(v.full_tensor(), refs[i][k]), (i, k)
+
+
 def fsdp_restore(path: str):
     from torch.distributed.device_mesh import init_device_mesh
     from hipsnapshot.models.llama import Llama, LlamaConfig

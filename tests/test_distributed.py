@@ -37,6 +37,10 @@ def test_fsdp2_dtensor_resharding(tmp_path, save_ws, load_ws):
     run_distributed(W.fsdp_restore, load_ws, p)
 
 
+def test_fsdp2_takes_reuse_plan_on_every_rank(tmp_path):
+    run_distributed(W.fsdp_take_reusing_plan, 2, str(tmp_path / "pc"))
+
+
 def test_async_take(tmp_path):
     run_distributed(W.async_take_ok, 2, str(tmp_path / "a"))
 

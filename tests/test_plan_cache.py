@@ -209,3 +209,15 @@ def test_new_view_objects_each_take_still_reuse(tmp_path, resident, monkeypatch)
         out = Holder()
         Snapshot(str(tmp_path / f"v{i}")).restore({"h": out})
         assert torch.equal(out.w, w) and torch.equal(out.b, b)
+
+
+def test_fresh_app_state_dict_each_take_reuses_plan(tmp_path, resident):
+    """``{"sd": sd, "progress": StateDict(step=i)}`` rebuilt every take: the
+    resident leaves are the same, so the plan is reused."""
+    sd = _state(resident, n=3)
+    for i in range(3):
+        Snapshot.take(str(tmp_path / f"f{i}"), {"sd": sd, "progress": StateDict(step=i)})
+    assert plan_cache.stats["hits"] == 2
+    prog = StateDict(step=-1)
+    Snapshot(str(tmp_path / "f2")).restore({"progress": prog})
+    assert prog["step"] == 2
