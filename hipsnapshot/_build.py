@@ -42,7 +42,8 @@ def _atomic_build(out: str, cmd_for) -> None:
 
 
 def build_hsio(force: bool = False) -> str:
-    srcs = [os.path.join(CSRC, "hsio.cpp"), os.path.join(CSRC, "hsz_cpu.cpp")]
+    srcs = [os.path.join(CSRC, "hsio.cpp"), os.path.join(CSRC, "hsz_cpu.cpp"),
+            os.path.join(CSRC, "hschk.cpp")]
     if force or _stale(HSIO_SO, srcs):
         cxx = shutil.which("g++") or shutil.which("c++") or os.path.join(ROCM, "llvm/bin/clang++")
         _atomic_build(HSIO_SO, lambda out: [cxx, "-O3", "-std=c++17", "-fPIC", "-shared",

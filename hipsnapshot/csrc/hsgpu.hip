@@ -574,6 +574,51 @@ hs_fp8_hadamard_dequant(const uint8_t* __restrict__ q, const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// ---- hs64 blob checksum (definition: csrc/hschk.cpp) -------------------------
+// Grid-stride over the blob's 64-bit words; each lane mixes its words with
+// their global index, a wave reduces with shuffles and adds its partial sum
+// to one device accumulator (a vector atomic per wave).  Memory-bound: a
+// staged blob is hashed in HBM right before its DMA to the host.
+constexpr uint64_t kHsM1 = 0x9E3779B97F4A7C15ull;
+
+__device__ __forceinline__ uint64_t hs_mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+
+__global__ void __launch_bounds__(kBlock)
+hs_hash64(const uint8_t* __restrict__ p, uint64_t n, uint64_t first_word,
+          unsigned long long* __restrict__ acc) {
+  const uint64_t nw = n / 8;
+  const bool aligned = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
+  uint64_t s = 0;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nw; i += stride) {
+    uint64_t w;
+    if (aligned) {
+      w = reinterpret_cast<const uint64_t*>(p)[i];
+    } else {
+      w = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w |= uint64_t(p[8 * i + k]) << (8 * k);
+    }
+    s += hs_mix64(w ^ ((first_word + i + 1) * kHsM1));
+  }
+  const uint64_t tail = n - 8 * nw;
+  if (tail && blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t w = 0;
+    for (uint64_t k = 0; k < tail; ++k) w |= uint64_t(p[8 * nw + k]) << (8 * k);
+    s += hs_mix64(w ^ ((first_word + nw + 1) * kHsM1));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(acc, static_cast<unsigned long long>(s));
+}
+
 // Host-side state: pinned pool, copy streams, launch helpers.
 // ---------------------------------------------------------------------------
 
@@ -822,6 +867,64 @@ int hsg_set_thread_grid_cap(int cap) {
 }
 
 int hsg_thread_grid_cap() { return t_grid_cap; }
+
+// ---- hs64 on the copy streams -------------------------------------------------
+// One 8-byte device accumulator (+ a pinned landing word) per copy stream.
+struct HashSlot {
+  unsigned long long* acc = nullptr;
+  uint64_t* host = nullptr;
+};
+std::map<StreamKey, HashSlot> g_hash_slots;
+
+int hash_slot(int dev, int slot, HashSlot** out) {
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  HashSlot& h = g_hash_slots[StreamKey{dev, slot}];
+  if (h.acc == nullptr) {
+    HS_CHECK(hipSetDevice(dev));
+    HS_CHECK(hipMalloc(reinterpret_cast<void**>(&h.acc), sizeof(unsigned long long)));
+    HS_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h.host), sizeof(uint64_t),
+                           hipHostMallocDefault));
+  }
+  *out = &h;
+  return 0;
+}
+
+// Enqueue hs64's partial sum of device bytes [p, p + n) (first word index
+// `first_word`) on copy stream (dev, slot); the stream is NOT synchronised.
+int hsg_hash64(int dev, int slot, const void* p, uint64_t n, uint64_t first_word) {
+  HS_CHECK(hipSetDevice(dev));
+  hipStream_t s;
+  hipEvent_t ev;
+  int r = get_stream(dev, slot, &s, &ev);
+  if (r) return r;
+  HashSlot* h;
+  r = hash_slot(dev, slot, &h);
+  if (r) return r;
+  HS_CHECK(hipMemsetAsync(h->acc, 0, sizeof(unsigned long long), s));
+  const uint64_t words = n / 8 + 1;
+  int grid = static_cast<int>(std::min<uint64_t>((words + kBlock - 1) / kBlock, 256 * 8));
+  if (t_grid_cap > 0) grid = std::min(grid, t_grid_cap);
+  hipLaunchKernelGGL(hs_hash64, dim3(std::max(grid, 1)), dim3(kBlock), 0, s,
+                     static_cast<const uint8_t*>(p), n, first_word, h->acc);
+  HS_CHECK(hipGetLastError());
+  return 0;
+}
+
+// The partial sum of the last hsg_hash64 on (dev, slot); synchronises the stream.
+int hsg_hash64_result(int dev, int slot, uint64_t* out) {
+  HS_CHECK(hipSetDevice(dev));
+  hipStream_t s;
+  hipEvent_t ev;
+  int r = get_stream(dev, slot, &s, &ev);
+  if (r) return r;
+  HashSlot* h;
+  r = hash_slot(dev, slot, &h);
+  if (r) return r;
+  HS_CHECK(hipMemcpyAsync(h->host, h->acc, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HS_CHECK(hipStreamSynchronize(s));
+  *out = *h->host;
+  return 0;
+}
 
 void* hsg_copy_stream(int dev, int slot) {
   hipStream_t s;

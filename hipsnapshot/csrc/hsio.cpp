@@ -236,6 +236,13 @@ class Engine {
     return 0;
   }
 
+  void ForgetDirOf(const std::string& path) {
+    size_t slash = path.rfind('/');
+    if (slash == std::string::npos) return;
+    std::lock_guard<std::mutex> g(dmu_);
+    dirs_.erase(path.substr(0, slash));
+  }
+
   int64_t Execute(const Job& j) {
     switch (j.op) {
       case Op::kWrite: return DoWrite(j);
@@ -256,6 +263,14 @@ class Engine {
     // the stale tail, if any, is cut with ftruncate below.
     int oflags = O_WRONLY | O_CREAT | O_CLOEXEC;
     int fd = ::open(j.path.c_str(), oflags, 0644);
+    if (fd < 0 && errno == ENOENT && (j.flags & kFlagMkdirs)) {
+      // the cached parent was removed since (e.g. a directory of a previous
+      // take deleted by its successor): forget it, recreate, retry once
+      ForgetDirOf(j.path);
+      int r = MkdirsFor(j.path);
+      if (r < 0) return r;
+      fd = ::open(j.path.c_str(), oflags, 0644);
+    }
     if (fd < 0) return -errno;
     int64_t res = 0;
     size_t body = 0;

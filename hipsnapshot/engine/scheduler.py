@@ -33,6 +33,7 @@ from typing import Dict, List, Optional
 import psutil
 
 from .. import knobs
+from ..ops import checksum
 from ..io_types import ReadIO, ReadReq, StagedBuffer, StoragePlugin, WriteIO, WriteReq, as_staged
 from ..utils.tracing import timeline
 
@@ -113,6 +114,7 @@ class PipelineStats:
         self.bytes_staged = 0
         self.bytes_written = 0
         self.n_reqs = 0
+        self.checksums: Dict[str, int] = {}  # blob path -> hs64 (knobs.checksum_enabled)
 
     def as_dict(self) -> dict:
         d = {"n_reqs": self.n_reqs, "bytes": self.bytes_written}
@@ -215,8 +217,16 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
 
     reporter = WriteReporter(rank, memory_budget_bytes)
 
+    want_sums = knobs.checksum_enabled()
+
     async def _write(wr: WriteReq, buf: StagedBuffer, cost: int) -> None:
+        hashing = None
         try:
+            if want_sums and buf.checksum is None:
+                # host-staged blob: hash it on the host while it is written
+                # (both only read the buffer; the GPU stager hashed the rest)
+                hashing = asyncio.get_running_loop().run_in_executor(
+                    None, checksum.hs64_host, buf.addr, buf.nbytes)
             async with io_sem:
                 if failure:  # the snapshot is failing: do not start more writes
                     return
@@ -225,10 +235,16 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                 timeline.add("write", "io", t_w, time.perf_counter(), path=wr.path,
                              bytes=buf.nbytes)
             stats.bytes_written += buf.nbytes
+            if want_sums:
+                stats.checksums[wr.path] = (await hashing) if hashing is not None \
+                    else buf.checksum
         except BaseException as e:  # noqa: BLE001
             failure.append(e)
             raise
         finally:
+            if hashing is not None and not hashing.done():
+                # the hash still reads the buffer: it must finish before release
+                await asyncio.gather(asyncio.shield(hashing), return_exceptions=True)
             buf.release()
             gate.release(cost)
             wake.set()
@@ -315,6 +331,7 @@ class DeferredIOWork:
         if self._second is not None:
             self.stats.bytes_written += self._second.stats.bytes_written
             self.stats.n_reqs += self._second.stats.n_reqs
+            self.stats.checksums.update(self._second.stats.checksums)
         self.stats.t_done = time.monotonic()
         for r in res:
             if isinstance(r, BaseException):

@@ -32,7 +32,7 @@ import torch
 
 from ..format.serialization import contiguous_cpu_bytes_view, tensor_from_bytes
 from ..io_types import StagedBuffer, buffer_address
-from ..ops import native
+from ..ops import checksum, native
 from ..utils.tracing import timeline
 
 _tls = threading.local()
@@ -107,6 +107,12 @@ def _pinned_staged(nbytes: int) -> Tuple[native.PinnedBuffer, StagedBuffer]:
 _sdma_ok: dict = {}
 
 
+def _checksums() -> bool:
+    from .. import knobs
+
+    return knobs.checksum_enabled()
+
+
 def _use_sdma(dev: int) -> bool:
     from .. import knobs
 
@@ -164,7 +170,15 @@ def d2h_tensor(t: torch.Tensor, producer: Optional[int],
     t_s = time.perf_counter()
     try:
         if t.is_contiguous():
-            bulk_d2h(dev, slot, pb.ptr, t.data_ptr(), nbytes, producer)
+            if _checksums():
+                # hash the bytes in HBM on the copy stream (ordered after the
+                # producer), then move them; the hash runs at HBM speed
+                native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
+                checksum.device_hash_start(dev, slot, t.data_ptr(), nbytes)
+                bulk_d2h(dev, slot, pb.ptr, t.data_ptr(), nbytes)
+                staged.checksum = checksum.device_hash_result(dev, slot, nbytes)
+            else:
+                bulk_d2h(dev, slot, pb.ptr, t.data_ptr(), nbytes, producer)
         else:
             # pack-to-host: kernel stores the packed view over PCIe into the
             # host-mapped pinned block, ordered after the producer stream.
@@ -217,7 +231,11 @@ def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dic
     nbytes = _read_u64_device(dev, slot, total.data_ptr())
     pb, staged = _pinned_staged(nbytes)
     try:
+        if _checksums():
+            checksum.device_hash_start(dev, slot, out.data_ptr(), nbytes)
         bulk_d2h(dev, slot, pb.ptr, out.data_ptr(), nbytes)
+        if _checksums():
+            staged.checksum = checksum.device_hash_result(dev, slot, nbytes)
     except BaseException:
         staged.release()
         raise
@@ -349,7 +367,11 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
             batch.add_tensor(t, base + off)
         keep = batch.launch(dev, stream, sync=False)
         if slab is not None:
+            if _checksums():
+                checksum.device_hash_start(dev, slot, slab.data_ptr(), total_bytes)
             bulk_d2h(dev, slot, pb.ptr, slab.data_ptr(), total_bytes)
+            if _checksums():
+                staged.checksum = checksum.device_hash_result(dev, slot, total_bytes)
         native.stream_sync(dev, slot)
         if keep is not None:
             keep[0].release()

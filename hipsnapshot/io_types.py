@@ -39,7 +39,7 @@ def buffer_address(buf) -> int:
 class StagedBuffer:
     """Bytes ready for storage: ``view`` + raw ``addr`` + release hook."""
 
-    __slots__ = ("view", "addr", "_release", "keepalive")
+    __slots__ = ("view", "addr", "_release", "keepalive", "checksum")
 
     def __init__(self, view: BufferType, addr: Optional[int] = None,
                  release: Optional[Callable[[], None]] = None, keepalive: Any = None) -> None:
@@ -50,6 +50,9 @@ class StagedBuffer:
         self.addr = buffer_address(mv) if addr is None else addr
         self._release = release
         self.keepalive = keepalive
+        # hs64 of the bytes when the stager computed it (on the GPU); None =
+        # the writer hashes them on the host (ops/checksum.py)
+        self.checksum: Optional[int] = None
 
     @property
     def nbytes(self) -> int:

@@ -120,6 +120,13 @@ def get_d2h_engine() -> str:
     return v
 
 
+def checksum_enabled() -> bool:
+    """Record an hs64 checksum of every blob a take writes
+    (``.snapshot_checksums/<rank>``, ops/checksum.py); ``Snapshot.verify``
+    checks them."""
+    return _get_bool("CHECKSUM", True)
+
+
 def get_drain_cus() -> int:
     """Grid cap (workgroups, ~CUs) for the kernels of an async-take drain
     while training continues; 0 (default) = uncapped.  Measured on Llama-3-8B

@@ -79,6 +79,8 @@ def hsio() -> ctypes.CDLL:
             _declare(lib, "hsio_alloc_aligned", c_void_p, [c_uint64])
             _declare(lib, "hsio_free_aligned", None, [c_void_p])
             _declare(lib, "hsio_parallel_memcpy", None, [c_void_p, c_void_p, c_uint64, c_int])
+            _declare(lib, "hs64_partial", c_uint64, [c_void_p, c_uint64, c_uint64, c_int])
+            _declare(lib, "hs64_finish", c_uint64, [c_uint64, c_uint64])
             _declare(lib, "hsz_max_encoded_bytes", c_uint64, [c_uint64, ctypes.c_uint32])
             _declare(lib, "hsz_encode_cpu", c_int64,
                      [c_void_p, c_uint64, c_int, ctypes.c_uint32, c_void_p, c_int])
@@ -258,6 +260,8 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
         _declare(lib, "hsg_hsz_last_error", c_char_p, [])
         _declare(lib, "hsg_set_thread_grid_cap", c_int, [c_int])
+        _declare(lib, "hsg_hash64", c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64])
+        _declare(lib, "hsg_hash64_result", c_int, [c_int, c_int, ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_sdma_last_error", c_char_p, [])
         _declare(lib, "hsg_sdma_engines", c_int, [c_int])
         _declare(lib, "hsg_sdma_d2h", c_int,

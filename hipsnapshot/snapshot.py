@@ -68,6 +68,7 @@ from .io.batcher import batch_read_requests, batch_write_requests
 from .io.preparer import prepare_read, prepare_write
 from .io.sharded import is_sharded
 from .io_types import ReadIO, ReadReq, StoragePlugin, WriteIO, WriteReq
+from .ops import checksum
 from .parallel.comm import Comm
 from .parallel.elasticity import get_manifest_for_rank, handle_sharded_tensor_elasticity
 from .parallel.partitioner import consolidate_replicated_entries, partition_write_reqs
@@ -184,6 +185,8 @@ class Snapshot:
             t_staged = time.monotonic()
             with roctx_range("hipsnapshot.take.drain_io"), timeline.span("drain_io"):
                 pending.sync_complete(loop)
+            _write_checksums(storage, loop, comm.get_rank(), comm.get_world_size(),
+                             pending.stats.checksums)
             with roctx_range("hipsnapshot.take.commit"), timeline.span("commit"):
                 with timeline.span("commit_barrier", "commit"):
                     comm.barrier()
@@ -266,6 +269,15 @@ class Snapshot:
             pass
         except Exception as e:  # noqa: BLE001 - e.g. plugins without delete
             logger.debug(f"could not remove previous metadata: {e}")
+        # the previous take's checksums go with its commit (this take may run
+        # with checksums off, or on fewer ranks); every rank writes its own
+        # file only after the metadata gather, i.e. after this
+        try:
+            loop.run_until_complete(storage.delete_dir(checksum.CHECKSUM_DIR))
+        except (FileNotFoundError, KeyError, NotImplementedError):
+            pass
+        except Exception as e:  # noqa: BLE001
+            logger.debug(f"could not remove previous checksums: {e}")
 
     @classmethod
     def _take_impl(cls, path: str, app_state: AppState, replicated: Set[str],
@@ -507,6 +519,14 @@ class Snapshot:
 
     def get_manifest(self) -> Dict[str, Entry]:
         return copy.deepcopy(self.metadata.manifest)
+
+    def verify(self, concurrency: int = 4):
+        """Re-read every blob and check it against the hs64 checksum its take
+        recorded (hipsnapshot extension; returns ``verify.VerifyReport``,
+        ``.ok`` is True iff every blob matched)."""
+        from .verify import verify_snapshot
+
+        return verify_snapshot(self.path, self._storage_options, concurrency)
 
     def read_object(self, path: str, obj_out: Optional[T] = None,
                     memory_budget_bytes: Optional[int] = None) -> T:
@@ -762,6 +782,18 @@ class _BackgroundGather:
         return self._out["v"]
 
 
+def _write_checksums(storage: StoragePlugin, loop: asyncio.AbstractEventLoop, rank: int,
+                     world_size: int, sums: Dict[str, int]) -> None:
+    """This rank's blob checksums, ``.snapshot_checksums/<rank>`` (written
+    before the commit barrier: a committed snapshot has all of them)."""
+    if not knobs.checksum_enabled():
+        return
+    doc = {"algo": checksum.ALGO, "rank": rank, "world_size": world_size,
+           "blobs": {p: checksum.to_hex(h) for p, h in sorted(sums.items())}}
+    storage.sync_write(WriteIO(path=checksum.rank_file(rank),
+                               buf=json.dumps(doc).encode("utf-8")), loop)
+
+
 def _commit_barrier(store, path: str, nonce: str, rank: int, world_size: int) -> LinearBarrier:
     return LinearBarrier(prefix=f"hipsnapshot_{nonce}_{path}", store=store, rank=rank,
                          world_size=world_size, leader_rank=0)
@@ -821,6 +853,8 @@ class PendingSnapshot:
             barrier = _commit_barrier(store, path, nonce, rank, world_size)
         try:
             pending_io_work.sync_complete(event_loop)
+            _write_checksums(storage, event_loop, rank, world_size,
+                             pending_io_work.stats.checksums)
             if barrier is not None:
                 barrier.arrive(timeout=self.DEFAULT_BARRIER_TIMEOUT)
             if rank == 0:

@@ -59,7 +59,7 @@ class MemoryStoragePlugin(StoragePlugin):
             _STORE.pop(self._key(path), None)
 
     async def delete_dir(self, path: str) -> None:
-        clear_memory_store(self._key(path))
+        clear_memory_store(self._key(path).rstrip("/") + "/")
 
     async def close(self) -> None:
         return None

@@ -6,6 +6,7 @@ import pytest
 
 import dist_workers as W
 from hipsnapshot.utils.test_utils import run_distributed
+from hipsnapshot.verify import verify_snapshot
 
 pytestmark = pytest.mark.multiproc
 
@@ -18,6 +19,8 @@ def test_comm_collectives():
 def test_ddp_take_restore_and_upscale(tmp_path, chunk):
     p = str(tmp_path / f"ddp_{chunk}")
     run_distributed(W.ddp_take, 2, p, chunk)
+    rep = verify_snapshot(p)  # replicated + per-rank blobs, both rank files
+    assert rep.ok and rep.checked == rep.blobs > 0, rep
     run_distributed(W.ddp_restore, 2, p, 2)
     run_distributed(W.ddp_restore, 3, p, 2)  # elastic: a new rank joins
 
@@ -34,6 +37,7 @@ def test_partition_plan():
 def test_fsdp2_dtensor_resharding(tmp_path, save_ws, load_ws):
     p = str(tmp_path / "fsdp")
     run_distributed(W.fsdp_take, save_ws, p)
+    assert verify_snapshot(p).ok
     run_distributed(W.fsdp_restore, load_ws, p)
 
 

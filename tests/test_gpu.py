@@ -850,3 +850,54 @@ def test_sdma_failure_falls_back_to_blit(gpu, tmp_path, monkeypatch):
     Snapshot(str(tmp_path / "s")).restore({"sd": out})
     torch.cuda.synchronize()
     assert torch.equal(out["w"], ref["w"]) and torch.equal(out["b"], ref["b"])
+
+
+# ---- hs64 blob checksums hashed in HBM (hs_hash64, ops/checksum.py) ----------
+
+@pytest.mark.parametrize("n,off", [(0, 0), (1, 0), (7, 3), (8, 0), (4095, 1), (1 << 20, 0),
+                                   ((64 << 20) + 13, 5), ((256 << 20) + 8, 0)])
+def test_gpu_hash_matches_host_definition(gpu, n, off):
+    from hipsnapshot.ops import checksum
+
+    x = torch.randint(0, 256, (n + off,), dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize()
+    checksum.device_hash_start(0, 0, x.data_ptr() + off, n)
+    got = checksum.device_hash_result(0, 0, n)
+    host = x.cpu().numpy()[off:]
+    assert got == checksum.hs64_of(host)
+    if n <= (1 << 20):
+        assert got == checksum.hs64_reference(host.tobytes())
+
+
+@pytest.mark.parametrize("compression", ["none", "hsz1"])
+def test_gpu_take_checksums_hashed_on_device_and_verify(gpu, tmp_path, compression, monkeypatch):
+    from hipsnapshot.ops import checksum
+
+    calls = []
+    real = checksum.device_hash_result
+
+    def counting(dev, slot, nbytes):
+        calls.append(nbytes)
+        return real(dev, slot, nbytes)
+
+    monkeypatch.setattr(checksum, "device_hash_result", counting)
+    sd = _compressible_state(gpu)
+    s = Snapshot.take(str(tmp_path / "s"), {"sd": sd}, compression=compression)
+    assert calls, "no blob was hashed on the GPU"
+    rep = s.verify()
+    assert rep.ok and rep.checked == rep.blobs, rep
+    calls.clear()
+    a = Snapshot.async_take(str(tmp_path / "a"), {"sd": sd}, compression=compression).wait()
+    assert calls
+    assert a.verify().ok
+    # flip one byte of the largest blob: the GPU-recorded hash must catch it
+    root = str(tmp_path / "s")
+    files = [os.path.join(d, f) for d, _, fs in os.walk(root) for f in fs
+             if not os.path.relpath(os.path.join(d, f), root).startswith(".snapshot")]
+    victim = max(files, key=os.path.getsize)
+    with open(victim, "r+b") as f:
+        f.seek(7)
+        b = f.read(1)
+        f.seek(7)
+        f.write(bytes([b[0] ^ 1]))
+    assert s.verify().mismatched == [os.path.relpath(victim, root)]

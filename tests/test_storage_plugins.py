@@ -257,3 +257,18 @@ def test_registry_custom_protocol_and_errors(tmp_path):
         url_to_storage_plugin("nosuchproto://x")
     with pytest.raises(RuntimeError):
         url_to_storage_plugin("s3://onlybucket")
+
+
+def test_fs_engine_recreates_a_cached_directory_removed_meanwhile(tmp_path):
+    import shutil
+
+    loop = asyncio.new_event_loop()
+    fs = FSStoragePlugin(str(tmp_path))
+    try:
+        fs.sync_write(WriteIO(path="d/e/x", buf=b"one"), loop)
+        shutil.rmtree(tmp_path / "d")  # the engine's directory cache still has d/e
+        fs.sync_write(WriteIO(path="d/e/y", buf=b"two"), loop)
+        assert (tmp_path / "d" / "e" / "y").read_bytes() == b"two"
+    finally:
+        fs.sync_close(loop)
+        loop.close()
