@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -594,25 +595,60 @@ __global__ void __launch_bounds__(kBlock)
 hs_hash64(const uint8_t* __restrict__ p, uint64_t n, uint64_t first_word,
           unsigned long long* __restrict__ acc) {
   const uint64_t nw = n / 8;
-  const bool aligned = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
+  const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nthr = uint64_t(gridDim.x) * blockDim.x;
   uint64_t s = 0;
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nw; i += stride) {
-    uint64_t w;
-    if (aligned) {
-      w = reinterpret_cast<const uint64_t*>(p)[i];
-    } else {
-      w = 0;
+  uint64_t done = 0;  // words covered by the vector loop
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    // 16 B per lane per load; the position keys advance by adding a
+    // constant instead of a 64-bit multiply per word
+    // (four independent loads in flight per lane: the launch is kept narrow
+    // on purpose, see hsg_hash64, so each lane must cover latency itself)
+    const uint64_t npair = nw / 2;
+    const ulonglong2* v = reinterpret_cast<const ulonglong2*>(p);
+    uint64_t key = (first_word + 2 * tid + 1) * kHsM1;
+    const uint64_t dkey = 2 * nthr * kHsM1;
+    uint64_t j = tid;
+    for (; j + 3 * nthr < npair; j += 4 * nthr, key += 4 * dkey) {
+      const ulonglong2 w0 = v[j], w1 = v[j + nthr], w2 = v[j + 2 * nthr], w3 = v[j + 3 * nthr];
+      s += hs_mix64(w0.x ^ key) + hs_mix64(w0.y ^ (key + kHsM1));
+      s += hs_mix64(w1.x ^ (key + dkey)) + hs_mix64(w1.y ^ (key + dkey + kHsM1));
+      s += hs_mix64(w2.x ^ (key + 2 * dkey)) + hs_mix64(w2.y ^ (key + 2 * dkey + kHsM1));
+      s += hs_mix64(w3.x ^ (key + 3 * dkey)) + hs_mix64(w3.y ^ (key + 3 * dkey + kHsM1));
+    }
+    for (; j < npair; j += nthr, key += dkey) {
+      const ulonglong2 w = v[j];
+      s += hs_mix64(w.x ^ key) + hs_mix64(w.y ^ (key + kHsM1));
+    }
+    done = 2 * npair;
+  } else if ((reinterpret_cast<uintptr_t>(p) & 7) == 0) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(p);
+    uint64_t key = (first_word + tid + 1) * kHsM1;
+    const uint64_t dkey = nthr * kHsM1;
+    for (uint64_t i = tid; i < nw; i += nthr, key += dkey) s += hs_mix64(w[i] ^ key);
+    done = nw;
+  } else {
+    for (uint64_t i = tid; i < nw; i += nthr) {
+      uint64_t w = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) w |= uint64_t(p[8 * i + k]) << (8 * k);
+      s += hs_mix64(w ^ ((first_word + i + 1) * kHsM1));
     }
-    s += hs_mix64(w ^ ((first_word + i + 1) * kHsM1));
+    done = nw;
   }
-  const uint64_t tail = n - 8 * nw;
-  if (tail && blockIdx.x == 0 && threadIdx.x == 0) {
-    uint64_t w = 0;
-    for (uint64_t k = 0; k < tail; ++k) w |= uint64_t(p[8 * nw + k]) << (8 * k);
-    s += hs_mix64(w ^ ((first_word + nw + 1) * kHsM1));
+  if (tid == 0) {
+    // the odd word after the pairs, then the zero-padded tail
+    for (uint64_t i = done; i < nw; ++i) {
+      uint64_t w = 0;
+      for (int k = 0; k < 8; ++k) w |= uint64_t(p[8 * i + k]) << (8 * k);
+      s += hs_mix64(w ^ ((first_word + i + 1) * kHsM1));
+    }
+    const uint64_t tail = n - 8 * nw;
+    if (tail) {
+      uint64_t w = 0;
+      for (uint64_t k = 0; k < tail; ++k) w |= uint64_t(p[8 * nw + k]) << (8 * k);
+      s += hs_mix64(w ^ ((first_word + nw + 1) * kHsM1));
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -869,20 +905,27 @@ int hsg_set_thread_grid_cap(int cap) {
 int hsg_thread_grid_cap() { return t_grid_cap; }
 
 // ---- hs64 on the copy streams -------------------------------------------------
-// One 8-byte device accumulator (+ a pinned landing word) per copy stream.
-struct HashSlot {
+// A ring of 8-byte device accumulators (+ pinned landing words) per device.
+// Every hash takes the next ring entry, so threads that share a copy stream
+// never share an accumulator; an entry comes round again only after
+// kHashRing later hashes, long after its result was read (each thread has at
+// most one hash in flight).
+constexpr int kHashRing = 4096;
+struct HashRing {
   unsigned long long* acc = nullptr;
   uint64_t* host = nullptr;
+  std::atomic<uint32_t> next{0};
 };
-std::map<StreamKey, HashSlot> g_hash_slots;
+std::mutex g_hash_mu;
+std::map<int, HashRing> g_hash_rings;
 
-int hash_slot(int dev, int slot, HashSlot** out) {
-  std::lock_guard<std::mutex> g(g_stream_mu);
-  HashSlot& h = g_hash_slots[StreamKey{dev, slot}];
+int hash_ring(int dev, HashRing** out) {
+  std::lock_guard<std::mutex> g(g_hash_mu);
+  HashRing& h = g_hash_rings[dev];
   if (h.acc == nullptr) {
     HS_CHECK(hipSetDevice(dev));
-    HS_CHECK(hipMalloc(reinterpret_cast<void**>(&h.acc), sizeof(unsigned long long)));
-    HS_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h.host), sizeof(uint64_t),
+    HS_CHECK(hipMalloc(reinterpret_cast<void**>(&h.acc), kHashRing * sizeof(unsigned long long)));
+    HS_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h.host), kHashRing * sizeof(uint64_t),
                            hipHostMallocDefault));
   }
   *out = &h;
@@ -890,39 +933,61 @@ int hash_slot(int dev, int slot, HashSlot** out) {
 }
 
 // Enqueue hs64's partial sum of device bytes [p, p + n) (first word index
-// `first_word`) on copy stream (dev, slot); the stream is NOT synchronised.
-int hsg_hash64(int dev, int slot, const void* p, uint64_t n, uint64_t first_word) {
+// `first_word`) on stream (dev, slot), ordered after everything queued so far
+// on stream (dev, after_slot) when after_slot >= 0: the hash of a blob then
+// runs beside its device->host copy (both only read it) instead of in front.
+// Nothing is synchronised; *handle names the result for hsg_hash64_result.
+//
+// `max_grid` bounds the launch (<= 0: whole chip).  A full-width hash reads
+// HBM at ~4 TB/s and slows concurrent SDMA reads of HBM by ~20 %
+// (scripts/hash_probe.py), while blobs only need hashing at the PCIe rate;
+// the staging path therefore launches it narrow.
+int hsg_hash64(int dev, int slot, int after_slot, const void* p, uint64_t n,
+               uint64_t first_word, int max_grid, int* handle) {
   HS_CHECK(hipSetDevice(dev));
   hipStream_t s;
   hipEvent_t ev;
   int r = get_stream(dev, slot, &s, &ev);
   if (r) return r;
-  HashSlot* h;
-  r = hash_slot(dev, slot, &h);
+  if (after_slot >= 0 && after_slot != slot) {
+    hipStream_t a;
+    hipEvent_t aev;
+    r = get_stream(dev, after_slot, &a, &aev);
+    if (r) return r;
+    HS_CHECK(hipEventRecord(aev, a));
+    HS_CHECK(hipStreamWaitEvent(s, aev, 0));
+  }
+  HashRing* h;
+  r = hash_ring(dev, &h);
   if (r) return r;
-  HS_CHECK(hipMemsetAsync(h->acc, 0, sizeof(unsigned long long), s));
+  const int k = static_cast<int>(h->next.fetch_add(1) % kHashRing);
+  HS_CHECK(hipMemsetAsync(h->acc + k, 0, sizeof(unsigned long long), s));
   const uint64_t words = n / 8 + 1;
   int grid = static_cast<int>(std::min<uint64_t>((words + kBlock - 1) / kBlock, 256 * 8));
+  if (max_grid > 0) grid = std::min(grid, max_grid);
   if (t_grid_cap > 0) grid = std::min(grid, t_grid_cap);
   hipLaunchKernelGGL(hs_hash64, dim3(std::max(grid, 1)), dim3(kBlock), 0, s,
-                     static_cast<const uint8_t*>(p), n, first_word, h->acc);
+                     static_cast<const uint8_t*>(p), n, first_word, h->acc + k);
   HS_CHECK(hipGetLastError());
+  *handle = k;
   return 0;
 }
 
-// The partial sum of the last hsg_hash64 on (dev, slot); synchronises the stream.
-int hsg_hash64_result(int dev, int slot, uint64_t* out) {
+// The partial sum of hash `handle`, started on stream (dev, slot); waits for it.
+int hsg_hash64_result(int dev, int slot, int handle, uint64_t* out) {
   HS_CHECK(hipSetDevice(dev));
+  if (handle < 0 || handle >= kHashRing) return hipErrorInvalidValue;
   hipStream_t s;
   hipEvent_t ev;
   int r = get_stream(dev, slot, &s, &ev);
   if (r) return r;
-  HashSlot* h;
-  r = hash_slot(dev, slot, &h);
+  HashRing* h;
+  r = hash_ring(dev, &h);
   if (r) return r;
-  HS_CHECK(hipMemcpyAsync(h->host, h->acc, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HS_CHECK(hipMemcpyAsync(h->host + handle, h->acc + handle, sizeof(uint64_t),
+                          hipMemcpyDeviceToHost, s));
   HS_CHECK(hipStreamSynchronize(s));
-  *out = *h->host;
+  *out = h->host[handle];
   return 0;
 }
 

@@ -62,6 +62,11 @@ def copy_slot() -> int:
     return s
 
 
+def hash_slot(slot: int) -> int:
+    """The stream that hashes blobs beside copy slot ``slot``'s DMAs."""
+    return NUM_COPY_SLOTS + slot
+
+
 def device_of(t: torch.Tensor) -> int:
     idx = t.device.index
     return torch.cuda.current_device() if idx is None else idx
@@ -111,6 +116,13 @@ def _checksums() -> bool:
     from .. import knobs
 
     return knobs.checksum_enabled()
+
+
+def _hash_finish(dev: int, hslot: int, handle: int, nbytes: int) -> int:
+    t_s = time.perf_counter()
+    h = checksum.device_hash_result(dev, hslot, handle, nbytes)
+    timeline.add("hash_wait", "d2h", t_s, time.perf_counter(), bytes=nbytes)
+    return h
 
 
 def _use_sdma(dev: int) -> bool:
@@ -171,12 +183,13 @@ def d2h_tensor(t: torch.Tensor, producer: Optional[int],
     try:
         if t.is_contiguous():
             if _checksums():
-                # hash the bytes in HBM on the copy stream (ordered after the
-                # producer), then move them; the hash runs at HBM speed
+                # hash the bytes in HBM on a side stream (ordered after the
+                # producer) while the DMA moves them; both only read them
                 native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
-                checksum.device_hash_start(dev, slot, t.data_ptr(), nbytes)
+                hslot = hash_slot(slot)
+                hs = checksum.device_hash_start(dev, hslot, t.data_ptr(), nbytes, slot)
                 bulk_d2h(dev, slot, pb.ptr, t.data_ptr(), nbytes)
-                staged.checksum = checksum.device_hash_result(dev, slot, nbytes)
+                staged.checksum = _hash_finish(dev, hslot, hs, nbytes)
             else:
                 bulk_d2h(dev, slot, pb.ptr, t.data_ptr(), nbytes, producer)
         else:
@@ -231,11 +244,12 @@ def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dic
     nbytes = _read_u64_device(dev, slot, total.data_ptr())
     pb, staged = _pinned_staged(nbytes)
     try:
+        hs = None
         if _checksums():
-            checksum.device_hash_start(dev, slot, out.data_ptr(), nbytes)
+            hs = checksum.device_hash_start(dev, hash_slot(slot), out.data_ptr(), nbytes, slot)
         bulk_d2h(dev, slot, pb.ptr, out.data_ptr(), nbytes)
-        if _checksums():
-            staged.checksum = checksum.device_hash_result(dev, slot, nbytes)
+        if hs is not None:
+            staged.checksum = _hash_finish(dev, hash_slot(slot), hs, nbytes)
     except BaseException:
         staged.release()
         raise
@@ -367,11 +381,13 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
             batch.add_tensor(t, base + off)
         keep = batch.launch(dev, stream, sync=False)
         if slab is not None:
+            hs = None
             if _checksums():
-                checksum.device_hash_start(dev, slot, slab.data_ptr(), total_bytes)
+                hs = checksum.device_hash_start(dev, hash_slot(slot), slab.data_ptr(),
+                                                total_bytes, slot)
             bulk_d2h(dev, slot, pb.ptr, slab.data_ptr(), total_bytes)
-            if _checksums():
-                staged.checksum = checksum.device_hash_result(dev, slot, total_bytes)
+            if hs is not None:
+                staged.checksum = _hash_finish(dev, hash_slot(slot), hs, total_bytes)
         native.stream_sync(dev, slot)
         if keep is not None:
             keep[0].release()

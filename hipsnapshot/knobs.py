@@ -127,6 +127,13 @@ def checksum_enabled() -> bool:
     return _get_bool("CHECKSUM", True)
 
 
+def get_hash_grid() -> int:
+    """Workgroups of one blob-checksum launch (0 = whole chip).  Narrow by
+    default: a full-width hash saturates HBM reads and slows the concurrent
+    SDMA copies (scripts/hash_probe.py); blobs only need hashing at PCIe rate."""
+    return _get_int("HASH_GRID", 64)
+
+
 def get_drain_cus() -> int:
     """Grid cap (workgroups, ~CUs) for the kernels of an async-take drain
     while training continues; 0 (default) = uncapped.  Measured on Llama-3-8B

@@ -76,22 +76,35 @@ def to_hex(h: int) -> str:
     return f"{h & _MASK:016x}"
 
 
-def device_hash_start(dev: int, slot: int, ptr: int, nbytes: int) -> None:
-    """Enqueue the hs64 partial sum of device bytes on copy stream (dev, slot)."""
+def device_hash_start(dev: int, slot: int, ptr: int, nbytes: int,
+                      after_slot: int = -1, max_grid: Optional[int] = None) -> int:
+    """Enqueue the hs64 partial sum of device bytes on stream (dev, slot),
+    after the work queued on stream (dev, after_slot) if that is >= 0, on at
+    most ``max_grid`` workgroups (default ``HIPSNAPSHOT_HASH_GRID``; 0 = the
+    whole chip).  Returns the handle ``device_hash_result`` takes."""
+    import ctypes
+
+    from .. import knobs
     from . import native
 
-    native._check(native.require_gpu_lib().hsg_hash64(dev, slot, ptr, nbytes, 0), "hsg_hash64")
+    if max_grid is None:
+        max_grid = knobs.get_hash_grid()
+    h = ctypes.c_int(-1)
+    native._check(native.require_gpu_lib().hsg_hash64(dev, slot, after_slot, ptr, nbytes, 0,
+                                                      max_grid, ctypes.byref(h)), "hsg_hash64")
+    return h.value
 
 
-def device_hash_result(dev: int, slot: int, nbytes: int) -> int:
-    """Finish the hash started by ``device_hash_start`` (syncs the stream)."""
+def device_hash_result(dev: int, slot: int, handle: int, nbytes: int) -> int:
+    """Wait for the hash ``handle`` started on stream (dev, slot) and finish it."""
     import ctypes
 
     from . import native
 
     out = ctypes.c_uint64(0)
-    native._check(native.require_gpu_lib().hsg_hash64_result(dev, slot, ctypes.byref(out)),
-                 "hsg_hash64_result")
+    native._check(native.require_gpu_lib().hsg_hash64_result(dev, slot, handle,
+                                                             ctypes.byref(out)),
+                  "hsg_hash64_result")
     return finish(out.value, nbytes)
 
 

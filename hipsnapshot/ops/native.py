@@ -260,8 +260,9 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
         _declare(lib, "hsg_hsz_last_error", c_char_p, [])
         _declare(lib, "hsg_set_thread_grid_cap", c_int, [c_int])
-        _declare(lib, "hsg_hash64", c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64])
-        _declare(lib, "hsg_hash64_result", c_int, [c_int, c_int, ctypes.POINTER(c_uint64)])
+        _declare(lib, "hsg_hash64", c_int, [c_int, c_int, c_int, c_void_p, c_uint64, c_uint64,
+                                             c_int, ctypes.POINTER(c_int)])
+        _declare(lib, "hsg_hash64_result", c_int, [c_int, c_int, c_int, ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_sdma_last_error", c_char_p, [])
         _declare(lib, "hsg_sdma_engines", c_int, [c_int])
         _declare(lib, "hsg_sdma_d2h", c_int,

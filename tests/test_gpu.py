@@ -854,15 +854,16 @@ def test_sdma_failure_falls_back_to_blit(gpu, tmp_path, monkeypatch):
 
 # ---- hs64 blob checksums hashed in HBM (hs_hash64, ops/checksum.py) ----------
 
-@pytest.mark.parametrize("n,off", [(0, 0), (1, 0), (7, 3), (8, 0), (4095, 1), (1 << 20, 0),
-                                   ((64 << 20) + 13, 5), ((256 << 20) + 8, 0)])
+@pytest.mark.parametrize("n,off", [(0, 0), (1, 0), (7, 3), (8, 0), (24, 0), (4095, 1),
+                                   (1 << 20, 0), ((1 << 20) + 8, 8), ((64 << 20) + 13, 5),
+                                   ((256 << 20) + 8, 0), ((256 << 20) + 3, 8)])
 def test_gpu_hash_matches_host_definition(gpu, n, off):
     from hipsnapshot.ops import checksum
 
     x = torch.randint(0, 256, (n + off,), dtype=torch.uint8, device=gpu)
     torch.cuda.synchronize()
-    checksum.device_hash_start(0, 0, x.data_ptr() + off, n)
-    got = checksum.device_hash_result(0, 0, n)
+    h = checksum.device_hash_start(0, 0, x.data_ptr() + off, n)
+    got = checksum.device_hash_result(0, 0, h, n)
     host = x.cpu().numpy()[off:]
     assert got == checksum.hs64_of(host)
     if n <= (1 << 20):
@@ -876,9 +877,9 @@ def test_gpu_take_checksums_hashed_on_device_and_verify(gpu, tmp_path, compressi
     calls = []
     real = checksum.device_hash_result
 
-    def counting(dev, slot, nbytes):
+    def counting(dev, slot, handle, nbytes):
         calls.append(nbytes)
-        return real(dev, slot, nbytes)
+        return real(dev, slot, handle, nbytes)
 
     monkeypatch.setattr(checksum, "device_hash_result", counting)
     sd = _compressible_state(gpu)
