@@ -1,0 +1,124 @@
+"""One rank's share of the Llama-3-8B FSDP save at world size W, on one GPU.
+
+At N GPUs every rank saves 1/N of every parameter: the same 291 tensors,
+each 1/N the size.  Per-take fixed costs (planning per tensor, per-blob
+launch and DMA latencies, commit) do not shrink with N, so they decide the
+scaling efficiency the 8-GPU node will show.  This benchmark builds exactly
+that share on one GPU -- each parameter's world-W local shard (dim 0 split
+like FSDP2's Shard(0)) as a DTensor over a 1-rank mesh, so the take goes
+through the same DTensor / sharded-entry path -- and times take, async_take
+unblock and restore.
+
+It leaves out what only a real N-GPU run has: collectives across ranks and
+N ranks sharing host memory bandwidth.  ``ideal_aggregate_GBps`` = N x the
+share's bytes / the share's take time, the upper bound if nothing else
+interfered.
+
+    python benchmarks/rank_share/main.py --world 8 [--compression hsz1]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--async-iters", type=int, default=5)
+    ap.add_argument("--restore-iters", type=int, default=3)
+    ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
+    ap.add_argument("--dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import DTensor, Shard
+
+    from hipsnapshot import Snapshot, StateDict
+    from hipsnapshot.models.llama import Llama, LlamaConfig
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    os.environ.update(RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    mesh = init_device_mesh("cuda", (1,))
+    cfg = LlamaConfig.llama3_8b()
+    with torch.device("meta"):
+        meta = Llama(cfg)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    params = {}
+    for name, p in meta.named_parameters():
+        rows = -(-p.shape[0] // args.world)
+        local = torch.randn((rows,) + tuple(p.shape[1:]), device=dev, generator=gen)
+        local = (local * 0.02).to(torch.bfloat16)
+        params[name] = DTensor.from_local(local, mesh, [Shard(0)], run_check=False)
+    del meta
+    share = sum(t._local_tensor.numel() * 2 for t in params.values())
+    app_state = {"model": StateDict(**params)}
+    root = os.path.join(args.dir, f"rank_share_w{args.world}")
+    shutil.rmtree(root, ignore_errors=True)
+    path = os.path.join(root, "ckpt")
+    torch.cuda.synchronize()
+
+    def take():
+        Snapshot.take(path, app_state, compression=args.compression)
+
+    for _ in range(args.warmup):
+        take()
+    times = []
+    for _ in range(args.steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        take()
+        times.append(time.perf_counter() - t0)
+    unblock, total = [], []
+    for _ in range(args.async_iters):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pending = Snapshot.async_take(path + "_async", app_state, compression=args.compression)
+        unblock.append(time.perf_counter() - t0)
+        pending.wait()
+        total.append(time.perf_counter() - t0)
+    refs = {k: v._local_tensor.clone() for k, v in params.items()}
+    rtimes = []
+    for _ in range(args.restore_iters):
+        for v in params.values():
+            v._local_tensor.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        Snapshot(path).restore(app_state)
+        torch.cuda.synchronize()
+        rtimes.append(time.perf_counter() - t0)
+    ok = all(torch.equal(refs[k], app_state["model"][k]._local_tensor) for k in refs)
+    med = statistics.median(times)
+    print(json.dumps({
+        "bench": "rank_share", "world": args.world, "compression": args.compression,
+        "tensors": len(params), "share_bytes": share,
+        "take_ms_median": round(med * 1e3, 2), "take_ms_min": round(min(times) * 1e3, 2),
+        "share_GBps": round(share / med / 1e9, 2),
+        "ideal_aggregate_GBps": round(args.world * share / med / 1e9, 1),
+        "unblock_ms_median": round(statistics.median(unblock) * 1e3, 2),
+        "async_total_ms_median": round(statistics.median(total) * 1e3, 2),
+        "restore_ms_median": round(statistics.median(rtimes) * 1e3, 2),
+        "restore_bitwise_ok": ok,
+    }), flush=True)
+    shutil.rmtree(root, ignore_errors=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -145,11 +145,16 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
     out: List[WriteReq] = []
     slabs: Dict[Optional[torch.device], List[Slab]] = {}
     relocation: Dict[str, Tuple[str, int, int]] = {}
-    # Tail taper: slabs are staged in creation order after the big blobs, and
-    # one file is written by one thread (buffered writes to a file serialize
-    # on its inode lock), so the LAST slab's write is the take's tail.  Once
-    # less than 2 slabs' worth of batchable bytes remain on a device, close
-    # slabs at a quarter of the threshold.
+    # Tail taper: slabs are staged after the big blobs (largest first), and
+    # one file is written by one thread at ~10-15 GB/s (buffered writes to a
+    # file serialize on its inode lock), while the DMA feeding the writes runs
+    # at ~56 GB/s.  A slab staged when R batchable bytes remain must be written
+    # before those R bytes have crossed PCIe (writes are ~5x slower per file),
+    # so once fewer than 8 full slabs remain on a device, slabs close at an
+    # eighth of what remains (a geometric taper down to 8 MiB).  With
+    # equal-sized slabs the last big writes outlived the staging by ~4 ms:
+    # the taper takes 1/8 off one rank's take at 8 GPUs (profiles/rank_share/).
+    floor = min(threshold, max(threshold // 16, 8 << 20))  # smaller slabs gain nothing
     remaining: Dict[Optional[torch.device], int] = defaultdict(int)
     info = []  # (batchable below threshold?, nbytes, device) once per request
     for wr in write_reqs:
@@ -168,9 +173,9 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
             out.append(wr)
             continue
         st = wr.buffer_stager
+        left = remaining[dev]  # batchable bytes on this device not placed yet
         remaining[dev] -= nbytes
-        cap = threshold if remaining[dev] + nbytes > 2 * threshold else \
-            max(threshold // 4, min(threshold, 16 << 20))
+        cap = threshold if left > 8 * threshold else max(floor, min(threshold, left // 8))
 
         def _new_slab(k: int) -> Slab:
             if name_prefix is None:
