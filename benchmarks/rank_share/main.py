@@ -39,7 +39,14 @@ def main() -> None:
     ap.add_argument("--restore-iters", type=int, default=3)
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
     ap.add_argument("--dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--ab", default=None,
+                    help="NAME=v1,v2[,...]: alternate env var NAME over the values take by "
+                         "take (same process, interleaved) and report each value's takes")
+    ap.add_argument("--switch-interval", type=float, default=None,
+                    help="sys.setswitchinterval for the run (GIL hand-over latency)")
     args = ap.parse_args()
+    if args.switch_interval:
+        sys.setswitchinterval(args.switch_interval)
 
     import torch
     import torch.distributed as dist
@@ -77,14 +84,35 @@ def main() -> None:
     def take():
         Snapshot.take(path, app_state, compression=args.compression)
 
+    ab_name, ab_vals = None, [None]
+    if args.ab:
+        ab_name, vals = args.ab.split("=", 1)
+        ab_vals = vals.split(",")
     for _ in range(args.warmup):
-        take()
+        for v in ab_vals:
+            if ab_name:
+                os.environ[ab_name] = v
+            take()
     times = []
+    per_val = {v: [] for v in ab_vals}
     for _ in range(args.steps):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        take()
-        times.append(time.perf_counter() - t0)
+        for v in ab_vals:
+            if ab_name:
+                os.environ[ab_name] = v
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            take()
+            dt = time.perf_counter() - t0
+            per_val[v].append(dt)
+            times.append(dt)
+    if ab_name:
+        print(json.dumps({"bench": "rank_share_ab", "world": args.world, "knob": ab_name,
+                          "compression": args.compression,
+                          "take_ms": {v: {"median": round(statistics.median(t) * 1e3, 2),
+                                          "min": round(min(t) * 1e3, 2),
+                                          "mean": round(statistics.mean(t) * 1e3, 2)}
+                                      for v, t in per_val.items()}}), flush=True)
+        os.environ[ab_name] = ab_vals[0]
     unblock, total = [], []
     for _ in range(args.async_iters):
         torch.cuda.synchronize()

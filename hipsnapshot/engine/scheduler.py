@@ -140,15 +140,21 @@ class MemoryGate:
         self.limit = limit
         self.in_use = 0
         self._wakes: set = set()
+        # staging worker threads admit under this condition (thread-driven
+        # pipelines); releases happen on the event-loop thread
+        self.cond = threading.Condition()
 
     def try_admit(self, cost: int) -> bool:
-        if self.in_use + cost > self.limit and self.in_use > 0:
-            return False
-        self.in_use += cost
-        return True
+        with self.cond:
+            if self.in_use + cost > self.limit and self.in_use > 0:
+                return False
+            self.in_use += cost
+            return True
 
     def release(self, cost: int) -> None:
-        self.in_use -= cost
+        with self.cond:
+            self.in_use -= cost
+            self.cond.notify_all()
         for ev in self._wakes:
             ev.set()
 
@@ -219,6 +225,13 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
 
     want_sums = knobs.checksum_enabled()
 
+    def _staged(wr: WriteReq, buf: StagedBuffer, cost: int, t_s: float) -> None:
+        timeline.add("stage", "stage", t_s, time.perf_counter(), path=wr.path,
+                     bytes=buf.nbytes)
+        stats.bytes_staged += buf.nbytes
+        io_tasks.add(asyncio.ensure_future(_write(wr, buf, cost)))
+        reporter.maybe_report(len(pending), 0, len(io_tasks), gate.in_use, stats.bytes_written)
+
     async def _write(wr: WriteReq, buf: StagedBuffer, cost: int) -> None:
         hashing = None
         try:
@@ -249,6 +262,26 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             gate.release(cost)
             wake.set()
 
+    if pending and knobs.thread_staging_enabled() and \
+            all(getattr(wr.buffer_stager, "thread_staging", False) for wr in pending):
+        try:
+            await _stage_on_threads(pending, stage_threads, executor, gate, failure,
+                                    lambda wr, buf, cost, t_s: _staged(wr, buf, cost, t_s))
+        except BaseException:
+            gate.unsubscribe(wake)
+            # writes already issued keep their buffers until the engine is done
+            await asyncio.gather(*io_tasks, return_exceptions=True)
+            executor.shutdown(wait=False)
+            raise
+        gate.unsubscribe(wake)
+        if failure:
+            await asyncio.gather(*io_tasks, return_exceptions=True)
+            executor.shutdown(wait=True)
+            raise failure[0]
+        stats.t_staged = time.monotonic()
+        logger.debug(f"Rank {rank} completed staging in {stats.t_staged - stats.t_start:.3f}s")
+        return PendingIOWork(io_tasks, executor, stats, failure, gate)
+
     try:
         while pending or staging:
             while pending and len(staging) < stage_threads and not failure:
@@ -277,11 +310,7 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                     gate.release(cost)
                     failure.append(exc)
                     continue
-                buf = as_staged(task.result())
-                timeline.add("stage", "stage", t_s, time.perf_counter(), path=wr.path,
-                             bytes=buf.nbytes)
-                stats.bytes_staged += buf.nbytes
-                io_tasks.add(asyncio.ensure_future(_write(wr, buf, cost)))
+                _staged(wr, as_staged(task.result()), cost, t_s)
         if failure:
             for t in staging:
                 t.cancel()
@@ -300,6 +329,58 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     stats.t_staged = time.monotonic()
     logger.debug(f"Rank {rank} completed staging in {stats.t_staged - stats.t_start:.3f}s")
     return PendingIOWork(io_tasks, executor, stats, failure, gate)
+
+
+async def _stage_on_threads(pending: deque, nthreads: int, executor: ThreadPoolExecutor,
+                            gate: MemoryGate, failure: List[BaseException], on_staged) -> None:
+    """Stage ``pending`` on ``nthreads`` long-running executor workers.
+
+    Each worker takes the next request the memory gate admits, stages it
+    (``stage_buffer_sync``: D2H / encode / gather on the worker's own copy
+    stream) and goes straight on to the next one; only the hand-off of the
+    staged buffer to the writer goes through the event loop.  With one
+    round trip through the loop per request instead, the DMA engine sat idle
+    for 0.7-1.4 ms between blobs whenever all workers waited for the loop
+    (17 % of a take of one rank's 8-GPU share, profiles/rank_share/)."""
+    loop = asyncio.get_running_loop()
+    cond = gate.cond
+
+    def worker() -> None:
+        while True:
+            with cond:
+                while True:
+                    if failure or not pending:
+                        return
+                    wr = pending[0]
+                    cost = wr.buffer_stager.get_staging_cost_bytes()
+                    if gate.in_use + cost <= gate.limit or gate.in_use == 0:
+                        gate.in_use += cost
+                        pending.popleft()
+                        break
+                    cond.wait(0.05)
+            t_s = time.perf_counter()
+            try:
+                buf = as_staged(wr.buffer_stager.stage_buffer_sync())
+            except BaseException as e:  # noqa: BLE001 - reported by the caller
+                with cond:
+                    failure.append(e)
+                    cond.notify_all()
+                loop.call_soon_threadsafe(gate.release, cost)
+                return
+            try:
+                loop.call_soon_threadsafe(on_staged, wr, buf, cost, t_s)
+            except RuntimeError:  # the loop is gone (the take was abandoned)
+                buf.release()
+                return
+
+    futs = [executor.submit(worker) for _ in range(max(1, min(nthreads, len(pending))))]
+    try:
+        await asyncio.gather(*(asyncio.wrap_future(f) for f in futs))
+    except BaseException:
+        with cond:  # stop the workers at their next request
+            failure.append(asyncio.CancelledError())
+            cond.notify_all()
+        raise
 
 
 class DeferredIOWork:

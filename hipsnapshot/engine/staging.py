@@ -142,12 +142,14 @@ def bulk_d2h(dev: int, slot: int, dst: int, src: int, nbytes: int,
     copy stream (dev, slot) and, if given, after ``producer``.  Runs on the
     SDMA engines when ``HIPSNAPSHOT_D2H_ENGINE=sdma`` (no CU time taken from
     a concurrent training step), else as hipMemcpyAsync."""
+    t_s = time.perf_counter()
     if nbytes and _use_sdma(dev):
         if producer is not None:
             native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
             producer = None  # the copy stream is ordered after it now
         try:
             native.sdma_d2h(dev, dst, src, nbytes, native.copy_stream(dev, slot))
+            timeline.add("dma", "d2h", t_s, time.perf_counter(), bytes=nbytes, slot=slot)
             return
         except native.HipError as e:
             # nothing is left in flight after a failed SDMA copy (every issued
@@ -158,6 +160,7 @@ def bulk_d2h(dev: int, slot: int, dst: int, src: int, nbytes: int,
                 f"SDMA device->host copy failed on cuda:{dev} ({e}); using hipMemcpyAsync")
             _sdma_ok[dev] = False
     native.memcpy(dev, slot, dst, src, nbytes, native.D2H, producer, sync=True)
+    timeline.add("dma", "d2h", t_s, time.perf_counter(), bytes=nbytes, slot=slot)
 
 
 def _elem_strides_ok(t: torch.Tensor) -> bool:
@@ -238,11 +241,19 @@ def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dic
                                                  int(codec["frame_bytes"]), launch=False)
     except torch.cuda.OutOfMemoryError:
         return _encode_on_host(dev, slot, src_u8, codec)
+    t_a = time.perf_counter()
     _join_current_stream(dev, slot)
     hsz.launch_encode(src_u8, int(codec["w"]), stream, int(codec["frame_bytes"]), out, total,
                       meta)
+    t_l = time.perf_counter()
     nbytes = _read_u64_device(dev, slot, total.data_ptr())
+    t_n = time.perf_counter()
     pb, staged = _pinned_staged(nbytes)
+    t_p = time.perf_counter()
+    timeline.add("enc_alloc", "enc", t_s, t_a)
+    timeline.add("enc_launch", "enc", t_a, t_l)
+    timeline.add("enc_wait", "enc", t_l, t_n)
+    timeline.add("enc_pinned", "enc", t_n, t_p)
     try:
         hs = None
         if _checksums():

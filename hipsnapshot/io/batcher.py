@@ -79,8 +79,13 @@ class BatchedBufferStager(BufferStager):
         self.total = total
         self.codec: Optional[dict] = None
 
+    thread_staging = True  # stage_buffer_sync may run on a scheduler worker
+
     async def stage_buffer(self, executor: Optional[Executor] = None):
         return await run_in_executor(executor, self._stage_sync)
+
+    def stage_buffer_sync(self) -> StagedBuffer:
+        return self._stage_sync()
 
     def _stage_sync(self) -> StagedBuffer:
         raw = self._gather()
@@ -119,8 +124,13 @@ class GPUBatchedBufferStager(BufferStager):
         self.total = total
         self.codec: Optional[dict] = None  # HSZ1 info when the slab is compressed
 
+    thread_staging = True
+
     async def stage_buffer(self, executor: Optional[Executor] = None):
         return await run_in_executor(executor, self._stage_sync)
+
+    def stage_buffer_sync(self) -> StagedBuffer:
+        return self._stage_sync()
 
     def _stage_sync(self) -> StagedBuffer:
         for ev in {id(st.wait_event): st.wait_event for _, st in self.members

@@ -28,7 +28,12 @@ class ObjectBufferStager(BufferStager):
         # serialize eagerly: the object is captured at take time (async-safe)
         self._buf = torch_save_as_bytes(obj)
 
+    thread_staging = True
+
     async def stage_buffer(self, executor: Optional[Executor] = None):
+        return self._buf
+
+    def stage_buffer_sync(self):
         return self._buf
 
     def get_staging_cost_bytes(self) -> int:

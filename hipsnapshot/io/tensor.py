@@ -215,11 +215,26 @@ class TensorBufferStager(BufferStager):
         return t.detach()
 
     async def stage_buffer(self, executor: Optional[Executor] = None):
-        t = self._source()
+        if self._tensor_prepare_func is not None:
+            # the user's prepare func runs on the event-loop thread, as in the
+            # reference; only the copy goes to the executor
+            t = self._source()
+            return await run_in_executor(executor, self._stage_source, t)
+        return await run_in_executor(executor, self.stage_buffer_sync)
+
+    @property
+    def thread_staging(self) -> bool:
+        """``stage_buffer_sync`` may run on a scheduler worker thread."""
+        return self._tensor_prepare_func is None
+
+    def stage_buffer_sync(self):
+        return self._stage_source(self._source())
+
+    def _stage_source(self, t: torch.Tensor):
         ser = self.entry.serializer
         if ser == Serializer.BUFFER_PROTOCOL.value:
             if t.is_cuda:
-                return await run_in_executor(executor, self._d2h, t)
+                return self._d2h(t)
             # async snapshots must not alias live host memory (Appendix C #1);
             # a prepare-func result that owns fresh storage needs no copy.
             fresh = (self._tensor_prepare_func is not None
@@ -227,14 +242,14 @@ class TensorBufferStager(BufferStager):
                      != self.tensor.untyped_storage().data_ptr())
             copy = self.is_async_snapshot and not self.frozen and not fresh
             if self.codec is not None:
-                return await run_in_executor(executor, self._encode_host, t)
-            return await run_in_executor(executor, staging.cpu_tensor_bytes, t, copy)
+                return self._encode_host(t)
+            return staging.cpu_tensor_bytes(t, copy)
         if ser == Serializer.FP8_BLOCK.value:
             from ..ops.quant import stage_fp8
 
-            return await run_in_executor(executor, stage_fp8, t, self.entry, self.producer)
+            return stage_fp8(t, self.entry, self.producer)
         if ser == Serializer.TORCH_SAVE.value:
-            return await run_in_executor(executor, _torch_save_tensor, t)
+            return _torch_save_tensor(t)
         raise ValueError(f"Unrecognized serializer: {ser}.")
 
     def _encode_host(self, t: torch.Tensor):

@@ -120,6 +120,19 @@ def get_d2h_engine() -> str:
     return v
 
 
+def get_gil_switch_us() -> int:
+    """GIL switch interval (microseconds) while a take / restore runs on the
+    calling thread; 0 = leave Python's (5000)."""
+    return _get_int("GIL_SWITCH_US", 0)
+
+
+def thread_staging_enabled() -> bool:
+    """Stage writes on long-running worker threads that pull the next request
+    themselves (engine/scheduler.py ``_stage_on_threads``); 0 = one event-loop
+    round trip per request (custom stagers always take that path)."""
+    return _get_bool("THREAD_STAGING", True)
+
+
 def checksum_enabled() -> bool:
     """Record an hs64 checksum of every blob a take writes
     (``.snapshot_checksums/<rank>``, ops/checksum.py); ``Snapshot.verify``

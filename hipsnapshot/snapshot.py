@@ -225,8 +225,12 @@ class Snapshot:
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.async_take")
         with paused_gc():
-            return cls._async_take(path, app_state, pg, replicated, storage_options,
-                                   _custom_tensor_prepare_func, quantize, compression)
+            pending = cls._async_take(path, app_state, pg, replicated, storage_options,
+                                      _custom_tensor_prepare_func, quantize, compression)
+        # the commit thread starts draining only now: its staging workers would
+        # otherwise hold the GIL while this thread is still on its way out
+        pending._go.set()
+        return pending
 
     @classmethod
     def _async_take(cls, path, app_state, pg, replicated, storage_options,
@@ -835,6 +839,7 @@ class PendingSnapshot:
         self._done = False
         self._storage_options = storage_options
         self.stats: Dict[str, float] = {}
+        self._go = threading.Event()  # set by async_take once it is returning
         store = get_or_create_store(comm) if comm.get_world_size() > 1 else None
         self.thread = threading.Thread(
             target=self._complete_snapshot, name="hipsnapshot-commit",
@@ -848,6 +853,7 @@ class PendingSnapshot:
                            storage: StoragePlugin, event_loop: asyncio.AbstractEventLoop,
                            store, nonce: str, plan=None) -> None:
         # WARNING: no collectives in this thread
+        self._go.wait()
         barrier = None
         if store is not None:
             barrier = _commit_barrier(store, path, nonce, rank, world_size)
