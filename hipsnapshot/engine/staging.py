@@ -226,6 +226,34 @@ def _read_u64_device(dev: int, slot: int, addr: int) -> int:
         pb.release()
 
 
+_encode_locks: dict = {}
+_encode_locks_mu = threading.Lock()
+
+
+@contextmanager
+def _encode_turn(dev: int, nbytes: int) -> Iterator[None]:
+    """Large HSZ1 encodes take turns per device (``HIPSNAPSHOT_SERIAL_ENCODE``).
+
+    Encodes launched by several staging threads at once share the CUs, so
+    each finishes only when all do: at the start of a take four 512 MiB
+    chunks were encoded together and the first DMA waited ~2.3 ms for them.
+    Taking turns, each runs on the whole chip (~1 TB/s) and its DMA starts
+    as soon as it is done; the encoder stays far ahead of PCIe either way.
+    Encodes below 256 MiB (slabs) finish in ~0.1 ms and keep running
+    side by side (serialising them measured slightly slower)."""
+    from .. import knobs
+
+    if nbytes < (256 << 20) or not knobs.serial_encode():
+        yield
+        return
+    lock = _encode_locks.get(dev)
+    if lock is None:
+        with _encode_locks_mu:
+            lock = _encode_locks.setdefault(dev, threading.Lock())
+    with lock:
+        yield
+
+
 def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dict
                            ) -> StagedBuffer:
     """HSZ1-encode a contiguous device byte tensor on the copy stream, then
@@ -243,10 +271,11 @@ def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dic
         return _encode_on_host(dev, slot, src_u8, codec)
     t_a = time.perf_counter()
     _join_current_stream(dev, slot)
-    hsz.launch_encode(src_u8, int(codec["w"]), stream, int(codec["frame_bytes"]), out, total,
-                      meta)
-    t_l = time.perf_counter()
-    nbytes = _read_u64_device(dev, slot, total.data_ptr())
+    with _encode_turn(dev, src_u8.numel()):
+        hsz.launch_encode(src_u8, int(codec["w"]), stream, int(codec["frame_bytes"]), out,
+                          total, meta)
+        t_l = time.perf_counter()
+        nbytes = _read_u64_device(dev, slot, total.data_ptr())
     t_n = time.perf_counter()
     pb, staged = _pinned_staged(nbytes)
     t_p = time.perf_counter()

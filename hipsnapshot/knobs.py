@@ -120,6 +120,12 @@ def get_d2h_engine() -> str:
     return v
 
 
+def serial_encode() -> bool:
+    """Staging threads take turns launching (and waiting for) HSZ1 encodes on
+    a device instead of sharing the CUs (engine/staging.py ``_encode_turn``)."""
+    return _get_bool("SERIAL_ENCODE", True)
+
+
 def get_gil_switch_us() -> int:
     """GIL switch interval (microseconds) while a take / restore runs on the
     calling thread; 0 = leave Python's (5000)."""
