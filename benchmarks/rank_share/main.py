@@ -123,14 +123,26 @@ def main() -> None:
         total.append(time.perf_counter() - t0)
     refs = {k: v._local_tensor.clone() for k, v in params.items()}
     rtimes = []
+    r_per_val = {v: [] for v in ab_vals}
     for _ in range(args.restore_iters):
-        for v in params.values():
-            v._local_tensor.zero_()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        Snapshot(path).restore(app_state)
-        torch.cuda.synchronize()
-        rtimes.append(time.perf_counter() - t0)
+        for val in ab_vals:
+            if ab_name:
+                os.environ[ab_name] = val
+            for v in params.values():
+                v._local_tensor.zero_()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            Snapshot(path).restore(app_state)
+            torch.cuda.synchronize()
+            rtimes.append(time.perf_counter() - t0)
+            r_per_val[val].append(rtimes[-1])
+    if ab_name and args.restore_iters > 1:
+        print(json.dumps({"bench": "rank_share_restore_ab", "world": args.world,
+                          "knob": ab_name, "compression": args.compression,
+                          "restore_ms": {v: {"median": round(statistics.median(t) * 1e3, 2),
+                                             "min": round(min(t) * 1e3, 2)}
+                                         for v, t in r_per_val.items()}}), flush=True)
+        os.environ[ab_name] = ab_vals[0]
     ok = all(torch.equal(refs[k], app_state["model"][k]._local_tensor) for k in refs)
     med = statistics.median(times)
     print(json.dumps({

@@ -529,27 +529,54 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
     del scratch
 
 
+_elem_sizes: dict = {}
+
+
+def _elem_size(dtype: torch.dtype) -> int:
+    es = _elem_sizes.get(dtype)
+    if es is None:
+        es = _elem_sizes[dtype] = torch.empty(0, dtype=dtype).element_size()
+    return es
+
+
 def _copy_regions(scratch: torch.Tensor, regions, dev: int, slot: int) -> None:
     """ONE copy/cast launch from the device buffer ``scratch`` (region offsets
     are relative to it) into every destination view, then a stream sync."""
+    t0 = time.perf_counter()
     batch = native.CopyBatch()
     fallbacks = []
+    base = scratch.data_ptr()
     for src_dtype, src_shape, off, narrows, dst in regions:
-        es = torch.empty(0, dtype=src_dtype).element_size()
-        n = 1
-        for z in src_shape:
-            n *= int(z)
-        src = scratch[off: off + n * es].view(src_dtype).view(list(src_shape))
-        if narrows:
-            for d, s, ln in narrows:
-                src = src.narrow(d, s, ln)
+        es = _elem_size(src_dtype)
         if native.can_cast_on_device(src_dtype, dst.dtype) and dst.dim() <= native.MAX_DIMS:
-            batch.add(src.data_ptr(), src.dtype, src.stride(), dst.data_ptr(), dst.dtype,
-                      dst.stride(), list(src.shape), src.element_size())
+            # the source view's pointer / shape / strides in plain integers (a
+            # C-order block at ``off``, narrowed): no torch view per region
+            shape = [int(z) for z in src_shape]
+            strides = _contig_strides(shape)
+            ptr = base + off
+            if narrows:
+                for d, st, ln in narrows:
+                    ptr += st * strides[d] * es
+                    shape[d] = ln
+            batch.add(ptr, src_dtype, strides, dst.data_ptr(), dst.dtype, dst.stride(), shape,
+                      es)
         else:
+            n = 1
+            for z in src_shape:
+                n *= int(z)
+            src = scratch[off: off + n * es].view(src_dtype).view(list(src_shape))
+            if narrows:
+                for d, st, ln in narrows:
+                    src = src.narrow(d, st, ln)
             fallbacks.append((src, dst))
+    t1 = time.perf_counter()
     keep = batch.launch(dev, native.copy_stream(dev, slot), sync=False)
+    t2 = time.perf_counter()
     native.stream_sync(dev, slot)
+    t3 = time.perf_counter()
+    timeline.add("regions_build", "h2d", t0, t1, n=len(regions))
+    timeline.add("regions_launch", "h2d", t1, t2)
+    timeline.add("dec_wait", "h2d", t2, t3)
     if keep is not None:
         keep[0].release()
     if fallbacks:
@@ -589,23 +616,48 @@ def _scatter_compressed(span, regions, dev: int, producer: Optional[int] = None)
                 and dst.dtype == src_dtype and dst.is_contiguous()
                 and dst.data_ptr() % 16 == 0):
             direct = dst
+    t0 = time.perf_counter()
     enc = torch.empty(c_n, dtype=torch.uint8, device=f"cuda:{dev}")
-    offs = torch.tensor([o - c_lo for o in h.offsets[first:last + 1]], dtype=torch.int64)
-    offs_dev = torch.empty(offs.numel(), dtype=torch.int64, device=f"cuda:{dev}")
+    # frame offsets go up from pinned memory: a pageable source would make
+    # the async H2D wait for the encoded frames' copy queued before it
+    n_offs = last - first + 1
+    offs_pb = native.PinnedBuffer(8 * n_offs)
+    offs = np.frombuffer(offs_pb.view, dtype=np.int64, count=n_offs)
+    offs[:] = np.asarray(h.offsets[first:last + 1], dtype=np.int64) - c_lo
+    try:
+        _decode_span(span, regions, dev, slot, direct, enc, offs_pb, n_offs, c_n, log_lo, log_n,
+                     first, last, t0)
+    finally:
+        del offs
+        try:
+            native.stream_sync(dev, slot)  # no-op normally; on errors: H2D done
+        finally:
+            offs_pb.release()
+
+
+def _decode_span(span, regions, dev, slot, direct, enc, offs_pb, n_offs, c_n, log_lo, log_n,
+                 first, last, t0) -> None:
+    h = span.header
+    offs_dev = torch.empty(n_offs, dtype=torch.int64, device=f"cuda:{dev}")
     out = None if direct is not None else torch.empty(log_n, dtype=torch.uint8,
                                                      device=f"cuda:{dev}")
+    t1 = time.perf_counter()
     _join_current_stream(dev, slot)
     native.memcpy(dev, slot, enc.data_ptr(), span.buf.addr, c_n, native.H2D, None, sync=False)
-    native.memcpy(dev, slot, offs_dev.data_ptr(), offs.data_ptr(), offs.numel() * 8,
-                  native.H2D, None, sync=False)
+    native.memcpy(dev, slot, offs_dev.data_ptr(), offs_pb.ptr, 8 * n_offs, native.H2D, None,
+                  sync=False)
     stream = native.copy_stream(dev, slot)
     err = native.DecodeErrorWord()
     native.hsz_decode_gpu(dev, enc.data_ptr(), offs_dev.data_ptr(), first, last - first,
                           h.logical_size, h.elem_width, h.frame_bytes,
                           (direct if direct is not None else out).data_ptr(), stream,
                           err.addr)
+    t2 = time.perf_counter()
+    timeline.add("dec_alloc", "h2d", t0, t1)
+    timeline.add("dec_launch", "h2d", t1, t2)
     if direct is not None:
         native.stream_sync(dev, slot)
+        timeline.add("dec_wait", "h2d", t2, time.perf_counter(), bytes=c_n)
         err.check(f"frames [{first}, {last})")
         return
     shift = span.lo - log_lo

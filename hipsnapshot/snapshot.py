@@ -477,29 +477,35 @@ class Snapshot:
         if stateful is None:
             return
         with timeline.span("restore_plan_view"):
-            manifest, merged = get_manifest_for_rank(self.metadata, comm.get_rank())
-            _, flat = flatten(_state_dict_view(stateful), prefix=key)
-        flat = {k: v for k, v in flat.items() if isinstance(v, torch.Tensor) or is_sharded(v)}
-        prefix = flat_prefix(key)
-        manifest = {k: v for k, v in manifest.items()
-                    if k == prefix or k.startswith(prefix + "/")}
-        merged_here = {k: v for k, v in merged.items() if k.startswith(prefix + "/")}
-        handle_sharded_tensor_elasticity(manifest, merged_here, list(flat.keys()))
+            with timeline.span("manifest_for_rank"):
+                manifest, merged = get_manifest_for_rank(self.metadata, comm.get_rank())
+            with timeline.span("state_dict_view"):
+                _, flat = flatten(_state_dict_view(stateful), prefix=key)
+        with timeline.span("restore_filter"):
+            flat = {k: v for k, v in flat.items()
+                    if isinstance(v, torch.Tensor) or is_sharded(v)}
+            prefix = flat_prefix(key)
+            manifest = {k: v for k, v in manifest.items()
+                        if k == prefix or k.startswith(prefix + "/")}
+            merged_here = {k: v for k, v in merged.items() if k.startswith(prefix + "/")}
+            handle_sharded_tensor_elasticity(manifest, merged_here, list(flat.keys()))
         containers: Dict[str, Entry] = {}
         reads: List[ReadReq] = []
         futs = {}
-        for logical, entry in manifest.items():
-            if is_container_entry(entry):
-                containers[logical] = entry
-                continue
-            rrs, fut = prepare_read(entry, obj_out=flat.get(logical),
-                                    trust_objects=self.trust_objects)
-            reads += rrs
-            futs[logical] = fut
-            flat.pop(logical, None)
-        if not knobs.is_batching_disabled():
-            reads = batch_read_requests(reads)
-        reads = order_reads_for_pipeline(reads)
+        with timeline.span("prepare_read", n=len(manifest)):
+            for logical, entry in manifest.items():
+                if is_container_entry(entry):
+                    containers[logical] = entry
+                    continue
+                rrs, fut = prepare_read(entry, obj_out=flat.get(logical),
+                                        trust_objects=self.trust_objects)
+                reads += rrs
+                futs[logical] = fut
+                flat.pop(logical, None)
+        with timeline.span("batch_reads", n=len(reads)):
+            if not knobs.is_batching_disabled():
+                reads = batch_read_requests(reads)
+            reads = order_reads_for_pipeline(reads)
         budget = get_process_memory_budget_bytes(comm)
         with timeline.span("read_pipeline", n=len(reads)):
             sync_execute_read_reqs(reads, storage, budget, comm.get_rank(), loop)

@@ -7,7 +7,7 @@ mkdir -p $HIPSNAPSHOT_BENCH_DIR
 tag=$(echo "$AB" | tr '=,' '__')
 for w in ${WS:-8 1}; do for c in ${COMP:-hsz1}; do
   timeout -k 10 300 python benchmarks/rank_share/main.py --world $w --compression $c --steps ${STEPS:-25} --warmup 2 \
-      --async-iters 1 --restore-iters 1 --ab "$AB" > $out/${tag}_w${w}_$c.json 2> $out/${tag}_w${w}_$c.err \
+      --async-iters 1 --restore-iters ${RITERS:-1} --ab "$AB" > $out/${tag}_w${w}_$c.json 2> $out/${tag}_w${w}_$c.err \
       || { echo FAIL; tail $out/${tag}_w${w}_$c.err; exit 1; }
-  grep rank_share_ab $out/${tag}_w${w}_$c.json
+  grep "rank_share_ab\|rank_share_restore_ab" $out/${tag}_w${w}_$c.json
 done; done
