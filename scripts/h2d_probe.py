@@ -24,7 +24,8 @@ def main():
     torch.cuda.set_device(dev)
     n = 46 << 20
     iters = 40
-    for nthreads in (1, 2, 4, 8):
+    serial = threading.Lock()
+    for nthreads, locked in ((1, False), (4, False), (4, True), (8, False), (8, True)):
         bufs = [native.PinnedBuffer(n) for _ in range(nthreads)]
         dsts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(nthreads)]
         call_ms = []
@@ -35,8 +36,13 @@ def main():
             slot = 20 + i
             for _ in range(iters):
                 t0 = time.perf_counter()
-                native.memcpy(0, slot, dsts[i].data_ptr(), bufs[i].ptr, n, native.H2D, None,
-                              sync=False)
+                if locked:
+                    with serial:
+                        native.memcpy(0, slot, dsts[i].data_ptr(), bufs[i].ptr, n, native.H2D,
+                                      None, sync=False)
+                else:
+                    native.memcpy(0, slot, dsts[i].data_ptr(), bufs[i].ptr, n, native.H2D, None,
+                                  sync=False)
                 t1 = time.perf_counter()
                 native.stream_sync(0, slot)
                 with lock:
@@ -51,7 +57,7 @@ def main():
         for t in ths:
             t.join()
         dt = time.perf_counter() - t0
-        print(json.dumps({"probe": "h2d_hipMemcpyAsync", "threads": nthreads,
+        print(json.dumps({"probe": "h2d_hipMemcpyAsync", "threads": nthreads, "locked": locked,
                           "GBps": round(nthreads * iters * n / dt / 1e9, 1),
                           "call_ms_p50": round(statistics.median(call_ms), 3),
                           "call_ms_max": round(max(call_ms), 3)}), flush=True)
