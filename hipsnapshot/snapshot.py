@@ -459,8 +459,9 @@ class Snapshot:
             app_state = dict(app_state)
             rng_item = self._pop_rng_state(app_state)
             gathered: List[Any] = [None] * comm.get_world_size()
-            comm.all_gather_object(gathered, list(app_state.keys()))
-            keys = sorted(set(itertools.chain.from_iterable(gathered)))
+            comm.all_gather_object(gathered, (list(app_state.keys()), socket.gethostname()))
+            keys = sorted(set(itertools.chain.from_iterable(g[0] for g in gathered)))
+            knobs.set_local_ranks_hint([g[1] for g in gathered].count(socket.gethostname()))
             for key in keys:
                 with timeline.span("load_stateful", key=key):
                     self._load_stateful(key, app_state.get(key), storage, comm, loop)
@@ -635,6 +636,7 @@ class Snapshot:
                            f"from replicated paths verified across all ranks: {rep}")
         keys = sorted(set(itertools.chain.from_iterable(g[2] for g in gathered)))
         hostnames = [g[3] for g in gathered]
+        knobs.set_local_ranks_hint(hostnames.count(socket.gethostname()))
         if knobs.get_memory_budget_override() is None:
             # seed the budget cache from this gather (no hostname collective later)
             import psutil

@@ -37,13 +37,21 @@ class FSStoragePlugin(StoragePlugin):
         self.root = root
         self.direct_io = bool(opts.get("direct_io", knobs.use_direct_io()))
         self.fsync = bool(opts.get("fsync", knobs.use_fsync()))
-        self.io_threads = int(opts.get("io_threads", knobs.get_io_threads()))
+        # None: knobs.get_io_threads() when the engine starts (it depends on
+        # how many ranks share this host, learnt by the take's first collective)
+        self._io_threads_opt = opts.get("io_threads")
         self._engine = None
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._pending: Dict[int, tuple] = {}
         self._native_ok = True
         self.bytes_written = 0
         self.bytes_read = 0
+
+    @property
+    def io_threads(self) -> int:
+        if self._io_threads_opt is not None:
+            return int(self._io_threads_opt)
+        return knobs.get_io_threads()
 
     # -- engine plumbing ---------------------------------------------------
 

@@ -70,3 +70,28 @@ def test_two_pipelines_share_one_budget():
 
     held, end = asyncio.run(main())
     assert held[0] <= 100 and end == 0
+
+
+def test_io_threads_follow_cpu_share_and_local_ranks(monkeypatch):
+    """Default native I/O workers: 2 x CPUs / ranks on the host, in [4, 16];
+    an explicit HIPSNAPSHOT_IO_THREADS wins."""
+    import os
+
+    from hipsnapshot import knobs
+
+    monkeypatch.delenv("HIPSNAPSHOT_IO_THREADS", raising=False)
+    monkeypatch.delenv("TORCHSNAPSHOT_IO_THREADS", raising=False)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))
+    try:
+        knobs.set_local_ranks_hint(1)
+        assert knobs.get_io_threads() == 16
+        knobs.set_local_ranks_hint(4)
+        assert knobs.get_io_threads() == 8
+        knobs.set_local_ranks_hint(8)
+        assert knobs.get_io_threads() == 4
+        knobs.set_local_ranks_hint(64)
+        assert knobs.get_io_threads() == 4
+        monkeypatch.setenv("HIPSNAPSHOT_IO_THREADS", "12")
+        assert knobs.get_io_threads() == 12
+    finally:
+        knobs.set_local_ranks_hint(1)
