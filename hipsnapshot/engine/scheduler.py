@@ -106,6 +106,26 @@ def get_process_memory_budget_bytes(pg=None) -> int:
     return budget
 
 
+_aux = {"pid": None, "pool": None}
+_aux_lock = threading.Lock()
+
+
+def aux_pool() -> ThreadPoolExecutor:
+    """Process-wide pool for short host-side helpers of the pipelines (host
+    hashing, pinned read destinations).  An event loop's default executor
+    would do, but every take / restore runs its own loop, so its threads
+    were started and joined again on every call."""
+    pool = _aux["pool"]
+    if pool is None or _aux["pid"] != os.getpid():
+        with _aux_lock:
+            if _aux["pool"] is None or _aux["pid"] != os.getpid():
+                _aux["pool"] = ThreadPoolExecutor(max_workers=8,
+                                                  thread_name_prefix="hipsnapshot-aux")
+                _aux["pid"] = os.getpid()
+            pool = _aux["pool"]
+    return pool
+
+
 class PipelineStats:
     def __init__(self) -> None:
         self.t_start = time.monotonic()
@@ -239,7 +259,7 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                 # host-staged blob: hash it on the host while it is written
                 # (both only read the buffer; the GPU stager hashed the rest)
                 hashing = asyncio.get_running_loop().run_in_executor(
-                    None, checksum.hs64_host, buf.addr, buf.nbytes)
+                    aux_pool(), checksum.hs64_host, buf.addr, buf.nbytes)
             async with io_sem:
                 if failure:  # the snapshot is failing: do not start more writes
                     return
@@ -485,7 +505,7 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                     # whole blob: ONE read of header + frames (no header round
                     # trip; the read enters the engine queue in request order)
                     full = await asyncio.get_running_loop().run_in_executor(
-                        None, rr.buffer_consumer.get_compressed_read_dest, stored)
+                        aux_pool(), rr.buffer_consumer.get_compressed_read_dest, stored)
                     if full is None:
                         full = as_staged(bytearray(max(stored, 1)))
                     dest = full
@@ -507,7 +527,7 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                     c_lo, c_hi = header.offsets[first], header.offsets[last]
                     hsz.validate_offsets(header, header.offsets[-1])
                     dest = await asyncio.get_running_loop().run_in_executor(
-                        None, rr.buffer_consumer.get_compressed_read_dest, c_hi - c_lo)
+                        aux_pool(), rr.buffer_consumer.get_compressed_read_dest, c_hi - c_lo)
                     if dest is None:
                         dest = as_staged(bytearray(max(c_hi - c_lo, 1)))
                     body_io = ReadIO(path=rr.path, byte_range=(c_lo, c_hi), dest=dest)
@@ -543,7 +563,7 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                 # pinned-pool misses cost a hipHostMalloc: keep them off the
                 # event loop so completions of earlier reads are not delayed
                 dest = await asyncio.get_running_loop().run_in_executor(
-                    None, rr.buffer_consumer.get_read_dest, nbytes)
+                    aux_pool(), rr.buffer_consumer.get_read_dest, nbytes)
             read_io = ReadIO(path=rr.path, byte_range=rr.byte_range, dest=dest)
             async with io_sem:
                 if failing:

@@ -273,15 +273,17 @@ class Snapshot:
             pass
         except Exception as e:  # noqa: BLE001 - e.g. plugins without delete
             logger.debug(f"could not remove previous metadata: {e}")
-        # the previous take's checksums go with its commit (this take may run
-        # with checksums off, or on fewer ranks); every rank writes its own
-        # file only after the metadata gather, i.e. after this
-        try:
-            loop.run_until_complete(storage.delete_dir(checksum.CHECKSUM_DIR))
-        except (FileNotFoundError, KeyError, NotImplementedError):
-            pass
-        except Exception as e:  # noqa: BLE001
-            logger.debug(f"could not remove previous checksums: {e}")
+        # a take with checksums rewrites every rank's file (verify reads only
+        # ranks < world size); one without them must not leave the previous
+        # take's behind.  (Removing the directory on every take cost ~1.5 ms
+        # of rank 0's critical path on an overlay filesystem.)
+        if not knobs.checksum_enabled():
+            try:
+                loop.run_until_complete(storage.delete_dir(checksum.CHECKSUM_DIR))
+            except (FileNotFoundError, KeyError, NotImplementedError):
+                pass
+            except Exception as e:  # noqa: BLE001
+                logger.debug(f"could not remove previous checksums: {e}")
 
     @classmethod
     def _take_impl(cls, path: str, app_state: AppState, replicated: Set[str],
@@ -768,6 +770,8 @@ class _BackgroundGather:
     adopts the caller's HIP device (current device is per thread and RCCL
     object collectives stage their bytes on it)."""
 
+    _pool: Dict[str, Any] = {"pid": None, "ex": None}
+
     def __init__(self, fn, manifest, comm: Comm, plan) -> None:
         self._out: Dict[str, Any] = {}
         dev = torch.cuda.current_device() if torch.cuda.is_initialized() else None
@@ -781,14 +785,22 @@ class _BackgroundGather:
             except BaseException as e:  # noqa: BLE001 - re-raised in result()
                 self._out["e"] = e
 
-        self._th = threading.Thread(target=run, name="hipsnapshot-manifest", daemon=True)
-        self._th.start()
+        # one long-lived helper thread per process (a new thread per take
+        # cost its start-up on the take's critical path)
+        pool = _BackgroundGather._pool
+        if pool["ex"] is None or pool["pid"] != os.getpid():
+            from concurrent.futures import ThreadPoolExecutor
+
+            pool["ex"] = ThreadPoolExecutor(max_workers=1,
+                                            thread_name_prefix="hipsnapshot-manifest")
+            pool["pid"] = os.getpid()
+        self._fut = pool["ex"].submit(run)
 
     def join_quietly(self) -> None:
-        self._th.join()
+        self._fut.result()
 
     def result(self):
-        self._th.join()
+        self._fut.result()
         if "e" in self._out:
             raise self._out["e"]
         return self._out["v"]
