@@ -95,3 +95,90 @@ def test_io_threads_follow_cpu_share_and_local_ranks(monkeypatch):
         assert knobs.get_io_threads() == 12
     finally:
         knobs.set_local_ranks_hint(1)
+
+
+class _ThreadStager(BufferStager):
+    """Stager with the synchronous entry point: staged on scheduler workers."""
+
+    thread_staging = True
+
+    def __init__(self, n, track, fail=False):
+        self.n, self.track, self.fail = n, track, fail
+
+    async def stage_buffer(self, executor=None):
+        return self.stage_buffer_sync()
+
+    def stage_buffer_sync(self):
+        import threading
+        import time
+
+        if self.fail:
+            raise RuntimeError("staging failed")
+        with self.track["lock"]:
+            self.track["live"] += self.n
+            self.track["peak"] = max(self.track["peak"], self.track["live"])
+            self.track["threads"].add(threading.get_ident())
+        time.sleep(0.002)
+
+        def release():
+            with self.track["lock"]:
+                self.track["live"] -= self.n
+
+        return StagedBuffer(bytearray(self.n), release=release)
+
+    def get_staging_cost_bytes(self):
+        return self.n
+
+
+class _SlowStorage(MemoryStoragePlugin):
+    async def write(self, write_io):
+        await asyncio.sleep(0.003)
+        await super().write(write_io)
+
+
+def _track():
+    import threading
+
+    return {"lock": threading.Lock(), "live": 0, "peak": 0, "threads": set()}
+
+
+def test_thread_staging_respects_budget_and_writes_everything():
+    """Worker threads pull requests themselves: host memory held by staged,
+    not yet written buffers stays within the budget (one oversized request
+    aside), several workers take part, and every blob is written."""
+    from hipsnapshot.storage.memory import _STORE
+
+    track = _track()
+    reqs = [WriteReq(path=f"b{i}", buffer_stager=_ThreadStager(100 + i, track))
+            for i in range(40)]
+
+    async def main():
+        storage = _SlowStorage(root="tstage")
+        pending = await execute_write_reqs(reqs, storage, memory_budget_bytes=350, rank=0,
+                                           stage_threads=4, io_concurrency=4)
+        await pending.complete()
+        return pending.stats
+
+    stats = asyncio.new_event_loop().run_until_complete(main())
+    assert stats.bytes_written == sum(100 + i for i in range(40))
+    assert all(f"tstage/b{i}" in _STORE for i in range(40))
+    assert track["peak"] <= 350 and track["live"] == 0
+    assert len(track["threads"]) > 1
+
+
+def test_thread_staging_failure_stops_workers_and_releases_buffers():
+    track = _track()
+    reqs = [WriteReq(path=f"f{i}", buffer_stager=_ThreadStager(64, track, fail=(i == 5)))
+            for i in range(30)]
+
+    async def main():
+        storage = _SlowStorage(root="tfail")
+        pending = await execute_write_reqs(reqs, storage, memory_budget_bytes=256, rank=0,
+                                           stage_threads=3, io_concurrency=2)
+        await pending.complete()
+
+    import pytest
+
+    with pytest.raises(RuntimeError, match="staging failed"):
+        asyncio.new_event_loop().run_until_complete(main())
+    assert track["live"] == 0  # every staged buffer went back
