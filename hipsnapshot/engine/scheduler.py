@@ -373,8 +373,7 @@ async def _stage_on_threads(pending: deque, nthreads: int, executor: ThreadPoolE
                         return
                     wr = pending[0]
                     cost = wr.buffer_stager.get_staging_cost_bytes()
-                    if gate.in_use + cost <= gate.limit or gate.in_use == 0:
-                        gate.in_use += cost
+                    if gate.try_admit(cost):  # re-enters cond (an RLock)
                         pending.popleft()
                         break
                     cond.wait(0.05)
