@@ -33,34 +33,32 @@ inline uint64_t mix64(uint64_t x) {
   return x;
 }
 
+// Sum over `nw` whole words.  One plain loop the compiler vectorises; the
+// clones give it 64-bit vector multiplies (AVX-512DQ vpmullq) or AVX2 where
+// the CPU has them, picked at load time (the .so is built once, here, and
+// runs on whichever host the GPU box has).
+__attribute__((target_clones("arch=skylake-avx512", "avx2", "default")))
+uint64_t words_sum(const uint8_t* p, uint64_t nw, uint64_t w0) {
+  uint64_t s = 0;
+  for (uint64_t i = 0; i < nw; ++i) {
+    uint64_t a;
+    std::memcpy(&a, p + 8 * i, 8);
+    s += mix64(a ^ ((w0 + i + 1) * kM1));
+  }
+  return s;
+}
+
 // Sum over the bytes [p, p + n) whose first word has global index `w0`.
 uint64_t partial(const uint8_t* p, uint64_t n, uint64_t w0) {
   const uint64_t nw = n / 8;
-  uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // 4 independent chains
-  uint64_t i = 0;
-  for (; i + 4 <= nw; i += 4) {
-    uint64_t a, b, c, d;
-    std::memcpy(&a, p + 8 * i, 8);
-    std::memcpy(&b, p + 8 * i + 8, 8);
-    std::memcpy(&c, p + 8 * i + 16, 8);
-    std::memcpy(&d, p + 8 * i + 24, 8);
-    s0 += mix64(a ^ ((w0 + i + 1) * kM1));
-    s1 += mix64(b ^ ((w0 + i + 2) * kM1));
-    s2 += mix64(c ^ ((w0 + i + 3) * kM1));
-    s3 += mix64(d ^ ((w0 + i + 4) * kM1));
-  }
-  for (; i < nw; ++i) {
-    uint64_t a;
-    std::memcpy(&a, p + 8 * i, 8);
-    s0 += mix64(a ^ ((w0 + i + 1) * kM1));
-  }
+  uint64_t s = words_sum(p, nw, w0);
   const uint64_t tail = n - 8 * nw;
   if (tail) {
     uint64_t t = 0;
     std::memcpy(&t, p + 8 * nw, tail);
-    s1 += mix64(t ^ ((w0 + nw + 1) * kM1));
+    s += mix64(t ^ ((w0 + nw + 1) * kM1));
   }
-  return s0 + s1 + s2 + s3;
+  return s;
 }
 
 }  // namespace

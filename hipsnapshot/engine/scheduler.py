@@ -258,8 +258,9 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             if want_sums and buf.checksum is None:
                 # host-staged blob: hash it on the host while it is written
                 # (both only read the buffer; the GPU stager hashed the rest)
+                # (2 threads per blob: several blobs hash at once on the pool)
                 hashing = asyncio.get_running_loop().run_in_executor(
-                    aux_pool(), checksum.hs64_host, buf.addr, buf.nbytes)
+                    aux_pool(), checksum.hs64_host, buf.addr, buf.nbytes, 2)
             async with io_sem:
                 if failure:  # the snapshot is failing: do not start more writes
                     return

@@ -112,6 +112,12 @@ def _pinned_staged(nbytes: int) -> Tuple[native.PinnedBuffer, StagedBuffer]:
 _sdma_ok: dict = {}
 
 
+def _is_managed(t: torch.Tensor) -> bool:
+    from ..ops.uvm import is_uvm_tensor
+
+    return is_uvm_tensor(t)
+
+
 def _checksums() -> bool:
     from .. import knobs
 
@@ -185,9 +191,12 @@ def d2h_tensor(t: torch.Tensor, producer: Optional[int],
     t_s = time.perf_counter()
     try:
         if t.is_contiguous():
-            if _checksums():
+            if _checksums() and not _is_managed(t):
                 # hash the bytes in HBM on a side stream (ordered after the
-                # producer) while the DMA moves them; both only read them
+                # producer) while the DMA moves them; both only read them.
+                # (Managed tables usually live in host memory: a GPU hash
+                # would pull them over the PCIe link the DMA is using -- the
+                # writer hashes the pinned copy on the host instead.)
                 native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
                 hslot = hash_slot(slot)
                 hs = checksum.device_hash_start(dev, hslot, t.data_ptr(), nbytes, slot)
