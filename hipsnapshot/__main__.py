@@ -3,6 +3,8 @@
     python -m hipsnapshot verify PATH [--json] [--concurrency N]
         re-read every blob of the snapshot at PATH and check its recorded
         hs64 checksum (hipsnapshot/verify.py); exit status 0 iff all match
+    torchrun --nproc-per-node N -m hipsnapshot verify PATH --distributed
+        the same, each rank checking 1/N of the blobs
     python -m hipsnapshot info PATH
         print the snapshot's version, world size and entry counts
 """
@@ -18,7 +20,21 @@ from collections import Counter
 def _verify(args) -> int:
     from .verify import verify_snapshot
 
-    rep = verify_snapshot(args.path, concurrency=args.concurrency)
+    if args.distributed:
+        # under torchrun: every rank checks its share of the blobs (gloo;
+        # only the report crosses the network)
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    rep = verify_snapshot(args.path, concurrency=args.concurrency,
+                          distributed=args.distributed)
+    if args.distributed:
+        import torch.distributed as dist
+
+        rank = dist.get_rank()
+        dist.destroy_process_group()
+        if rank != 0:
+            return 0 if rep.ok else 1
     if args.json:
         print(json.dumps(rep.as_dict()))
     else:
@@ -50,6 +66,8 @@ def main(argv=None) -> int:
     v.add_argument("path")
     v.add_argument("--json", action="store_true")
     v.add_argument("--concurrency", type=int, default=4)
+    v.add_argument("--distributed", action="store_true",
+                   help="split the blobs over the ranks of a torchrun launch")
     v.set_defaults(fn=_verify)
     i = sub.add_parser("info", help="summarise a snapshot's metadata")
     i.add_argument("path")

@@ -533,13 +533,16 @@ class Snapshot:
     def get_manifest(self) -> Dict[str, Entry]:
         return copy.deepcopy(self.metadata.manifest)
 
-    def verify(self, concurrency: int = 4):
+    def verify(self, concurrency: int = 4, distributed: bool = False):
         """Re-read every blob and check it against the hs64 checksum its take
         recorded (hipsnapshot extension; returns ``verify.VerifyReport``,
-        ``.ok`` is True iff every blob matched)."""
+        ``.ok`` is True iff every blob matched).  ``distributed``: every rank
+        of this snapshot's process group checks its share of the blobs (a
+        collective call) and gets the merged report."""
         from .verify import verify_snapshot
 
-        return verify_snapshot(self.path, self._storage_options, concurrency)
+        return verify_snapshot(self.path, self._storage_options, concurrency,
+                               distributed=distributed, pg=self.pg)
 
     def read_object(self, path: str, obj_out: Optional[T] = None,
                     memory_budget_bytes: Optional[int] = None) -> T:

@@ -78,9 +78,9 @@ async def _read_checksums(storage: StoragePlugin, world_size: int) -> Optional[D
 
 
 async def _verify(storage: StoragePlugin, manifest: Dict[str, Entry], world_size: int,
-                  report: VerifyReport, concurrency: int) -> None:
+                  report: VerifyReport, concurrency: int, part: int = 0, parts: int = 1) -> None:
     sums = await _read_checksums(storage, world_size)
-    locs = sorted(blob_locations(manifest))
+    locs = sorted(blob_locations(manifest))[part::parts]
     report.blobs = len(locs)
     if sums is None:
         report.has_checksums = False
@@ -113,21 +113,43 @@ async def _verify(storage: StoragePlugin, manifest: Dict[str, Entry], world_size
 
 
 def verify_snapshot(path: str, storage_options: Optional[Dict[str, Any]] = None,
-                    concurrency: int = 4) -> VerifyReport:
-    """Check every blob of the committed snapshot at ``path`` (see module doc)."""
+                    concurrency: int = 4, distributed: bool = False, pg=None) -> VerifyReport:
+    """Check every blob of the committed snapshot at ``path`` (see module doc).
+
+    ``distributed``: a collective over ``pg`` (default: the world group);
+    every rank checks 1/world_size of the blobs and all ranks return the
+    merged report (one object all-gather)."""
+    from .parallel.comm import Comm
     from .snapshot import Snapshot
     from .storage.registry import url_to_storage_plugin_in_event_loop
 
     t0 = time.monotonic()
+    comm = Comm(pg) if distributed else None
+    rank, ws = (comm.get_rank(), comm.get_world_size()) if comm is not None else (0, 1)
     report = VerifyReport(path=path)
     loop = asyncio.new_event_loop()
     storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
     try:
         md = Snapshot._read_snapshot_metadata(storage, loop)
         loop.run_until_complete(_verify(storage, md.manifest, md.world_size, report,
-                                        concurrency))
+                                        concurrency, rank, ws))
     finally:
         storage.sync_close(loop)
         loop.close()
     report.seconds = time.monotonic() - t0
+    if ws > 1:
+        parts: List[Any] = [None] * ws
+        comm.all_gather_object(parts, report)
+        merged = VerifyReport(path=path, has_checksums=all(p.has_checksums for p in parts))
+        for p in parts:
+            merged.blobs += p.blobs
+            merged.checked += p.checked
+            merged.bytes += p.bytes
+            merged.seconds = max(merged.seconds, p.seconds)
+            merged.mismatched += p.mismatched
+            merged.missing_blobs += p.missing_blobs
+            merged.missing_checksums += p.missing_checksums
+        for lst in (merged.mismatched, merged.missing_blobs, merged.missing_checksums):
+            lst.sort()
+        return merged
     return report

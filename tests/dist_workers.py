@@ -340,3 +340,32 @@ def committed_on_return(path):
         out = StateDict(t=torch.zeros(1000), step=-1)
         Snapshot(p).restore({"sd": out})
         assert out["step"] == i and torch.equal(out["t"], torch.full((1000,), float(rank + i)))
+
+
+def distributed_verify(path: str):
+    """Every rank checks its share of the blobs; all get the merged report,
+    and a corrupted blob shows up in it whichever rank checked it."""
+    rank = dist.get_rank()
+    ws = dist.get_world_size()
+    torch.manual_seed(rank)
+    sd = StateDict(w=torch.randn(1000 + rank, 17), **{f"t{i}": torch.randn(300, 40)
+                                                    for i in range(6)})
+    snap = Snapshot.take(path, {"sd": sd}, replicated=[])
+    rep = snap.verify(distributed=True)
+    assert rep.ok and rep.checked == rep.blobs > 0, rep
+    whole = snap.verify()  # local, single-process
+    assert whole.blobs == rep.blobs and whole.ok
+    dist.barrier()
+    if rank == 0:
+        victim = sorted(
+            os.path.join(d, f) for d, _, fs in os.walk(path) for f in fs
+            if not os.path.relpath(os.path.join(d, f), path).startswith(".snapshot"))[-1]
+        with open(victim, "r+b") as f:
+            f.seek(3)
+            b = f.read(1)
+            f.seek(3)
+            f.write(bytes([b[0] ^ 0xFF]))
+    dist.barrier()
+    rep = snap.verify(distributed=True)
+    assert not rep.ok and len(rep.mismatched) == 1, rep
+    assert ws > 1

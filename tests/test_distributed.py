@@ -82,3 +82,7 @@ def test_take_returns_after_commit_on_every_rank(tmp_path):
     # reference quirk: take() returned before rank 0 wrote the metadata, so a
     # rank that read the snapshot at once could find nothing
     run_distributed(W.committed_on_return, 3, str(tmp_path / "c"))
+
+
+def test_distributed_verify(tmp_path):
+    run_distributed(W.distributed_verify, 3, str(tmp_path / "dv"))
