@@ -495,7 +495,7 @@ class Snapshot:
         containers: Dict[str, Entry] = {}
         reads: List[ReadReq] = []
         futs = {}
-        with timeline.span("prepare_read", n=len(manifest)):
+        with timeline.span("prepare_read", n=len(manifest)), staging.plan_scope():
             for logical, entry in manifest.items():
                 if is_container_entry(entry):
                     containers[logical] = entry
