@@ -368,6 +368,7 @@ async def _stage_on_threads(pending: deque, nthreads: int, executor: ThreadPoolE
 
     def worker() -> None:
         while True:
+            t_w = time.perf_counter()
             with cond:
                 while True:
                     if failure or not pending:
@@ -379,6 +380,7 @@ async def _stage_on_threads(pending: deque, nthreads: int, executor: ThreadPoolE
                         break
                     cond.wait(0.05)
             t_s = time.perf_counter()
+            timeline.add("admit", "stage", t_w, t_s)
             try:
                 buf = as_staged(wr.buffer_stager.stage_buffer_sync())
             except BaseException as e:  # noqa: BLE001 - reported by the caller

@@ -451,13 +451,17 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
 
 def _gather_encoded(members, total_bytes: int, producers, codec: dict) -> StagedBuffer:
     """Slab gather into HBM (one launch), HSZ1 encode, D2H of the encoded bytes."""
+    t0 = time.perf_counter()
     dev = device_of(members[0][0])
     slot = copy_slot()
     stream = native.copy_stream(dev, slot)
     for producer in producers:
         native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
+    t1 = time.perf_counter()
     try:
         slab = torch.zeros(total_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+        timeline.add("slab_join", "stage", t0, t1)
+        timeline.add("slab_zeros", "stage", t1, time.perf_counter())
     except torch.cuda.OutOfMemoryError:
         # no HBM for the slab: gather into host memory, encode on the CPU
         raw = gather_to_host(members, total_bytes, producers, via_device_slab=False)

@@ -21,6 +21,7 @@ different data path:
 from __future__ import annotations
 
 import os
+import time
 import uuid
 from collections import defaultdict
 from concurrent.futures import Executor
@@ -30,6 +31,7 @@ import torch
 
 from .. import knobs
 from ..engine import staging
+from ..utils.tracing import timeline
 from ..format.manifest import Entry, iter_tensor_entries
 from ..format.serialization import Serializer, string_to_dtype
 from ..io_types import (BufferConsumer, BufferStager, CompressedSpan, ReadReq, StagedBuffer,
@@ -133,11 +135,13 @@ class GPUBatchedBufferStager(BufferStager):
         return self._stage_sync()
 
     def _stage_sync(self) -> StagedBuffer:
+        t0 = time.perf_counter()
         for ev in {id(st.wait_event): st.wait_event for _, st in self.members
                    if st.wait_event is not None}.values():
             ev.synchronize()
         producers = sorted({st.producer for _, st in self.members if st.producer is not None})
         pairs = [(st._source(), lo) for (lo, _hi), st in self.members]
+        timeline.add("slab_sources", "stage", t0, time.perf_counter(), n=len(pairs))
         return staging.gather_to_host(pairs, self.total, producers,
                                       via_device_slab=knobs.use_gpu_gather_for_slabs(),
                                       codec=self.codec)
