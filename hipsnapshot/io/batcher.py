@@ -140,7 +140,7 @@ class GPUBatchedBufferStager(BufferStager):
                    if st.wait_event is not None}.values():
             ev.synchronize()
         producers = sorted({st.producer for _, st in self.members if st.producer is not None})
-        pairs = [(st._source(), lo) for (lo, _hi), st in self.members]
+        pairs = [(st._source_view(), lo) for (lo, _hi), st in self.members]
         timeline.add("slab_sources", "stage", t0, time.perf_counter(), n=len(pairs))
         return staging.gather_to_host(pairs, self.total, producers,
                                       via_device_slab=knobs.use_gpu_gather_for_slabs(),
