@@ -261,4 +261,60 @@ int hsg_sdma_d2h(int dev, void* dst, const void* src, uint64_t n, int max_engine
   return rc;
 }
 
+// Asynchronous form of hsg_sdma_d2h with one request: orders the copy after
+// `stream` (system-scope release, as above), submits it and returns at once
+// with *handle naming its completion signal.  The caller must pass the
+// handle to hsg_sdma_wait exactly once (the source and destination must stay
+// valid until then).  Staging workers submit a blob's copy and go on to
+// encode the next one while the engine works through its queue.
+int hsg_sdma_d2h_submit(int dev, void* dst, const void* src, uint64_t n, void* stream,
+                        uint64_t* handle) {
+  *handle = 0;
+  DevInfo* d = dev_info(dev);
+  if (!d) return -1;
+  if (n == 0) return 0;
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return -2;
+  {
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToSystem) !=
+        hipSuccess)
+      return -3;
+    e = hipEventRecord(ev, static_cast<hipStream_t>(stream));
+    if (e == hipSuccess) e = hipEventSynchronize(ev);
+    hipEventDestroy(ev);
+    if (e != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "release event: %s", hipGetErrorString(e));
+      return -4;
+    }
+  }
+  hsa_signal_t s = take_signal();
+  if (s.handle == 0) return -5;
+  g_api.signal_store(s, 1);
+  const hsa_status_t st = g_api.async_copy(dst, d->cpu, src, d->gpu, n, 0, nullptr, s);
+  if (st != HSA_STATUS_SUCCESS) {
+    give_signal(s);
+    snprintf(g_err, sizeof(g_err), "hsa_amd_memory_async_copy: status 0x%x", unsigned(st));
+    return -6;
+  }
+  *handle = s.handle;
+  return 0;
+}
+
+// Wait for a copy submitted by hsg_sdma_d2h_submit; 0 = done, < 0 = the
+// engine reported an error (the copy did not complete).  handle 0: no-op.
+int hsg_sdma_wait(uint64_t handle) {
+  if (handle == 0) return 0;
+  hsa_signal_t s;
+  s.handle = handle;
+  const hsa_signal_value_t v =
+      g_api.signal_wait(s, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+  give_signal(s);
+  if (v < 0) {
+    snprintf(g_err, sizeof(g_err), "SDMA copy reported an error (%ld)", long(v));
+    return -7;
+  }
+  return 0;
+}
+
 }  // extern "C"

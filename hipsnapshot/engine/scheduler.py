@@ -126,6 +126,26 @@ def aux_pool() -> ThreadPoolExecutor:
     return pool
 
 
+async def _wait_ready(buf: StagedBuffer) -> None:
+    """Wait (off the loop) for ``buf``'s asynchronous copy; a cancellation
+    waits for the copy anyway, then re-raises (the buffer must not be
+    released while the engine writes into it)."""
+    fut = asyncio.get_running_loop().run_in_executor(aux_pool(), buf.ready)
+    cancelled = False
+    while True:
+        try:
+            await asyncio.shield(fut)
+            break
+        except asyncio.CancelledError:
+            if fut.done():
+                break
+            cancelled = True
+    buf.ready = None
+    if cancelled:
+        raise asyncio.CancelledError()
+    fut.result()
+
+
 class PipelineStats:
     def __init__(self) -> None:
         self.t_start = time.monotonic()
@@ -255,6 +275,9 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     async def _write(wr: WriteReq, buf: StagedBuffer, cost: int) -> None:
         hashing = None
         try:
+            if buf.ready is not None:
+                # the blob's device -> host copy is still on the SDMA engine
+                await _wait_ready(buf)
             if want_sums and buf.checksum is None:
                 # host-staged blob: hash it on the host while it is written
                 # (both only read the buffer; the GPU stager hashed the rest)
@@ -279,6 +302,10 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             if hashing is not None and not hashing.done():
                 # the hash still reads the buffer: it must finish before release
                 await asyncio.gather(asyncio.shield(hashing), return_exceptions=True)
+            if buf.ready is not None:
+                # an early exit (failure, cancellation): the copy may still be
+                # writing into the buffer
+                await asyncio.gather(_wait_ready(buf), return_exceptions=True)
             buf.release()
             gate.release(cost)
             wake.set()

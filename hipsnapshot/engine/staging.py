@@ -169,6 +169,96 @@ def bulk_d2h(dev: int, slot: int, dst: int, src: int, nbytes: int,
     timeline.add("dma", "d2h", t_s, time.perf_counter(), bytes=nbytes, slot=slot)
 
 
+_dma_limits: dict = {}
+
+
+def _dma_limit(dev: int) -> threading.BoundedSemaphore:
+    lim = _dma_limits.get(dev)
+    if lim is None:
+        from .. import knobs
+
+        with _slot_lock:
+            lim = _dma_limits.setdefault(dev, threading.BoundedSemaphore(knobs.get_dma_inflight()))
+    return lim
+
+
+def d2h_staged(dev: int, slot: int, staged: StagedBuffer, src: int, nbytes: int,
+               keep: list, hash_handle: Optional[int] = None,
+               producer: Optional[int] = None) -> None:
+    """Device -> pinned copy of ``nbytes`` at ``src`` into ``staged`` (and the
+    hash started as ``hash_handle`` on ``hash_slot(slot)``, if any).
+
+    On the SDMA engines (``HIPSNAPSHOT_ASYNC_DMA``, default on) the copy is
+    only SUBMITTED here: ``staged.ready`` then waits for it (the writer calls
+    it before writing) and the staging worker goes on to prepare its next
+    blob while the engine works through its queue -- the engine no longer
+    idles while every worker encodes.  ``keep`` holds the device buffers the
+    copy reads; they are dropped once it is done.  At most
+    ``HIPSNAPSHOT_DMA_INFLIGHT`` copies per device are in flight (device
+    buffers of queued blobs stay allocated until then)."""
+    from .. import knobs
+
+    hslot = hash_slot(slot)
+    if nbytes and knobs.async_dma() and _use_sdma(dev):
+        if producer is not None:
+            native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
+        lim = _dma_limit(dev)
+        lim.acquire()
+        t_s = time.perf_counter()
+        try:
+            h = native.sdma_d2h_submit(dev, staged.addr, src, nbytes,
+                                       native.copy_stream(dev, slot))
+        except native.HipError as e:
+            lim.release()
+            import logging
+
+            logging.getLogger(__name__).warning(
+                f"SDMA device->host copy failed on cuda:{dev} ({e}); using hipMemcpyAsync")
+            _sdma_ok[dev] = False
+        else:
+            done = [False]
+
+            def ready() -> None:
+                if done[0]:
+                    return
+                try:
+                    try:
+                        native.sdma_wait(h)
+                    except native.HipError as e:
+                        import logging
+
+                        logging.getLogger(__name__).warning(
+                            f"SDMA device->host copy failed on cuda:{dev} ({e}); "
+                            "redoing it with hipMemcpyAsync")
+                        _sdma_ok[dev] = False
+                        native.memcpy(dev, copy_slot(), staged.addr, src, nbytes, native.D2H,
+                                      None, sync=True)
+                    timeline.add("dma", "d2h", t_s, time.perf_counter(), bytes=nbytes,
+                                 slot=slot)
+                    if hash_handle is not None:
+                        staged.checksum = _hash_finish(dev, hslot, hash_handle, nbytes)
+                finally:
+                    done[0] = True
+                    keep.clear()
+                    lim.release()
+
+            staged.ready = ready
+            return
+    bulk_d2h(dev, slot, staged.addr, src, nbytes, producer)
+    if hash_handle is not None:
+        staged.checksum = _hash_finish(dev, hslot, hash_handle, nbytes)
+    keep.clear()
+
+
+def wait_ready(staged: StagedBuffer) -> StagedBuffer:
+    """Block until ``staged``'s bytes have arrived (asynchronous copy)."""
+    ready = staged.ready
+    if ready is not None:
+        staged.ready = None
+        ready()
+    return staged
+
+
 def _elem_strides_ok(t: torch.Tensor) -> bool:
     return t.dim() <= native.MAX_DIMS
 
@@ -191,6 +281,7 @@ def d2h_tensor(t: torch.Tensor, producer: Optional[int],
     t_s = time.perf_counter()
     try:
         if t.is_contiguous():
+            hs = None
             if _checksums() and not _is_managed(t):
                 # hash the bytes in HBM on a side stream (ordered after the
                 # producer) while the DMA moves them; both only read them.
@@ -198,12 +289,10 @@ def d2h_tensor(t: torch.Tensor, producer: Optional[int],
                 # would pull them over the PCIe link the DMA is using -- the
                 # writer hashes the pinned copy on the host instead.)
                 native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
-                hslot = hash_slot(slot)
-                hs = checksum.device_hash_start(dev, hslot, t.data_ptr(), nbytes, slot)
-                bulk_d2h(dev, slot, pb.ptr, t.data_ptr(), nbytes)
-                staged.checksum = _hash_finish(dev, hslot, hs, nbytes)
-            else:
-                bulk_d2h(dev, slot, pb.ptr, t.data_ptr(), nbytes, producer)
+                producer = None
+                hs = checksum.device_hash_start(dev, hash_slot(slot), t.data_ptr(), nbytes,
+                                                slot)
+            d2h_staged(dev, slot, staged, t.data_ptr(), nbytes, [t], hs, producer)
         else:
             # pack-to-host: kernel stores the packed view over PCIe into the
             # host-mapped pinned block, ordered after the producer stream.
@@ -296,9 +385,7 @@ def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dic
         hs = None
         if _checksums():
             hs = checksum.device_hash_start(dev, hash_slot(slot), out.data_ptr(), nbytes, slot)
-        bulk_d2h(dev, slot, pb.ptr, out.data_ptr(), nbytes)
-        if hs is not None:
-            staged.checksum = _hash_finish(dev, hash_slot(slot), hs, nbytes)
+        d2h_staged(dev, slot, staged, out.data_ptr(), nbytes, [out, total, meta], hs)
     except BaseException:
         staged.release()
         raise
@@ -434,11 +521,11 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
             if _checksums():
                 hs = checksum.device_hash_start(dev, hash_slot(slot), slab.data_ptr(),
                                                 total_bytes, slot)
-            bulk_d2h(dev, slot, pb.ptr, slab.data_ptr(), total_bytes)
-            if hs is not None:
-                staged.checksum = _hash_finish(dev, hash_slot(slot), hs, total_bytes)
-        native.stream_sync(dev, slot)
+            d2h_staged(dev, slot, staged, slab.data_ptr(), total_bytes, [slab], hs)
+        else:
+            native.stream_sync(dev, slot)  # the kernel wrote host memory directly
         if keep is not None:
+            # the gather kernel is done: submitting the copy waited for it
             keep[0].release()
         del slab
     except BaseException:

@@ -39,7 +39,7 @@ def buffer_address(buf) -> int:
 class StagedBuffer:
     """Bytes ready for storage: ``view`` + raw ``addr`` + release hook."""
 
-    __slots__ = ("view", "addr", "_release", "keepalive", "checksum")
+    __slots__ = ("view", "addr", "_release", "keepalive", "checksum", "ready")
 
     def __init__(self, view: BufferType, addr: Optional[int] = None,
                  release: Optional[Callable[[], None]] = None, keepalive: Any = None) -> None:
@@ -53,6 +53,9 @@ class StagedBuffer:
         # hs64 of the bytes when the stager computed it (on the GPU); None =
         # the writer hashes them on the host (ops/checksum.py)
         self.checksum: Optional[int] = None
+        # set when the bytes are still arriving (asynchronous SDMA copy):
+        # call it (blocking, once) before reading the buffer
+        self.ready: Optional[Callable[[], None]] = None
 
     @property
     def nbytes(self) -> int:

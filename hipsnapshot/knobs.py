@@ -142,6 +142,17 @@ def get_d2h_engine() -> str:
     return v
 
 
+def async_dma() -> bool:
+    """Staging workers submit their SDMA copy and move on; the writer waits
+    for it (engine/staging.py ``d2h_staged``)."""
+    return _get_bool("ASYNC_DMA", True)
+
+
+def get_dma_inflight() -> int:
+    """Device -> host SDMA copies in flight per device (async staging)."""
+    return max(1, _get_int("DMA_INFLIGHT", 4))
+
+
 def serial_encode() -> bool:
     """Staging threads take turns launching (and waiting for) HSZ1 encodes on
     a device instead of sharing the CUs (engine/staging.py ``_encode_turn``)."""

@@ -267,6 +267,9 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_sdma_engines", c_int, [c_int])
         _declare(lib, "hsg_sdma_d2h", c_int,
                  [c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p])
+        _declare(lib, "hsg_sdma_d2h_submit", c_int,
+                 [c_int, c_void_p, c_void_p, c_uint64, c_void_p, ctypes.POINTER(c_uint64)])
+        _declare(lib, "hsg_sdma_wait", c_int, [c_uint64])
         _declare(lib, "hsg_hsz_meta_bytes", c_uint64, [ctypes.c_uint32])
         _declare(lib, "hsg_hsz_encode", c_int,
                  [c_int, c_void_p, c_uint64, c_int, ctypes.c_uint32, c_void_p, c_void_p,
@@ -411,6 +414,27 @@ def sdma_d2h(dev: int, dst: int, src: int, nbytes: int, stream=None,
     if r != 0:
         msg = lib.hsg_sdma_last_error()
         raise HipError(f"hsg_sdma_d2h failed ({r}): {msg.decode() if msg else ''}")
+
+
+def sdma_d2h_submit(dev: int, dst: int, src: int, nbytes: int, stream=None) -> int:
+    """Submit one device -> pinned-host SDMA copy ordered after ``stream``;
+    returns the handle ``sdma_wait`` takes (exactly once)."""
+    lib = require_gpu_lib()
+    h = c_uint64(0)
+    r = lib.hsg_sdma_d2h_submit(dev, dst, src, nbytes, _stream_handle(stream) or None,
+                                ctypes.byref(h))
+    if r != 0:
+        msg = lib.hsg_sdma_last_error()
+        raise HipError(f"hsg_sdma_d2h_submit failed ({r}): {msg.decode() if msg else ''}")
+    return h.value
+
+
+def sdma_wait(handle: int) -> None:
+    lib = require_gpu_lib()
+    r = lib.hsg_sdma_wait(handle)
+    if r != 0:
+        msg = lib.hsg_sdma_last_error()
+        raise HipError(f"hsg_sdma_wait failed ({r}): {msg.decode() if msg else ''}")
 
 
 def copy_stream(dev: int, slot: int) -> int:

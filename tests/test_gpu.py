@@ -709,7 +709,7 @@ def test_copy_workspace_ordered_after_busy_default_stream(gpu):
             offs = [sum((1000 + j) * 4 for j in range(i)) for i in range(8)]
             total = offs[-1] + (1007) * 4
             while not stop.is_set():
-                st = staging.gather_to_host(list(zip(ts, offs)), total, [])
+                st = staging.wait_ready(staging.gather_to_host(list(zip(ts, offs)), total, []))
                 got = torch.frombuffer(bytearray(st.view), dtype=torch.float32)
                 st.release()
                 if not torch.equal(got, refs):
@@ -833,13 +833,29 @@ def test_plan_reuse_gpu_sync_and_async(gpu, tmp_path):
     plan_cache.clear()
 
 
-def test_sdma_failure_falls_back_to_blit(gpu, tmp_path, monkeypatch):
+@pytest.mark.parametrize("where", ["submit", "wait", "blocking"])
+def test_sdma_failure_falls_back_to_blit(gpu, tmp_path, monkeypatch, where):
+    """An SDMA copy that fails to start (submit / blocking call) or that the
+    engine reports failed (wait) is redone with hipMemcpyAsync, and SDMA is
+    switched off for the device."""
     from hipsnapshot.engine import staging
 
     def broken(*a, **k):
         raise native.HipError("injected SDMA failure")
 
-    monkeypatch.setattr(native, "sdma_d2h", broken)
+    if where == "submit":
+        monkeypatch.setattr(native, "sdma_d2h_submit", broken)
+    elif where == "wait":
+        real_wait = native.sdma_wait
+
+        def wait_then_fail(h):
+            real_wait(h)  # the copy must be over before its buffer is reused
+            raise native.HipError("injected SDMA failure")
+
+        monkeypatch.setattr(native, "sdma_wait", wait_then_fail)
+    else:
+        monkeypatch.setenv("HIPSNAPSHOT_ASYNC_DMA", "0")
+        monkeypatch.setattr(native, "sdma_d2h", broken)
     monkeypatch.setattr(staging, "_sdma_ok", {0: True})
     sd = StateDict(w=torch.randn(3000, 1000, device=gpu), b=torch.randn(77, device=gpu))
     ref = {k: v.clone() for k, v in sd.items()}
