@@ -173,13 +173,17 @@ _dma_limits: dict = {}
 
 
 def _dma_limit(dev: int) -> threading.BoundedSemaphore:
-    lim = _dma_limits.get(dev)
-    if lim is None:
-        from .. import knobs
+    from .. import knobs
 
+    n = knobs.get_dma_inflight()
+    got = _dma_limits.get(dev)
+    if got is None or got[0] != n:
+        # (a changed knob takes effect for copies submitted from now on)
         with _slot_lock:
-            lim = _dma_limits.setdefault(dev, threading.BoundedSemaphore(knobs.get_dma_inflight()))
-    return lim
+            got = _dma_limits.get(dev)
+            if got is None or got[0] != n:
+                got = _dma_limits[dev] = (n, threading.BoundedSemaphore(n))
+    return got[1]
 
 
 def d2h_staged(dev: int, slot: int, staged: StagedBuffer, src: int, nbytes: int,

@@ -150,7 +150,7 @@ def async_dma() -> bool:
 
 def get_dma_inflight() -> int:
     """Device -> host SDMA copies in flight per device (async staging)."""
-    return max(1, _get_int("DMA_INFLIGHT", 4))
+    return max(1, _get_int("DMA_INFLIGHT", 8))
 
 
 def serial_encode() -> bool:
