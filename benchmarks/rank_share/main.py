@@ -1,4 +1,4 @@
-"""One rank's share of the Llama-3-8B FSDP save at world size W, on one GPU.
+"""One rank's share of the Llama-3 FSDP save at world size W, on one GPU.
 
 At N GPUs every rank saves 1/N of every parameter: the same 291 tensors,
 each 1/N the size.  Per-take fixed costs (planning per tensor, per-blob
@@ -15,6 +15,7 @@ share's bytes / the share's take time, the upper bound if nothing else
 interfered.
 
     python benchmarks/rank_share/main.py --world 8 [--compression hsz1]
+    python benchmarks/rank_share/main.py --model llama3_70b --world 8   # BASELINE config 5's share
 """
 
 from __future__ import annotations
@@ -33,6 +34,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--model", default="llama3_8b", choices=["llama3_8b", "llama3_70b"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--async-iters", type=int, default=5)
@@ -63,7 +65,7 @@ def main() -> None:
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
     mesh = init_device_mesh("cuda", (1,))
-    cfg = LlamaConfig.llama3_8b()
+    cfg = getattr(LlamaConfig, args.model)()
     with torch.device("meta"):
         meta = Llama(cfg)
     gen = torch.Generator(device=dev).manual_seed(0)
@@ -146,7 +148,7 @@ def main() -> None:
     ok = all(torch.equal(refs[k], app_state["model"][k]._local_tensor) for k in refs)
     med = statistics.median(times)
     print(json.dumps({
-        "bench": "rank_share", "world": args.world, "compression": args.compression,
+        "bench": "rank_share", "model": args.model, "world": args.world, "compression": args.compression,
         "tensors": len(params), "share_bytes": share,
         "take_ms_median": round(med * 1e3, 2), "take_ms_min": round(min(times) * 1e3, 2),
         "share_GBps": round(share / med / 1e9, 2),
