@@ -21,6 +21,9 @@
 //                   block scan of the analyze pass's lane sizes) while the
 //                   low-byte plane streams out with 8-B stores; the finished
 //                   streams leave LDS with coalesced 4-B stores
+//   hsz_encode2x<2> mode 2 for bf16/fp16: the same stream layout, packed by
+//                   1024 threads, 4 per lane stream (each piece's bit offset
+//                   comes from per-piece byte counters in the analyze pass)
 // Decode (after H2D) = 2 launches, one workgroup per frame each:
 //   hsz_decode<W>   modes 0/1 (escape positions are collected from the nibble
 //                   plane first, then every element is rebuilt)
@@ -37,6 +40,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 
 extern "C" int hsg_thread_grid_cap();  // hsgpu.hip
@@ -55,6 +59,8 @@ constexpr int kMaxLen = 11;
 constexpr int kLut = 1 << kMaxLen;
 constexpr uint32_t kMaxCoded = 65535;
 constexpr int kLaneTable = 2 * kLanes;
+constexpr int kSub = 4;                    // hsz_encode2x: pieces (threads) per lane stream
+constexpr int kThreadsX = kLanes * kSub;   // 1024
 
 struct FrameMeta {
   uint32_t mode;
@@ -66,7 +72,9 @@ struct FrameMeta {
   uint64_t size;     // padded frame bytes
   uint64_t offset;   // absolute offset in the blob
 };
-// meta buffer = FrameMeta[n_frames] followed by uint16 lane_bytes[n_frames][256]
+// meta buffer = FrameMeta[n_frames], then uint16 lane_bytes[n_frames][256], then
+// uint32 piece_bits[n_frames][kSub - 1][256]: bits of lane t's stream up to the
+// end of its piece s (hsz_encode2x splits every stream into kSub pieces)
 
 __device__ __forceinline__ uint64_t align16(uint64_t n) { return (n + 15) & ~uint64_t(15); }
 
@@ -290,10 +298,17 @@ __device__ __forceinline__ uint32_t get_lo(const uint64_t* lw, int e) {
   return uint32_t(x) & ((1u << L) - 1);
 }
 
+// A lane's count of one index: the column word, or with per-piece byte
+// counters (hsz_analyze's "packed" mode) the sum of its 4 bytes.
+__device__ __forceinline__ uint32_t col_count(uint32_t w, bool packed) {
+  return packed ? (w & 255) + ((w >> 8) & 255) + ((w >> 16) & 255) + (w >> 24) : w;
+}
+
 template <int W>
 __device__ inline void
 hsz_analyze_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
-            FrameMeta* __restrict__ meta, uint16_t* __restrict__ lane_bytes_all) {
+            FrameMeta* __restrict__ meta, uint16_t* __restrict__ lane_bytes_all,
+            uint32_t* __restrict__ piece_bits_all) {
   __shared__ uint32_t hist[256];
   __shared__ uint8_t dict[16];
   __shared__ uint8_t code_of[260];  // indexed through cslot()
@@ -326,13 +341,31 @@ hsz_analyze_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t lo
       __syncthreads();
       const uint64_t groups = n / 8;
       const bool aligned = (reinterpret_cast<uintptr_t>(s) & 15) == 0;
+      // the next group's load is in flight while this one is counted, and
+      // each count is one ds_add (no read-modify-write round trip per element:
+      // the thread owns its column, so nothing contends)
+      // encode2x splits lane t's stream into kSub pieces of pq consecutive
+      // groups and needs each piece's bit offset: while a piece has < 256
+      // elements ("packed"), the count of piece p lives in byte p of the
+      // column word (one ds_add of 1 << 8p), so the same pass yields them
+      const uint32_t pq = uint32_t((groups + kLanes - 1) / kLanes + kSub - 1) / kSub;
+      const bool packed = pq * 8 < 256;
+      uint32_t left = pq, inc = 1;
+      uint32_t nx[2 * W];
+      if (threadIdx.x < groups) load_group<W>(s, threadIdx.x, aligned, nx);
       for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
         uint32_t wd[2 * W];
-        load_group<W>(s, g, aligned, wd);
+#pragma unroll
+        for (int q = 0; q < 2 * W; ++q) wd[q] = nx[q];
+        if (g + kThreads < groups) load_group<W>(s, g + kThreads, aligned, nx);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t c = code_of[cslot(group_elem<W>(wd, e) >> (8 * (W - 1)))];
-          lcnt[c * kLanes + threadIdx.x] += 1;
+          atomicAdd(&lcnt[c * kLanes + threadIdx.x], inc);
+        }
+        if (--left == 0) {
+          left = pq;
+          if (packed) inc <<= 8;
         }
       }
       __syncthreads();
@@ -342,7 +375,7 @@ hsz_analyze_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t lo
         for (int c = 4 * q; c < 4 * q + 4; ++c) {
           uint32_t v = 0;
 #pragma unroll
-          for (int r = 0; r < kLanes; r += 64) v += lcnt[c * kLanes + r + lane];
+          for (int r = 0; r < kLanes; r += 64) v += col_count(lcnt[c * kLanes + r + lane], packed);
           v = wave_sum_u32(v);
           if (lane == 0) fcnt[c] = v;
         }
@@ -354,10 +387,28 @@ hsz_analyze_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t lo
       }
       __syncthreads();
       uint32_t bits = 0;
+      uint32_t pbits[kSub - 1];  // bits up to the end of piece sp
 #pragma unroll
-      for (int c = 0; c < 16; ++c) bits += lcnt[c * kLanes + threadIdx.x] * hlen[c];
+      for (int sp = 0; sp < kSub - 1; ++sp) pbits[sp] = 0;
+#pragma unroll 1
+      for (int c = 0; c < 16; ++c) {
+        const uint32_t w = lcnt[c * kLanes + threadIdx.x];
+        const uint32_t hl = hlen[c];
+        bits += col_count(w, packed) * hl;
+        uint32_t cum = 0;
+#pragma unroll
+        for (int sp = 0; sp < kSub - 1; ++sp) {
+          cum += (w >> (8 * sp)) & 255;
+          pbits[sp] += cum * hl;
+        }
+      }
       const uint32_t lb = (bits + 7) / 8;
       lane_bytes_all[f * kLanes + threadIdx.x] = uint16_t(lb < 65535u ? lb : 65535u);
+      if (packed) {
+#pragma unroll
+        for (int sp = 0; sp < kSub - 1; ++sp)
+          piece_bits_all[(f * (kSub - 1) + sp) * kLanes + threadIdx.x] = pbits[sp];
+      }
       const int c_bytes = block_sum(int(lb), red);
       if (threadIdx.x == 0) {
         const uint32_t esc = fcnt[kEsc];
@@ -420,11 +471,12 @@ hsz_analyze_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t lo
 // background drain caps it, hsg_set_thread_grid_cap) each workgroup walks
 // several frames, so the encoder occupies only that many CUs.
 template <int W>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, 8)  // 8 waves / SIMD: what LDS allows (8 workgroups / CU)
 hsz_analyze(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
-            FrameMeta* __restrict__ meta, uint16_t* __restrict__ lane_bytes_all, uint32_t nf) {
+            FrameMeta* __restrict__ meta, uint16_t* __restrict__ lane_bytes_all,
+            uint32_t* __restrict__ piece_bits_all, uint32_t nf) {
   for (uint64_t f = blockIdx.x; f < nf; f += gridDim.x) {
-    hsz_analyze_frame<W>(f, src, logical, frame_bytes, meta, lane_bytes_all);
+    hsz_analyze_frame<W>(f, src, logical, frame_bytes, meta, lane_bytes_all, piece_bits_all);
     __syncthreads();  // the next frame reuses this workgroup's LDS
   }
 }
@@ -475,9 +527,10 @@ hsz_layout(FrameMeta* __restrict__ meta, uint32_t n_frames, uint8_t* __restrict_
 
 // Writes frame f's escape values in element order: entries (idx, value) were
 // appended in arbitrary order; each one's rank = #entries with a smaller idx.
+template <int NT = kThreads>
 __device__ void write_escapes(const uint32_t* eidx, const uint8_t* evals, int n_esc,
                               uint8_t* dst) {
-  for (int i = threadIdx.x; i < n_esc; i += kThreads) {
+  for (int i = threadIdx.x; i < n_esc; i += NT) {
     const uint32_t me = eidx[i];
     int rank = 0;
     for (int j = 0; j < n_esc; ++j) rank += eidx[j] < me;
@@ -794,6 +847,201 @@ hsz_encode2(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_by
     hsz_encode2_frame<W>(f, src, logical, frame_bytes, meta, lane_bytes_all, out);
     __syncthreads();  // the next frame reuses this workgroup's LDS
   }
+}
+
+// Mode-2 encoder, split streams (W = 2 or 4): kSub threads per lane stream.
+//
+// hsz_encode2 gives each of the frame's 256 lane streams ONE thread, which
+// codes its groups in one serial chain, and its 64 KiB LDS stream buffer caps
+// the CU at 2 such workgroups (8 waves): the chains' load and LDS latencies
+// are barely hidden.  Here a 1024-thread workgroup splits every lane's groups
+// into kSub consecutive pieces.  The analyze pass already recorded each
+// piece's bit offset inside its stream, so every thread streams its piece
+// (next group's load in flight) and packs its codes at that offset with the
+// same LDS atomic-OR word assembly -- 32 waves per CU (2 workgroups), chains
+// a quarter as long.  The output is byte-identical to hsz_encode2.
+template <int W>
+__device__ inline void
+hsz_encode2x_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t logical,
+                   uint32_t frame_bytes, const FrameMeta* __restrict__ meta,
+                   const uint16_t* __restrict__ lane_bytes_all,
+                   const uint32_t* __restrict__ piece_bits_all, uint8_t* __restrict__ out) {
+  __shared__ uint32_t coded32[(kMaxCoded + 1 + 8 + 3) / 4];
+  __shared__ uint8_t code_of[260];   // indexed through cslot()
+  __shared__ uint32_t enc_tab[257];  // eslot(high byte) -> codeword | len << 16 | escape << 31
+  __shared__ uint16_t hcode[16];
+  __shared__ uint8_t hlen[16];
+  __shared__ uint32_t eidx[kMaxEsc];
+  __shared__ uint8_t evals[kMaxEsc];
+  __shared__ uint32_t loffs[kLanes];  // byte offset of each lane stream
+  __shared__ uint32_t wsum[4];
+  __shared__ int ecount;
+  const FrameMeta& m = meta[f];  // arrays indexed at run time: read from memory
+  if (m.mode != 2) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kLanes - 1);
+  const int sub = tid >> 8;
+  const uint64_t base = f * frame_bytes;
+  const uint64_t len = min(uint64_t(frame_bytes), logical - base);
+  const uint64_t n = len / W;
+  const uint8_t* s = src + base;
+  uint8_t* fr = out + m.offset;
+  write_frame_header(m, fr);
+  if (tid < 256) code_of[cslot(tid)] = kEsc;
+  const uint32_t c_words = (m.coded + 3) / 4;
+  for (uint32_t i = tid; i < c_words; i += kThreadsX) coded32[i] = 0;
+  if (tid < 64) {
+    const uint32_t l = tid < 16 ? m.lens[tid] : 0u;
+    const uint32_t code = wave_canonical_code(l);
+    if (tid < 16) {
+      hlen[tid] = uint8_t(l);
+      hcode[tid] = uint16_t(code);
+    }
+    if (tid == 0) ecount = 0;
+  }
+  // this thread's piece: groups lane + 256 k for k in [k0, k0 + pq); the
+  // first load is issued before the table setup
+  const uint64_t groups = n / 8;
+  const uint32_t pq = uint32_t((groups + kLanes - 1) / kLanes + kSub - 1) / kSub;
+  const uint64_t g0 = uint64_t(lane) + uint64_t(kLanes) * (uint64_t(sub) * pq);
+  const uint64_t g_end = min(groups, g0 + uint64_t(kLanes) * pq);
+  const bool aligned = (reinterpret_cast<uintptr_t>(s) & 15) == 0;
+  uint32_t nx[2 * W];
+  if (g0 < g_end) load_group<W>(s, g0, aligned, nx);
+  uint32_t start = 0;  // bit offset of the piece inside the lane stream
+  if (sub > 0) start = piece_bits_all[(f * (kSub - 1) + (sub - 1)) * kLanes + lane];
+  __syncthreads();
+  if (tid < m.nsel) code_of[cslot(m.dict[tid])] = uint8_t(tid);
+  uint32_t lb = 0, x = 0;
+  if (tid < kLanes) {  // waves 0-3: exclusive scan of the lane stream sizes
+    lb = lane_bytes_all[f * kLanes + tid];
+    x = lb;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if ((tid & 63) >= o) x += y;
+    }
+    if ((tid & 63) == 63) wsum[tid >> 6] = x;
+  }
+  __syncthreads();
+  if (tid < kLanes) {
+    const uint32_t c = code_of[cslot(tid)];
+    enc_tab[eslot(tid)] = uint32_t(hcode[c]) | (uint32_t(hlen[c]) << 16) |
+                          (c == kEsc ? 0x80000000u : 0u);
+    uint32_t b = 0;
+    for (int i = 0; i < (tid >> 6); ++i) b += wsum[i];
+    loffs[tid] = b + x - lb;
+  }
+  uint8_t* body = fr + kFrameHeader;
+  uint8_t* lo = body;
+  const uint64_t nlo = uint64_t(W - 1) * n;
+  uint16_t* table = reinterpret_cast<uint16_t*>(body + nlo);  // n % 8 == 0: aligned
+  if (tid < kLanes) table[tid] = uint16_t(lb);
+  uint8_t* streams = body + nlo + kLaneTable;
+  __syncthreads();  // enc_tab, loffs ready
+  // bit cursor: word wpos, nb pending bits in acc (the low nb are placeholders
+  // for bits owned by the piece or lane before this one: OR-ed in LDS)
+  start += loffs[lane] * 8;
+  uint32_t wpos = start >> 5;
+  uint64_t acc = 0;
+  int nb = int(start & 31);
+  const bool lo_aligned = (reinterpret_cast<uintptr_t>(lo) & 7) == 0;
+  for (uint64_t g = g0; g < g_end; g += kLanes) {
+    uint32_t wd[2 * W];
+#pragma unroll
+    for (int q = 0; q < 2 * W; ++q) wd[q] = nx[q];
+    if (g + kLanes < g_end) load_group<W>(s, g + kLanes, aligned, nx);
+    // the group's 8 table lookups are issued together (one LDS wait), and
+    // the rare escapes take one branch per group, not one per element
+    uint32_t ent[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ent[e] = enc_tab[eslot(group_elem<W>(wd, e) >> (8 * (W - 1)))];
+    uint64_t lw[W - 1];
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k) lw[k] = 0;
+    uint32_t esc = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      put_lo<W>(lw, e, group_elem<W>(wd, e));
+      esc |= (ent[e] >> 31) << e;
+    }
+    if (esc) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if ((esc >> e) & 1) {
+          const int k = atomicAdd(&ecount, 1);
+          if (k < kMaxEsc) {
+            eidx[k] = uint32_t(g * 8 + e);
+            evals[k] = uint8_t(group_elem<W>(wd, e) >> (8 * (W - 1)));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t en = ent[p * 2 + h];
+        acc |= uint64_t(en & 0xffffu) << nb;
+        nb += (en >> 16) & 31;
+      }
+      if (nb >= 32) {  // <= 31 + 22 bits after two codes: at most one full word
+        atomicOr(&coded32[wpos], uint32_t(acc));
+        ++wpos;
+        acc >>= 32;
+        nb -= 32;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k) {
+      if (lo_aligned) {
+        reinterpret_cast<uint64_t*>(lo)[g * (W - 1) + k] = lw[k];
+      } else {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) lo[8 * ((W - 1) * g + k) + b] = uint8_t(lw[k] >> (8 * b));
+      }
+    }
+  }
+  if (nb > 0) atomicOr(&coded32[wpos], uint32_t(acc));  // < 32 bits left
+  __syncthreads();
+  const uint8_t* coded = reinterpret_cast<const uint8_t*>(coded32);
+  const uint32_t c_bytes = m.coded;
+  if ((reinterpret_cast<uintptr_t>(streams) & 3) == 0) {
+    const uint32_t nw = c_bytes / 4;
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(coded);
+    uint32_t* sw = reinterpret_cast<uint32_t*>(streams);
+    for (uint32_t i = tid; i < nw; i += kThreadsX) sw[i] = cw[i];
+    for (uint32_t j = nw * 4 + tid; j < c_bytes; j += kThreadsX) streams[j] = coded[j];
+  } else {
+    for (uint32_t j = tid; j < c_bytes; j += kThreadsX) streams[j] = coded[j];
+  }
+  uint8_t* escp = streams + c_bytes;
+  write_escapes<kThreadsX>(eidx, evals, min(ecount, kMaxEsc), escp);
+  uint8_t* tail = escp + m.n_esc;
+  const uint64_t tail_len = len - W * n;
+  const uint64_t used = uint64_t(tail - body);
+  const uint64_t padded_end = m.size - kFrameHeader;
+  for (uint64_t j = tid; used + j < padded_end; j += kThreadsX)
+    tail[j] = j < tail_len ? s[W * n + j] : 0;
+}
+
+template <int W>
+__global__ void __launch_bounds__(kThreadsX, 8)  // 2 workgroups / CU: <= 64 VGPRs
+hsz_encode2x(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
+             const FrameMeta* __restrict__ meta, const uint16_t* __restrict__ lane_bytes_all,
+             const uint32_t* __restrict__ piece_bits_all, uint8_t* __restrict__ out,
+             uint32_t nf) {
+  for (uint64_t f = blockIdx.x; f < nf; f += gridDim.x) {
+    hsz_encode2x_frame<W>(f, src, logical, frame_bytes, meta, lane_bytes_all, piece_bits_all,
+                          out);
+    __syncthreads();  // the next frame reuses this workgroup's LDS
+  }
+}
+
+// hsz_encode2x needs the analyze pass's piece offsets, recorded while a
+// piece holds < 256 elements (byte counters): frames up to ~1 MiB of bf16.
+__host__ __device__ constexpr bool encode2x_fits(int w, uint64_t frame_bytes) {
+  return ((frame_bytes / uint64_t(w) / 8 + kLanes - 1) / kLanes + kSub - 1) / kSub * 8 < 256;
 }
 
 // A rejected (corrupt / truncated) frame is reported through `err` (host-
@@ -1135,6 +1383,13 @@ int fail(const char* what, hipError_t e) {
   return -static_cast<int>(e) - 1;
 }
 
+// HIPSNAPSHOT_SPLIT_ENCODE=0 selects the one-thread-per-stream mode-2 encoder
+// (A/B switch; read per launch so a process can alternate).
+bool hsz_split_encode() {
+  const char* v = getenv("HIPSNAPSHOT_SPLIT_ENCODE");
+  return v == nullptr || v[0] != '0';
+}
+
 }  // namespace
 
 extern "C" {
@@ -1142,7 +1397,8 @@ extern "C" {
 const char* hsg_hsz_last_error() { return g_hsz_err; }
 
 uint64_t hsg_hsz_meta_bytes(uint32_t n_frames) {
-  return uint64_t(n_frames) * (sizeof(FrameMeta) + sizeof(uint16_t) * kLanes);
+  return uint64_t(n_frames) *
+         (sizeof(FrameMeta) + sizeof(uint16_t) * kLanes + sizeof(uint32_t) * (kSub - 1) * kLanes);
 }
 
 // Encode `logical` bytes at device `src` (16-B aligned) into device `out`
@@ -1162,11 +1418,12 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
   auto* o = static_cast<uint8_t*>(out);
   const int cap = hsg_thread_grid_cap();
   const uint32_t g = cap > 0 ? std::min<uint32_t>(nf, uint32_t(cap)) : nf;
+  auto* pbits = reinterpret_cast<uint32_t*>(lanes + uint64_t(nf) * kLanes);
   switch (w) {
-    case 1: hipLaunchKernelGGL(hsz_analyze<1>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, nf); break;
-    case 2: hipLaunchKernelGGL(hsz_analyze<2>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, nf); break;
-    case 4: hipLaunchKernelGGL(hsz_analyze<4>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, nf); break;
-    case 8: hipLaunchKernelGGL(hsz_analyze<8>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, nf); break;
+    case 1: hipLaunchKernelGGL(hsz_analyze<1>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, pbits, nf); break;
+    case 2: hipLaunchKernelGGL(hsz_analyze<2>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, pbits, nf); break;
+    case 4: hipLaunchKernelGGL(hsz_analyze<4>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, pbits, nf); break;
+    case 8: hipLaunchKernelGGL(hsz_analyze<8>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, lanes, pbits, nf); break;
     default: return -1001;
   }
   hipLaunchKernelGGL(hsz_layout, dim3(1), dim3(1024), 0, s, m, nf, o, logical, uint32_t(w),
@@ -1177,7 +1434,14 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
     case 4: hipLaunchKernelGGL(hsz_encode<4>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o, nf); break;
     default: hipLaunchKernelGGL(hsz_encode<8>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes, m, o, nf); break;
   }
-  if (w == 2)
+  // bf16/fp16: split-stream encoder (802 -> 420 us per GiB); fp32 stays on
+  // hsz_encode2 (449 us vs 525 us: twice the bytes per group under the split
+  // kernel's 64-VGPR budget) -- profiles/codec_r2/split_encode.md
+  const bool split = w == 2 && encode2x_fits(w, frame_bytes) && hsz_split_encode();
+  if (split)
+    hipLaunchKernelGGL(hsz_encode2x<2>, dim3(g), dim3(kThreadsX), 0, s, src8, logical,
+                       frame_bytes, m, lanes, pbits, o, nf);
+  else if (w == 2)
     hipLaunchKernelGGL(hsz_encode2<2>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes,
                        m, lanes, o, nf);
   else if (w == 4)
