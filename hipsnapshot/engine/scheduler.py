@@ -517,12 +517,14 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
 
     async def _one_compressed(rr: ReadReq) -> None:
         from ..ops import codec as hsz
-        from ..io_types import CompressedSpan
+        from ..io_types import CompressedSpan, SpanTail
 
         info = rr.codec
         logical = int(info["blob_bytes"])
         nf = hsz.n_frames_for(logical, int(info["frame_bytes"]))
         dest = None
+        tail = None
+        rest_task = None
         try:
             async with io_sem:
                 if failing:
@@ -531,14 +533,27 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                 whole = rr.byte_range is None or tuple(rr.byte_range) == (0, logical)
                 stored = await storage.size(rr.path) if whole else None
                 if stored is not None:
-                    # whole blob: ONE read of header + frames (no header round
-                    # trip; the read enters the engine queue in request order)
+                    # whole blob: header + frames without a header round trip
+                    # (reads enter the engine queue in request order).  A large
+                    # blob is read as a head and the rest: the consumer moves
+                    # the head's frames to the GPU while the rest arrives.
                     full = await asyncio.get_running_loop().run_in_executor(
                         aux_pool(), rr.buffer_consumer.get_compressed_read_dest, stored)
                     if full is None:
                         full = as_staged(bytearray(max(stored, 1)))
                     dest = full
-                    await storage.read(ReadIO(path=rr.path, byte_range=(0, stored), dest=full))
+                    head_n = knobs.get_read_head_bytes()
+                    split = 0 < head_n and 2 * head_n <= stored \
+                        and hsz.payload_start(nf) <= head_n
+                    head_end = head_n if split else stored
+                    head_read = storage.read(ReadIO(
+                        path=rr.path, byte_range=(0, head_end),
+                        dest=StagedBuffer(full.view[:head_end], full.addr)))
+                    if split:
+                        rest_task = asyncio.ensure_future(storage.read(ReadIO(
+                            path=rr.path, byte_range=(head_end, stored),
+                            dest=StagedBuffer(full.view[head_end:], full.addr + head_end))))
+                    await head_read
                     header = hsz.parse_header(full.view[:hsz.payload_start(nf)])
                     hsz.validate_offsets(header, stored)
                     lo, hi = 0, header.logical_size
@@ -546,6 +561,12 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                     c_lo, c_hi = header.offsets[0], header.offsets[-1]
                     dest = StagedBuffer(full.view[c_lo:c_hi], full.addr + c_lo,
                                         release=full.release, keepalive=full)
+                    if rest_task is not None:
+                        tail = SpanTail(max(head_end - c_lo, 0))
+                        rest_task.add_done_callback(
+                            lambda t, tl=tail: tl.arrived(
+                                None if t.cancelled() or t.exception() is None
+                                else t.exception()))
                 else:
                     head_io = ReadIO(path=rr.path, byte_range=(0, hsz.payload_start(nf)))
                     await storage.read(head_io)
@@ -564,16 +585,24 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                         await storage.read(body_io)
                 t_c = time.perf_counter()
         except BaseException:
+            if rest_task is not None:
+                # the engine may still be filling the rest: not before it is done
+                await asyncio.gather(rest_task, return_exceptions=True)
             if dest is not None:
                 dest.release()
             raise
-        span = CompressedSpan(dest, header, first, last, lo, hi)
+        span = CompressedSpan(dest, header, first, last, lo, hi, tail=tail)
         timeline.add("read", "io", t_r, t_c, path=rr.path, bytes=c_hi - c_lo, logical=hi - lo)
         stats.bytes_written += hi - lo
         try:
             await rr.buffer_consumer.consume_buffer(span, executor)
         finally:
+            if rest_task is not None:
+                await asyncio.gather(rest_task, return_exceptions=True)
             span.release()
+        if rest_task is not None and not rest_task.cancelled() \
+                and rest_task.exception() is not None:
+            raise rest_task.exception()
         timeline.add("consume", "stage", t_c, time.perf_counter(), path=rr.path, bytes=hi - lo)
 
     async def _one(rr: ReadReq, cost: int) -> None:

@@ -747,7 +747,20 @@ def _decode_span(span, regions, dev, slot, direct, enc, offs_pb, n_offs, c_n, lo
                                                      device=f"cuda:{dev}")
     t1 = time.perf_counter()
     _join_current_stream(dev, slot)
-    native.memcpy(dev, slot, enc.data_ptr(), span.buf.addr, c_n, native.H2D, None, sync=False)
+    tail = span.tail
+    if tail is not None and 0 < tail.offset < c_n:
+        # the head's frames go up while the rest of the blob is still being read
+        native.memcpy(dev, slot, enc.data_ptr(), span.buf.addr, tail.offset, native.H2D, None,
+                      sync=False)
+        t_w = time.perf_counter()
+        tail.wait()
+        timeline.add("tail_wait", "h2d", t_w, time.perf_counter())
+        native.memcpy(dev, slot, enc.data_ptr() + tail.offset, span.buf.addr + tail.offset,
+                      c_n - tail.offset, native.H2D, None, sync=False)
+    else:
+        span.wait_tail()
+        native.memcpy(dev, slot, enc.data_ptr(), span.buf.addr, c_n, native.H2D, None,
+                      sync=False)
     native.memcpy(dev, slot, offs_dev.data_ptr(), offs_pb.ptr, 8 * n_offs, native.H2D, None,
                   sync=False)
     stream = native.copy_stream(dev, slot)

@@ -107,6 +107,28 @@ class BufferConsumer(ABC):
         return None
 
 
+class SpanTail:
+    """The part of a compressed span's buffer that a second read is still
+    filling: bytes from ``offset`` on.  The read's completion (on the event
+    loop) calls ``arrived``; consumer threads call ``wait``."""
+
+    def __init__(self, offset: int) -> None:
+        import threading
+
+        self.offset = offset
+        self._event = threading.Event()
+        self._error: Optional[BaseException] = None
+
+    def arrived(self, error: Optional[BaseException] = None) -> None:
+        self._error = error
+        self._event.set()
+
+    def wait(self) -> None:
+        self._event.wait()
+        if self._error is not None:
+            raise self._error
+
+
 class CompressedSpan:
     """Encoded frames [first, last) of an HSZ1 blob covering the logical byte
     range [lo, hi) a read asked for.  Consumers that restore into HBM move
@@ -114,13 +136,21 @@ class CompressedSpan:
     (``engine.staging.scatter_compressed``); others call ``decode_host``."""
 
     def __init__(self, buf: "StagedBuffer", header, first: int, last: int, lo: int,
-                 hi: int) -> None:
+                 hi: int, tail: Optional["SpanTail"] = None) -> None:
         self.buf = buf
         self.header = header
         self.first = first
         self.last = last
         self.lo = lo
         self.hi = hi
+        # bytes of ``buf`` from ``tail.offset`` on may still be arriving
+        self.tail = tail
+
+    def wait_tail(self) -> None:
+        """Block until every byte of ``buf`` has arrived (raises if the read
+        of the rest failed)."""
+        if self.tail is not None:
+            self.tail.wait()
 
     @property
     def nbytes(self) -> int:
@@ -133,6 +163,8 @@ class CompressedSpan:
     def decode_host(self) -> memoryview:
         """Logical bytes [lo, hi) decoded by the C++ codec into host memory."""
         from .ops import codec
+
+        self.wait_tail()
 
         h = self.header
         n_log = min(self.last * h.frame_bytes, h.logical_size) - self.frames_logical_lo

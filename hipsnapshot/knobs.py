@@ -195,6 +195,14 @@ def get_drain_cus() -> int:
     return max(0, _get_int("DRAIN_CUS", 0))
 
 
+def get_read_head_bytes() -> int:
+    """Whole HSZ1 blobs larger than twice this are read as a head of this
+    many bytes and the rest, as two requests: the head's frames go to the GPU
+    while the rest is still being read (the restore's first H2D starts after
+    the head, not after the whole first blob).  0 = one read per blob."""
+    return max(0, _get_int("READ_HEAD_BYTES", 16 * 1024 * 1024))
+
+
 def get_read_order() -> str:
     """Restore read order: ``plan`` (manifest order, default) or ``pipeline``
     (a small lead read, then largest first).  Measured A/B on one MI355X,

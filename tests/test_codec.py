@@ -317,3 +317,56 @@ def test_ratio_holds_for_trained_weights_and_adam_state():
         blob = codec.encode_cpu(raw, 2, 64 * 1024)
         assert len(blob) / len(raw) < bound, (name, len(blob) / len(raw))
         assert codec.decode_cpu(blob.tobytes()).tobytes() == raw
+
+
+# ---- whole blobs read as a head and the rest (knobs.get_read_head_bytes) ----------
+
+@pytest.mark.parametrize("batching", [True, False])
+def test_compressed_restore_with_split_head_read(tmp_path, host_compression, monkeypatch,
+                                                 batching):
+    """Blobs larger than twice the head are read as two requests; the consumer
+    decodes once the rest has arrived (host path: decode_host waits)."""
+    from hipsnapshot import Snapshot, StateDict
+    from hipsnapshot.knobs import override_is_batching_disabled
+    from hipsnapshot.storage import fs as fs_mod
+
+    monkeypatch.setenv("HIPSNAPSHOT_READ_HEAD_BYTES", str(64 * 1024))
+    ranges = []
+    orig = fs_mod.FSStoragePlugin.read
+
+    async def spy(self, read_io):
+        ranges.append(read_io.byte_range)
+        await orig(self, read_io)
+
+    monkeypatch.setattr(fs_mod.FSStoragePlugin, "read", spy)
+    src = _weights(3)
+    with override_is_batching_disabled(not batching):
+        Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(**src)}, compression="hsz1")
+        out = StateDict(**{k: torch.zeros_like(v) for k, v in src.items()})
+        Snapshot(str(tmp_path / "s")).restore({"sd": out})
+    for k, v in src.items():
+        assert torch.equal(out[k], v), k
+    assert (0, 64 * 1024) in ranges  # a head read happened
+    assert any(r is not None and r[0] == 64 * 1024 for r in ranges)  # and its rest
+
+
+def test_compressed_restore_fails_when_rest_read_fails(tmp_path, host_compression, monkeypatch):
+    """A failing read of a blob's rest fails the restore (no hang, no decode of
+    bytes that never arrived)."""
+    from hipsnapshot import Snapshot, StateDict
+    from hipsnapshot.storage import fs as fs_mod
+
+    src = {"big_bf16": _weights(4)["big_bf16"]}
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(**src)}, compression="hsz1")
+    monkeypatch.setenv("HIPSNAPSHOT_READ_HEAD_BYTES", str(64 * 1024))
+    orig = fs_mod.FSStoragePlugin.read
+
+    async def flaky(self, read_io):
+        if read_io.byte_range is not None and read_io.byte_range[0] == 64 * 1024:
+            raise OSError(5, "injected read failure")
+        await orig(self, read_io)
+
+    monkeypatch.setattr(fs_mod.FSStoragePlugin, "read", flaky)
+    out = StateDict(big_bf16=torch.zeros_like(src["big_bf16"]))
+    with pytest.raises(OSError, match="injected"):
+        Snapshot(str(tmp_path / "s")).restore({"sd": out})

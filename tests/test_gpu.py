@@ -918,3 +918,29 @@ def test_gpu_take_checksums_hashed_on_device_and_verify(gpu, tmp_path, compressi
         f.seek(7)
         f.write(bytes([b[0] ^ 1]))
     assert s.verify().mismatched == [os.path.relpath(victim, root)]
+
+
+@pytest.mark.parametrize("batching", [True, False])
+def test_gpu_compressed_restore_with_split_head_read(gpu, tmp_path, monkeypatch, batching):
+    """Whole HSZ1 blobs read as a head and the rest: the head's frames go up
+    by H2D while the rest is read, then one decode -- direct into the target
+    (plain tensors) and through the scratch + region copy (slabs)."""
+    from hipsnapshot.knobs import override_is_batching_disabled
+
+    monkeypatch.setenv("HIPSNAPSHOT_READ_HEAD_BYTES", str(64 * 1024))
+    torch.manual_seed(5)
+    sd = StateDict(
+        w=(torch.randn(1500, 1000, device=gpu) * 0.02).to(torch.bfloat16),
+        v=(torch.randn(700, 900, device=gpu) * 0.02).to(torch.bfloat16),
+        f=torch.randn(400, 1000, device=gpu) * 1e-2,
+    )
+    ref = {k: v.clone() for k, v in sd.items()}
+    with override_is_batching_disabled(not batching), \
+            override_slab_size_threshold_bytes(8 << 20):
+        Snapshot.take(str(tmp_path / "s"), {"sd": sd}, compression="hsz1")
+        for v in sd.values():
+            v.zero_()
+        Snapshot(str(tmp_path / "s")).restore({"sd": sd})
+    torch.cuda.synchronize()
+    for k, v in ref.items():
+        assert torch.equal(sd[k], v), k
