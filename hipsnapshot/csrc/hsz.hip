@@ -1026,7 +1026,7 @@ hsz_encode2x_frame(const uint64_t f, const uint8_t* __restrict__ src, uint64_t l
 }
 
 template <int W>
-__global__ void __launch_bounds__(kThreadsX, 8)  // 2 workgroups / CU: <= 64 VGPRs
+__global__ void __launch_bounds__(kThreadsX, W == 2 ? 8 : 4)  // bf16: 2 workgroups / CU (<= 64 VGPRs)
 hsz_encode2x(const uint8_t* __restrict__ src, uint64_t logical, uint32_t frame_bytes,
              const FrameMeta* __restrict__ meta, const uint16_t* __restrict__ lane_bytes_all,
              const uint32_t* __restrict__ piece_bits_all, uint8_t* __restrict__ out,
@@ -1383,11 +1383,12 @@ int fail(const char* what, hipError_t e) {
   return -static_cast<int>(e) - 1;
 }
 
-// HIPSNAPSHOT_SPLIT_ENCODE=0 selects the one-thread-per-stream mode-2 encoder
+// HIPSNAPSHOT_SPLIT_ENCODE: 0 = one-thread-per-stream mode-2 encoder for every
+// width, 1 (default) = split encoder for 2-byte elements, 2 = for 4-byte too
 // (A/B switch; read per launch so a process can alternate).
-bool hsz_split_encode() {
+int hsz_split_encode() {
   const char* v = getenv("HIPSNAPSHOT_SPLIT_ENCODE");
-  return v == nullptr || v[0] != '0';
+  return v == nullptr || v[0] == '\0' ? 1 : atoi(v);
 }
 
 }  // namespace
@@ -1437,9 +1438,13 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
   // bf16/fp16: split-stream encoder (802 -> 420 us per GiB); fp32 stays on
   // hsz_encode2 (449 us vs 525 us: twice the bytes per group under the split
   // kernel's 64-VGPR budget) -- profiles/codec_r2/split_encode.md
-  const bool split = w == 2 && encode2x_fits(w, frame_bytes) && hsz_split_encode();
-  if (split)
+  const int split_mode = hsz_split_encode();
+  const bool split = encode2x_fits(w, frame_bytes) && (w == 2 ? split_mode > 0 : split_mode > 1);
+  if (split && w == 2)
     hipLaunchKernelGGL(hsz_encode2x<2>, dim3(g), dim3(kThreadsX), 0, s, src8, logical,
+                       frame_bytes, m, lanes, pbits, o, nf);
+  else if (split && w == 4)
+    hipLaunchKernelGGL(hsz_encode2x<4>, dim3(g), dim3(kThreadsX), 0, s, src8, logical,
                        frame_bytes, m, lanes, pbits, o, nf);
   else if (w == 2)
     hipLaunchKernelGGL(hsz_encode2<2>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes,
