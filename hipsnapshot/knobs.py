@@ -29,6 +29,7 @@ MI355X-specific knobs:
 
 from __future__ import annotations
 
+import math
 import os
 from contextlib import contextmanager
 from typing import Any, Generator, Optional
@@ -97,21 +98,52 @@ def set_local_ranks_hint(n: int) -> None:
     _local_ranks_hint[0] = max(1, int(n))
 
 
-def get_io_threads() -> int:
-    """Native I/O workers per storage plugin: ``HIPSNAPSHOT_IO_THREADS``, else
-    2 x (CPUs this process may run on) / (ranks on this host), within
-    [4, 16].  Buffered writes scale with threads only up to the CPU share:
-    8 processes x 16 writer threads on 16 CPUs wrote 26 GB/s to the page
-    cache, 8 x 2 threads 108 GB/s (scripts/pagecache_write_probe.py,
-    profiles/pagecache/)."""
-    v = _get("IO_THREADS")
-    if v is not None:
-        return int(v)
+def _cgroup_cpu_quota(root: str = "/sys/fs/cgroup") -> Optional[float]:
+    """CPUs' worth of time the cgroup may use (CFS bandwidth quota / period),
+    None when unlimited or unknown.  cgroup v2 ``cpu.max``, else v1
+    ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``."""
+    try:
+        with open(os.path.join(root, "cpu.max")) as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else int(quota) / int(period)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open(os.path.join(root, "cpu", "cpu.cfs_quota_us")) as f:
+            quota = int(f.read())
+        with open(os.path.join(root, "cpu", "cpu.cfs_period_us")) as f:
+            period = int(f.read())
+        return None if quota <= 0 else quota / period
+    except (OSError, ValueError):
+        return None
+
+
+def available_cpus() -> int:
+    """CPUs this process can actually use: its affinity mask, capped by the
+    cgroup's CPU quota.  (A GPU box here shows 256 CPUs in the mask and a
+    16-CPU quota in ``cpu.max``: every thread above the quota only makes the
+    whole group wait for the next period.)"""
     try:
         cpus = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):  # pragma: no cover - non-Linux
         cpus = os.cpu_count() or 16
-    return max(4, min(16, 2 * cpus // _local_ranks_hint[0]))
+    quota = _cgroup_cpu_quota()
+    if quota is not None:
+        cpus = min(cpus, max(1, int(math.ceil(quota))))
+    return cpus
+
+
+def get_io_threads() -> int:
+    """Native I/O workers per storage plugin: ``HIPSNAPSHOT_IO_THREADS``, else
+    2 x (CPUs this process can use, ``available_cpus``) / (ranks on this
+    host), within [4, 16].  Buffered writes scale with threads only up to the
+    CPU share: 8 processes x 16 writer threads on 16 CPUs wrote 26 GB/s to
+    the page cache, 8 x 2 threads 108 GB/s (scripts/pagecache_write_probe.py,
+    profiles/pagecache/)."""
+    v = _get("IO_THREADS")
+    if v is not None:
+        return int(v)
+    return max(4, min(16, 2 * available_cpus() // _local_ranks_hint[0]))
 
 
 def compress_host_tensors() -> bool:

@@ -82,6 +82,7 @@ def test_io_threads_follow_cpu_share_and_local_ranks(monkeypatch):
     monkeypatch.delenv("HIPSNAPSHOT_IO_THREADS", raising=False)
     monkeypatch.delenv("TORCHSNAPSHOT_IO_THREADS", raising=False)
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))
+    monkeypatch.setattr(knobs, "_cgroup_cpu_quota", lambda root="": None)
     try:
         knobs.set_local_ranks_hint(1)
         assert knobs.get_io_threads() == 16
@@ -182,3 +183,34 @@ def test_thread_staging_failure_stops_workers_and_releases_buffers():
     with pytest.raises(RuntimeError, match="staging failed"):
         asyncio.new_event_loop().run_until_complete(main())
     assert track["live"] == 0  # every staged buffer went back
+
+
+def test_io_threads_respect_cgroup_cpu_quota(tmp_path, monkeypatch):
+    """A 16-CPU quota on a 256-CPU affinity mask sizes writers by the quota:
+    1 rank -> 16 workers, 8 ranks on the host -> 4 each (not 16 each)."""
+    from hipsnapshot import knobs
+
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    assert knobs._cgroup_cpu_quota(str(tmp_path)) == 16.0
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert knobs._cgroup_cpu_quota(str(tmp_path)) is None
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("400000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert knobs._cgroup_cpu_quota(str(v1)) == 4.0
+
+    monkeypatch.delenv("HIPSNAPSHOT_IO_THREADS", raising=False)
+    monkeypatch.delenv("TORCHSNAPSHOT_IO_THREADS", raising=False)
+    monkeypatch.setattr(knobs.os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setattr(knobs, "_cgroup_cpu_quota", lambda root="": 16.0)
+    old = knobs._local_ranks_hint[0]
+    try:
+        knobs._local_ranks_hint[0] = 1
+        assert knobs.available_cpus() == 16 and knobs.get_io_threads() == 16
+        knobs._local_ranks_hint[0] = 8
+        assert knobs.get_io_threads() == 4
+        monkeypatch.setattr(knobs, "_cgroup_cpu_quota", lambda root="": None)
+        assert knobs.get_io_threads() == 16  # 2 x 256 / 8, capped
+    finally:
+        knobs._local_ranks_hint[0] = old
