@@ -52,6 +52,8 @@ def main() -> None:
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--baseline-steps", type=int, default=5)
+    ap.add_argument("--window-steps", type=int, default=12,
+                    help="train_time_lost_ms covers at least this many steps after async_take")
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
     ap.add_argument("--storage", default="fs", choices=["fs", "s3"])
     ap.add_argument("--path", default=None)
@@ -157,10 +159,19 @@ def main() -> None:
         during.append(step())
     pending.wait()
     drain = time.perf_counter() - t0
+    # training time lost to the checkpoint: wall time from the async_take call
+    # through a window of at least --window-steps steps (the unblock and every
+    # step slowed by the drain inside it) minus the same steps at baseline
+    extra = 0
+    while len(during) + extra < args.window_steps:
+        step()
+        extra += 1
+    lost = (time.perf_counter() - t0) - (len(during) + extra) * base_ms / 1e3
     # every rank must finish its loop before collectives resume
     unblock = max_over_ranks(unblock, dev)
     drain = max_over_ranks(drain, dev)
     n_during = int(max_over_ranks(float(len(during)), dev))
+    lost = max_over_ranks(lost, dev)
     mean_ms = max_over_ranks(statistics.mean(during) if during else 0.0, dev) * 1e3
     max_ms = max_over_ranks(max(during) if during else 0.0, dev) * 1e3
 
@@ -187,6 +198,7 @@ def main() -> None:
           "steps_during_drain": n_during, "step_ms_during_drain_mean": round(mean_ms, 2),
           "step_ms_during_drain_max": round(max_ms, 2),
           "slowdown_during_drain": round(mean_ms / base_ms - 1.0, 4) if during else None,
+          "window_steps": len(during) + extra, "train_time_lost_ms": round(lost * 1e3, 1),
           "restore_bitwise_ok": bool(okt.item()), "stored_bytes": stored,
           "data": "synthetic tokens, random init"})
     sync(dev)
