@@ -152,6 +152,9 @@ def main() -> None:
         Snapshot.take(path, app_state, storage_options=opts, compression=args.compression)
         log(f"warmup {i}: {time.monotonic() - t0:.3f}s")
 
+    from hipsnapshot.utils.tracing import GcWatch
+
+    gcw = GcWatch().start()  # Python GC time inside the timed regions (reported)
     barrier_sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -159,7 +162,9 @@ def main() -> None:
         Snapshot.take(path, app_state, storage_options=opts, compression=args.compression)
         log(f"step {i}: {time.perf_counter() - ts:.3f}s")
     barrier_sync()
-    elapsed = time.perf_counter() - t0
+    t_end = time.perf_counter()
+    elapsed = t_end - t0
+    gc_take_ms = gcw.ms_between(t0, t_end)
     e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
     elapsed = float(e.item())
@@ -192,11 +197,13 @@ def main() -> None:
     restore_ok = None
     restore_gbps = None
     restore_each = None
+    gc_restore_ms = None
     if not args.no_restore_check:
         # bitwise restore check of EVERY local shard (HBM holds the copies)
         named = list(model.named_parameters())
         refs = [p._local_tensor.clone() for _, p in named]
         times, bad = [], []
+        gc_restore_ms = 0.0
         for _ in range(max(1, args.restore_iters)):
             for _, p in named:
                 p._local_tensor.zero_()
@@ -205,6 +212,7 @@ def main() -> None:
             Snapshot(path).restore(app_state)
             barrier_sync()
             times.append(time.perf_counter() - tr)
+            gc_restore_ms += gcw.ms_between(tr, tr + times[-1])
             # compare against the parameters as they are NOW (load_state_dict
             # may re-point a module's parameter)
             named = list(model.named_parameters())
@@ -275,6 +283,10 @@ def main() -> None:
             "restore_GBps_each": restore_each,
             "compression": args.compression,
             "stored_bytes": stored,
+            # rank 0's Python cyclic-GC time inside the timed takes / restores
+            "gc_ms_in_timed_takes": round(gc_take_ms, 2),
+            "gc_ms_in_timed_restores": round(gc_restore_ms, 2) if gc_restore_ms is not None
+            else None,
             "raw_GBps": round(raw_gbps, 3) if raw_gbps else None,
             "raw_note": "same save with uncompressed reference-format blobs "
                         f"({args.raw_steps} timed takes after 1 warmup)",

@@ -34,7 +34,8 @@ import psutil
 
 from .. import knobs
 from ..ops import checksum
-from ..io_types import ReadIO, ReadReq, StagedBuffer, StoragePlugin, WriteIO, WriteReq, as_staged
+from ..io_types import (ReadIO, ReadReq, StagedBuffer, StoragePlugin, WriteIO, WriteReq, as_staged,
+                        run_sync)
 from ..utils.tracing import timeline
 
 logger = logging.getLogger(__name__)
@@ -235,7 +236,7 @@ class PendingIOWork:
                     f"{st.t_done - st.t_start:.3f}s")
 
     def sync_complete(self, event_loop: asyncio.AbstractEventLoop) -> None:
-        event_loop.run_until_complete(self.complete())
+        run_sync(event_loop, self.complete())
 
 
 async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
@@ -468,13 +469,13 @@ class DeferredIOWork:
                 raise r
 
     def sync_complete(self, event_loop: asyncio.AbstractEventLoop) -> None:
-        event_loop.run_until_complete(self.complete())
+        run_sync(event_loop, self.complete())
 
 
 def sync_execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                             memory_budget_bytes: int, rank: int,
                             event_loop: asyncio.AbstractEventLoop) -> PendingIOWork:
-    return event_loop.run_until_complete(
+    return run_sync(event_loop,
         execute_write_reqs(write_reqs, storage, memory_budget_bytes, rank))
 
 
@@ -689,7 +690,7 @@ def order_reads_for_pipeline(read_reqs: List[ReadReq], lead_min_bytes: int = 1 <
 def sync_execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                            memory_budget_bytes: int, rank: int,
                            event_loop: asyncio.AbstractEventLoop) -> PipelineStats:
-    return event_loop.run_until_complete(
+    return run_sync(event_loop,
         execute_read_reqs(read_reqs, storage, memory_budget_bytes, rank))
 
 

@@ -264,11 +264,36 @@ class StoragePlugin(ABC):
         _run(self.close(), event_loop)
 
 
+async def _capture(coro):
+    try:
+        return await coro, None
+    except BaseException as e:  # noqa: BLE001 - re-raised by run_sync
+        return None, e
+
+
+def run_sync(loop: asyncio.AbstractEventLoop, coro):
+    """``loop.run_until_complete(coro)`` without a reference cycle on error.
+
+    An exception raised through ``run_until_complete`` keeps its frame, whose
+    ``future`` local is the task holding that same exception: a cycle that
+    pins every caller frame's locals (a take's whole plan: entries, write
+    requests, stagers) until the next full collection.  ``_uncommit``'s
+    expected FileNotFoundError on a fresh path did exactly that.  Here the
+    task ends normally and the exception is re-raised from this frame only."""
+    res, err = loop.run_until_complete(_capture(coro))
+    if err is None:
+        return res
+    try:
+        raise err
+    finally:
+        del err
+
+
 def _run(coro, loop: Optional[asyncio.AbstractEventLoop]):
     if loop is None:
         loop = asyncio.new_event_loop()
         try:
-            return loop.run_until_complete(coro)
+            return run_sync(loop, coro)
         finally:
             loop.close()
-    return loop.run_until_complete(coro)
+    return run_sync(loop, coro)

@@ -67,7 +67,7 @@ from .format.manifest import (
 from .io.batcher import batch_read_requests, batch_write_requests
 from .io.preparer import prepare_read, prepare_write
 from .io.sharded import is_sharded
-from .io_types import ReadIO, ReadReq, StoragePlugin, WriteIO, WriteReq
+from .io_types import ReadIO, ReadReq, StoragePlugin, WriteIO, WriteReq, run_sync
 from .ops import checksum
 from .parallel.comm import Comm
 from .parallel.elasticity import get_manifest_for_rank, handle_sharded_tensor_elasticity
@@ -279,7 +279,7 @@ class Snapshot:
         # of rank 0's critical path on an overlay filesystem.)
         if not knobs.checksum_enabled():
             try:
-                loop.run_until_complete(storage.delete_dir(checksum.CHECKSUM_DIR))
+                run_sync(loop, storage.delete_dir(checksum.CHECKSUM_DIR))
             except (FileNotFoundError, KeyError, NotImplementedError):
                 pass
             except Exception as e:  # noqa: BLE001
@@ -723,7 +723,7 @@ class Snapshot:
         metadata.__dict__.pop("_json_async", None)  # later edits re-encode
         commit = getattr(storage, "commit_metadata", None)
         if commit is not None:
-            loop.run_until_complete(commit(SNAPSHOT_METADATA_FNAME, buf))
+            run_sync(loop, commit(SNAPSHOT_METADATA_FNAME, buf))
         else:
             storage.sync_write(WriteIO(path=SNAPSHOT_METADATA_FNAME, buf=buf), loop)
 

@@ -155,6 +155,49 @@ class Timeline:
 timeline = Timeline()
 
 
+class GcWatch:
+    """Records the duration of every Python cyclic-GC pass (``gc.callbacks``).
+
+    A generation-2 pass walks the whole heap -- 100+ ms in a process that
+    imported torch and built a model -- and lands wherever the allocation
+    counters run over, e.g. right after a take re-enables GC.  Benchmarks use
+    this to report how much of a timed region was GC; with a timeline enabled
+    each pass is also a ``gc`` span."""
+
+    def __init__(self) -> None:
+        self.events: list = []  # (generation, t_start, t_end)
+        self._t = 0.0
+        self._on = False
+
+    def start(self) -> "GcWatch":
+        import gc
+
+        if not self._on:
+            gc.callbacks.append(self._cb)
+            self._on = True
+        return self
+
+    def stop(self) -> None:
+        import gc
+
+        if self._on:
+            gc.callbacks.remove(self._cb)
+            self._on = False
+
+    def _cb(self, phase: str, info: dict) -> None:
+        if phase == "start":
+            self._t = time.perf_counter()
+            return
+        t1 = time.perf_counter()
+        self.events.append((info.get("generation", -1), self._t, t1))
+        timeline.add(f"gc_gen{info.get('generation', -1)}", "gc", self._t, t1,
+                     collected=info.get("collected", 0))
+
+    def ms_between(self, t_start: float, t_end: float, min_generation: int = 0) -> float:
+        return 1e3 * sum(max(0.0, min(b, t_end) - max(a, t_start))
+                         for g, a, b in self.events if g >= min_generation)
+
+
 @contextlib.contextmanager
 def paused_gc():
     """Suspend Python's cyclic GC for a bounded critical section (and, with

@@ -183,3 +183,58 @@ def test_quantize_fp8_cpu(tmp_path):
     Snapshot(str(tmp_path / "s")).restore({"sd": out})
     rel = (out["w"] - w).abs().max() / w.abs().max()
     assert rel < 0.08 and torch.equal(out["i"], torch.arange(5))
+
+
+def _cyclic_garbage(fn):
+    import gc
+
+    gc.collect()
+    gc.set_debug(gc.DEBUG_SAVEALL)
+    try:
+        fn()
+        gc.collect()
+        found = list(gc.garbage)
+    finally:
+        gc.garbage.clear()
+        gc.set_debug(0)
+    return found
+
+
+def test_take_leaves_no_reference_cycles(tmp_path):
+    """A take to a fresh path hits the expected FileNotFoundError when it
+    removes an older commit; that error must not leave a cycle (task <->
+    traceback frame) pinning the take's plan until a full GC."""
+    from hipsnapshot.io_types import WriteReq
+
+    st = StateDict({f"w{i}": torch.randn(32, 8) for i in range(20)})
+    for name, fn in [
+        ("take", lambda: Snapshot.take(str(tmp_path / "s"), {"m": st})),
+        ("async_take", lambda: Snapshot.async_take(str(tmp_path / "a"), {"m": st}).wait()),
+        ("restore", lambda: Snapshot(str(tmp_path / "s")).restore({"m": st})),
+    ]:
+        found = _cyclic_garbage(fn)
+        assert not [o for o in found if isinstance(o, (WriteReq, BaseException))], name
+
+
+def test_run_sync_reraises_without_cycle():
+    import asyncio
+
+    from hipsnapshot.io_types import run_sync
+
+    async def boom():
+        raise FileNotFoundError("x")
+
+    async def ok():
+        return 7
+
+    loop = asyncio.new_event_loop()
+    try:
+        assert run_sync(loop, ok()) == 7
+
+        def fail():
+            with pytest.raises(FileNotFoundError):
+                run_sync(loop, boom())
+
+        assert not [o for o in _cyclic_garbage(fail) if isinstance(o, BaseException)]
+    finally:
+        loop.close()
