@@ -1,0 +1,13 @@
+#!/bin/bash
+# restore in a fresh process (restart case), then the same with a phase timeline
+set -o pipefail
+out=gpurun_out/cold_restore; mkdir -p $out
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
+mkdir -p $HIPSNAPSHOT_BENCH_DIR
+timeout -k 10 400 python benchmarks/cold_restore/main.py > $out/cold.json 2> $out/cold.err \
+    || { echo COLD_FAIL; tail -30 $out/cold.err; exit 1; }
+cat $out/cold.json
+HIPSNAPSHOT_TIMELINE=$PWD/$out/t timeout -k 10 400 python benchmarks/cold_restore/main.py \
+    > $out/cold_tl.json 2> $out/cold_tl.err || { echo COLD_TL_FAIL; tail -30 $out/cold_tl.err; exit 1; }
+cat $out/cold_tl.json
+ls $out
