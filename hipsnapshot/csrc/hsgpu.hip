@@ -39,6 +39,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <type_traits>
 #include <vector>
@@ -784,8 +785,29 @@ void* alloc_thp_registered(size_t want) {
   char* p = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(base) + kHuge - 1) & ~(kHuge - 1));
   (void)madvise(p, want, MADV_HUGEPAGE);
   // fault every page in now (a huge page per 2 MiB where the kernel grants
-  // one): registration then maps resident pages, and no copy pays a fault
-  for (size_t off = 0; off < want; off += 4096) p[off] = 0;
+  // one): registration then maps resident pages, and no copy pays a fault.
+  // The kernel zeroes each page on its first touch; a large block is split
+  // over a few threads (HIPSNAPSHOT_PINNED_FAULT_THREADS, default 4) so a
+  // cold process's first blocks -- a restore's first reads -- wait less.
+  const size_t kSplit = size_t(32) << 20;
+  int nt = 4;
+  if (const char* fv = getenv("HIPSNAPSHOT_PINNED_FAULT_THREADS")) nt = std::max(1, atoi(fv));
+  nt = static_cast<int>(std::min<size_t>(size_t(nt), std::max<size_t>(1, want / kSplit)));
+  auto touch = [p](size_t lo, size_t hi) {
+    for (size_t off = lo; off < hi; off += 4096) p[off] = 0;
+  };
+  if (nt <= 1) {
+    touch(0, want);
+  } else {
+    const size_t per = (want / nt + kHuge - 1) / kHuge * kHuge;
+    std::vector<std::thread> th;
+    for (int i = 1; i < nt; ++i) {
+      const size_t lo = std::min(want, per * i), hi = std::min(want, per * (i + 1));
+      if (lo < hi) th.emplace_back(touch, lo, hi);
+    }
+    touch(0, std::min(want, per));
+    for (auto& t : th) t.join();
+  }
   if (hipHostRegister(p, want, hipHostRegisterDefault) != hipSuccess) {
     (void)hipGetLastError();
     munmap(base, len);
