@@ -538,8 +538,10 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                     # (reads enter the engine queue in request order).  A large
                     # blob is read as a head and the rest: the consumer moves
                     # the head's frames to the GPU while the rest arrives.
+                    t_d = time.perf_counter()
                     full = await asyncio.get_running_loop().run_in_executor(
                         aux_pool(), rr.buffer_consumer.get_compressed_read_dest, stored)
+                    timeline.add("read_dest", "io", t_d, time.perf_counter(), bytes=stored)
                     if full is None:
                         full = as_staged(bytearray(max(stored, 1)))
                     dest = full
