@@ -803,7 +803,12 @@ void* alloc_thp_registered(size_t want) {
     std::vector<std::thread> th;
     for (int i = 1; i < nt; ++i) {
       const size_t lo = std::min(want, per * i), hi = std::min(want, per * (i + 1));
-      if (lo < hi) th.emplace_back(touch, lo, hi);
+      if (lo >= hi) continue;
+      try {
+        th.emplace_back(touch, lo, hi);
+      } catch (...) {  // no thread to be had: touch this part here
+        touch(lo, hi);
+      }
     }
     touch(0, std::min(want, per));
     for (auto& t : th) t.join();
