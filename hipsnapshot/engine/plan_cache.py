@@ -118,11 +118,11 @@ def fast_signatures(resident: Dict[str, Any]) -> Optional[tuple]:
     for k, v in resident.items():
         lt = getattr(v, "_local_tensor", None)
         if lt is not None:
-            out.append((id(v), lt.data_ptr(), lt.shape, lt.stride(), id(v._spec)))
+            out.append((id(v), lt.data_ptr(), lt.shape, lt.stride(), lt.dtype, id(v._spec)))
         elif ShardedTensor is not None and isinstance(v, ShardedTensor):
             return None
         else:
-            out.append((id(v), v.data_ptr(), v.shape, v.stride()))
+            out.append((id(v), v.data_ptr(), v.shape, v.stride(), v.dtype, v.device))
     return tuple(out)
 
 

@@ -244,9 +244,13 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                              stage_threads: Optional[int] = None,
                              io_concurrency: Optional[int] = None,
                              gate: Optional[MemoryGate] = None,
-                             background: bool = False) -> PendingIOWork:
+                             background: bool = False,
+                             wait_copies: bool = False) -> PendingIOWork:
     """``background``: the pipeline runs while the caller keeps using the GPU
-    (async-take drain); its staging kernels get a capped grid."""
+    (async-take drain); its staging kernels get a capped grid.
+    ``wait_copies``: return only once every staged buffer's asynchronous
+    device copy (and on-device hash) has finished, i.e. nothing reads the
+    source tensors any more (async take from live, un-frozen tensors)."""
     stage_threads = stage_threads or knobs.get_stage_threads()
     io_concurrency = io_concurrency or knobs.get_io_threads()
     executor = _acquire_pool("stage_bg" if background else "stage", stage_threads, rank)
@@ -265,20 +269,36 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     reporter = WriteReporter(rank, memory_budget_bytes)
 
     want_sums = knobs.checksum_enabled()
+    copies: List[asyncio.Future] = []  # waits for in-flight device -> host copies
 
     def _staged(wr: WriteReq, buf: StagedBuffer, cost: int, t_s: float) -> None:
         timeline.add("stage", "stage", t_s, time.perf_counter(), path=wr.path,
                      bytes=buf.nbytes)
         stats.bytes_staged += buf.nbytes
-        io_tasks.add(asyncio.ensure_future(_write(wr, buf, cost)))
+        copy = None
+        if buf.ready is not None:
+            # the blob's device -> host copy is still on the SDMA engine
+            copy = asyncio.ensure_future(_wait_ready(buf))
+            if wait_copies:
+                copies.append(copy)
+        io_tasks.add(asyncio.ensure_future(_write(wr, buf, cost, copy)))
         reporter.maybe_report(len(pending), 0, len(io_tasks), gate.in_use, stats.bytes_written)
 
-    async def _write(wr: WriteReq, buf: StagedBuffer, cost: int) -> None:
+    async def _copies_done() -> None:
+        """``wait_copies``: block until no copy reads a source tensor."""
+        res = await asyncio.gather(*copies, return_exceptions=True)
+        copies.clear()
+        errs = [r for r in res if isinstance(r, BaseException)]
+        if errs:
+            await asyncio.gather(*io_tasks, return_exceptions=True)
+            raise errs[0]
+
+    async def _write(wr: WriteReq, buf: StagedBuffer, cost: int,
+                     copy: Optional[asyncio.Future]) -> None:
         hashing = None
         try:
-            if buf.ready is not None:
-                # the blob's device -> host copy is still on the SDMA engine
-                await _wait_ready(buf)
+            if copy is not None:
+                await asyncio.shield(copy)
             if want_sums and buf.checksum is None:
                 # host-staged blob: hash it on the host while it is written
                 # (both only read the buffer; the GPU stager hashed the rest)
@@ -303,6 +323,8 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             if hashing is not None and not hashing.done():
                 # the hash still reads the buffer: it must finish before release
                 await asyncio.gather(asyncio.shield(hashing), return_exceptions=True)
+            if copy is not None and not copy.done():
+                await asyncio.wait([copy])  # (a cancelled wait leaves the copy running)
             if buf.ready is not None:
                 # an early exit (failure, cancellation): the copy may still be
                 # writing into the buffer
@@ -327,6 +349,8 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
             await asyncio.gather(*io_tasks, return_exceptions=True)
             executor.shutdown(wait=True)
             raise failure[0]
+        if wait_copies:
+            await _copies_done()
         stats.t_staged = time.monotonic()
         logger.debug(f"Rank {rank} completed staging in {stats.t_staged - stats.t_start:.3f}s")
         return PendingIOWork(io_tasks, executor, stats, failure, gate)
@@ -361,12 +385,23 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                     continue
                 _staged(wr, as_staged(task.result()), cost, t_s)
         if failure:
-            for t in staging:
-                t.cancel()
+            # stage tasks in flight are NOT cancelled: their executor jobs
+            # would still submit copies whose buffers nobody waits for (a
+            # leaked DMA slot, a pinned block the engine still writes into).
+            # Let them finish, then wait for each copy and free its buffer.
+            res = await asyncio.gather(*staging, return_exceptions=True)
+            for (wr, cost, _t), r in zip(staging.values(), res):
+                if not isinstance(r, BaseException):
+                    buf = as_staged(r)
+                    if buf.ready is not None:
+                        await asyncio.gather(_wait_ready(buf), return_exceptions=True)
+                    buf.release()
+                gate.release(cost)
+            staging.clear()
             # writes already handed to the I/O engine are NOT cancelled: their
             # pinned buffers may only go back to the pool once the engine is
             # done reading them (queued ones return without writing)
-            await asyncio.gather(*staging, *io_tasks, return_exceptions=True)
+            await asyncio.gather(*io_tasks, return_exceptions=True)
             executor.shutdown(wait=True)
             raise failure[0]
     except BaseException:
@@ -375,6 +410,8 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     finally:
         # staging is over: later wake-ups (write completions) are not needed
         gate.unsubscribe(wake)
+    if wait_copies:
+        await _copies_done()
     stats.t_staged = time.monotonic()
     logger.debug(f"Rank {rank} completed staging in {stats.t_staged - stats.t_start:.3f}s")
     return PendingIOWork(io_tasks, executor, stats, failure, gate)
@@ -420,7 +457,12 @@ async def _stage_on_threads(pending: deque, nthreads: int, executor: ThreadPoolE
             try:
                 loop.call_soon_threadsafe(on_staged, wr, buf, cost, t_s)
             except RuntimeError:  # the loop is gone (the take was abandoned)
-                buf.release()
+                from .staging import wait_ready
+
+                try:
+                    wait_ready(buf)  # the engine may still write into it
+                finally:
+                    buf.release()
                 return
 
     futs = [executor.submit(worker) for _ in range(max(1, min(nthreads, len(pending))))]
@@ -474,9 +516,11 @@ class DeferredIOWork:
 
 def sync_execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                             memory_budget_bytes: int, rank: int,
-                            event_loop: asyncio.AbstractEventLoop) -> PendingIOWork:
+                            event_loop: asyncio.AbstractEventLoop,
+                            wait_copies: bool = False) -> PendingIOWork:
     return run_sync(event_loop,
-        execute_write_reqs(write_reqs, storage, memory_budget_bytes, rank))
+        execute_write_reqs(write_reqs, storage, memory_budget_bytes, rank,
+                           wait_copies=wait_copies))
 
 
 def _expected_read_bytes(rr: ReadReq) -> Optional[int]:

@@ -9,7 +9,10 @@ write
   dim into <= ``max_shard_size`` pieces stored at
   ``sharded/<logical_path>_<off0>_<off1>...``.  For a DTensor, ranks whose
   coordinate along a ``Replicate`` mesh dim is not 0 write nothing (HSDP /
-  replicated DTensors are saved once); ``Partial`` is reduced first.
+  replicated DTensors are saved once); ``Partial`` is reduced first.  Any
+  mesh rank and any mix of ``Shard`` / ``_StridedShard`` placements (FSDP2 x
+  TP) is decomposed into the global boxes the local tensor holds
+  (``dim_index_runs``): a strided layout saves several boxes per rank.
 
 read (elastic)
   every saved piece x local shard overlap is computed once; each saved piece
@@ -77,15 +80,118 @@ class LocalBox:
         self.sharding_dim = sharding_dim
 
 
-# DTensorSpec (hashable, hash cached by torch) -> (skip, local shape, global
-# offset, sharding dim): the same layouts recur every snapshot of a training
-# job, and FSDP2 state dicts share one spec object per parameter.
+# DTensorSpec (hashable, hash cached by torch) -> (skip, boxes, sharding dim):
+# the same layouts recur every snapshot of a training job, and FSDP2 state
+# dicts share one spec object per parameter.
 _LAYOUT_CACHE: dict = {}
 
 
-def _dtensor_layout(dt, for_write: bool):
-    from torch.distributed.tensor._utils import compute_local_shape_and_global_offset
+def _shard_dim_of(p, ndim: int) -> Optional[int]:
+    """Tensor dim split by placement ``p`` (``Shard`` or ``_StridedShard``)."""
+    if isinstance(p, DShard) or type(p).__name__ == "_StridedShard":
+        d = int(p.dim)
+        return d + ndim if d < 0 else d
+    return None
 
+
+def _chunk_bounds(n: int, k: int, i: int) -> Tuple[int, int]:
+    """Piece ``i`` of ``n`` items split ``k`` ways with ``torch.chunk``
+    semantics (ceil-sized pieces, trailing pieces empty)."""
+    cs = -(-n // k) if n else 0
+    lo = min(i * cs, n)
+    return lo, min(lo + cs, n)
+
+
+def _select_runs(runs: List[Tuple[int, int]], lo: int, hi: int) -> List[Tuple[int, int]]:
+    """Sub-sequence ``[lo, hi)`` (local positions) of a run-encoded index list."""
+    out, pos = [], 0
+    for g, ln in runs:
+        a, b = max(lo, pos), min(hi, pos + ln)
+        if b > a:
+            out.append((g + a - pos, b - a))
+        pos += ln
+    return out
+
+
+def dim_index_runs(global_shape: Sequence[int], mesh_shape: Sequence[int],
+                   coord: Sequence[int], placements: Sequence[Any]) -> List[List[Tuple[int, int]]]:
+    """Per tensor dim, the global indices the local tensor holds, in local
+    order, as ``(global_start, length)`` runs.
+
+    Placements are applied left to right over the mesh dims, each splitting
+    the index list the previous ones left on its tensor dim.  ``Shard(d)``
+    takes ``torch.chunk`` piece ``coord``.  ``_StridedShard(d, sf)`` (FSDP2
+    over tensor parallel) first cuts the list into ``sf`` pieces, cuts each of
+    those ``mesh`` ways and concatenates piece ``coord`` of each -- so a local
+    tensor can hold several disjoint runs of a dim.  Multi-dim meshes (HSDP,
+    FSDP x TP, 2-D TP) compose the same way.  Equivalent of the reference's
+    shard metadata (`/root/reference/torchsnapshot/io_preparers/sharded_tensor.py:127-170`),
+    which only knows one box per shard.
+    """
+    runs = [[(0, int(n))] for n in global_shape]
+    for mdim, p in enumerate(placements):
+        d = _shard_dim_of(p, len(global_shape))
+        if d is None:
+            continue
+        n = sum(ln for _, ln in runs[d])
+        k, r = int(mesh_shape[mdim]), int(coord[mdim])
+        sf = int(getattr(p, "split_factor", 1)) if type(p).__name__ == "_StridedShard" else 1
+        new: List[Tuple[int, int]] = []
+        for j in range(sf):
+            a, b = _chunk_bounds(n, sf, j)
+            c0, c1 = _chunk_bounds(b - a, k, r)
+            for g, ln in _select_runs(runs[d], a + c0, a + c1):
+                if new and new[-1][0] + new[-1][1] == g:
+                    new[-1] = (new[-1][0], new[-1][1] + ln)
+                else:
+                    new.append((g, ln))
+        runs[d] = new
+    return runs
+
+
+def runs_to_boxes(runs: List[List[Tuple[int, int]]]
+                  ) -> List[Tuple[List[int], List[int], List[int]]]:
+    """Cartesian product of per-dim runs -> ``(local_offsets, global_offsets,
+    sizes)`` boxes.  One box for every contiguous (Shard-only) layout."""
+    boxes: List[Tuple[List[int], List[int], List[int]]] = [([], [], [])]
+    for dim_runs in runs:
+        nxt = []
+        for lo, go, sz in boxes:
+            pos = 0
+            for g, ln in dim_runs:
+                nxt.append((lo + [pos], go + [g], sz + [ln]))
+                pos += ln
+        boxes = nxt
+    return boxes
+
+
+def _implicit_replica(mesh) -> bool:
+    """True when this rank holds a copy of a submesh DTensor that another rank
+    writes.  A DTensor on a submesh (FSDP2 x TP's norm weights live on the dp
+    submesh of a (dp, tp) mesh) is implicitly replicated over the root mesh
+    dims the submesh does not span; only coordinate 0 along those dims
+    writes.  A root dim is spanned when stepping along it from this rank stays
+    inside the submesh's ranks (works for sliced and flattened submeshes)."""
+    get_root = getattr(mesh, "_get_root_mesh", None)
+    root = get_root() if get_root is not None else None
+    if root is None or root is mesh or root.mesh.numel() == mesh.mesh.numel():
+        return False
+    rc = root.get_coordinate()
+    if rc is None:
+        return False
+    members = set(int(r) for r in mesh.mesh.flatten().tolist())
+    grid = root.mesh
+    for i, c in enumerate(rc):
+        if grid.shape[i] == 1:
+            continue
+        other = list(rc)
+        other[i] = 1 if c == 0 else 0
+        if int(grid[tuple(other)]) not in members and c != 0:
+            return True
+    return False
+
+
+def _dtensor_layout(dt, for_write: bool):
     key = (dt._spec, for_write)
     hit = _LAYOUT_CACHE.get(key)
     if hit is not None:
@@ -93,12 +199,13 @@ def _dtensor_layout(dt, for_write: bool):
     placements = list(dt.placements)
     mesh = dt.device_mesh
     coord = mesh.get_coordinate()
-    skip = coord is None or (for_write and any(
-        isinstance(p, Replicate) and coord[mdim] != 0 for mdim, p in enumerate(placements)))
-    shape, offset = ((), ()) if coord is None else \
-        compute_local_shape_and_global_offset(dt.shape, mesh, placements)
-    sdim = next((p.dim for p in placements if isinstance(p, DShard)), 0)
-    hit = (skip, [int(x) for x in shape], [int(x) for x in offset], sdim)
+    skip = coord is None or (for_write and (any(
+        isinstance(p, Replicate) and coord[mdim] != 0 for mdim, p in enumerate(placements))
+        or _implicit_replica(mesh)))
+    boxes = [] if coord is None else runs_to_boxes(
+        dim_index_runs(dt.shape, mesh.shape, coord, placements))
+    sdim = next((d for d in (_shard_dim_of(p, dt.dim()) for p in placements) if d is not None), 0)
+    hit = (skip, boxes, sdim)
     if len(_LAYOUT_CACHE) > 65536:
         _LAYOUT_CACHE.clear()
     _LAYOUT_CACHE[key] = hit
@@ -107,21 +214,25 @@ def _dtensor_layout(dt, for_write: bool):
 
 def _dtensor_boxes(dt, for_write: bool) -> List[LocalBox]:
     placements = dt.placements
-    for p in placements:
-        if type(p).__name__ == "_StridedShard":
-            raise NotImplementedError("DTensor _StridedShard placements are not supported yet")
     if any(isinstance(p, Partial) for p in placements):
         dt = dt.redistribute(dt.device_mesh,
                              [Replicate() if isinstance(p, Partial) else p for p in placements])
-    skip, shape, offset, sdim = _dtensor_layout(dt, for_write)
+    skip, boxes, sdim = _dtensor_layout(dt, for_write)
     if skip:
         return []
     local = dt._local_tensor
-    if local.dim() == 0 and len(shape) == 0:
+    if local.dim() == 0:
         return [LocalBox([], [], local, 0)]
-    if any(s == 0 for s in shape):
-        return []
-    return [LocalBox(offset, shape, local, sdim)]
+    out = []
+    for lo, go, sz in boxes:
+        if any(s == 0 for s in sz):
+            continue
+        view = local
+        for d, (o, s) in enumerate(zip(lo, sz)):
+            if o or s != view.shape[d]:
+                view = view.narrow(d, o, s)
+        out.append(LocalBox(go, sz, view, sdim))
+    return out
 
 
 def local_boxes(obj: Any, for_write: bool = False) -> List[LocalBox]:

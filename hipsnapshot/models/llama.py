@@ -192,3 +192,43 @@ def build_fsdp_llama(cfg: LlamaConfig, device: torch.device,
     model.to_empty(device=device)
     init_weights_(model, std=1.0 / math.sqrt(cfg.dim))
     return model
+
+
+def llama_tp_plan(model: "Llama") -> dict:
+    """Megatron-style tensor-parallel plan: column-wise q/k/v/w1/w3 and the
+    output head, row-wise wo/w2 and the token embedding."""
+    from torch.distributed.tensor.parallel import ColwiseParallel, RowwiseParallel
+
+    plan = {"tok_embeddings": RowwiseParallel(), "output": ColwiseParallel()}
+    for i in range(len(model.layers)):
+        for n in ("attention.wq", "attention.wk", "attention.wv", "feed_forward.w1",
+                  "feed_forward.w3"):
+            plan[f"layers.{i}.{n}"] = ColwiseParallel()
+        for n in ("attention.wo", "feed_forward.w2"):
+            plan[f"layers.{i}.{n}"] = RowwiseParallel()
+    return plan
+
+
+def build_2d_llama(cfg: LlamaConfig, device: torch.device, mesh,
+                   dtype: torch.dtype = torch.bfloat16, tp_dim: str = "tp",
+                   dp_dim: str = "dp") -> nn.Module:
+    """Llama with tensor parallelism on ``mesh[tp_dim]`` and FSDP2 on
+    ``mesh[dp_dim]`` (2-D parallel).  Parameters that TP already split on dim
+    0 carry ``(_StridedShard(0), Shard(0))`` placements; row-wise ones carry
+    ``(Shard(0), Shard(1))``; norms ``(Shard(0), Replicate())``."""
+    from torch.distributed.fsdp import fully_shard
+    from torch.distributed.tensor.parallel import parallelize_module
+
+    with torch.device("meta"):
+        model = Llama(cfg).to(dtype)
+    tp = mesh[tp_dim]
+    parallelize_module(model, tp, llama_tp_plan(model))
+    for layer in model.layers:  # local head counts after the column split
+        layer.attention.n_heads //= tp.size()
+        layer.attention.n_kv //= tp.size()
+    for layer in model.layers:
+        fully_shard(layer, mesh=mesh[dp_dim])
+    fully_shard(model, mesh=mesh[dp_dim])
+    model.to_empty(device=device)
+    init_weights_(model, std=1.0 / math.sqrt(cfg.dim))
+    return model

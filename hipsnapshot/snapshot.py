@@ -343,6 +343,10 @@ class Snapshot:
                     cache_key = plan_cache.settings_key(everything, rank, comm.get_world_size(),
                                                         is_async, quantize, comp)
                     plan = plan_cache.lookup(cache_key, resident)
+                    if progress is not None and plan is not None:
+                        # owned by this take from here on: a failure anywhere
+                        # below must release it (``_release_plan``)
+                        progress["plan"] = plan
         to_plan = flattened if plan is None else \
             {k: v for k, v in flattened.items() if k not in resident}
         t_prep = time.perf_counter()
@@ -430,7 +434,11 @@ class Snapshot:
             gather = _BackgroundGather(cls._gather_metadata, manifest, comm, plan)
         try:
             with timeline.span("stage", n=len(write_reqs)):
-                pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop)
+                # async: whatever was not frozen in HBM is copied from the
+                # LIVE tensors -- every such copy (and its hash) must have
+                # finished before async_take returns and training resumes
+                pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop,
+                                                  wait_copies=is_async)
         except BaseException:
             if gather is not None:
                 gather.join_quietly()  # the staging error is the one to report

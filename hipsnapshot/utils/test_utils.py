@@ -168,7 +168,9 @@ def run_distributed(fn: Callable, world_size: int, *args, backend: str = "gloo",
     while not errq.empty():
         errors.append(errq.get())
     if errors:
-        rank, tb = sorted(errors)[0]
+        # a peer's "connection closed" is a consequence: report the cause
+        secondary = ("Connection closed by peer", "Connection reset by peer")
+        rank, tb = sorted(errors, key=lambda e: (any(s in e[1] for s in secondary), e[0]))[0]
         raise RuntimeError(f"rank {rank} failed:\n{tb}")
     if alive:
         raise TimeoutError(f"{len(alive)} rank(s) timed out after {timeout}s")

@@ -234,6 +234,28 @@ def test_async_take_host_fallback_when_hbm_short(gpu, tmp_path):
     assert torch.equal(Snapshot(str(tmp_path / "s")).read_object("0/sd/w"), ref.cpu())
 
 
+@pytest.mark.parametrize("compression", ["none", "hsz1"])
+def test_async_take_unfrozen_large_tensor_not_raced(gpu, tmp_path, compression):
+    """No HBM room: a 256 MiB contiguous tensor (above the slab threshold) is
+    copied straight from the LIVE tensor by the asynchronous SDMA path, with
+    its on-device hash.  async_take must not return before that copy and hash
+    are done: a zero_() right after it must not reach the snapshot."""
+    w = torch.randn(64 << 20, device=gpu)
+    ref = w.clone()
+    with override_knob("HBM_STAGING_RESERVE_BYTES", str(1 << 50)), \
+            override_knob("CHECKSUM", "1"):
+        pending = Snapshot.async_take(str(tmp_path / "s"), {"sd": StateDict(w=w)},
+                                      compression=compression)
+        w.zero_()
+        pending.wait()
+    got = torch.zeros_like(w)
+    Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=got)})
+    assert torch.equal(got, ref)
+    from hipsnapshot.verify import verify_snapshot
+
+    assert verify_snapshot(str(tmp_path / "s")).ok
+
+
 def test_async_take_partial_hbm_freeze(gpu, tmp_path):
     """Arena smaller than the state: the requests that fit are frozen in HBM,
     the rest is host-staged before async_take returns -- both consistent."""

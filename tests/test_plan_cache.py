@@ -221,3 +221,39 @@ def test_fresh_app_state_dict_each_take_reuses_plan(tmp_path, resident):
     prog = StateDict(step=-1)
     Snapshot(str(tmp_path / "f2")).restore({"progress": prog})
     assert prog["step"] == 2
+
+
+@pytest.mark.parametrize("is_async", [False, True])
+def test_failed_planning_releases_reused_plan(tmp_path, resident, monkeypatch, is_async):
+    """A take that found a cached plan and then failed while planning the rest
+    (batching here) must hand the plan back: the next take reuses it."""
+    import hipsnapshot.snapshot as snapmod
+
+    def take(path):
+        if is_async:
+            Snapshot.async_take(path, {"sd": sd}).wait()
+        else:
+            Snapshot.take(path, {"sd": sd})
+
+    sd = _state(resident)
+    take(str(tmp_path / "s0"))  # plans are per mode (sync / async)
+    orig = snapmod.batch_write_requests
+
+    def boom(*a, **k):
+        raise RuntimeError("planning failed")
+
+    monkeypatch.setattr(snapmod, "batch_write_requests", boom)
+    with pytest.raises(RuntimeError, match="planning failed"):
+        take(str(tmp_path / "s1"))
+    monkeypatch.setattr(snapmod, "batch_write_requests", orig)
+    assert plan_cache.stats["hits"] == 1
+    for k, v in sd.items():
+        if isinstance(v, torch.Tensor):
+            v.add_(1.0)
+    ref = _snap(sd)
+    take(str(tmp_path / "s2"))
+    assert plan_cache.stats["hits"] == 2, plan_cache.stats
+    got = _restore(str(tmp_path / "s2"), ref)
+    for k, v in ref.items():
+        if isinstance(v, torch.Tensor):
+            assert torch.equal(got[k], v), k

@@ -77,6 +77,27 @@ class _AliasFinder(importlib.abc.MetaPathFinder):
         return importlib.util.spec_from_loader(fullname, _AliasLoader(target_name))
 
 
+def _warn_if_shadowing() -> None:
+    """The hipsnapshot wheel ships this top-level ``torchsnapshot`` package;
+    a real TorchSnapshot distribution installed alongside would overwrite (or
+    be overwritten by) it.  Say so instead of failing in odd ways later."""
+    import importlib.metadata as md
+    import warnings
+
+    for dist_name in ("torchsnapshot", "torchsnapshot-nightly"):
+        try:
+            md.distribution(dist_name)
+        except md.PackageNotFoundError:
+            continue
+        warnings.warn(
+            f"the '{dist_name}' distribution is installed next to hipsnapshot's torchsnapshot "
+            "alias package; they share the top-level 'torchsnapshot' name. Uninstall one of "
+            "them (hipsnapshot's alias maps the reference API onto hipsnapshot).",
+            RuntimeWarning, stacklevel=3)
+
+
+_warn_if_shadowing()
+
 if not any(isinstance(f, _AliasFinder) for f in sys.meta_path):
     sys.meta_path.insert(0, _AliasFinder())
 
