@@ -20,6 +20,19 @@ bytes / step time; ``stored_bytes`` reports what was written.  The same save
 with raw, reference-format blobs is timed afterwards (``--raw-steps``) and
 reported as ``raw_GBps``; ``--compression none`` makes raw blobs the headline.
 
+Self-audit keys next to the headline (each with its step count):
+
+* ``freeze_gpu_ms`` -- event-timed busy time of the trainer's stream during
+  ``async_take`` (the HBM freeze kernel), and ``unblock_incl_freeze_ms``: host
+  time until that stream is free again;
+* ``fresh_path_GBps`` -- the same take into a NEW ``step_<i>/`` directory each
+  time (fresh files, as a training loop writes them); the headline rewrites
+  one path;
+* ``vs_baseline_same_config`` -- the reference's own published config (DDP,
+  200 x 100 MB fp32 params = 20 GB, replicated, raw blobs) timed in the same
+  run, vs its 13.91 s (1 GPU) / 3.38 s (8 GPUs).  ``vs_baseline`` divides the
+  headline by the same reference number, i.e. it mixes configs.
+
 Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
 """
@@ -38,6 +51,7 @@ import time
 # published reference numbers: DDP 20 GB save on p4d.24xlarge,
 # local FS -- 1 GPU 13.91 s (1.44 GB/s), 1 node x 8 GPUs 3.38 s (5.92 GB/s)
 BASELINE_GBPS = {1: 20.0 / 13.91, 8: 20.0 / 3.38}
+REF_DDP_S = {1: 13.91, 8: 3.38}  # the same DDP 20 GB config, seconds per save
 
 
 def _free_port() -> int:
@@ -69,6 +83,12 @@ def main() -> None:
                          "(reference-format, uncompressed) blobs -> raw_GBps (0 = skip)")
     ap.add_argument("--restore-iters", type=int, default=3,
                     help="restores to time (median reported); each is checked bitwise")
+    ap.add_argument("--fresh-steps", type=int, default=3,
+                    help="takes to a NEW step_<i>/ directory each (as a training loop "
+                         "writes them), timed one by one -> fresh_path_GBps (0 = skip)")
+    ap.add_argument("--ddp-steps", type=int, default=2,
+                    help="timed takes of the reference's own DDP config (200 x 100 MB fp32 "
+                         "params, replicated, raw blobs) -> vs_baseline_same_config (0 = skip)")
     ap.add_argument("--fsync", action="store_true")
     ap.add_argument("--direct-io", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
@@ -172,22 +192,39 @@ def main() -> None:
     gbps = total_bytes / (ms_per_step / 1e3) / 1e9
 
     # async_take: time-to-unblock
+    # time_to_unblock: host time until async_take returns.  The HBM freeze
+    # it enqueued on the trainer's stream runs after that: freeze_gpu_ms is
+    # that stream's busy time between events recorded before and after the
+    # call (event-timed), unblock_incl_freeze_ms the host time until the
+    # stream is free again -- what a trainer whose next kernel waits sees.
     unblock = []
     drain = []
+    freeze = []
+    unblock_gpu = []
     for i in range(args.async_iters):
         barrier_sync()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
         ts = time.perf_counter()
         pending = Snapshot.async_take(path + "_async", app_state, storage_options=opts,
                                       compression=args.compression)
         tu = time.perf_counter() - ts
+        e1.record()
+        e1.synchronize()
+        tg = time.perf_counter() - ts
         pending.wait()
         torch.cuda.synchronize()
         td = time.perf_counter() - ts
-        u = torch.tensor([tu, td], dtype=torch.float64, device=dev)
+        u = torch.tensor([tu, td, e0.elapsed_time(e1) / 1e3, tg], dtype=torch.float64,
+                         device=dev)
         dist.all_reduce(u, op=dist.ReduceOp.MAX)
         unblock.append(float(u[0].item()) * 1e3)
         drain.append(float(u[1].item()) * 1e3)
-        log(f"async {i}: unblock {unblock[-1]:.1f} ms, total {drain[-1]:.1f} ms")
+        freeze.append(float(u[2].item()) * 1e3)
+        unblock_gpu.append(float(u[3].item()) * 1e3)
+        log(f"async {i}: unblock {unblock[-1]:.1f} ms (stream free at {unblock_gpu[-1]:.1f} ms, "
+            f"freeze kernel {freeze[-1]:.2f} ms), total {drain[-1]:.1f} ms")
 
     stored = 0
     if rank == 0:
@@ -251,6 +288,73 @@ def main() -> None:
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         raw_gbps = total_bytes / (float(e.item()) / args.raw_steps) / 1e9
         log(f"raw (uncompressed) save: {raw_gbps:.2f} GB/s")
+        if rank == 0:
+            shutil.rmtree(raw_path, ignore_errors=True)
+        dist.barrier()
+
+    # the headline rewrites one path; a training loop writes step_<i>/
+    # directories: every take here creates fresh files (page cache
+    # allocation, metadata).  Only the take is timed; removing the
+    # directory from two steps back (keep-last-2) is not.
+    fresh_gbps = fresh_each = None
+    if args.fresh_steps > 0:
+        if rank == 0:
+            shutil.rmtree(path + "_async", ignore_errors=True)
+        fdir = os.path.join(root, "fresh")
+        Snapshot.take(os.path.join(fdir, "warm"), app_state, storage_options=opts,
+                      compression=args.compression)
+        fresh_each = []
+        for i in range(args.fresh_steps):
+            barrier_sync()
+            tf = time.perf_counter()
+            Snapshot.take(os.path.join(fdir, f"step_{i}"), app_state, storage_options=opts,
+                          compression=args.compression)
+            barrier_sync()
+            e = torch.tensor([time.perf_counter() - tf], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            fresh_each.append(float(e.item()))
+            if rank == 0:
+                shutil.rmtree(os.path.join(fdir, "warm" if i == 0 else f"step_{i - 1}"),
+                              ignore_errors=True)
+        fresh_gbps = total_bytes / statistics.mean(fresh_each) / 1e9
+        log(f"fresh-directory save: {fresh_gbps:.2f} GB/s "
+            f"({[round(x * 1e3, 1) for x in fresh_each]} ms)")
+        if rank == 0:
+            shutil.rmtree(fdir, ignore_errors=True)
+        dist.barrier()
+
+    # the reference's published config, in this same process: DDP, 200 x
+    # 100 MB fp32 parameters, replicated=["**"], reference-format blobs
+    # (/root/reference/benchmarks/ddp/main.py:18-70: 13.91 s on 1 GPU,
+    # 3.38 s on 8 GPUs of a p4d.24xlarge)
+    ddp_s = ddp_each = None
+    if args.ddp_steps > 0:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+
+        from hipsnapshot.models.ddp_bench import ManyParams
+
+        ddp = DDP(ManyParams(200, 100, dev), device_ids=[gpu_index])
+        ddp_bytes = 200 * 100 * 1000 * 1000
+        dpath = os.path.join(root, "ddp20gb")
+        Snapshot.take(dpath, {"model": ddp}, replicated=["**"], storage_options=opts,
+                      compression="none")
+        ddp_each = []
+        for _ in range(args.ddp_steps):
+            barrier_sync()
+            tf = time.perf_counter()
+            Snapshot.take(dpath, {"model": ddp}, replicated=["**"], storage_options=opts,
+                          compression="none")
+            barrier_sync()
+            e = torch.tensor([time.perf_counter() - tf], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            ddp_each.append(float(e.item()))
+        ddp_s = statistics.median(ddp_each)
+        log(f"DDP 20 GB fp32 (reference config): {ddp_s:.3f} s "
+            f"({ddp_bytes / ddp_s / 1e9:.2f} GB/s)")
+        del ddp
+        torch.cuda.empty_cache()
+        if rank == 0:
+            shutil.rmtree(dpath, ignore_errors=True)
 
     base = BASELINE_GBPS.get(world)
     if rank == 0:
@@ -277,6 +381,11 @@ def main() -> None:
             # median over the async iterations (each value listed below)
             "time_to_unblock_ms": round(statistics.median(unblock), 2) if unblock else None,
             "time_to_unblock_ms_each": [round(u, 2) for u in unblock],
+            "freeze_gpu_ms": round(statistics.median(freeze), 3) if freeze else None,
+            "freeze_gpu_ms_each": [round(f, 3) for f in freeze],
+            "unblock_incl_freeze_ms": round(statistics.median(unblock_gpu), 2)
+            if unblock_gpu else None,
+            "async_iters": args.async_iters,
             "async_total_ms": round(statistics.median(drain), 2) if drain else None,
             "restore_bitwise_ok": restore_ok,
             "restore_GBps": round(restore_gbps, 2) if restore_gbps else None,
@@ -290,6 +399,16 @@ def main() -> None:
             "raw_GBps": round(raw_gbps, 3) if raw_gbps else None,
             "raw_note": "same save with uncompressed reference-format blobs "
                         f"({args.raw_steps} timed takes after 1 warmup)",
+            "fresh_path_GBps": round(fresh_gbps, 3) if fresh_gbps else None,
+            "fresh_path_ms_each": [round(x * 1e3, 1) for x in fresh_each] if fresh_each
+            else None,
+            "fresh_path_steps": args.fresh_steps,
+            "ddp20gb_fp32_s": round(ddp_s, 3) if ddp_s else None,
+            "ddp20gb_fp32_s_each": [round(x, 3) for x in ddp_each] if ddp_each else None,
+            "ddp20gb_fp32_GBps": round(20.0 / ddp_s, 2) if ddp_s else None,
+            "ddp20gb_steps": args.ddp_steps,
+            "vs_baseline_same_config": round(REF_DDP_S[world] / ddp_s, 2)
+            if ddp_s and world in REF_DDP_S else None,
             "baseline_note": "reference DDP 20GB save, p4d: 1 GPU 1.44 GB/s, 8 GPU 5.92 GB/s; "
                              "no published number for 2/4 GPUs",
         }

@@ -243,6 +243,18 @@ def get_read_order() -> str:
     return str(_get("READ_ORDER") or "plan")
 
 
+def get_state_dict_barriers() -> str:
+    """Barrier after every app-state key's ``state_dict()`` during a take
+    (the reference always does, `snapshot.py:362-368`, so user
+    ``state_dict()`` collectives cannot interleave across ranks).  ``auto``
+    (default): skipped when EVERY rank's statefuls are of kinds whose
+    ``state_dict()`` runs no collective (StateDict, RNGState, optimizers,
+    modules without FSDP1 wrappers or a custom ``state_dict``); ``always``;
+    ``never``."""
+    v = str(_get("STATE_DICT_BARRIERS") or "auto").strip().lower()
+    return {"1": "always", "true": "always", "0": "never", "false": "never"}.get(v, v)
+
+
 def plan_cache_enabled() -> bool:
     """Reuse a take's plan for the next take of the same device-resident
     tensors (``engine/plan_cache.py``)."""

@@ -10,7 +10,14 @@ protocol).  Orchestration differences on MI355X:
   whose result every rank computes identically (no follow-up broadcast), so a
   take issues 4 metadata collectives + K per-key barriers + 2 commit barriers
   (before rank 0 writes the metadata, and after, so that take() returns on
-  every rank only once the snapshot is readable).
+  every rank only once the snapshot is readable).  The K per-key barriers are
+  skipped when no rank's ``state_dict()`` can run a collective
+  (``knobs.get_state_dict_barriers``).
+* ``async_take`` runs ONE collective before returning (the coalesce
+  all-gather; DDP-replicated state adds the partition gathers): the manifest
+  exchange moved into the commit thread, through the c10d store (rank 0
+  assembles the metadata after the commit barrier), so the unblock path does
+  not grow with the rank count.
 * ``async_take`` freezes all HBM-resident state with ONE gather-kernel launch
   into a spare-HBM arena (enqueued on the trainer's stream, so no host sync
   is needed for consistency) and returns; D2H + storage writes drain in the
@@ -116,6 +123,26 @@ def _state_dict_view(stateful: Any) -> Any:
         if isinstance(v, torch.Tensor) and v.requires_grad and not isinstance(v, DTensor):
             sd[k] = v.detach()
     return sd
+
+
+def _state_dict_is_local(stateful: Any) -> bool:
+    """True when ``stateful.state_dict()`` is known to issue no collective:
+    StateDict / RNGState, optimizers, and modules that keep
+    ``nn.Module.state_dict`` and contain no FSDP1 wrapper (whose full state
+    dicts all-gather).  FSDP2 (``fully_shard``) and DDP modules qualify."""
+    import torch.nn as nn
+
+    from .stateful import StateDict
+
+    if isinstance(stateful, (StateDict, RNGState, torch.optim.Optimizer)):
+        return True
+    if isinstance(stateful, nn.Module) and type(stateful).state_dict is nn.Module.state_dict:
+        try:
+            from torch.distributed.fsdp import FullyShardedDataParallel as FSDP1
+        except Exception:  # pragma: no cover
+            return True
+        return not any(isinstance(m, FSDP1) for m in stateful.modules())
+    return False
 
 
 class Snapshot:
@@ -249,7 +276,7 @@ class Snapshot:
                                                compression, progress=progress)
         except BaseException as e:
             _release_plan(progress)
-            if progress.get("metadata_gathered"):
+            if progress.get("collectives_done"):
                 # peers that staged successfully are already in (or about to
                 # start) their commit threads: fail their barrier now instead
                 # of letting them wait DEFAULT_BARRIER_TIMEOUT
@@ -315,9 +342,11 @@ class Snapshot:
                 manifest.update(m)
                 flattened.update(f)
             # user state_dict() implementations may run collectives: keep them
-            # from interleaving across ranks
-            with timeline.span("barrier"):
-                comm.barrier()
+            # from interleaving across ranks (skipped when no rank's can:
+            # ``_coalesce``)
+            if getattr(comm, "state_dict_barriers", True):
+                with timeline.span("barrier"):
+                    comm.barrier()
         if rng_item is not None:
             rng_item[1].load_state_dict(rng_sd)
 
@@ -404,14 +433,17 @@ class Snapshot:
         manifest.update(object_entries)
         metadata = None
         if is_async:
-            # async: every rank has the metadata before any staging can fail;
-            # a rank whose staging fails after this point reports the error
-            # through the commit barrier (``_report_async_failure``), so its
-            # peers' commit threads fail at once instead of timing out
-            with timeline.span("gather_manifest"):
-                metadata = cls._gather_metadata(manifest, comm, plan)
+            # async: no metadata collective before returning.  The commit
+            # thread publishes this rank's manifest through the c10d store
+            # and rank 0 assembles it after the commit barrier
+            # (``PendingSnapshot``), so nothing on the unblock path scales
+            # with the rank count.  A rank whose staging fails after this
+            # point reports the error through the commit barrier
+            # (``_report_async_failure``): its peers' commit threads fail at
+            # once instead of timing out.
+            metadata = _DeferredMetadata(manifest, plan)
             if progress is not None:
-                progress["metadata_gathered"] = True
+                progress["collectives_done"] = True
 
         budget = get_process_memory_budget_bytes(comm)
         deferred: List[WriteReq] = []
@@ -635,10 +667,16 @@ class Snapshot:
         """ONE all-gather: path (rank 0 wins), replication globs (intersection),
         app-state keys (sorted union), hostnames (local world size), nonce."""
         rank, ws = comm.get_rank(), comm.get_world_size()
+        mode = knobs.get_state_dict_barriers()
+        local = mode == "never" or (mode == "auto" and all(
+            _state_dict_is_local(v) for v in app_state.values()))
         mine = (path, cls._infer_replicated(replicated, app_state), list(app_state.keys()),
-                socket.gethostname(), uuid.uuid4().hex)
+                socket.gethostname(), uuid.uuid4().hex, local)
         gathered: List[Any] = [None] * ws
         comm.all_gather_object(gathered, mine)
+        # per-key barriers only when some rank's state_dict() may run a
+        # collective (every rank sees the same gathered flags)
+        comm.state_dict_barriers = ws > 1 and not all(g[5] for g in gathered)
         root_path = gathered[0][0]
         if root_path != path:
             logger.warning(f"Rank {rank} specified a path ({path}) different from rank 0 "
@@ -676,32 +714,32 @@ class Snapshot:
         return set.intersection(*[set(g) for g in gathered])
 
     @staticmethod
-    def _gather_metadata(manifest: Dict[str, Entry], comm: Comm,
-                         plan=None) -> SnapshotMetadata:
-        """ONE all-gather of (replicated entries, pre-encoded JSON fragments of
-        every other entry).  Each rank JSON-encodes its own entries in
-        parallel; the committing rank only consolidates the replicated ones
-        and joins strings (reference: all-gather of entry objects, then rank 0
-        encodes the whole manifest, `snapshot.py:842-853`).  Entries of a
-        reused take plan keep the JSON encoded by the first take."""
+    def _metadata_payload(manifest: Dict[str, Entry], plan=None
+                          ) -> Tuple[Dict[str, Entry], List[Tuple[str, str]]]:
+        """This rank's part of the metadata: (replicated entries, pre-encoded
+        JSON fragments of every other entry).  Entries of a reused take plan
+        keep the JSON encoded by the first take."""
         rep = {k: e for k, e in manifest.items() if is_replicated(e)}
         if plan is None:
-            frags = [(k, entry_json(e)) for k, e in manifest.items() if k not in rep]
-        else:
-            cached, planned = plan.json, plan.entries
-            frags = []
-            for k, e in manifest.items():
-                if k in rep:
-                    continue
-                js = cached.get(k)
-                if js is None:
-                    js = entry_json(e)
-                    if k in planned:
-                        cached[k] = js
-                frags.append((k, js))
-        ws = comm.get_world_size()
-        gathered: List[Any] = [None] * ws
-        comm.all_gather_object(gathered, (rep, frags))
+            return rep, [(k, entry_json(e)) for k, e in manifest.items() if k not in rep]
+        cached, planned = plan.json, plan.entries
+        frags = []
+        for k, e in manifest.items():
+            if k in rep:
+                continue
+            js = cached.get(k)
+            if js is None:
+                js = entry_json(e)
+                if k in planned:
+                    cached[k] = js
+            frags.append((k, js))
+        return rep, frags
+
+    @staticmethod
+    def _assemble_metadata(gathered: List[Any], ws: int) -> SnapshotMetadata:
+        """Every rank's ``_metadata_payload`` -> the snapshot metadata: the
+        committing rank only consolidates replicated entries and joins
+        strings."""
         rank_reps = consolidate_replicated_entries([g[0] for g in gathered])
         parts = []
         for rank, (_, fr) in enumerate(gathered):
@@ -711,6 +749,18 @@ class Snapshot:
                 parts.append(json.dumps(f"{rank}/{logical}") + ":" + entry_json(entry))
         return LazySnapshotMetadata(metadata_json_from_parts(__version__, ws, parts),
                                     __version__, ws)
+
+    @classmethod
+    def _gather_metadata(cls, manifest: Dict[str, Entry], comm: Comm,
+                         plan=None) -> SnapshotMetadata:
+        """ONE all-gather of every rank's ``_metadata_payload``; each rank
+        JSON-encodes its own entries in parallel (reference: all-gather of
+        entry objects, then rank 0 encodes the whole manifest,
+        `snapshot.py:842-853`)."""
+        ws = comm.get_world_size()
+        gathered: List[Any] = [None] * ws
+        comm.all_gather_object(gathered, cls._metadata_payload(manifest, plan))
+        return cls._assemble_metadata(gathered, ws)
 
     @staticmethod
     def _gather_manifest(manifest: Dict[str, Entry], comm: Comm) -> Dict[str, Entry]:
@@ -829,6 +879,34 @@ def _write_checksums(storage: StoragePlugin, loop: asyncio.AbstractEventLoop, ra
                                buf=json.dumps(doc).encode("utf-8")), loop)
 
 
+class _DeferredMetadata:
+    """An async take's manifest; its metadata is assembled in the commit
+    thread (``PendingSnapshot._complete_snapshot``), not on the unblock path."""
+
+    __slots__ = ("manifest", "plan")
+
+    def __init__(self, manifest: Dict[str, Entry], plan) -> None:
+        self.manifest = manifest
+        self.plan = plan
+
+
+def _manifest_key(path: str, nonce: str, rank: int) -> str:
+    return f"hipsnapshot_{nonce}_{path}/manifest/{rank}"
+
+
+def _encode_payload(rep: Dict[str, Entry], frags: List[Tuple[str, str]]) -> bytes:
+    return json.dumps({"rep": {k: e.to_dict() for k, e in rep.items()},
+                       "frags": frags}).encode("utf-8")
+
+
+def _decode_payload(raw: bytes) -> Tuple[Dict[str, Entry], List[Tuple[str, str]]]:
+    from .format.manifest import entry_from_dict
+
+    d = json.loads(bytes(raw).decode("utf-8"))
+    return ({k: entry_from_dict(v) for k, v in d["rep"].items()},
+            [(k, js) for k, js in d["frags"]])
+
+
 def _commit_barrier(store, path: str, nonce: str, rank: int, world_size: int) -> LinearBarrier:
     return LinearBarrier(prefix=f"hipsnapshot_{nonce}_{path}", store=store, rank=rank,
                          world_size=world_size, leader_rank=0)
@@ -889,12 +967,35 @@ class PendingSnapshot:
         if store is not None:
             barrier = _commit_barrier(store, path, nonce, rank, world_size)
         try:
+            if isinstance(metadata, _DeferredMetadata):
+                # the metadata exchange happens here, through the store (not a
+                # collective): every rank publishes its part before it
+                # arrives at the commit barrier; rank 0 assembles them after
+                with timeline.span("manifest_payload", "commit"):
+                    payload = Snapshot._metadata_payload(metadata.manifest, metadata.plan)
+                    if store is None:
+                        metadata = Snapshot._assemble_metadata([payload], world_size)
+                    else:
+                        store.set(_manifest_key(path, nonce, rank), _encode_payload(*payload))
+                        metadata = None
             pending_io_work.sync_complete(event_loop)
             _write_checksums(storage, event_loop, rank, world_size,
                              pending_io_work.stats.checksums)
             if barrier is not None:
                 barrier.arrive(timeout=self.DEFAULT_BARRIER_TIMEOUT)
             if rank == 0:
+                if metadata is None:
+                    with timeline.span("manifest_assemble", "commit"):
+                        keys = [_manifest_key(path, nonce, r) for r in range(world_size)]
+                        raw = store.multi_get(keys) if hasattr(store, "multi_get") \
+                            else [store.get(k) for k in keys]
+                        metadata = Snapshot._assemble_metadata(
+                            [_decode_payload(b) for b in raw], world_size)
+                        for k in keys:
+                            try:
+                                store.delete_key(k)
+                            except Exception:  # noqa: BLE001 - best effort cleanup
+                                pass
                 Snapshot._write_snapshot_metadata(metadata, storage, event_loop)
             if barrier is not None:
                 barrier.depart(timeout=self.DEFAULT_BARRIER_TIMEOUT)

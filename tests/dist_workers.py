@@ -369,3 +369,104 @@ def distributed_verify(path: str):
     rep = snap.verify(distributed=True)
     assert not rep.ok and len(rep.mismatched) == 1, rep
     assert ws > 1
+
+
+def async_metadata_via_store(path: str):
+    """async_take exchanges manifests through the c10d store in the commit
+    thread (no collective before it returns): replicated (DDP), sharded
+    (DTensor) and per-rank entries all land in the metadata, identical in
+    shape to a sync take's, and the store keys are cleaned up."""
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import Shard, distribute_tensor
+
+    from unittest import mock
+
+    import hipsnapshot.snapshot as snapmod
+    from hipsnapshot.parallel.store import get_or_create_store
+
+    rank, ws = dist.get_rank(), dist.get_world_size()
+    mesh = init_device_mesh("cpu", (ws,))
+    torch.manual_seed(0)
+    full = torch.randn(33, 7)
+    ddp = torch.nn.parallel.DistributedDataParallel(_ddp_model(0))
+    app = {"ddp": ddp, "sd": StateDict(own=torch.full((5,), float(rank)),
+                                       dt=distribute_tensor(full, mesh, [Shard(0)]),
+                                       step=rank)}
+    Snapshot.take(path + "_sync", app)
+    used = []
+    orig_key = snapmod._manifest_key
+
+    def spy(*a):
+        used.append(orig_key(*a))
+        return used[-1]
+
+    with mock.patch.object(snapmod, "_manifest_key", spy):
+        pending = Snapshot.async_take(path + "_async", app)
+        snap = pending.wait()
+    m_sync = Snapshot(path + "_sync").get_manifest()
+    m_async = snap.get_manifest()
+    assert sorted(m_sync) == sorted(m_async), set(m_sync) ^ set(m_async)
+    for k in m_sync:
+        assert type(m_sync[k]) is type(m_async[k]), k
+    store = get_or_create_store(Comm())
+    dist.barrier()
+    # every rank published its manifest; rank 0 removed them after assembling
+    assert used
+    for k in used:
+        assert not store.check([k]), k
+    out = {"ddp": torch.nn.parallel.DistributedDataParallel(_ddp_model(1)), "sd": StateDict(own=torch.zeros(5),
+                                                 dt=distribute_tensor(torch.zeros_like(full),
+                                                                      mesh, [Shard(0)]),
+                                                 step=-1)}
+    snap.restore(out)
+    assert out["sd"]["step"] == rank
+    assert torch.equal(out["sd"]["own"], torch.full((5,), float(rank)))
+    assert torch.equal(out["sd"]["dt"].full_tensor(), full)
+    for a, b in zip(out["ddp"].parameters(), ddp.parameters()):
+        assert torch.equal(a, b)
+
+
+class _CollectiveStateful:
+    """A stateful whose state_dict() runs a collective (unknown kind)."""
+
+    def __init__(self):
+        self.t = torch.ones(3)
+
+    def state_dict(self):
+        x = torch.ones(1)
+        dist.all_reduce(x)
+        return {"t": self.t, "n": int(x.item())}
+
+    def load_state_dict(self, sd):
+        self.t.copy_(sd["t"])
+
+
+def state_dict_barriers():
+    """Per-key barriers run only when some rank's state_dict() may issue a
+    collective: StateDict/module-only app states skip them."""
+    import tempfile
+    from unittest import mock
+
+    from hipsnapshot.parallel.comm import Comm as C
+
+    calls = []
+    orig = C.barrier
+
+    def counting(self, *a, **k):
+        calls.append(1)
+        return orig(self, *a, **k)
+
+    d = tempfile.mkdtemp() if dist.get_rank() == 0 else None
+    box = [d]
+    dist.broadcast_object_list(box)
+    with mock.patch.object(C, "barrier", counting):
+        app = {"a": StateDict(x=torch.ones(2)), "b": torch.nn.Linear(2, 2),
+               "c": StateDict(y=1)}
+        Snapshot.take(box[0] + "/p", app)
+        n_local = len(calls)
+        calls.clear()
+        app["d"] = _CollectiveStateful()
+        Snapshot.take(box[0] + "/q", app)
+        n_coll = len(calls)
+    # commit barriers only vs + one per app-state key (4 keys)
+    assert n_coll - n_local == 4, (n_local, n_coll)

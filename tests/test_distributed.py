@@ -86,3 +86,11 @@ def test_take_returns_after_commit_on_every_rank(tmp_path):
 
 def test_distributed_verify(tmp_path):
     run_distributed(W.distributed_verify, 3, str(tmp_path / "dv"))
+
+
+def test_async_take_metadata_through_store(tmp_path):
+    run_distributed(W.async_metadata_via_store, 3, str(tmp_path / "a"))
+
+
+def test_state_dict_barriers_only_when_needed():
+    run_distributed(W.state_dict_barriers, 2)
