@@ -10,6 +10,15 @@ HIP device, so ``Comm`` pins the device once (``torch.cuda.set_device`` is the
 caller's job -- we assert it is set to a device this rank owns when the
 backend is RCCL).
 
+Ordering: with RCCL every collective (and the frame's host <-> device
+copies) runs with a dedicated side stream as the current stream.  ProcessGroup
+collectives make the communication stream wait on the CURRENT stream, and a
+blocking ``.cpu()`` waits for it too: on the trainer's stream a metadata
+all-gather would first wait for every kernel the training step had queued
+(torch's own object collectives do exactly that), so ``async_take`` would
+only return once the GPU drained the step.  The side stream carries nothing
+but these small collectives.
+
 Latency: torch's ``all_gather_object`` is two collectives (sizes, then padded
 payload).  ``Comm.all_gather_object`` is ONE collective when every payload
 fits a fixed 64 KiB frame (header with the true length + bytes), and falls
@@ -20,15 +29,30 @@ SURVEY 3.5).  Results are identical to torch's.
 
 from __future__ import annotations
 
+import contextlib
 import pickle
 import struct
-from typing import Any, List, Optional
+import threading
+from typing import Any, Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
 _FRAME = 64 * 1024
 _HDR = struct.Struct("<q")
+
+_side: Dict[int, "torch.cuda.Stream"] = {}
+_side_lock = threading.Lock()
+
+
+def _side_stream(dev: int) -> "torch.cuda.Stream":
+    s = _side.get(dev)
+    if s is None:
+        with _side_lock:
+            s = _side.get(dev)
+            if s is None:
+                s = _side[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 class Comm:
@@ -54,28 +78,44 @@ class Comm:
             return torch.device("cuda", torch.cuda.current_device())
         return torch.device("cpu")
 
+    def _on_side_stream(self):
+        """RCCL: run the collective with the side stream as current stream
+        (see the module docstring); a no-op for CPU backends."""
+        if "nccl" not in str(self.backend()):
+            return contextlib.nullcontext()
+        return torch.cuda.stream(_side_stream(torch.cuda.current_device()))
+
     # -- collectives -------------------------------------------------------
 
     def barrier(self) -> None:
         if self.pg is None or self.get_world_size() == 1:
             return
         if "nccl" in str(self.backend()):
-            dist.barrier(group=self.pg, device_ids=[torch.cuda.current_device()])
+            with self._on_side_stream():
+                dist.barrier(group=self.pg, device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier(group=self.pg)
 
     def broadcast_object_list(self, obj_list: List[Any], src: int = 0) -> None:
         if self.pg is None or self.get_world_size() == 1:
             return
-        dist.broadcast_object_list(obj_list, src=dist.get_global_rank(self.pg, src)
-                                   if self.pg is not dist.group.WORLD else src,
-                                   group=self.pg, device=self._device())
+        with self._on_side_stream():
+            dist.broadcast_object_list(obj_list, src=dist.get_global_rank(self.pg, src)
+                                       if self.pg is not dist.group.WORLD else src,
+                                       group=self.pg, device=self._device())
 
-    def all_gather_object(self, obj_list: List[Any], obj: Any) -> None:
+    def all_gather_object(self, obj_list: List[Any], obj: Any, frame: int = _FRAME) -> None:
+        """``frame``: bytes per rank of the first (usually only) round; small
+        payloads (the coalesce gather) pass a smaller one."""
         ws = self.get_world_size()
         if self.pg is None or ws == 1:
             obj_list[0] = obj
             return
+        with self._on_side_stream():
+            self._all_gather_object(obj_list, obj, max(frame, 64))
+
+    def _all_gather_object(self, obj_list: List[Any], obj: Any, _FRAME: int) -> None:
+        ws = self.get_world_size()
         payload = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
         dev = self._device()
         frame = torch.zeros(_FRAME, dtype=torch.uint8)

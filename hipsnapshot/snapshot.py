@@ -267,8 +267,11 @@ class Snapshot:
         loop = asyncio.new_event_loop()
         comm = Comm(pg)
         t0 = time.monotonic()
-        path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
-        storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
+        tp0 = time.perf_counter()
+        with timeline.span("coalesce"):
+            path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
+        with timeline.span("storage_open"):
+            storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
         progress: Dict[str, Any] = {}
         try:
             pending, metadata = cls._take_impl(path, app_state, rep, keys, comm, storage, loop,
@@ -284,11 +287,15 @@ class Snapshot:
             storage.sync_close(loop)
             loop.close()
             raise
+        with timeline.span("pending_init"):
+            ps = PendingSnapshot(path=path, pending_io_work=pending, comm=comm, metadata=metadata,
+                                 storage=storage, event_loop=loop,
+                                 storage_options=storage_options, nonce=nonce,
+                                 plan=progress.get("plan"))
         TakeStats.last = {"unblock_s": time.monotonic() - t0}
+        timeline.add("unblock", "phase", tp0, time.perf_counter())
         timeline.dump("async_take", comm.get_rank())
-        return PendingSnapshot(path=path, pending_io_work=pending, comm=comm, metadata=metadata,
-                               storage=storage, event_loop=loop, storage_options=storage_options,
-                               nonce=nonce, plan=progress.get("plan"))
+        return ps
 
     @staticmethod
     def _uncommit(storage: StoragePlugin, loop: asyncio.AbstractEventLoop) -> None:
@@ -673,7 +680,7 @@ class Snapshot:
         mine = (path, cls._infer_replicated(replicated, app_state), list(app_state.keys()),
                 socket.gethostname(), uuid.uuid4().hex, local)
         gathered: List[Any] = [None] * ws
-        comm.all_gather_object(gathered, mine)
+        comm.all_gather_object(gathered, mine, frame=4096)
         # per-key barriers only when some rank's state_dict() may run a
         # collective (every rank sees the same gathered flags)
         comm.state_dict_barriers = ws > 1 and not all(g[5] for g in gathered)
