@@ -3,8 +3,10 @@
 
 BASELINE config 4 (TorchRec DLRM, 100 GB tables, uvm_tensor path); reference
 script /root/reference/benchmarks/torchrec/main.py:54-151 (sync vs async take,
-time-to-unblock).  Tables are DTensor(Shard(0)) over the ranks; ``--uvm``
-puts every local shard in hipMallocManaged memory.
+time-to-unblock).  Tables are DTensors over the ranks in the ``--sharding``
+layout (row = Shard(0), column = Shard(1), table = each table whole on one
+rank, round-robin); ``--uvm`` puts every local shard in hipMallocManaged
+memory.
 """
 
 import argparse
@@ -29,6 +31,7 @@ def main():
     ap.add_argument("--tables", type=int, default=8)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--uvm", action="store_true")
+    ap.add_argument("--sharding", default="row", choices=["row", "column", "table"])
     ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
     args = ap.parse_args()
     rank, ws, dev = init_dist()
@@ -36,9 +39,11 @@ def main():
 
     mesh = init_device_mesh(dev.type, (ws,))
     rows = int(args.total_gb * 1e9 / 4 / args.dim / args.tables)
-    model = DLRM([rows] * args.tables, dim=args.dim, device=dev, mesh=mesh, uvm=args.uvm)
+    model = DLRM([rows] * args.tables, dim=args.dim, device=dev, mesh=mesh, uvm=args.uvm,
+                 sharding=args.sharding)
     nbytes = sum(p.numel() * 4 for p in model.parameters())
-    log(f"DLRM: {args.tables} tables x {rows} rows x {args.dim} (uvm={args.uvm}), "
+    log(f"DLRM: {args.tables} tables x {rows} rows x {args.dim} (uvm={args.uvm}, "
+        f"{args.sharding}-wise), "
         f"{nbytes / 1e9:.2f} GB")
     root = os.path.join(args.work_dir, "hs_dlrm")
     if rank == 0:
@@ -56,7 +61,8 @@ def main():
     unblock = max_over_ranks(tu.s, dev)
     pending.wait()
     sync(dev)
-    emit({"bench": "dlrm_uvm" if args.uvm else "dlrm_hbm", "world_size": ws, "bytes": nbytes,
+    emit({"bench": "dlrm_uvm" if args.uvm else "dlrm_hbm", "sharding": args.sharding,
+          "world_size": ws, "bytes": nbytes,
           "sync_take_s": round(sync_s, 3), "sync_GBps": round(nbytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 1)})
     if rank == 0:
