@@ -105,10 +105,10 @@ def test_dim_index_runs_matches_torch_random():
 # multi-rank save / restore
 
 
-def _mesh2d(order):
+def _mesh2d(order, device="cpu"):
     from torch.distributed.device_mesh import init_device_mesh
 
-    return init_device_mesh("cpu", (2, 2), mesh_dim_names=order)
+    return init_device_mesh(torch.device(device).type, (2, 2), mesh_dim_names=order)
 
 
 def _with_adamw(model):
@@ -125,11 +125,11 @@ def _full(v):
 
 
 def _flat_state(model, opt):
-    out = {f"m/{k}": _full(v).clone() for k, v in model.state_dict().items()}
+    out = {f"m/{k}": _full(v).cpu().clone() for k, v in model.state_dict().items()}
     for i, st in opt.state_dict()["state"].items():
         for k, v in st.items():
             if torch.is_tensor(v) and v.dim() > 0:
-                out[f"o/{i}/{k}"] = _full(v).clone()
+                out[f"o/{i}/{k}"] = _full(v).cpu().clone()
     return out
 
 
@@ -142,7 +142,7 @@ def _zero_(model, opt):
                 (v._local_tensor if hasattr(v, "_local_tensor") else v).zero_()
 
 
-def _save_worker(tmp: str):
+def _save_worker(tmp: str, device: str = "cpu"):
     import torch.distributed as dist
 
     from hipsnapshot import Snapshot
@@ -150,14 +150,15 @@ def _save_worker(tmp: str):
     from hipsnapshot.knobs import override_max_shard_size_bytes
     from hipsnapshot.models.llama import build_2d_llama
 
-    model = build_2d_llama(_cfg(), torch.device("cpu"), _mesh2d(("dp", "tp")), torch.float32)
+    model = build_2d_llama(_cfg(), torch.device(device), _mesh2d(("dp", "tp"), device),
+                           torch.float32)
     opt = _with_adamw(model)
     with torch.no_grad():
         # globally consistent moments (TP replicas of a norm's state agree)
         gen = torch.Generator().manual_seed(100)
         for st in opt.state.values():
             for k in ("exp_avg", "exp_avg_sq"):
-                full = torch.rand(st[k].shape, generator=gen)
+                full = torch.rand(st[k].shape, generator=gen).to(device)
                 for b in local_boxes(st[k]):
                     b.tensor.copy_(full[tuple(slice(o, o + s)
                                               for o, s in zip(b.offsets, b.sizes))])
@@ -189,7 +190,7 @@ def _check(model, opt, ref, tag):
         assert torch.equal(got[k], ref[k]), (tag, k)
 
 
-def _restore_worker(tmp: str, target: str):
+def _restore_worker(tmp: str, target: str, device: str = "cpu"):
     import torch.distributed as dist
     from torch.distributed.device_mesh import init_device_mesh
 
@@ -197,15 +198,16 @@ def _restore_worker(tmp: str, target: str):
     from hipsnapshot.models.llama import Llama, build_2d_llama, build_fsdp_llama
 
     ref = torch.load(f"{tmp}/ref.pt", weights_only=True)
+    dev = torch.device(device)
     if target == "2d_swapped":
-        model = build_2d_llama(_cfg(), torch.device("cpu"), _mesh2d(("tp", "dp")), torch.float32)
+        model = build_2d_llama(_cfg(), dev, _mesh2d(("tp", "dp"), device), torch.float32)
     elif target == "2d_same":
-        model = build_2d_llama(_cfg(), torch.device("cpu"), _mesh2d(("dp", "tp")), torch.float32)
+        model = build_2d_llama(_cfg(), dev, _mesh2d(("dp", "tp"), device), torch.float32)
     elif target == "fsdp":
-        mesh = init_device_mesh("cpu", (dist.get_world_size(),))
-        model = build_fsdp_llama(_cfg(), torch.device("cpu"), torch.float32, mesh=mesh)
+        mesh = init_device_mesh(dev.type, (dist.get_world_size(),))
+        model = build_fsdp_llama(_cfg(), dev, torch.float32, mesh=mesh)
     else:
-        model = Llama(_cfg())
+        model = Llama(_cfg()).to(dev)
     opt = _with_adamw(model)
     for src in ("sync", "async"):
         _zero_(model, opt)
@@ -216,20 +218,28 @@ def _restore_worker(tmp: str, target: str):
     for name in ("layers.0.attention.wq.weight", "layers.1.feed_forward.w2.weight",
                  "tok_embeddings.weight"):
         for budget in (None, 2048):
-            plain = torch.zeros_like(ref[f"m/{name}"])
+            plain = torch.zeros_like(ref[f"m/{name}"]).to(dev)
             Snapshot(f"{tmp}/async").read_object(f"0/model/{name}", obj_out=plain,
                                                  memory_budget_bytes=budget)
-            assert torch.equal(plain, ref[f"m/{name}"]), (name, budget)
+            assert torch.equal(plain.cpu(), ref[f"m/{name}"]), (name, budget)
 
 
-pytestmark = pytest.mark.multiproc
-
-
+@pytest.mark.multiproc
 def test_fsdp_over_tp_save_and_reshard(tmp_path):
     run_distributed(_save_worker, 4, str(tmp_path))
     for target in ("2d_same", "2d_swapped", "fsdp"):
         run_distributed(_restore_worker, 4, str(tmp_path), target)
     run_distributed(_restore_worker, 1, str(tmp_path), "plain")
+
+
+@pytest.mark.gpu
+def test_fsdp_over_tp_save_and_reshard_gpu(gpu, tmp_path):
+    """The same on HIP tensors (4 gloo ranks sharing cuda:0): strided-shard
+    boxes are staged and scattered by the device path."""
+    run_distributed(_save_worker, 4, str(tmp_path), "cuda:0", timeout=600)
+    for target in ("2d_swapped", "fsdp"):
+        run_distributed(_restore_worker, 4, str(tmp_path), target, "cuda:0", timeout=600)
+    run_distributed(_restore_worker, 1, str(tmp_path), "plain", "cuda:0", timeout=600)
 
 
 def _hsdp_worker(tmp: str):
@@ -261,5 +271,6 @@ def _hsdp_worker(tmp: str):
         assert torch.equal(out.full_tensor(), full), src_key
 
 
+@pytest.mark.multiproc
 def test_hsdp_and_block_layouts(tmp_path):
     run_distributed(_hsdp_worker, 4, str(tmp_path))
