@@ -206,37 +206,48 @@ def main():
     emit(test="pack_column_shard_bf16", GBps=nb2 / best / 1e9, median_GBps=nb2 / med / 1e9)
     assert torch.equal(out2.view(col.shape), col.contiguous())
 
-    # fp8 blockwise quantization (plain + MFMA Hadamard-32) of a 1 GiB bf16 tensor
+    # fp8 quantization of a 1 GiB bf16 tensor: MX (E8M0 scale per 32, the
+    # default), fp32 scale per 128, and the MFMA Hadamard-32 variant
     from hipsnapshot.ops import quant
 
     w = torch.empty(512 << 20, dtype=torch.bfloat16, device="cuda:0").normal_()
     nw = w.numel()
     hs = int(torch.cuda.current_stream().cuda_stream)
-    for rot in ("none", "hadamard32"):
-        info = quant.fp8_entry_quant_info(w, rotation=rot)
+    for mode in ("mx_e8m0", "none", "hadamard32"):
+        if mode == "mx_e8m0":
+            info = quant.fp8_entry_quant_info(w, rotation="none")
+            assert quant.is_mx(info)
+        else:
+            os.environ["HIPSNAPSHOT_FP8_SCALE"] = "fp32"
+            info = quant.fp8_entry_quant_info(w, rotation=mode)
+            del os.environ["HIPSNAPSHOT_FP8_SCALE"]
         blob = torch.zeros(info["total_bytes"], dtype=torch.uint8, device="cuda:0")
         payload = info["payload_bytes"]
-        scales = blob[payload:].view(torch.float32)
+        scales = blob[payload:] if mode == "mx_e8m0" else blob[payload:].view(torch.float32)
         back = torch.empty_like(w)
 
         def q():
-            if rot == "none":
+            if mode == "mx_e8m0":
+                native.mx8_quantize(dev, w, blob[:payload], scales, hs)
+            elif mode == "none":
                 native.fp8_quantize(dev, w, blob[:payload], scales, info["vpt"], hs)
             else:
                 native.fp8_hadamard_quantize(dev, w, blob[:payload], scales, hs)
 
         def dq():
-            if rot == "none":
+            if mode == "mx_e8m0":
+                native.mx8_dequantize(dev, blob[:nw], scales, back, hs)
+            elif mode == "none":
                 native.fp8_dequantize(dev, blob[:nw], scales, back, info["vpt"], hs)
             else:
                 native.fp8_hadamard_dequantize(dev, blob[:payload], scales, back, hs)
 
         best, med = timeit(q)
-        traffic = nw * 2 + payload + 4 * info["nblocks"]
-        emit(test=f"fp8_quant_{rot}_1GiB_bf16", GBps=traffic / best / 1e9,
+        traffic = nw * 2 + info["total_bytes"]
+        emit(test=f"fp8_quant_{mode}_1GiB_bf16", GBps=traffic / best / 1e9,
              median_GBps=traffic / med / 1e9, ms=best * 1e3, note="HBM bytes read+written")
         best, med = timeit(dq)
-        emit(test=f"fp8_dequant_{rot}_1GiB_bf16", GBps=traffic / best / 1e9,
+        emit(test=f"fp8_dequant_{mode}_1GiB_bf16", GBps=traffic / best / 1e9,
              median_GBps=traffic / med / 1e9, ms=best * 1e3)
         del blob, back
     del w

@@ -486,6 +486,228 @@ hs_fp8_dequant(const uint8_t* __restrict__ q, const float* __restrict__ scales, 
 }
 
 // ---------------------------------------------------------------------------
+// MX fp8: OCP e4m3fn elements + one E8M0 (power-of-two) scale byte per
+// 32-element block.  Scale 2^k with the smallest k such that amax <= 448*2^k
+// (exact, from frexp: amax = m*2^e, k = e-9 if m <= 0.875 else e-8), so
+// x * 2^-k is exact (v_ldexp_f32, no division, no clamp needed) and restore is
+// q * 2^k, exact in f32.  Streaming layout for the HBM roof:
+//   * every 16-B load instruction is contiguous across the wave (lane l
+//     reads bytes [16 l, 16 l + 16) of a 1 KiB wave segment), U = 4 of them in
+//     flight per lane;
+//   * a 32-element block spans LPB = 32 / (16 / es) lanes (4 for bf16/f16, 8
+//     for f32): amax is an in-register max over the lane's 16 B then a
+//     log2(LPB)-step xor-shuffle;
+//   * fp8 bytes leave as one 8-B (bf16) / 4-B (f32) store per lane per load,
+//     again contiguous across the wave.
+// ---------------------------------------------------------------------------
+
+constexpr int kMxBlock = 32;
+typedef unsigned int mx_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int mx_u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float fp8_byte_to_f32(uint32_t w, int b) {
+  switch (b) {  // the byte select must be an immediate
+    case 0: return __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(w), 0);
+    case 1: return __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(w), 1);
+    case 2: return __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(w), 2);
+    default: return __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(w), 3);
+  }
+}
+
+__device__ __forceinline__ int mx_exp(float amax) {
+  if (!(amax > 0.f) || !(amax < __builtin_huge_valf())) return 0;  // zero / inf / nan
+  int e;
+  const float m = frexpf(amax, &e);
+  const int k = (m <= 0.875f) ? e - 9 : e - 8;
+  return k < -127 ? -127 : (k > 127 ? 127 : k);
+}
+
+template <int DT>
+__device__ __forceinline__ float mx_unpack(uint32_t w, int half) {
+  if constexpr (DT == kBF16) return __uint_as_float(half ? (w & 0xffff0000u) : (w << 16));
+  else {
+    _Float16 h;
+    const uint16_t b = static_cast<uint16_t>(half ? (w >> 16) : (w & 0xffffu));
+    __builtin_memcpy(&h, &b, 2);
+    return static_cast<float>(h);
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kBlock)
+hs_mx8_quant(const char* __restrict__ src, int64_t n, int64_t payload,
+             uint8_t* __restrict__ out, uint8_t* __restrict__ scales) {
+  constexpr int ES = (DT == kF32) ? 4 : 2;
+  constexpr int EPL = 16 / ES;
+  constexpr int LPB = kMxBlock / EPL;
+  constexpr int U = 4;
+  constexpr int64_t kChunk = 64LL * EPL * U;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  const int64_t nchunks = (n + kChunk - 1) / kChunk;
+  for (int64_t c = wave0; c < nchunks; c += nwaves) {
+    const int64_t base = c * kChunk;
+    const bool full = base + kChunk <= n;
+    uint4 raw[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e0 = base + (int64_t(u) * 64 + lane) * EPL;
+      if (full) {
+        const mx_u32x4 t =
+            __builtin_nontemporal_load(reinterpret_cast<const mx_u32x4*>(src + e0 * ES));
+        raw[u] = make_uint4(t.x, t.y, t.z, t.w);
+      } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int j = 0; j < EPL; ++j) {
+          if (e0 + j >= n) break;
+          uint32_t bits;
+          if constexpr (ES == 4) bits = *reinterpret_cast<const uint32_t*>(src + (e0 + j) * 4);
+          else bits = *reinterpret_cast<const uint16_t*>(src + (e0 + j) * 2);
+          w[(j * ES) >> 2] |= bits << (((j * ES) & 3) * 8);
+        }
+        raw[u] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t ws[4] = {raw[u].x, raw[u].y, raw[u].z, raw[u].w};
+      float v[EPL];
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) {
+        if constexpr (ES == 4) v[j] = __uint_as_float(ws[j]);
+        else v[j] = mx_unpack<DT>(ws[j >> 1], j & 1);
+      }
+      float amax = 0.f;  // over the finite elements (inf / nan do not set the scale)
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) {
+        const float a = fabsf(v[j]);
+        amax = fmaxf(amax, a < __builtin_huge_valf() ? a : 0.f);
+      }
+#pragma unroll
+      for (int o = 1; o < LPB; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+      const int k = mx_exp(amax);
+      const int64_t e0 = base + (int64_t(u) * 64 + lane) * EPL;
+      if ((lane % LPB) == 0 && e0 < n) scales[e0 / kMxBlock] = static_cast<uint8_t>(k + 127);
+      uint32_t q[EPL / 4];
+#pragma unroll
+      for (int w = 0; w < EPL / 4; ++w) {
+        int word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * w], -k), ldexpf(v[4 * w + 1], -k),
+                                                   0, false);
+        word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * w + 2], -k),
+                                               ldexpf(v[4 * w + 3], -k), word, true);
+        // non-finite elements: e4m3fn NaN with the element's sign (torch's cast)
+        uint32_t fix = 0, fixmask = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t b = __float_as_uint(v[4 * w + j]);
+          if ((b & 0x7f800000u) == 0x7f800000u) {
+            fixmask |= 0xffu << (8 * j);
+            fix |= ((b >> 31) ? 0xffu : 0x7fu) << (8 * j);
+          }
+        }
+        q[w] = (static_cast<uint32_t>(word) & ~fixmask) | fix;
+      }
+      if (full) {
+        if constexpr (EPL == 8) {
+          mx_u32x2 t;
+          t.x = q[0];
+          t.y = q[1];
+          __builtin_nontemporal_store(t, reinterpret_cast<mx_u32x2*>(out + e0));
+        } else
+          __builtin_nontemporal_store(q[0], reinterpret_cast<uint32_t*>(out + e0));
+      } else {
+        for (int j = 0; j < EPL; ++j) {
+          const int64_t e = e0 + j;
+          if (e < payload) out[e] = e < n ? static_cast<uint8_t>(q[j >> 2] >> (8 * (j & 3))) : 0;
+        }
+      }
+    }
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void mx_store(char* p, const float* f) {
+  // 16 B of output: 8 x bf16/f16, 4 x f32 or 2 x f64
+  if constexpr (DT == kF32) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  } else if constexpr (DT == kF64) {
+    *reinterpret_cast<double2*>(p) = make_double2(static_cast<double>(f[0]),
+                                                  static_cast<double>(f[1]));
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint16_t lo, hi;
+      if constexpr (DT == kBF16) {
+        lo = f32_to_bf16(f[2 * i]);
+        hi = f32_to_bf16(f[2 * i + 1]);
+      } else {
+        const _Float16 a = static_cast<_Float16>(f[2 * i]), b = static_cast<_Float16>(f[2 * i + 1]);
+        __builtin_memcpy(&lo, &a, 2);
+        __builtin_memcpy(&hi, &b, 2);
+      }
+      w[i] = uint32_t(lo) | (uint32_t(hi) << 16);
+    }
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kBlock)
+hs_mx8_dequant(const uint8_t* __restrict__ q, const uint8_t* __restrict__ scales, int64_t n,
+               char* __restrict__ dst) {
+  constexpr int DES = (DT == kF32) ? 4 : (DT == kF64 ? 8 : 2);
+  constexpr int EPL = 16 / DES;  // fp8 bytes per lane per step = one 16-B store
+  constexpr int U = 4;
+  constexpr int64_t kChunk = 64LL * EPL * U;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  const int64_t nchunks = (n + kChunk - 1) / kChunk;
+  for (int64_t c = wave0; c < nchunks; c += nwaves) {
+    const int64_t base = c * kChunk;
+    const bool full = base + kChunk <= n;
+    uint32_t raw[U][(EPL + 3) / 4];
+    uint8_t sb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e0 = base + (int64_t(u) * 64 + lane) * EPL;
+      if (full) {
+        if constexpr (EPL == 8) {
+          const uint2 t = *reinterpret_cast<const uint2*>(q + e0);
+          raw[u][0] = t.x;
+          raw[u][1] = t.y;
+        } else if constexpr (EPL == 4) {
+          raw[u][0] = *reinterpret_cast<const uint32_t*>(q + e0);
+        } else {
+          raw[u][0] = *reinterpret_cast<const uint16_t*>(q + e0);
+        }
+      } else {
+        for (int w = 0; w < (EPL + 3) / 4; ++w) raw[u][w] = 0;
+        for (int j = 0; j < EPL && e0 + j < n; ++j)
+          raw[u][j >> 2] |= uint32_t(q[e0 + j]) << (8 * (j & 3));
+      }
+      sb[u] = e0 < n ? scales[e0 / kMxBlock] : 127;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e0 = base + (int64_t(u) * 64 + lane) * EPL;
+      const int k = int(sb[u]) - 127;
+      float f[EPL];
+#pragma unroll
+      for (int j = 0; j < EPL; ++j)
+        f[j] = ldexpf(fp8_byte_to_f32(raw[u][j >> 2], j & 3), k);
+      if (full) {
+        mx_store<DT>(dst + e0 * DES, f);
+      } else {
+        for (int j = 0; j < EPL && e0 + j < n; ++j) store_from_f32(dst + (e0 + j) * DES, DT, f[j]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Hadamard-rotated fp8 (MFMA).  The flat tensor is viewed as rows of 32
 // ("groups"); every group is rotated by the 32x32 Sylvester Hadamard matrix H
 // (entries +-1, H*H = 32 I) before blockwise e4m3 quantization, which spreads
@@ -1186,6 +1408,53 @@ int hsg_fp8_dequantize(int dev, const void* q, const void* scales, int64_t n, vo
     case 8: hipLaunchKernelGGL(hs_fp8_dequant<8>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;
     case 16: hipLaunchKernelGGL(hs_fp8_dequant<16>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;
     default: snprintf(g_err, sizeof(g_err), "unsupported vpt %d", vpt); return -1001;
+  }
+  HS_CHECK(hipGetLastError());
+  return 0;
+}
+
+// MX fp8: src (bf16/f16/f32, contiguous) -> out [payload = round_up(n, 16)
+// bytes; [n, payload) zero-filled] + scales [ceil(n / 32) E8M0 bytes].  Every
+// output byte is written (the blob needs no zero-fill).
+int hsg_mx8_quantize(int dev, const void* src, int src_dtype, int64_t n, void* out,
+                     void* scales, void* stream) {
+  HS_CHECK(hipSetDevice(dev));
+  if (n <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t payload = (n + 15) / 16 * 16;
+  const int64_t chunk = (src_dtype == kF32) ? 64 * 4 * 4 : 64 * 8 * 4;
+  const int64_t waves = (n + chunk - 1) / chunk;
+  const int grid = static_cast<int>(std::min<int64_t>((waves + 3) / 4, 256 * 16));
+  const char* sp = static_cast<const char*>(src);
+  uint8_t* op = static_cast<uint8_t*>(out);
+  uint8_t* sc = static_cast<uint8_t*>(scales);
+  switch (src_dtype) {
+    case kBF16: hipLaunchKernelGGL(hs_mx8_quant<kBF16>, dim3(grid), dim3(kBlock), 0, s, sp, n, payload, op, sc); break;
+    case kF16: hipLaunchKernelGGL(hs_mx8_quant<kF16>, dim3(grid), dim3(kBlock), 0, s, sp, n, payload, op, sc); break;
+    case kF32: hipLaunchKernelGGL(hs_mx8_quant<kF32>, dim3(grid), dim3(kBlock), 0, s, sp, n, payload, op, sc); break;
+    default: snprintf(g_err, sizeof(g_err), "unsupported mx8 source dtype %d", src_dtype); return -1002;
+  }
+  HS_CHECK(hipGetLastError());
+  return 0;
+}
+
+int hsg_mx8_dequantize(int dev, const void* q, const void* scales, int64_t n, void* dst,
+                       int dst_dtype, void* stream) {
+  HS_CHECK(hipSetDevice(dev));
+  if (n <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t epl = (dst_dtype == kF32) ? 4 : (dst_dtype == kF64 ? 2 : 8);
+  const int64_t waves = (n + 64 * epl * 4 - 1) / (64 * epl * 4);
+  const int grid = static_cast<int>(std::min<int64_t>((waves + 3) / 4, 256 * 16));
+  const uint8_t* qp = static_cast<const uint8_t*>(q);
+  const uint8_t* sc = static_cast<const uint8_t*>(scales);
+  char* dp = static_cast<char*>(dst);
+  switch (dst_dtype) {
+    case kBF16: hipLaunchKernelGGL(hs_mx8_dequant<kBF16>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp); break;
+    case kF16: hipLaunchKernelGGL(hs_mx8_dequant<kF16>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp); break;
+    case kF32: hipLaunchKernelGGL(hs_mx8_dequant<kF32>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp); break;
+    case kF64: hipLaunchKernelGGL(hs_mx8_dequant<kF64>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp); break;
+    default: snprintf(g_err, sizeof(g_err), "unsupported mx8 dest dtype %d", dst_dtype); return -1002;
   }
   HS_CHECK(hipGetLastError());
   return 0;

@@ -255,6 +255,10 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p])
         _declare(lib, "hsg_fp8_hadamard_dequantize", c_int,
                  [c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p])
+        _declare(lib, "hsg_mx8_quantize", c_int,
+                 [c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p])
+        _declare(lib, "hsg_mx8_dequantize", c_int,
+                 [c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p])
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
@@ -684,6 +688,29 @@ def fp8_hadamard_dequantize(dev: int, q: torch.Tensor, scales: torch.Tensor, dst
     _check(lib.hsg_fp8_hadamard_dequantize(dev, q.data_ptr(), scales.data_ptr(), n,
                                            dst.data_ptr(), dtype_code(dst.dtype), stream_handle),
            "hsg_fp8_hadamard_dequantize")
+
+
+def mx8_quantize(dev: int, src: torch.Tensor, out: torch.Tensor, scales: torch.Tensor,
+                 stream_handle: int) -> None:
+    """MX fp8 (e4m3fn + E8M0 scale per 32 elements, hs_mx8_quant): ``out``
+    gets round_up(n, 16) bytes (padding zeroed), ``scales`` ceil(n / 32)."""
+    lib = require_gpu_lib()
+    n = src.numel()
+    assert src.is_contiguous() and dtype_code(src.dtype) in (10, 11, 12)
+    assert out.numel() >= (n + 15) // 16 * 16 and scales.numel() >= (n + 31) // 32
+    assert out.dtype == torch.uint8 and scales.dtype == torch.uint8
+    _check(lib.hsg_mx8_quantize(dev, src.data_ptr(), dtype_code(src.dtype), n, out.data_ptr(),
+                                scales.data_ptr(), stream_handle), "hsg_mx8_quantize")
+
+
+def mx8_dequantize(dev: int, q: torch.Tensor, scales: torch.Tensor, dst: torch.Tensor,
+                   stream_handle: int) -> None:
+    lib = require_gpu_lib()
+    n = dst.numel()
+    assert dst.is_contiguous() and dtype_code(dst.dtype) in (10, 11, 12, 13)
+    assert q.numel() >= n and scales.numel() >= (n + 31) // 32
+    _check(lib.hsg_mx8_dequantize(dev, q.data_ptr(), scales.data_ptr(), n, dst.data_ptr(),
+                                  dtype_code(dst.dtype), stream_handle), "hsg_mx8_dequantize")
 
 
 # ---- managed memory -------------------------------------------------------------

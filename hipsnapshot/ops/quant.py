@@ -27,6 +27,26 @@ converts to OCP e4m3fn natively).
 
 Scale rule (both): ``scale = amax / 448`` (correctly rounded; 1 when the block
 is all zeros), ``q = e4m3fn(clamp(y / scale))`` with round-to-nearest-even.
+
+MX layout (default for un-rotated tensors; ``HIPSNAPSHOT_FP8_SCALE=fp32``
+selects the fp32-scale layout above)::
+
+    {"format": "fp8_e4m3fn_mx", "block": 32, "scale": "e8m0", "rotation": "none",
+     "payload_bytes": P = round_up(n, 16), "nblocks": B = ceil(n / 32),
+     "total_bytes": P + B}
+
+blob = ``[fp8 payload (P bytes, zero padded)][B E8M0 scale bytes]`` -- the OCP
+MX block format: one power-of-two scale ``2^k`` per 32 elements, byte
+``k + 127``.  ``k`` is the smallest exponent with ``amax <= 448 * 2^k``
+(``amax`` over the block's finite elements; inf / nan are stored as e4m3fn
+NaN with their sign, as torch's cast does)
+(``amax = m * 2^e`` by frexp: ``k = e - 9`` if ``m <= 0.875`` else ``e - 8``;
+0 for all-zero / non-finite blocks, clamped to [-127, 127]), so ``x * 2^-k``
+is EXACT: no division, no saturation, and restore ``q * 2^k`` is exact in
+fp32.  That takes the per-element correctly rounded division off the GPU
+(``hs_mx8_quant`` streams at the HBM roof) while the blob stays bit-identical
+to the torch reference below.  Same 1/32 scale overhead as fp32 scales per
+128 elements, at 4x finer granularity.
 """
 
 from __future__ import annotations
@@ -60,6 +80,20 @@ def default_rotation() -> str:
     return r if r in ("hadamard32", "none") else "none"
 
 
+def default_scale() -> str:
+    """``e8m0`` (MX, default) or ``fp32`` (``HIPSNAPSHOT_FP8_SCALE``) for
+    un-rotated quantization."""
+    v = os.environ.get("HIPSNAPSHOT_FP8_SCALE", "e8m0").lower()
+    return v if v in ("e8m0", "fp32") else "e8m0"
+
+
+MX_BLOCK = 32
+
+
+def is_mx(info: Dict[str, Any]) -> bool:
+    return info.get("format") == "fp8_e4m3fn_mx"
+
+
 def fp8_supported(t: torch.Tensor) -> bool:
     return t.dtype in FP8_QUANTIZABLE_DTYPES and hasattr(torch, "float8_e4m3fn") \
         and t.numel() > 0
@@ -73,6 +107,12 @@ def fp8_entry_quant_info(t: torch.Tensor, vpt: int = DEFAULT_VPT,
                          rotation: str = None) -> Dict[str, Any]:
     rotation = rotation or default_rotation()
     n = t.numel()
+    if rotation == "none" and default_scale() == "e8m0":
+        payload = _round_up(n, 16)
+        nblocks = (n + MX_BLOCK - 1) // MX_BLOCK
+        return {"format": "fp8_e4m3fn_mx", "block": MX_BLOCK, "scale": "e8m0",
+                "rotation": "none", "orig_dtype": dtype_to_string(t.dtype),
+                "payload_bytes": payload, "nblocks": nblocks, "total_bytes": payload + nblocks}
     if rotation == "hadamard32":
         block = 128
         n_q = _round_up(n, GROUP)
@@ -117,6 +157,48 @@ def dequantize_reference(q: torch.Tensor, scale: torch.Tensor, block: int,
     padded = torch.zeros(nblocks * block, dtype=torch.float32, device=q.device)
     padded[:n] = q.float()
     return (padded.view(nblocks, block) * scale[:, None]).reshape(-1)[:n].to(dtype)
+
+
+def pow2(e: torch.Tensor) -> torch.Tensor:
+    """Exact float32 ``2**e`` for integer ``e`` in [-149, 127] (bit-built:
+    normal exponents, or the subnormal bit below -126)."""
+    e = e.to(torch.int32)
+    normal = (e + 127).clamp(min=1) << 23
+    sub = torch.ones_like(e) << (e + 149).clamp(0, 22)
+    return torch.where(e >= -126, normal, sub).view(torch.float32)
+
+
+def mx_exponents(amax: torch.Tensor) -> torch.Tensor:
+    """Per-block ``k``: smallest exponent with ``amax <= 448 * 2^k``."""
+    m, e = torch.frexp(amax)
+    k = torch.where(m <= 0.875, e - 9, e - 8)
+    ok = (amax > 0) & torch.isfinite(amax)
+    return torch.where(ok, k, torch.zeros_like(k)).clamp(-127, 127).to(torch.int32)
+
+
+def mx_quantize_reference(x: torch.Tensor):
+    """MX reference: returns (q[n] e4m3fn, scale bytes[nblocks] uint8)."""
+    flat = x.detach().reshape(-1).float()
+    n = flat.numel()
+    nblocks = (n + MX_BLOCK - 1) // MX_BLOCK
+    blocks = torch.zeros(nblocks * MX_BLOCK, dtype=torch.float32, device=flat.device)
+    blocks[:n] = flat
+    blocks = blocks.view(nblocks, MX_BLOCK)
+    a = blocks.abs()
+    amax = torch.where(torch.isfinite(a), a, torch.zeros_like(a)).amax(dim=1)  # finite only
+    k = mx_exponents(amax)
+    q = (blocks * pow2(-k)[:, None]).to(torch.float8_e4m3fn)
+    return q.reshape(-1)[:n], (k + 127).to(torch.uint8)
+
+
+def mx_dequantize_reference(q: torch.Tensor, sbytes: torch.Tensor,
+                            dtype: torch.dtype) -> torch.Tensor:
+    n = q.numel()
+    nblocks = sbytes.numel()
+    padded = torch.zeros(nblocks * MX_BLOCK, dtype=torch.float32, device=q.device)
+    padded[:n] = q.float()
+    k = sbytes.to(torch.int32) - 127
+    return (padded.view(nblocks, MX_BLOCK) * pow2(k)[:, None]).reshape(-1)[:n].to(dtype)
 
 
 def hadamard_matrix(n: int = GROUP, device=None) -> torch.Tensor:
@@ -169,6 +251,8 @@ def stage_fp8(t: torch.Tensor, entry: TensorEntry, producer: int) -> StagedBuffe
     info = entry.quant
     rot = info.get("rotation", "none")
     payload, nblocks, total = info["payload_bytes"], info["nblocks"], info["total_bytes"]
+    if is_mx(info):
+        return _stage_mx(t, info, producer)
     if t.is_cuda:
         from ..engine import staging
         from . import native
@@ -202,6 +286,32 @@ def stage_fp8(t: torch.Tensor, entry: TensorEntry, producer: int) -> StagedBuffe
     return StagedBuffer(contiguous_cpu_bytes_view(blob), keepalive=blob)
 
 
+def _stage_mx(t: torch.Tensor, info: Dict[str, Any], producer: int) -> StagedBuffer:
+    payload, total = info["payload_bytes"], info["total_bytes"]
+    if t.is_cuda:
+        from ..engine import staging
+        from . import native
+
+        dev = staging.device_of(t)
+        stream = torch.cuda.current_stream(t.device)
+        if producer is not None and producer != stream.cuda_stream:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.default_stream(t.device) if producer == 0
+                      else torch.cuda.ExternalStream(producer))
+            stream.wait_event(ev)
+        src = t if t.is_contiguous() else t.contiguous()
+        blob = torch.empty(total, dtype=torch.uint8, device=t.device)  # kernel writes all of it
+        native.mx8_quantize(dev, src, blob[:payload], blob[payload:], int(stream.cuda_stream))
+        return staging.d2h_tensor(blob, int(stream.cuda_stream))
+    q, sbytes = mx_quantize_reference(t)
+    blob = torch.zeros(total, dtype=torch.uint8)
+    blob[: q.numel()] = q.view(torch.uint8)
+    blob[payload:] = sbytes
+    from ..format.serialization import contiguous_cpu_bytes_view
+
+    return StagedBuffer(contiguous_cpu_bytes_view(blob), keepalive=blob)
+
+
 def _split_blob(raw: torch.Tensor, info: Dict[str, Any], n: int):
     rot = info.get("rotation", "none")
     nq = _round_up(n, GROUP) if rot == "hadamard32" else n
@@ -219,8 +329,13 @@ def dequantize_host_fp8(buf, entry: TensorEntry) -> torch.Tensor:
         n *= int(s)
     mv = memoryview(buf.view if isinstance(buf, StagedBuffer) else buf).cast("B")
     raw = torch.frombuffer(bytearray(mv[: info["total_bytes"]]), dtype=torch.uint8)
-    rot, q, scale = _split_blob(raw, info, n)
     dtype = string_to_dtype(entry.dtype)
+    if is_mx(info):
+        p = info["payload_bytes"]
+        out = mx_dequantize_reference(raw[:n].view(torch.float8_e4m3fn),
+                                      raw[p: p + info["nblocks"]], dtype)
+        return out.view(list(entry.shape))
+    rot, q, scale = _split_blob(raw, info, n)
     if rot == "hadamard32":
         out = hadamard_dequantize_reference(q.view(torch.float8_e4m3fn), scale, n, dtype,
                                             info["block"])
@@ -235,9 +350,13 @@ def dequantize_device(blob_dev: torch.Tensor, entry: TensorEntry, dst: torch.Ten
 
     info = entry.quant
     n = dst.numel()
-    rot, q, scale = _split_blob(blob_dev, info, n)
     stream = int(torch.cuda.current_stream(dst.device).cuda_stream)
     dev = dst.device.index or 0
+    if is_mx(info):
+        p = info["payload_bytes"]
+        native.mx8_dequantize(dev, blob_dev[:n], blob_dev[p: p + info["nblocks"]], dst, stream)
+        return
+    rot, q, scale = _split_blob(blob_dev, info, n)
     if rot == "hadamard32":
         native.fp8_hadamard_dequantize(dev, q, scale, dst, stream)
     else:

@@ -158,6 +158,59 @@ def test_fp8_hadamard_mfma_vs_reference(gpu, dtype, n):
     assert torch.equal(out, ref), (out.float() - ref.float()).abs().max()
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("n", [1, 31, 32, 1000, 2048, 4096 + 17, (1 << 20) + 5, 3 << 20])
+def test_mx8_quant_dequant_vs_reference(gpu, dtype, n):
+    """MX fp8 (E8M0 scale per 32, hs_mx8_quant/dequant): payload, padding and
+    scale bytes bit-identical to the torch reference; dequantization into
+    every float dtype bit-identical too."""
+    from hipsnapshot.ops.quant import mx_dequantize_reference, mx_quantize_reference
+
+    torch.manual_seed(5)
+    x = (torch.randn(n, device=gpu) * torch.logspace(-12, 12, n, device=gpu)).to(dtype)
+    if n >= 1000:  # special values: zero block, inf, nan
+        x[:32] = 0
+        x[40] = float("inf")
+        x[77] = float("nan")
+    payload = (n + 15) // 16 * 16
+    nb = (n + 31) // 32
+    blob = torch.full((payload + nb,), 0xAB, dtype=torch.uint8, device=gpu)  # no zero-fill
+    stream = int(torch.cuda.current_stream().cuda_stream)
+    native.mx8_quantize(0, x, blob[:payload], blob[payload:], stream)
+    rq, rs = mx_quantize_reference(x)
+    torch.cuda.synchronize()
+    assert torch.equal(blob[payload:], rs), (blob[payload:] != rs).sum()
+    assert torch.equal(blob[:n], rq.view(torch.uint8)), (blob[:n] != rq.view(torch.uint8)).sum()
+    assert not blob[n:payload].any()  # padding written as zeros
+    for out_dtype in (torch.bfloat16, torch.float16, torch.float32, torch.float64):
+        out = torch.empty(n, dtype=out_dtype, device=gpu)
+        native.mx8_dequantize(0, blob[:n], blob[payload:], out, stream)
+        ref = mx_dequantize_reference(rq, rs, out_dtype)
+        torch.cuda.synchronize()
+        assert torch.equal(out.isnan(), ref.isnan())
+        ok = ~ref.isnan()
+        assert torch.equal(out[ok], ref[ok]), (out_dtype, (out[ok] != ref[ok]).sum())
+
+
+def test_mx8_snapshot_gpu(gpu, tmp_path):
+    """Default fp8 quantized save is the MX layout; GPU save + GPU restore
+    equal the torch reference, and a CPU restore of the same blob too."""
+    from hipsnapshot.ops.quant import mx_dequantize_reference, mx_quantize_reference
+
+    w = torch.randn(777, 333, device=gpu, dtype=torch.bfloat16)
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/*"])
+    e = Snapshot(str(tmp_path / "s")).get_manifest()["0/sd/w"]
+    assert e.quant["format"] == "fp8_e4m3fn_mx"
+    q, s = mx_quantize_reference(w)
+    ref = mx_dequantize_reference(q, s, torch.bfloat16).view(w.shape)
+    out = torch.zeros_like(w)
+    Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=out)})
+    assert torch.equal(out, ref)
+    host = torch.zeros(w.shape, dtype=torch.bfloat16)
+    Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=host)})
+    assert torch.equal(host, ref.cpu())
+
+
 def test_fp8_hadamard_snapshot_gpu(gpu, tmp_path):
     from hipsnapshot.ops.quant import hadamard_dequantize_reference, hadamard_quantize_reference
     from hipsnapshot.utils.test_utils import env
@@ -300,8 +353,11 @@ def test_async_take_partial_hbm_freeze(gpu, tmp_path):
 def test_fp8_quantized_save_gpu(gpu, tmp_path):
     from hipsnapshot.ops.quant import dequantize_reference, quantize_reference
 
+    from hipsnapshot.utils.test_utils import env
+
     w = torch.randn(1000, 333, device=gpu, dtype=torch.bfloat16)
-    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/*"])
+    with env(HIPSNAPSHOT_FP8_SCALE="fp32"):  # the fp32-scale layout (MX: test_mx8_*)
+        Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/*"])
     out = torch.zeros_like(w)
     Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=out)})
     q, s = quantize_reference(w, 128)

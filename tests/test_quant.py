@@ -6,6 +6,10 @@ import torch
 from hipsnapshot import Snapshot, StateDict
 from hipsnapshot.ops.quant import (
     dequantize_reference,
+    mx_dequantize_reference,
+    mx_exponents,
+    mx_quantize_reference,
+    pow2,
     hadamard_dequantize_reference,
     hadamard_matrix,
     hadamard_quantize_reference,
@@ -53,19 +57,84 @@ def test_rotation_error_tradeoff():
     assert (r_plain[:, 1:] == 0).all()
 
 
-@pytest.mark.parametrize("rotation", ["none", "hadamard32"])
-def test_snapshot_fp8_formats(tmp_path, rotation):
+@pytest.mark.parametrize("rotation,scale", [("none", "e8m0"), ("none", "fp32"),
+                                            ("hadamard32", "fp32")])
+def test_snapshot_fp8_formats(tmp_path, rotation, scale):
     w = torch.randn(257, 129)
-    with env(HIPSNAPSHOT_FP8_ROTATION=rotation):
+    with env(HIPSNAPSHOT_FP8_ROTATION=rotation, HIPSNAPSHOT_FP8_SCALE=scale):
         Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/w"])
     e = Snapshot(str(tmp_path / "s")).get_manifest()["0/sd/w"]
     assert e.quant["rotation"] == rotation
     out = torch.zeros_like(w)
     Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=out)})
-    if rotation == "none":
+    if rotation == "none" and scale == "e8m0":
+        assert e.quant["format"] == "fp8_e4m3fn_mx" and e.quant["block"] == 32
+        assert e.quant["total_bytes"] == (w.numel() + 15) // 16 * 16 + (w.numel() + 31) // 32
+        q, s = mx_quantize_reference(w)
+        ref = mx_dequantize_reference(q, s, torch.float32).view_as(w)
+    elif rotation == "none":
         q, s = quantize_reference(w, 128)
         ref = dequantize_reference(q, s, 128, torch.float32).view_as(w)
     else:
         q, s = hadamard_quantize_reference(w, 128)
         ref = hadamard_dequantize_reference(q, s, w.numel(), torch.float32).view_as(w)
     assert torch.equal(out, ref)
+
+
+def test_pow2_exact():
+    e = torch.arange(-149, 128)
+    assert torch.equal(pow2(e).double(), torch.pow(2.0, e.double()))
+
+
+def test_mx_exponent_rule():
+    """k is the smallest exponent with amax <= 448 * 2^k (brute force)."""
+    g = torch.Generator().manual_seed(0)
+    amax = torch.cat([torch.rand(2000, generator=g) * 10.0 ** torch.randint(-30, 30, (2000,),
+                                                                             generator=g),
+                      torch.tensor([448.0, 448.0 * 2, 449.0, 447.9, 1.0, 0.875, 1e-42, 3e38])])
+    k = mx_exponents(amax)
+    for a, kk in zip(amax.tolist(), k.tolist()):
+        if kk in (-127, 127):
+            continue
+        assert a <= 448.0 * 2.0 ** kk and a > 448.0 * 2.0 ** (kk - 1), (a, kk)
+    special = mx_exponents(torch.tensor([0.0, float("inf"), float("nan")]))
+    assert special.tolist() == [0, 0, 0]
+
+
+def test_mx_scaling_is_exact_and_unsaturated():
+    """x * 2^-k never exceeds 448 and dequantization error is only the fp8
+    rounding of each element (relative error <= 2^-4 for normal values)."""
+    torch.manual_seed(1)
+    x = torch.randn(64, 32) * torch.logspace(-20, 20, 64)[:, None]
+    q, sb = mx_quantize_reference(x)
+    assert not torch.isnan(q.float()).any()
+    assert q.float().abs().max() <= 448.0
+    back = mx_dequantize_reference(q, sb, torch.float32).view_as(x)
+    amax = x.abs().amax(dim=1, keepdim=True)
+    big = x.abs() > amax * 2 ** -6  # far from the fp8 subnormal range
+    rel = ((back - x).abs() / x.abs())[big]
+    assert rel.max() <= 2 ** -4
+    # the block's largest element keeps 3 mantissa bits: never clipped
+    assert torch.all((back.abs().amax(dim=1) - amax[:, 0]).abs() <= amax[:, 0] * 2 ** -4)
+
+
+def test_mx_special_values_and_tails():
+    x = torch.tensor([0.0] * 32 + [float("inf"), 1.0] + [0.0] * 30 + [float("nan"), 2.0, 3.0])
+    q, sb = mx_quantize_reference(x)
+    assert sb.numel() == 3 and sb.tolist()[0] == 127  # all-zero block: scale 1
+    back = mx_dequantize_reference(q, sb, torch.float32)
+    assert torch.equal(back[:32], torch.zeros(32))
+    assert torch.isnan(back[32]) and back[33] == 1.0  # e4m3fn has no inf
+    # the inf did not set block 1's scale: 1.0 kept its full precision
+    assert sb.tolist()[1] == 127 - 8
+    assert torch.isnan(back[64]) and back[65] == 2.0 and back[66] == 3.0
+
+
+def test_mx_error_not_worse_than_fp32_block128():
+    torch.manual_seed(2)
+    x = torch.randn(512, 256) * 0.02
+    q, sb = mx_quantize_reference(x)
+    e_mx = (mx_dequantize_reference(q, sb, torch.float32).view_as(x) - x).norm()
+    q0, s0 = quantize_reference(x, 128)
+    e_128 = (dequantize_reference(q0, s0, 128, torch.float32).view_as(x) - x).norm()
+    assert e_mx < 1.15 * e_128
