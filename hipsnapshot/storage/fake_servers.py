@@ -1,9 +1,11 @@
-"""In-process fake S3 and GCS servers (aiohttp.web) for tests and benchmarks.
+"""Fake S3 and GCS servers for tests and benchmarks.
 
 There is no network on the build or GPU boxes, so the S3/GCS plugins are
 exercised end to end against these: the fake S3 server VERIFIES every SigV4
 signature (recomputed from the raw request with the shared secret) and
-implements PUT/GET(Range)/DELETE, multipart uploads and ListObjectsV2; the
+implements PUT/GET(Range)/HEAD/DELETE, multipart uploads and ListObjectsV2
+on a threaded HTTP/1.1 server that can also run as its own process
+(``FakeS3Process``); the
 fake GCS server implements media + resumable uploads (308 / Range protocol),
 ranged ``alt=media`` downloads and DELETE.  Both support fault injection
 (``fail_next(n, status)``) to test the retry paths.
@@ -73,100 +75,256 @@ class _ServerThread:
         self.stop()
 
 
-class FakeS3Server(_ServerThread):
-    def __init__(self, access_key: str = "AKIDFAKE", secret: str = "fake-secret",
-                 region: str = "us-east-1") -> None:
-        super().__init__()
-        self.access_key, self.secret, self.region = access_key, secret, region
-        self.objects: Dict[str, bytes] = {}
-        self.uploads: Dict[str, Dict[int, bytes]] = {}
-        app = web.Application(client_max_size=1 << 40)
-        app.router.add_route("*", "/{bucket}", self._bucket)
-        app.router.add_route("*", "/{bucket}/{key:.*}", self._object)
-        self.start(app)
+class _S3Object:
+    """An object as the list of its uploaded bodies (a multipart object is
+    never re-joined): ranged GETs send slices of the parts."""
 
-    def _verify(self, req: web.Request, body: bytes) -> Optional[web.Response]:
-        auth = req.headers.get("Authorization", "")
+    __slots__ = ("parts", "size")
+
+    def __init__(self, parts) -> None:
+        self.parts = list(parts)
+        self.size = sum(len(p) for p in self.parts)
+
+    def __eq__(self, other) -> bool:  # tests compare with bytes
+        return bytes(self) == bytes(other)
+
+    def __bytes__(self) -> bytes:
+        return b"".join(bytes(p) for p in self.parts)
+
+    def slices(self, lo: int, hi: int):
+        pos = 0
+        for p in self.parts:
+            a, b = max(lo, pos), min(hi, pos + len(p))
+            if b > a:
+                yield memoryview(p)[a - pos: b - pos]
+            pos += len(p)
+
+
+class FakeS3Server:
+    """S3 subset over a THREADED HTTP/1.1 server (one thread per keep-alive
+    connection; bodies are received with ``readinto`` into one bytearray and
+    sent from memoryview slices, so the server moves GB/s and the client is
+    what gets measured).  Verifies every SigV4 signature.  Runs in-process
+    (tests: ``objects`` / ``fail_next`` are visible) or in its own process
+    (``FakeS3Process``, benchmarks: the snapshot process's GIL is not
+    shared with the server)."""
+
+    def __init__(self, access_key: str = "AKIDFAKE", secret: str = "fake-secret",
+                 region: str = "us-east-1", port: int = 0) -> None:
+        import http.server
+
+        self.access_key, self.secret, self.region = access_key, secret, region
+        self.objects: Dict[str, _S3Object] = {}
+        self.uploads: Dict[str, Dict[int, bytearray]] = {}
+        self.fail_queue: list = []
+        self.requests = 0
+        self._lock = threading.Lock()
+        server = self
+
+        class Handler(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *a):  # quiet
+                pass
+
+            def _body(self) -> bytearray:
+                n = int(self.headers.get("Content-Length") or 0)
+                buf = bytearray(n)
+                view, got = memoryview(buf), 0
+                while got < n:
+                    r = self.rfile.readinto(view[got:])
+                    if not r:
+                        raise ConnectionResetError("client closed mid-body")
+                    got += r
+                return buf
+
+            def _send(self, status: int, body=b"", headers=None) -> None:
+                self.send_response(status)
+                for k, v in (headers or {}).items():
+                    self.send_header(k, v)
+                if not any(k.lower() == "content-length" for k in (headers or {})):
+                    self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                if body and self.command != "HEAD":
+                    self.wfile.write(body)
+
+            def _handle(self) -> None:
+                body = self._body()
+                resp = server._dispatch(self, body)
+                if resp is not None:
+                    self._send(*resp)
+
+            do_GET = do_PUT = do_POST = do_DELETE = do_HEAD = _handle
+
+        class Server(http.server.ThreadingHTTPServer):
+            daemon_threads = True
+            request_queue_size = 256
+
+        self._httpd = Server(("127.0.0.1", port), Handler)
+        self.port = self._httpd.server_address[1]
+        self._thread = threading.Thread(target=self._httpd.serve_forever, daemon=True,
+                                        kwargs={"poll_interval": 0.1})
+        self._thread.start()
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.port}"
+
+    def fail_next(self, n: int = 1, status: int = 503) -> None:
+        self.fail_queue.extend([status] * n)
+
+    def stop(self) -> None:
+        self._httpd.shutdown()
+        self._httpd.server_close()
+        self._thread.join(10)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()
+
+    # -- request handling ---------------------------------------------------------
+
+    def _verify(self, h, path: str, query: Dict[str, str], body) -> Optional[tuple]:
+        import hashlib
+
+        auth = h.headers.get("Authorization", "")
         m = re.match(r"AWS4-HMAC-SHA256 Credential=([^/]+)/(\d{8})/([^/]+)/s3/aws4_request, "
                      r"SignedHeaders=([^,]+), Signature=([0-9a-f]{64})$", auth)
         if not m or m.group(1) != self.access_key:
-            return web.Response(status=403, text=f"bad auth header {auth!r}")
+            return 403, f"bad auth header {auth!r}".encode()
         signed = m.group(4).split(";")
-        hdrs = {h: req.headers.get(h, "") for h in signed
-                if h not in ("host", "x-amz-date", "x-amz-content-sha256")}
-        now = _dt.datetime.strptime(req.headers["x-amz-date"], "%Y%m%dT%H%M%SZ").replace(
+        hdrs = {k: h.headers.get(k, "") for k in signed
+                if k not in ("host", "x-amz-date", "x-amz-content-sha256")}
+        now = _dt.datetime.strptime(h.headers["x-amz-date"], "%Y%m%dT%H%M%SZ").replace(
             tzinfo=_dt.timezone.utc)
-        query = {k: v for k, v in req.query.items()}
-        expect = sigv4_headers(req.method, req.headers["Host"], req.path, query, hdrs,
-                               req.headers["x-amz-content-sha256"], self.access_key,
-                               self.secret, m.group(3), now=now,
-                               session_token=req.headers.get("x-amz-security-token"))
+        expect = sigv4_headers(h.command, h.headers["Host"], path, query, hdrs,
+                               h.headers["x-amz-content-sha256"], self.access_key, self.secret,
+                               m.group(3), now=now,
+                               session_token=h.headers.get("x-amz-security-token"))
         if expect["Authorization"] != auth:
-            return web.Response(status=403, text="SignatureDoesNotMatch")
-        ph = req.headers["x-amz-content-sha256"]
-        if ph not in ("UNSIGNED-PAYLOAD",):
-            import hashlib
-
-            if hashlib.sha256(body).hexdigest() != ph:
-                return web.Response(status=400, text="XAmzContentSHA256Mismatch")
+            return 403, b"SignatureDoesNotMatch"
+        ph = h.headers["x-amz-content-sha256"]
+        if ph != "UNSIGNED-PAYLOAD" and hashlib.sha256(body).hexdigest() != ph:
+            return 400, b"XAmzContentSHA256Mismatch"
         return None
 
-    async def _bucket(self, req: web.Request) -> web.Response:
-        body = await req.read()
-        bad = self._maybe_fail() or self._verify(req, body)
-        if bad is not None:
-            return bad
-        bucket = req.match_info["bucket"]
-        if req.method == "GET" and req.query.get("list-type") == "2":
-            prefix = req.query.get("prefix", "")
-            keys = sorted(k.split("/", 1)[1] for k in self.objects
-                          if k.startswith(f"{bucket}/{prefix}"))
-            xml = "<ListBucketResult>" + "".join(f"<Contents><Key>{k}</Key></Contents>"
-                                                 for k in keys) + "</ListBucketResult>"
-            return web.Response(text=xml, content_type="application/xml")
-        return web.Response(status=400)
+    def _dispatch(self, h, body: bytearray):
+        from urllib.parse import parse_qsl, unquote, urlsplit
 
-    async def _object(self, req: web.Request) -> web.Response:
-        body = await req.read()
-        bad = self._maybe_fail() or self._verify(req, body)
+        u = urlsplit(h.path)
+        path = unquote(u.path)
+        q = dict(parse_qsl(u.query, keep_blank_values=True))
+        with self._lock:
+            self.requests += 1
+            fail = self.fail_queue.pop(0) if self.fail_queue else None
+        if fail is not None:
+            return fail, b"injected"
+        bad = self._verify(h, path, q, body)
         if bad is not None:
             return bad
-        key = f"{req.match_info['bucket']}/{req.match_info['key']}"
-        q = req.query
-        if req.method == "POST" and "uploads" in q:
+        bucket, _, obj = path.lstrip("/").partition("/")
+        m = h.command
+        if not obj:  # bucket-level: ListObjectsV2
+            if m == "GET" and q.get("list-type") == "2":
+                prefix = q.get("prefix", "")
+                with self._lock:
+                    keys = sorted(k.split("/", 1)[1] for k in self.objects
+                                  if k.startswith(f"{bucket}/{prefix}"))
+                xml = "<ListBucketResult>" + "".join(f"<Contents><Key>{k}</Key></Contents>"
+                                                     for k in keys) + "</ListBucketResult>"
+                return 200, xml.encode(), {"Content-Type": "application/xml"}
+            return 400, b""
+        key = f"{bucket}/{obj}"
+        if m == "POST" and "uploads" in q:
             uid = uuid.uuid4().hex
-            self.uploads[uid] = {}
-            return web.Response(text=f"<InitiateMultipartUploadResult><UploadId>{uid}</UploadId>"
-                                     "</InitiateMultipartUploadResult>",
-                                content_type="application/xml")
-        if req.method == "PUT" and "uploadId" in q:
-            self.uploads[q["uploadId"]][int(q["partNumber"])] = body
-            return web.Response(headers={"ETag": f'"{q["partNumber"]}-{len(body)}"'})
-        if req.method == "POST" and "uploadId" in q:
-            parts = self.uploads.pop(q["uploadId"])
+            with self._lock:
+                self.uploads[uid] = {}
+            return 200, (f"<InitiateMultipartUploadResult><UploadId>{uid}</UploadId>"
+                         "</InitiateMultipartUploadResult>").encode()
+        if m == "PUT" and "uploadId" in q:
+            with self._lock:
+                self.uploads[q["uploadId"]][int(q["partNumber"])] = body
+            return 200, b"", {"ETag": f'"{q["partNumber"]}-{len(body)}"'}
+        if m == "POST" and "uploadId" in q:
             nums = [int(n) for n in re.findall(r"<PartNumber>(\d+)</PartNumber>", body.decode())]
-            self.objects[key] = b"".join(parts[n] for n in nums)
-            return web.Response(text="<CompleteMultipartUploadResult/>",
-                                content_type="application/xml")
-        if req.method == "DELETE" and "uploadId" in q:
-            self.uploads.pop(q["uploadId"], None)
-            return web.Response(status=204)
-        if req.method == "PUT":
-            self.objects[key] = body
-            return web.Response(headers={"ETag": '"x"'})
-        if req.method == "GET":
-            if key not in self.objects:
-                return web.Response(status=404, text="NoSuchKey")
-            data = self.objects[key]
-            rng = req.headers.get("Range")
+            with self._lock:
+                parts = self.uploads.pop(q["uploadId"])
+                self.objects[key] = _S3Object(parts[n] for n in nums)
+            return 200, b"<CompleteMultipartUploadResult/>"
+        if m == "DELETE" and "uploadId" in q:
+            with self._lock:
+                self.uploads.pop(q["uploadId"], None)
+            return 204, b""
+        if m == "PUT":
+            with self._lock:
+                self.objects[key] = _S3Object([body])
+            return 200, b"", {"ETag": '"x"'}
+        if m in ("GET", "HEAD"):
+            with self._lock:
+                o = self.objects.get(key)
+            if o is None:
+                return 404, b"NoSuchKey"
+            if m == "HEAD":
+                return 200, b"", {"Content-Length": str(o.size)}
+            rng = h.headers.get("Range")
+            lo, hi, status = 0, o.size, 200
             if rng:
-                lo, hi = map(int, rng.split("=", 1)[1].split("-"))
-                return web.Response(status=206, body=data[lo:hi + 1])
-            return web.Response(body=data)
-        if req.method == "DELETE":
-            self.objects.pop(key, None)
-            return web.Response(status=204)
-        return web.Response(status=405)
+                a, b = rng.split("=", 1)[1].split("-")
+                lo, hi, status = int(a), min(int(b) + 1, o.size), 206
+            h.send_response(status)
+            h.send_header("Content-Length", str(max(hi - lo, 0)))
+            if status == 206:
+                h.send_header("Content-Range", f"bytes {lo}-{hi - 1}/{o.size}")
+            h.end_headers()
+            for sl in o.slices(lo, hi):
+                h.wfile.write(sl)
+            return None
+        if m == "DELETE":
+            with self._lock:
+                self.objects.pop(key, None)
+            return 204, b""
+        return 405, b""
+
+
+class FakeS3Process:
+    """``FakeS3Server`` in its own process (``python -m
+    hipsnapshot.storage.fake_servers s3``): benchmarks measure the client
+    without sharing its GIL with the server.  ``stop()`` ends exactly the
+    process this object started."""
+
+    def __init__(self, access_key: str = "AKIDFAKE", secret: str = "fake-secret") -> None:
+        import subprocess
+        import sys
+
+        self.proc = subprocess.Popen(
+            [sys.executable, "-m", "hipsnapshot.storage.fake_servers", "s3", access_key, secret],
+            stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+        line = self.proc.stdout.readline().decode().split()
+        if len(line) != 2 or line[0] != "PORT":
+            self.proc.kill()
+            raise RuntimeError(f"fake S3 process did not start: {line}")
+        self.port = int(line[1])
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.port}"
+
+    def stop(self) -> None:
+        if self.proc.poll() is None:
+            self.proc.stdin.close()  # the server exits when its stdin closes
+            try:
+                self.proc.wait(30)
+            except Exception:  # noqa: BLE001
+                self.proc.kill()
+                self.proc.wait()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()
 
 
 class FakeGCSServer(_ServerThread):
@@ -242,3 +400,19 @@ class FakeGCSServer(_ServerThread):
             return bad
         self.objects.pop(f"{req.match_info['bucket']}/{req.match_info['name']}", None)
         return web.Response(status=204)
+
+
+def _main() -> None:
+    import sys
+
+    if len(sys.argv) >= 2 and sys.argv[1] == "s3":
+        srv = FakeS3Server(*sys.argv[2:4])
+        print(f"PORT {srv.port}", flush=True)
+        sys.stdin.read()  # until the parent closes our stdin (or exits)
+        srv.stop()
+    else:
+        raise SystemExit("usage: python -m hipsnapshot.storage.fake_servers s3 [key secret]")
+
+
+if __name__ == "__main__":
+    _main()

@@ -1,4 +1,4 @@
-"""Amazon S3 (and S3-compatible) storage over aiohttp with SigV4 signing.
+"""Amazon S3 (and S3-compatible) storage with SigV4 signing.
 
 Reference: `/root/reference/torchsnapshot/storage_plugins/s3.py:16-74` uses
 aiobotocore (not available in this stack: no AWS SDK, no network).  This is a
@@ -8,17 +8,21 @@ self-contained client:
   (``aws_access_key_id`` / ``aws_secret_access_key`` / ``aws_session_token`` /
   ``region`` / ``endpoint_url``) or the standard ``AWS_*`` environment
   variables; ``endpoint_url`` switches to path-style addressing (MinIO, the
-  in-process fake used by the tests);
+  fake servers used by tests and benchmarks);
 * AWS Signature Version 4 (header auth); payloads are sent as
   ``UNSIGNED-PAYLOAD`` by default (TLS protects integrity; hashing GBs of
   checkpoint on the host would cost more than the upload) or signed with
   ``sign_payload=True``;
-* blobs >= ``multipart_threshold`` (64 MiB) use multipart upload with
-  ``max_concurrency`` parallel parts -- one slow 512 MiB PUT was the S3
-  bottleneck of the reference; parts stream zero-copy from the staged
-  (pinned) buffer;
-* ranged GETs land directly in the consumer-provided destination buffer;
-* bounded exponential-backoff retries on 5xx / connection errors.
+* every request runs on a worker thread of a blocking keep-alive connection
+  pool (``http_pool``): bodies are sent straight from the staged (pinned)
+  buffer and received straight into the consumer's destination -- no
+  ``tobytes()``, no intermediate ``bytes`` -- and ``max_concurrency`` transfers
+  move in parallel on as many cores (the reference: one event-loop thread,
+  single-shot ``put_object`` of up to 512 MiB);
+* blobs >= ``multipart_threshold`` (64 MiB) are uploaded as parallel
+  multipart parts; reads of >= ``part_size`` are split into parallel ranged
+  GETs, each landing in its slice of the destination;
+* bounded exponential-backoff retries on 5xx / 429 / connection errors.
 """
 
 from __future__ import annotations
@@ -30,10 +34,12 @@ import hmac
 import os
 import random
 import xml.etree.ElementTree as ET
+from concurrent.futures import ThreadPoolExecutor
 from typing import Any, Dict, List, Optional, Tuple
-from urllib.parse import quote
+from urllib.parse import quote, urlsplit
 
 from ..io_types import ReadIO, StoragePlugin, WriteIO
+from .http_pool import HTTPPool
 
 EMPTY_SHA256 = hashlib.sha256(b"").hexdigest()
 UNSIGNED = "UNSIGNED-PAYLOAD"
@@ -112,9 +118,11 @@ class S3StoragePlugin(StoragePlugin):
         self.sign_payload = bool(opts.get("sign_payload", False))
         self.multipart_threshold = int(opts.get("multipart_threshold", 64 << 20))
         self.part_size = max(int(opts.get("part_size", 32 << 20)), 5 << 20)
-        self.max_concurrency = int(opts.get("max_concurrency", 8))
+        self.max_concurrency = int(opts.get("max_concurrency", 16))
         self.retries = int(opts.get("retries", 4))
-        self._session = None
+        self._pool: Optional[HTTPPool] = None
+        self._exec: Optional[ThreadPoolExecutor] = None
+        self._sem: Optional[asyncio.Semaphore] = None
 
     # -- plumbing ---------------------------------------------------------------
 
@@ -130,44 +138,51 @@ class S3StoragePlugin(StoragePlugin):
     def _key(self, path: str) -> str:
         return f"{self.prefix}/{path}" if self.prefix else path
 
-    async def _get_session(self):
-        if self._session is None or self._session.closed:
-            import aiohttp
-
-            self._session = aiohttp.ClientSession(
-                connector=aiohttp.TCPConnector(limit=64),
-                timeout=aiohttp.ClientTimeout(total=None, sock_read=300))
-        return self._session
+    def _transport(self) -> Tuple[HTTPPool, ThreadPoolExecutor]:
+        if self._pool is None:
+            base, _, _ = self._url_parts("")
+            u = urlsplit(base)
+            self._pool = HTTPPool(u.scheme, u.hostname, u.port, max_conns=self.max_concurrency)
+            self._exec = ThreadPoolExecutor(max_workers=self.max_concurrency,
+                                            thread_name_prefix="hipsnapshot-s3")
+        return self._pool, self._exec
 
     async def _request(self, method: str, key: str, query: Optional[Dict[str, str]] = None,
                        headers: Optional[Dict[str, str]] = None, body=None,
-                       expect=(200, 204, 206)) -> Tuple[int, Dict[str, str], bytes]:
+                       expect=(200, 204, 206), dest: Optional[memoryview] = None
+                       ) -> Tuple[int, Dict[str, str], bytes, int]:
+        """One signed request with retries.  ``dest``: a 2xx body is received
+        straight into it (4th value: bytes received there)."""
         query = query or {}
         headers = dict(headers or {})
-        base, host, path = self._url_parts(key)
+        _, host, path = self._url_parts(key)
         if body is None:
             phash = EMPTY_SHA256
         elif self.sign_payload:
             phash = hashlib.sha256(body).hexdigest()
         else:
             phash = UNSIGNED
+        target = _uri_encode(path, encode_slash=False)
+        if query:
+            target += "?" + "&".join(f"{_uri_encode(k)}={_uri_encode(v)}"
+                                     for k, v in sorted(query.items()))
+        pool, ex = self._transport()
+        if self._sem is None:
+            self._sem = asyncio.Semaphore(self.max_concurrency)
+        loop = asyncio.get_running_loop()
         last_exc: Optional[BaseException] = None
         for attempt in range(self.retries + 1):
             signed = sigv4_headers(method, host, path, query, headers, phash, self.access_key,
                                    self.secret, self.region, session_token=self.token)
-            url = base + _uri_encode(path, encode_slash=False)
             try:
-                sess = await self._get_session()
-                async with sess.request(method, url, params=query or None, headers=signed,
-                                        data=body) as resp:
-                    data = await resp.read()
-                    status = resp.status
-                    rheaders = dict(resp.headers)
-            except (OSError, asyncio.TimeoutError) as e:  # aiohttp errors are OSErrors
+                async with self._sem:
+                    status, rheaders, data, n = await loop.run_in_executor(
+                        ex, pool.request, method, target, signed, body, dest)
+            except OSError as e:  # connection errors, timeouts (socket.timeout is one)
                 last_exc = e
             else:
                 if status in expect:
-                    return status, rheaders, data
+                    return status, rheaders, data, n
                 if status == 404:
                     raise FileNotFoundError(f"s3://{self.bucket}/{key}")
                 err = S3Error(f"S3 {method} {key} -> HTTP {status}: {data[:300]!r}")
@@ -183,24 +198,20 @@ class S3StoragePlugin(StoragePlugin):
         mv = memoryview(write_io.buf).cast("B")
         key = self._key(write_io.path)
         if mv.nbytes < self.multipart_threshold:
-            await self._request("PUT", key, body=mv.tobytes() if mv.nbytes < (1 << 20) else mv,
-                                headers={"Content-Length": str(mv.nbytes)})
+            await self._request("PUT", key, body=mv, headers={"Content-Length": str(mv.nbytes)})
             return
         await self._multipart_upload(key, mv)
 
     async def _multipart_upload(self, key: str, mv: memoryview) -> None:
-        _, _, data = await self._request("POST", key, query={"uploads": ""})
+        _, _, data, _ = await self._request("POST", key, query={"uploads": ""})
         upload_id = _xml_find(data, "UploadId")
         parts: List[Tuple[int, str]] = []
-        sem = asyncio.Semaphore(self.max_concurrency)
 
         async def put_part(num: int, lo: int, hi: int) -> None:
-            async with sem:
-                _, hdrs, _ = await self._request(
-                    "PUT", key, query={"partNumber": str(num), "uploadId": upload_id},
-                    body=mv[lo:hi], headers={"Content-Length": str(hi - lo)})
-                etag = {k.lower(): v for k, v in hdrs.items()}.get("etag", "")
-                parts.append((num, etag))
+            _, hdrs, _, _ = await self._request(
+                "PUT", key, query={"partNumber": str(num), "uploadId": upload_id},
+                body=mv[lo:hi], headers={"Content-Length": str(hi - lo)})
+            parts.append((num, hdrs.get("etag", "")))
 
         try:
             tasks = [put_part(i + 1, lo, min(lo + self.part_size, mv.nbytes))
@@ -218,18 +229,34 @@ class S3StoragePlugin(StoragePlugin):
                 pass
             raise
 
+    async def _size(self, key: str) -> int:
+        _, hdrs, _, _ = await self._request("HEAD", key, expect=(200,))
+        return int(hdrs["content-length"])
+
     async def read(self, read_io: ReadIO) -> None:
         key = self._key(read_io.path)
-        headers = {}
         if read_io.byte_range is not None:
             lo, hi = read_io.byte_range
-            headers["Range"] = f"bytes={lo}-{hi - 1}"  # HTTP ranges are inclusive
-        _, _, data = await self._request("GET", key, headers=headers)
-        if read_io.dest is not None and read_io.dest.nbytes >= len(data):
-            read_io.dest.view[: len(data)] = data
-            read_io.buf = read_io.dest.view[: len(data)]
         else:
-            read_io.buf = memoryview(data)
+            lo, hi = 0, await self._size(key)
+        total = hi - lo
+        if read_io.dest is not None and read_io.dest.nbytes >= total:
+            out = read_io.dest.view[:total]
+        else:
+            out = memoryview(bytearray(total))
+
+        async def get(a: int, b: int) -> None:
+            # HTTP ranges are inclusive; the body lands in out[a - lo : b - lo]
+            _, _, data, n = await self._request("GET", key,
+                                                headers={"Range": f"bytes={a}-{b - 1}"},
+                                                dest=out[a - lo: b - lo])
+            if n != b - a:
+                raise S3Error(f"S3 GET {key} bytes {a}-{b - 1}: got {n or len(data)} bytes")
+
+        if total > 0:
+            await asyncio.gather(*(get(a, min(a + self.part_size, hi))
+                                   for a in range(lo, hi, self.part_size)))
+        read_io.buf = out
 
     async def delete(self, path: str) -> None:
         await self._request("DELETE", self._key(path))
@@ -241,7 +268,7 @@ class S3StoragePlugin(StoragePlugin):
             q = {"list-type": "2", "prefix": prefix}
             if token:
                 q["continuation-token"] = token
-            _, _, data = await self._request("GET", "", query=q)
+            _, _, data, _ = await self._request("GET", "", query=q)
             keys = _xml_findall(data, "Key")
             await asyncio.gather(*(self._request("DELETE", k) for k in keys))
             token = _xml_find(data, "NextContinuationToken", required=False)
@@ -249,9 +276,10 @@ class S3StoragePlugin(StoragePlugin):
                 return
 
     async def close(self) -> None:
-        if self._session is not None and not self._session.closed:
-            await self._session.close()
-        self._session = None
+        if self._pool is not None:
+            self._pool.close()
+            self._exec.shutdown(wait=False)
+        self._pool = self._exec = self._sem = None
 
 
 def _strip_ns(tag: str) -> str:

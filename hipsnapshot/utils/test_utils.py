@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import asyncio
 import functools
+import time
 import os
 import socket
 import traceback
@@ -158,8 +159,17 @@ def run_distributed(fn: Callable, world_size: int, *args, backend: str = "gloo",
              for r in range(world_size)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout)
+    # poll: once a rank has failed, its peers usually block in a collective
+    # with it -- give them a short grace period instead of the full timeout
+    deadline = time.monotonic() + timeout
+    failed_at = None
+    while any(p.is_alive() for p in procs) and time.monotonic() < deadline:
+        if failed_at is None and any(p.exitcode not in (None, 0) for p in procs):
+            failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > 15:
+            break
+        for p in procs:
+            p.join(0.05)
     alive = [p for p in procs if p.is_alive()]
     for p in alive:
         p.kill()

@@ -6,9 +6,9 @@ set -o pipefail
 export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD
 REPO=$PWD
 mkdir -p gpurun_out/r3/fp8
-timeout -k 10 700 python -u -m pytest tests/test_dlrm_resharding.py tests/test_dtensor_2d.py tests/test_gpu.py \
-    -m gpu -x -v --timeout 600 --timeout-method thread \
-    -k "resharding or fsdp_over_tp or unfrozen or mx8 or fp8" > gpurun_out/r3/newgpu.log 2>&1 \
+timeout -k 10 700 python -u -m pytest -s tests/test_dlrm_resharding.py tests/test_dtensor_2d.py tests/test_gpu.py \
+    -m gpu -x -v --timeout 300 --timeout-method thread \
+    -k "resharding or fsdp_over_tp or unfrozen or mx8 or fp8" 2>&1 | tee gpurun_out/r3/newgpu.log | grep --line-buffered -E "dlrm case|PASS|FAIL|Timeout|Thread|File"  \
     || { echo TESTS_FAIL; grep -E "FAIL|Error|assert" gpurun_out/r3/newgpu.log | head -30; exit 1; }
 tail -2 gpurun_out/r3/newgpu.log
 timeout -k 10 120 python scripts/fp8_kernels_bench.py > gpurun_out/r3/fp8/host_timed.jsonl 2>&1 \

@@ -80,10 +80,19 @@ def _matrix_worker(tmp: str, device: str, batching: bool) -> None:
     from hipsnapshot.knobs import override_is_batching_disabled, override_max_shard_size_bytes
     from hipsnapshot.models.dlrm import DLRM, SHARDINGS
 
+    import faulthandler
+    import sys
+    import time
+
+    # a hang prints every thread's stack instead of waiting for the runner
+    faulthandler.dump_traceback_later(240, exit=True)
     dev = torch.device(device)
+    if dev.type == "cuda":  # every rank shares this GPU (not LOCAL_RANK's)
+        torch.cuda.set_device(dev)
     mesh = init_device_mesh(dev.type, (dist.get_world_size(),))
     ws = dist.get_world_size()
     cases = list(itertools.product(SHARDINGS, SHARDINGS, (False, True)))
+    t0 = time.monotonic()
     with override_is_batching_disabled(not batching):
         for n, (src_kind, dst_kind, use_async) in enumerate(cases):
             src = DLRM(TABLES, dim=DIM, device=dev, mesh=mesh, sharding=src_kind)
@@ -109,12 +118,16 @@ def _matrix_worker(tmp: str, device: str, batching: bool) -> None:
             snap.restore({"dlrm": dst, "optim": dopt})
             tag = (src_kind, dst_kind, use_async, batching)
             _check(dst, dopt, tag)
+            if dist.get_rank() == 0:
+                print(f"dlrm case {n} {tag} ok at {time.monotonic() - t0:.1f}s", file=sys.stderr,
+                      flush=True)
             # read_object of every table (sharded entry) into a plain tensor
             for i, rows in enumerate(TABLES):
                 for out_dev in {dev, torch.device("cpu")}:
                     plain = torch.zeros(rows, DIM, device=out_dev)
                     snap.read_object(f"0/dlrm/tables.{i}.weight", obj_out=plain)
                     assert torch.equal(plain.cpu(), _full("w", i, rows)), (tag, i, out_dev)
+    faulthandler.cancel_dump_traceback_later()
 
 
 @pytest.mark.multiproc
@@ -127,7 +140,7 @@ def test_dlrm_resharding_matrix_cpu(tmp_path, batching):
 @pytest.mark.parametrize("batching", [True, False])
 def test_dlrm_resharding_matrix_gpu(gpu, tmp_path, batching):
     run_distributed(_matrix_worker, 2, str(tmp_path), "cuda:0", batching, backend="gloo",
-                    timeout=600)
+                    timeout=300)
 
 
 def _forward_worker(device: str) -> None:

@@ -108,6 +108,8 @@ def test_dim_index_runs_matches_torch_random():
 def _mesh2d(order, device="cpu"):
     from torch.distributed.device_mesh import init_device_mesh
 
+    if torch.device(device).type == "cuda":  # all ranks share this GPU
+        torch.cuda.set_device(torch.device(device))
     return init_device_mesh(torch.device(device).type, (2, 2), mesh_dim_names=order)
 
 
@@ -204,6 +206,8 @@ def _restore_worker(tmp: str, target: str, device: str = "cpu"):
     elif target == "2d_same":
         model = build_2d_llama(_cfg(), dev, _mesh2d(("dp", "tp"), device), torch.float32)
     elif target == "fsdp":
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
         mesh = init_device_mesh(dev.type, (dist.get_world_size(),))
         model = build_fsdp_llama(_cfg(), dev, torch.float32, mesh=mesh)
     else:

@@ -272,3 +272,31 @@ def test_fs_engine_recreates_a_cached_directory_removed_meanwhile(tmp_path):
     finally:
         fs.sync_close(loop)
         loop.close()
+
+
+def test_s3_out_of_process_parallel_parts_land_in_dest():
+    """Out-of-process fake S3: multipart PUT from a memoryview, whole-object
+    read (HEAD + parallel ranged GETs) and a ranged read, both received
+    straight into the caller's destination buffer."""
+    from hipsnapshot.io_types import StagedBuffer
+    from hipsnapshot.storage.fake_servers import FakeS3Process
+
+    with FakeS3Process() as srv:
+        opts = dict(S3_OPTS, endpoint_url=srv.url, multipart_threshold=6 << 20,
+                    part_size=5 << 20, max_concurrency=4)
+
+        async def body():
+            p = url_to_storage_plugin("s3://bucket/run", opts)
+            big = bytearray(os.urandom((23 << 20) + 11))  # 5 parts
+            await p.write(WriteIO(path="b", buf=memoryview(big)))
+            dest = bytearray(len(big) + 100)
+            r = ReadIO(path="b", dest=StagedBuffer(memoryview(dest)))
+            await p.read(r)
+            assert bytes(r.data()) == bytes(big)
+            assert r.buf.obj is dest  # landed in the destination, no copy object
+            r = ReadIO(path="b", byte_range=(7, (11 << 20) + 3))
+            await p.read(r)
+            assert bytes(r.data()) == bytes(big[7:(11 << 20) + 3])
+            await p.close()
+
+        run(body())
