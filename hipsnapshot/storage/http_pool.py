@@ -210,8 +210,11 @@ class HTTPPool:
                 dest[:got] = conn.buf[:got]
                 del conn.buf[:got]
             view = dest[got:n]  # the rest of the body, straight from the socket
+            # plain TCP: one blocking syscall for the whole rest (GIL released
+            # once, not per 64 KiB segment); TLS sockets take no flags
+            flags = 0 if self._ssl is not None else socket.MSG_WAITALL
             while got < n:
-                r = conn.sock.recv_into(view, n - got)
+                r = conn.sock.recv_into(view, n - got, flags)
                 if r == 0:
                     raise ConnectionResetError("connection closed mid-body")
                 view = view[r:]

@@ -243,7 +243,11 @@ class S3StoragePlugin(StoragePlugin):
         if read_io.dest is not None and read_io.dest.nbytes >= total:
             out = read_io.dest.view[:total]
         else:
-            out = memoryview(bytearray(total))
+            import numpy as np
+
+            # uninitialised: no zero-fill pass on the event loop (the pages
+            # are first touched by recv_into on the transfer threads)
+            out = memoryview(np.empty(total, dtype=np.uint8))
 
         async def get(a: int, b: int) -> None:
             # HTTP ranges are inclusive; the body lands in out[a - lo : b - lo]
