@@ -14,6 +14,15 @@ N ranks sharing host memory bandwidth.  ``ideal_aggregate_GBps`` = N x the
 share's bytes / the share's take time, the upper bound if nothing else
 interfered.
 
+``--host-siblings K`` adds the host side of the other ranks: K processes
+(no GPU) replay, for every timed take, what a sibling rank's take does to
+the host -- a write pass over its staging memory standing in for the D2H
+DMA (``--sibling-dma-pass``), then the same blob sizes written through the
+same native FS engine (same I/O thread count) into their own directories --
+started together with the GPU rank's take.  ``contended_take_ms_median`` vs
+``take_ms_median`` is the cost of N ranks sharing this host's CPUs and
+memory bandwidth; ``contended_aggregate_GBps`` replaces the solo predictor.
+
     python benchmarks/rank_share/main.py --world 8 [--compression hsz1]
     python benchmarks/rank_share/main.py --model llama3_70b --world 8   # BASELINE config 5's share
 """
@@ -44,6 +53,10 @@ def main() -> None:
     ap.add_argument("--ab", default=None,
                     help="NAME=v1,v2[,...]: alternate env var NAME over the values take by "
                          "take (same process, interleaved) and report each value's takes")
+    ap.add_argument("--host-siblings", type=int, default=0,
+                    help="K host-only processes replaying sibling ranks' host work per take")
+    ap.add_argument("--sibling-dma-pass", type=int, default=1,
+                    help="siblings write their staging memory once per take (DMA stand-in)")
     ap.add_argument("--switch-interval", type=float, default=None,
                     help="sys.setswitchinterval for the run (GIL hand-over latency)")
     args = ap.parse_args()
@@ -95,7 +108,16 @@ def main() -> None:
             if ab_name:
                 os.environ[ab_name] = v
             take()
+    sib = None
+    if args.host_siblings > 0:
+        sizes = [os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(path)
+                 for f in fs if not f.startswith(".")]
+        sib = _Siblings(args.host_siblings, sizes, root, bool(args.sibling_dma_pass))
+        for _ in range(2):  # warm their engines / page cache
+            sib.go()
+            sib.wait()
     times = []
+    contended = []
     per_val = {v: [] for v in ab_vals}
     for _ in range(args.steps):
         for v in ab_vals:
@@ -115,6 +137,16 @@ def main() -> None:
                                           "mean": round(statistics.mean(t) * 1e3, 2)}
                                       for v, t in per_val.items()}}), flush=True)
         os.environ[ab_name] = ab_vals[0]
+    sib_ms = []
+    if sib is not None:
+        for _ in range(args.steps):
+            torch.cuda.synchronize()
+            sib.go()
+            t0 = time.perf_counter()
+            take()
+            contended.append(time.perf_counter() - t0)
+            sib_ms.append(max(sib.wait()) * 1e3)
+        sib.stop()
     unblock, total = [], []
     for _ in range(args.async_iters):
         torch.cuda.synchronize()
@@ -157,9 +189,90 @@ def main() -> None:
         "async_total_ms_median": round(statistics.median(total) * 1e3, 2),
         "restore_ms_median": round(statistics.median(rtimes) * 1e3, 2),
         "restore_bitwise_ok": ok,
+        **({"host_siblings": args.host_siblings, "sibling_dma_pass": bool(args.sibling_dma_pass),
+            "sibling_bytes_each": sum(sib.sizes),
+            "contended_take_ms_median": round(statistics.median(contended) * 1e3, 2),
+            "contended_take_ms_each": [round(t * 1e3, 1) for t in contended],
+            "sibling_host_ms_median": round(statistics.median(sib_ms), 2),
+            "contended_vs_solo": round(statistics.median(contended) / med, 3),
+            "contended_aggregate_GBps": round(
+                args.world * share / max(statistics.median(contended),
+                                         statistics.median(sib_ms) / 1e3) / 1e9, 1)}
+           if sib is not None else {}),
     }), flush=True)
     shutil.rmtree(root, ignore_errors=True)
     dist.destroy_process_group()
+
+
+def _sibling_main(i: int, sizes, root: str, dma_pass: bool, go, done) -> None:
+    """One sibling rank's host work per take (no GPU): a write pass over its
+    staging memory (the D2H DMA's DRAM writes), then every blob through the
+    native FS engine."""
+    import asyncio
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__)))))
+    from hipsnapshot.io_types import WriteIO
+    from hipsnapshot.storage.fs import FSStoragePlugin
+
+    buf = np.ones(max(sizes), dtype=np.uint8)  # touched: resident like the pinned pool
+    staging = np.empty(sum(sizes), dtype=np.uint8)
+    staging[:] = 1
+    d = os.path.join(root, f"sibling{i}")
+    os.makedirs(d, exist_ok=True)
+    loop = asyncio.new_event_loop()
+    fs = FSStoragePlugin(d)
+
+    async def write_all():
+        from hipsnapshot import knobs
+
+        sem = asyncio.Semaphore(knobs.get_io_threads())
+
+        async def one(j, n):
+            async with sem:
+                src = staging[sum(sizes[:j]): sum(sizes[:j]) + n] if dma_pass else buf[:n]
+                await fs.write(WriteIO(path=f"b{j}", buf=memoryview(src)))
+
+        await asyncio.gather(*(one(j, n) for j, n in enumerate(sizes)))
+
+    while go.get() is not None:
+        t0 = time.perf_counter()
+        if dma_pass:
+            staging.fill(2)
+        loop.run_until_complete(write_all())
+        done.put(time.perf_counter() - t0)
+    fs.sync_close(loop)
+    loop.close()
+
+
+class _Siblings:
+    def __init__(self, k: int, sizes, root: str, dma_pass: bool) -> None:
+        import multiprocessing as mp
+
+        ctx = mp.get_context("spawn")
+        self.sizes = sizes
+        self.go_qs = [ctx.Queue() for _ in range(k)]
+        self.done = ctx.Queue()
+        self.procs = [ctx.Process(target=_sibling_main,
+                                  args=(i, sizes, root, dma_pass, self.go_qs[i], self.done))
+                      for i in range(k)]
+        for p in self.procs:
+            p.start()
+
+    def go(self) -> None:
+        for q in self.go_qs:
+            q.put(1)
+
+    def wait(self):
+        return [self.done.get(timeout=120) for _ in self.procs]
+
+    def stop(self) -> None:
+        for q in self.go_qs:
+            q.put(None)
+        for p in self.procs:
+            p.join(30)
 
 
 if __name__ == "__main__":

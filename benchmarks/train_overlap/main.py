@@ -51,9 +51,13 @@ def main() -> None:
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=1)
-    ap.add_argument("--baseline-steps", type=int, default=5)
+    ap.add_argument("--baseline-steps", type=int, default=10)
     ap.add_argument("--window-steps", type=int, default=12,
                     help="train_time_lost_ms covers at least this many steps after async_take")
+    ap.add_argument("--checkpoints", type=int, default=1,
+                    help="async_takes back to back (each starts when the previous one has "
+                         "committed) inside ONE measured window: enough steps overlap a "
+                         "drain to rank changes; train_time_lost_ms is per checkpoint")
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
     ap.add_argument("--storage", default="fs", choices=["fs", "s3"])
     ap.add_argument("--path", default=None)
@@ -122,9 +126,9 @@ def main() -> None:
     srv = None
     opts = None
     if args.storage == "s3":
-        from hipsnapshot.storage.fake_servers import FakeS3Server
+        from hipsnapshot.storage.fake_servers import FakeS3Process
 
-        srv = FakeS3Server() if rank == 0 else None
+        srv = FakeS3Process() if rank == 0 else None
         url = [srv.url if srv else None]
         dist.broadcast_object_list(url, src=0)
         opts = {"aws_access_key_id": "AKIDFAKE", "aws_secret_access_key": "fake-secret",
@@ -137,42 +141,76 @@ def main() -> None:
             shutil.rmtree(root, ignore_errors=True)
     app = {"model": model, "optim": opt}
 
-    # blocking take (reference semantics) for comparison
+    # blocking take (reference semantics) for comparison: median of 3, the
+    # first one also builds the take plan
     log("phase: sync take")
-    sync(dev)
-    t0 = time.perf_counter()
-    Snapshot.take(f"{root}/sync", app, storage_options=opts, compression=args.compression)
-    sync_s = max_over_ranks(time.perf_counter() - t0, dev)
+    sync_each = []
+    for _ in range(3):
+        sync(dev)
+        t0 = time.perf_counter()
+        Snapshot.take(f"{root}/sync", app, storage_options=opts, compression=args.compression)
+        sync_each.append(max_over_ranks(time.perf_counter() - t0, dev))
+    sync_s = statistics.median(sync_each)
     if args.storage == "fs" and rank == 0:
         shutil.rmtree(f"{root}/sync", ignore_errors=True)  # keep the disk footprint to one copy
 
-    # async take while training continues
-    log(f"phase: async take (sync take {sync_s:.3f} s)")
+    # async takes while training continues: --checkpoints of them back to
+    # back, each starting at the first step boundary after the previous one
+    # committed (same path: a rewrite, as a ring of checkpoints would do)
+    log(f"phase: async take x{args.checkpoints} (sync take {sync_s:.3f} s)")
     sync(dev)
-    ref = {n: _local(p).detach().clone() for n, p in model.named_parameters()}
+    k_total = max(1, args.checkpoints)
+    pending, taken, t_ck = None, 0, 0.0
+    during, unblocks, drains = [], [], []
+    ref, clone_s = None, 0.0
+    def all_done(p) -> bool:
+        """``p.done()`` agreed across ranks (a step runs FSDP collectives:
+        every rank must run the same number of them)."""
+        d = p is None or p.done()
+        if ws == 1:
+            return d
+        f = torch.tensor([int(d)], device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        return bool(f.item())
+
     t0 = time.perf_counter()
-    pending = Snapshot.async_take(f"{root}/async", app, storage_options=opts,
-                                  compression=args.compression)
-    unblock = time.perf_counter() - t0
-    during = []
-    while not pending.done():
+    while True:
+        if all_done(pending):
+            if pending is not None:
+                pending.wait()
+                drains.append(time.perf_counter() - t_ck)
+            if taken == k_total:
+                break
+            if taken == k_total - 1:  # the restore check compares with this state
+                tc = time.perf_counter()
+                ref = {n: _local(p).detach().clone() for n, p in model.named_parameters()}
+                torch.cuda.current_stream(dev).synchronize() if dev.type == "cuda" else None
+                clone_s = time.perf_counter() - tc
+            t_ck = time.perf_counter()
+            pending = Snapshot.async_take(f"{root}/async", app, storage_options=opts,
+                                          compression=args.compression)
+            unblocks.append(time.perf_counter() - t_ck)
+            taken += 1
         during.append(step())
-    pending.wait()
-    drain = time.perf_counter() - t0
-    # training time lost to the checkpoint: wall time from the async_take call
-    # through a window of at least --window-steps steps (the unblock and every
-    # step slowed by the drain inside it) minus the same steps at baseline
+    drain = statistics.mean(drains)
+    unblock = statistics.median(unblocks)
+    # training time lost to the checkpoints: wall time from the first
+    # async_take call through a window of at least --window-steps steps (the
+    # unblocks and every step slowed by a drain inside it) minus the same
+    # steps at baseline, per checkpoint (the reference clone is not counted)
     extra = 0
     while len(during) + extra < args.window_steps:
         step()
         extra += 1
-    lost = (time.perf_counter() - t0) - (len(during) + extra) * base_ms / 1e3
+    lost = ((time.perf_counter() - t0) - clone_s
+            - (len(during) + extra) * base_ms / 1e3) / k_total
     # every rank must finish its loop before collectives resume
     unblock = max_over_ranks(unblock, dev)
     drain = max_over_ranks(drain, dev)
     n_during = int(max_over_ranks(float(len(during)), dev))
     lost = max_over_ranks(lost, dev)
     mean_ms = max_over_ranks(statistics.mean(during) if during else 0.0, dev) * 1e3
+    med_ms = max_over_ranks(statistics.median(during) if during else 0.0, dev) * 1e3
     max_ms = max_over_ranks(max(during) if during else 0.0, dev) * 1e3
 
     log(f"phase: restore (unblock {unblock * 1e3:.1f} ms, {len(during)} steps during drain)")
@@ -195,10 +233,14 @@ def main() -> None:
           "baseline_step_ms": round(base_ms, 2), "sync_take_s": round(sync_s, 3),
           "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 2), "async_drain_s": round(drain, 3),
+          "checkpoints": k_total, "async_unblock_ms_each": [round(u * 1e3, 2) for u in unblocks],
+          "async_drain_s_each": [round(d, 3) for d in drains],
           "steps_during_drain": n_during, "step_ms_during_drain_mean": round(mean_ms, 2),
+          "step_ms_during_drain_median": round(med_ms, 2),
           "step_ms_during_drain_max": round(max_ms, 2),
           "slowdown_during_drain": round(mean_ms / base_ms - 1.0, 4) if during else None,
           "window_steps": len(during) + extra, "train_time_lost_ms": round(lost * 1e3, 1),
+          "train_time_lost_vs_sync_take": round(lost / sync_s, 3),
           "restore_bitwise_ok": bool(okt.item()), "stored_bytes": stored,
           "data": "synthetic tokens, random init"})
     sync(dev)
