@@ -1,0 +1,348 @@
+// hsdrain: native drain of an async_take's frozen HBM arena to local files.
+//
+// After `Snapshot.async_take` froze the device state into one HBM arena
+// (engine/hbm_staging.py lays every blob out contiguously there, slab members
+// at their slab offsets with zeroed gaps), the background commit has to move
+// each blob arena -> host -> file.  Driven from Python, that took ~1 ms of
+// interpreter work per blob on staging threads that contend for the GIL with
+// the training loop, and a training step slowed by +68 % while a drain ran
+// (profiles/overlap/session4).  Here the whole drain is ONE call:
+//
+//   dma thread     per blob: one narrow-grid hs64 hash launch (hs_hash64 on
+//                  its own stream, beside the copies); per chunk of the blob
+//                  (<= slot size): take a free pinned slot, submit the SDMA
+//                  device->host copy (ROCr copy engine, no CUs), queue it;
+//   wait thread    waits the copies in submission order, hands chunks to
+//                  the writers;
+//   writers        pwrite() chunks at their file offsets (page cache), return
+//                  slots; the last chunk of a blob trims the file to size,
+//                  optionally fdatasync()s it and closes it.
+//
+// No Python runs until the caller collects the result: the trainer keeps the
+// GIL and the GPU's compute units (copies run on the SDMA engines, the hash on
+// a few workgroups).  Reference behaviour being replaced:
+// `/root/reference/torchsnapshot/scheduler.py:194-217` (drain of pending
+// writes) and `storage_plugins/fs.py:34-36` (file writes).
+
+#include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+extern "C" {
+int hsg_sdma_d2h_submit(int dev, void* dst, const void* src, uint64_t n, void* stream,
+                        uint64_t* handle);
+int hsg_sdma_wait(uint64_t handle);
+void* hsg_copy_stream(int dev, int slot);
+int hsg_hash64(int dev, int slot, int after_slot, const void* p, uint64_t n,
+               uint64_t first_word, int max_grid, int* handle);
+int hsg_hash64_result(int dev, int slot, int handle, uint64_t* out);
+void* hsg_pinned_acquire(uint64_t nbytes);
+int hsg_pinned_release(void* p);
+}
+
+namespace {
+
+constexpr int kDrainCopySlot = 1000;  // idle stream the SDMA submits order after
+constexpr int kDrainHashSlot = 1001;
+constexpr int kHashLag = 256;         // results collected this many blobs behind
+constexpr int kFlagSync = 1;
+constexpr int kFlagHash = 2;
+
+int mkdirs(const std::string& path) {
+  // parent directories of `path`
+  for (size_t i = 1; i < path.size(); ++i) {
+    if (path[i] != '/') continue;
+    std::string d = path.substr(0, i);
+    if (mkdir(d.c_str(), 0755) != 0 && errno != EEXIST) return -errno;
+  }
+  return 0;
+}
+
+struct Blob {
+  uint64_t src;
+  uint64_t nbytes;
+  std::string path;
+  int fd = -1;
+  std::atomic<int> chunks_left{0};
+  uint64_t sum = 0;
+  int hash_handle = -1;
+};
+
+struct Chunk {
+  int blob;
+  uint64_t off;
+  uint64_t n;
+  int slot;
+  uint64_t handle;
+};
+
+struct Job {
+  int dev;
+  int flags;
+  int max_hash_grid;
+  uint64_t slot_bytes;
+  std::vector<Blob> blobs;
+  std::vector<void*> slots;
+
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<int> free_slots;
+  std::deque<Chunk> inflight;   // submitted copies, in order
+  std::deque<Chunk> to_write;
+  bool submit_done = false;
+  bool wait_done = false;
+  std::atomic<int> err{0};
+  char errmsg[256] = {0};
+  std::atomic<uint64_t> bytes_written{0};
+  std::atomic<int> blobs_left{0};
+
+  std::vector<std::thread> threads;
+  bool finished = false;
+
+  void fail(int code, const char* what, const std::string& path) {
+    int expected = 0;
+    if (err.compare_exchange_strong(expected, code)) {
+      std::lock_guard<std::mutex> g(mu);
+      snprintf(errmsg, sizeof(errmsg), "%s %s: %s", what, path.c_str(),
+               code < 0 ? strerror(-code) : "error");
+    }
+    cv.notify_all();
+  }
+};
+
+void close_blob(Job* j, Blob& b) {
+  if (b.fd < 0) return;
+  struct stat st;
+  if (fstat(b.fd, &st) == 0 && uint64_t(st.st_size) != b.nbytes) {
+    if (ftruncate(b.fd, off_t(b.nbytes)) != 0) j->fail(-errno, "ftruncate", b.path);
+  }
+  if ((j->flags & kFlagSync) && fdatasync(b.fd) != 0) j->fail(-errno, "fdatasync", b.path);
+  close(b.fd);
+  b.fd = -1;
+}
+
+void dma_thread(Job* j) {
+  void* stream = hsg_copy_stream(j->dev, kDrainCopySlot);
+  int hashed = 0, collected = 0;
+  const int nb = static_cast<int>(j->blobs.size());
+  auto collect = [&](int upto) {
+    for (; collected < upto && collected < hashed; ++collected) {
+      Blob& b = j->blobs[collected];
+      if (b.hash_handle < 0) continue;
+      if (hsg_hash64_result(j->dev, kDrainHashSlot, b.hash_handle, &b.sum) != 0)
+        j->fail(-EIO, "hash result", b.path);
+    }
+  };
+  for (int i = 0; i < nb && !j->err.load(); ++i) {
+    Blob& b = j->blobs[i];
+    int r = mkdirs(b.path);
+    if (r == 0) {
+      b.fd = open(b.path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+      if (b.fd < 0) r = -errno;
+    }
+    if (r != 0) {
+      j->fail(r, "open", b.path);
+      break;
+    }
+    if (j->flags & kFlagHash) {
+      if (hsg_hash64(j->dev, kDrainHashSlot, -1, reinterpret_cast<const void*>(b.src),
+                     b.nbytes, 0, j->max_hash_grid, &b.hash_handle) != 0) {
+        j->fail(-EIO, "hash launch", b.path);
+        break;
+      }
+    }
+    hashed = i + 1;
+    collect(hashed - kHashLag);
+    const uint64_t nchunks = b.nbytes ? (b.nbytes + j->slot_bytes - 1) / j->slot_bytes : 0;
+    b.chunks_left.store(static_cast<int>(nchunks));
+    if (nchunks == 0) {
+      close_blob(j, b);
+      j->blobs_left.fetch_sub(1);
+      continue;
+    }
+    for (uint64_t c = 0; c < nchunks && !j->err.load(); ++c) {
+      int slot;
+      {
+        std::unique_lock<std::mutex> lk(j->mu);
+        j->cv.wait(lk, [&] { return !j->free_slots.empty() || j->err.load(); });
+        if (j->err.load()) break;
+        slot = j->free_slots.back();
+        j->free_slots.pop_back();
+      }
+      const uint64_t off = c * j->slot_bytes;
+      const uint64_t n = std::min(j->slot_bytes, b.nbytes - off);
+      uint64_t h = 0;
+      r = hsg_sdma_d2h_submit(j->dev, j->slots[slot], reinterpret_cast<const void*>(b.src + off),
+                              n, stream, &h);
+      if (r != 0) {
+        j->fail(-EIO, "sdma submit", b.path);
+        break;
+      }
+      {
+        std::lock_guard<std::mutex> g(j->mu);
+        j->inflight.push_back(Chunk{i, off, n, slot, h});
+      }
+      j->cv.notify_all();
+    }
+  }
+  collect(hashed);
+  {
+    std::lock_guard<std::mutex> g(j->mu);
+    j->submit_done = true;
+  }
+  j->cv.notify_all();
+}
+
+void wait_thread(Job* j) {
+  for (;;) {
+    Chunk c;
+    {
+      std::unique_lock<std::mutex> lk(j->mu);
+      j->cv.wait(lk, [&] { return !j->inflight.empty() || j->submit_done; });
+      if (j->inflight.empty()) break;
+      c = j->inflight.front();
+      j->inflight.pop_front();
+    }
+    // every submitted copy is waited for, even after an error: the engine
+    // must be done with a slot before it is reused or freed
+    if (hsg_sdma_wait(c.handle) != 0) j->fail(-EIO, "sdma copy", j->blobs[c.blob].path);
+    {
+      std::lock_guard<std::mutex> g(j->mu);
+      j->to_write.push_back(c);
+    }
+    j->cv.notify_all();
+  }
+  {
+    std::lock_guard<std::mutex> g(j->mu);
+    j->wait_done = true;
+  }
+  j->cv.notify_all();
+}
+
+void writer_thread(Job* j) {
+  for (;;) {
+    Chunk c;
+    {
+      std::unique_lock<std::mutex> lk(j->mu);
+      j->cv.wait(lk, [&] { return !j->to_write.empty() || j->wait_done; });
+      if (j->to_write.empty()) break;
+      c = j->to_write.front();
+      j->to_write.pop_front();
+    }
+    Blob& b = j->blobs[c.blob];
+    if (!j->err.load()) {
+      const char* p = static_cast<const char*>(j->slots[c.slot]);
+      uint64_t done = 0;
+      while (done < c.n) {
+        const ssize_t w = pwrite(b.fd, p + done, c.n - done, off_t(c.off + done));
+        if (w < 0) {
+          if (errno == EINTR) continue;
+          j->fail(-errno, "pwrite", b.path);
+          break;
+        }
+        done += uint64_t(w);
+      }
+      j->bytes_written.fetch_add(done);
+    }
+    {
+      std::lock_guard<std::mutex> g(j->mu);
+      j->free_slots.push_back(c.slot);
+    }
+    j->cv.notify_all();
+    if (b.chunks_left.fetch_sub(1) == 1) {
+      close_blob(j, b);
+      j->blobs_left.fetch_sub(1);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Start draining `n` blobs: blob i is device bytes [srcs[i], srcs[i] +
+// sizes[i]) -> file paths[i] (created with parent directories, overwritten
+// in place, trimmed to size).  `nslots` pinned slots of `slot_bytes` move
+// the data; `nwriters` threads write it.  flags: 1 = fdatasync every file,
+// 2 = hs64 hash every blob on the GPU (narrow grid `max_hash_grid`).
+// Returns a handle (> 0) for hsg_drain_wait, or 0 with *err set.
+void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* sizes,
+                      const char* const* paths, uint64_t slot_bytes, int nslots, int nwriters,
+                      int flags, int max_hash_grid, int* err) {
+  *err = 0;
+  if (hipSetDevice(dev) != hipSuccess) {
+    *err = -1;
+    return nullptr;
+  }
+  Job* j = new Job();
+  j->dev = dev;
+  j->flags = flags;
+  j->max_hash_grid = max_hash_grid;
+  j->slot_bytes = std::max<uint64_t>(slot_bytes, 1 << 20);
+  j->blobs = std::vector<Blob>(n);
+  for (int i = 0; i < n; ++i) {
+    j->blobs[i].src = srcs[i];
+    j->blobs[i].nbytes = sizes[i];
+    j->blobs[i].path = paths[i];
+  }
+  j->blobs_left.store(n);
+  nslots = std::max(nslots, 2);
+  for (int s = 0; s < nslots; ++s) {
+    void* p = hsg_pinned_acquire(j->slot_bytes);
+    if (!p) {
+      for (void* q : j->slots) hsg_pinned_release(q);
+      delete j;
+      *err = -2;
+      return nullptr;
+    }
+    j->slots.push_back(p);
+    j->free_slots.push_back(s);
+  }
+  j->threads.emplace_back(dma_thread, j);
+  j->threads.emplace_back(wait_thread, j);
+  for (int w = 0; w < std::max(nwriters, 1); ++w) j->threads.emplace_back(writer_thread, j);
+  return j;
+}
+
+// Wait for the drain (blocking; Python calls it without the GIL).  Returns 0
+// or the first error (negative errno); `sums` (n entries, may be null)
+// receives each blob's hs64 partial sum; `msg` (>= 256 bytes, may be null)
+// the error text.  Frees the job: call exactly once per handle.
+int hsg_drain_wait(void* handle, uint64_t* sums, uint64_t* bytes_written, char* msg) {
+  Job* j = static_cast<Job*>(handle);
+  for (auto& t : j->threads) t.join();
+  for (auto& b : j->blobs)
+    if (b.fd >= 0) close(b.fd);
+  for (void* p : j->slots) hsg_pinned_release(p);
+  const int e = j->err.load();
+  if (sums)
+    for (size_t i = 0; i < j->blobs.size(); ++i) sums[i] = j->blobs[i].sum;
+  if (bytes_written) *bytes_written = j->bytes_written.load();
+  if (msg) snprintf(msg, 256, "%s", j->errmsg);
+  delete j;
+  return e;
+}
+
+// Non-blocking progress: blobs not yet on storage (-1: bad handle).
+int hsg_drain_pending(void* handle) {
+  Job* j = static_cast<Job*>(handle);
+  return j ? j->blobs_left.load() : -1;
+}
+
+}  // extern "C"

@@ -17,6 +17,12 @@ copy bandwidth, so instead:
    built lazily by the drain) and wait on an event recorded after the launch;
    the background commit thread drains the arena to storage.
 
+The arena holds every blob exactly as it will be stored (``frozen_region``
+= (arena, offset, bytes) on the write request's stager): a tensor's C-order
+bytes, or a device slab with its members at their slab offsets and the gaps
+zero-filled by the same launch.  Raw blobs can then go arena -> file with no
+gather, through the native drain (``engine/native_drain.py``).
+
 When the whole state does not fit in free HBM minus
 ``HBM_STAGING_RESERVE_BYTES`` (or ``HBM_STAGING_MAX_BYTES``), write requests are
 frozen greedily in plan order until the arena is full and the rest takes the
@@ -28,7 +34,7 @@ from __future__ import annotations
 
 import logging
 from collections import defaultdict
-from typing import Dict, List
+from typing import Dict, List, Tuple
 
 import torch
 
@@ -71,18 +77,46 @@ def _nbytes(st) -> int:
     return (nb + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
+def _region(wr: WriteReq, sts) -> Tuple[int, List[int], int]:
+    """(arena bytes, member offsets in the region, blob bytes) of one write
+    request.  The region holds the blob exactly as it goes to storage: a
+    tensor's C-order bytes, or a device slab with every member at its slab
+    offset (the gaps are zero-filled by the freeze)."""
+    from ..io.batcher import GPUBatchedBufferStager
+
+    st = wr.buffer_stager
+    if isinstance(st, GPUBatchedBufferStager):
+        offs = [lo for (lo, _hi), _m in st.members]
+        return (st.total + _ALIGN - 1) // _ALIGN * _ALIGN, offs, st.total
+    t = sts[0].tensor
+    return _nbytes(sts[0]), [0], t.numel() * t.element_size()
+
+
+_zero_pages: Dict[int, torch.Tensor] = {}
+
+
+def _zeros(dev: int) -> torch.Tensor:
+    z = _zero_pages.get(dev)
+    if z is None:
+        z = _zero_pages[dev] = torch.zeros(4096, dtype=torch.uint8, device=f"cuda:{dev}")
+    return z
+
+
 def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
     """Returns {device: arena_bytes} for the devices that were (partly) frozen."""
     if not native.gpu_available():
         return {}
-    by_dev = defaultdict(list)  # device -> [(request bytes, stagers)]
+    by_dev = defaultdict(list)  # device -> [(region bytes, member offsets, blob bytes, wr, sts)]
     for wr in write_reqs:
+        # a previous take's region (reused plan) never carries over
+        wr.buffer_stager.__dict__.pop("frozen_region", None)
+        wr.buffer_stager.__dict__.pop("frozen_event", None)
         sts = _cuda_sources(wr)
         if not sts:
             continue
         t = sts[0].tensor
         dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
-        by_dev[dev].append((sum(_nbytes(st) for st in sts), sts))
+        by_dev[dev].append((*_region(wr, sts), wr, sts))
     frozen = {}
     cap = knobs.hbm_staging_max_bytes()
     for dev, reqs in by_dev.items():
@@ -92,24 +126,20 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
         # fresh allocation does not fit) -- a trainer's cache is often tens of GB
         cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
         room = min(free + max(cached, 0) - knobs.hbm_staging_reserve_bytes(), cap)
-        want = sum(nb for nb, _ in reqs)
-        sts, total = [], 0
-        for nb, req_sts in reqs:
-            if total + nb <= room:
-                sts.extend(req_sts)
-                total += nb
-        if not sts:
+        want = sum(r[0] for r in reqs)
+        chosen, total = [], 0
+        for r in reqs:
+            if total + r[0] <= room:
+                chosen.append(r)
+                total += r[0]
+        if not chosen:
             logger.info(f"HBM staging skipped on cuda:{dev}: need {want} B, room {room} B")
             continue
         if total < want:
             logger.info(f"HBM staging on cuda:{dev}: {total} of {want} B frozen, the rest "
                         "is staged to host before async_take returns")
-        offs, off = [], 0
-        for st in sts:
-            offs.append(off)
-            off += _nbytes(st)
         try:
-            _freeze(dev, sts, offs, total)
+            _freeze(dev, chosen, total)
         except torch.cuda.OutOfMemoryError:
             # fragmentation: the estimate above was optimistic -> host path
             logger.info(f"HBM staging on cuda:{dev}: arena of {total} B not allocatable")
@@ -118,7 +148,7 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
     return frozen
 
 
-def _freeze(dev: int, sts, offs, total: int) -> None:
+def _freeze(dev: int, chosen, total: int) -> None:
     _retire_launches()
     stream = torch.cuda.current_stream(dev)
     with torch.cuda.device(dev):
@@ -126,31 +156,44 @@ def _freeze(dev: int, sts, offs, total: int) -> None:
             arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
         batch = native.CopyBatch()
         base = arena.data_ptr()
-        for st, off in zip(sts, offs):
-            t = st.tensor.detach()
-            if t.numel():
-                batch.add_tensor(t, base + off)
+        zero = _zeros(dev).data_ptr()
+        placed = []  # (stager, arena offset)
+        off = 0
+        for region, moffs, blob, wr, sts in chosen:
+            end = 0
+            for st, mo in zip(sts, moffs):
+                if mo > end:  # slab gap: zeros, as the slab gather writes them
+                    batch.add_bytes(zero, base + off + end, mo - end)
+                t = st.tensor.detach()
+                if t.numel():
+                    batch.add_tensor(t, base + off + mo)
+                placed.append((st, off + mo))
+                end = mo + t.numel() * t.element_size()
+            wr.buffer_stager.frozen_region = (arena, off, blob)
+            off += region
+        sts_all = [st for st, _ in placed]
         # producers may differ from the current stream: order after them
-        for p in {st.producer for st in sts if st.producer is not None}:
+        for p in {st.producer for st in sts_all if st.producer is not None}:
             if p != stream.cuda_stream:
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.default_stream(dev) if p == 0
                           else torch.cuda.ExternalStream(p))
                 stream.wait_event(ev)
-        with timeline.span("freeze_launch", n=len(sts)):
+        with timeline.span("freeze_launch", n=len(sts_all)):
             keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
         done = torch.cuda.Event()
         done.record(stream)
     _live_launches.append((keep, done))
-    for st, off in zip(sts, offs):
-        st.frozen_at = (arena, off)  # _source() views the arena from now on
+    done_keep = (keep, done)
+    for st, o in placed:
+        st.frozen_at = (arena, o)  # _source() views the arena from now on
         st.producer = None  # ordering is carried by wait_event
         st.frozen = True
         st.wait_event = done
-    # keep the descriptor tables alive until the copy ran
-    done_keep = (keep, done)
-    for st in sts:
+        # keep the descriptor tables alive until the copy ran
         st.arena_keepalive = done_keep
+    for _r, _m, _b, wr, _s in chosen:
+        wr.buffer_stager.frozen_event = done
 
 
 def is_deferrable(wr: WriteReq) -> bool:

@@ -1,0 +1,94 @@
+"""Native drain of an async take's frozen HBM arena to the local FS.
+
+``DeferredIOWork`` (engine/scheduler.py) hands every eligible deferred write
+to ONE ``native.NativeDrain`` call (csrc/hsdrain.hip): SDMA copies arena ->
+pinned slots -> ``pwrite``, per-blob hs64 hashes on the GPU, optional
+fdatasync -- in native threads, so the training loop keeps the GIL and the
+compute units while a checkpoint drains.  Eligible: a raw blob (no HSZ1
+codec, buffer-protocol serializer) whose bytes sit contiguously in the arena
+(``frozen_region``, engine/hbm_staging.py), written by the FS plugin without
+O_DIRECT.  Everything else drains through the Python pipeline as before.
+
+Reference counterpart: `/root/reference/torchsnapshot/snapshot.py:891-933`
+(the commit thread draining pending storage I/O) and
+`/root/reference/torchsnapshot/scheduler.py:194-217`.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import time
+from typing import Dict, List, Tuple
+
+from .. import knobs
+from ..io_types import StoragePlugin, WriteReq
+from ..ops import checksum, native
+from ..utils.tracing import timeline
+
+logger = logging.getLogger(__name__)
+
+
+def _root(storage: StoragePlugin):
+    fn = getattr(storage, "native_drain_root", None)
+    return fn() if fn is not None else None
+
+
+def eligible(wr: WriteReq, storage: StoragePlugin) -> bool:
+    from ..format.serialization import Serializer
+    from ..io.batcher import GPUBatchedBufferStager
+    from ..io.tensor import TensorBufferStager
+
+    st = wr.buffer_stager
+    if getattr(st, "frozen_region", None) is None or getattr(st, "codec", None) is not None:
+        return False
+    if isinstance(st, TensorBufferStager):
+        if st.entry.serializer != Serializer.BUFFER_PROTOCOL.value or \
+                st._tensor_prepare_func is not None:
+            return False
+    elif not isinstance(st, GPUBatchedBufferStager):
+        return False
+    return _root(storage) is not None
+
+
+def split(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[List[WriteReq], List[WriteReq]]:
+    """(native, python) parts of an async take's deferred writes."""
+    if not knobs.native_drain_enabled() or not native.gpu_available() or _root(storage) is None:
+        return [], list(reqs)
+    nat, py = [], []
+    for wr in reqs:
+        (nat if eligible(wr, storage) else py).append(wr)
+    return nat, py
+
+
+def drain(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[Dict[str, int], int]:
+    """Write every request's frozen region to its file; returns ({blob path:
+    hs64}, bytes written).  Blocks (call it off the event loop)."""
+    root, fsync = _root(storage)
+    by_dev: Dict[int, List[WriteReq]] = {}
+    for wr in reqs:
+        arena = wr.buffer_stager.frozen_region[0]
+        by_dev.setdefault(arena.device.index or 0, []).append(wr)
+    sums: Dict[str, int] = {}
+    total = 0
+    want_sums = knobs.checksum_enabled()
+    for dev, wrs in by_dev.items():
+        t0 = time.perf_counter()
+        # the freeze copy must have landed before the engines read the arena
+        for ev in {id(wr.buffer_stager.frozen_event): wr.buffer_stager.frozen_event
+                   for wr in wrs}.values():
+            ev.synchronize()
+        blobs = []
+        for wr in wrs:
+            arena, off, nbytes = wr.buffer_stager.frozen_region
+            blobs.append((arena.data_ptr() + off, nbytes, os.path.join(root, wr.path)))
+        job = native.NativeDrain(dev, blobs, knobs.get_drain_slot_bytes(),
+                                 knobs.get_drain_slots(), knobs.get_drain_writers(), fsync,
+                                 want_sums, knobs.get_hash_grid())
+        partial, written = job.wait()
+        total += written
+        if want_sums:
+            for wr, (_p, n, _path), s in zip(wrs, blobs, partial):
+                sums[wr.path] = checksum.finish(s, n)
+        timeline.add("native_drain", "io", t0, time.perf_counter(), n=len(wrs), bytes=written)
+    return sums, total

@@ -28,7 +28,7 @@ import threading
 import time
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
-from typing import Dict, List, Optional
+from typing import Any, Dict, List, Optional
 
 import psutil
 
@@ -494,17 +494,37 @@ class DeferredIOWork:
         self._second: Optional[PendingIOWork] = None
 
     async def complete(self) -> None:
+        from . import native_drain
+
+        native_reqs, py_reqs = native_drain.split(self.deferred, self.storage)
+        native_out: Dict[str, Any] = {}
+
         async def run_deferred() -> None:
-            p = await execute_write_reqs(self.deferred, self.storage, self.budget, self.rank,
+            if not py_reqs:
+                return
+            p = await execute_write_reqs(py_reqs, self.storage, self.budget, self.rank,
                                          gate=self.first.gate, background=True)
             self._second = p
             await p.complete()
 
-        res = await asyncio.gather(self.first.complete(), run_deferred(), return_exceptions=True)
+        async def run_native() -> None:
+            # one native call for every raw frozen blob: no Python (and no
+            # GIL) between the arena and the files while the trainer runs
+            if native_reqs:
+                native_out["sums"], native_out["bytes"] = \
+                    await asyncio.get_running_loop().run_in_executor(
+                        aux_pool(), native_drain.drain, native_reqs, self.storage)
+
+        res = await asyncio.gather(self.first.complete(), run_deferred(), run_native(),
+                                   return_exceptions=True)
         if self._second is not None:
             self.stats.bytes_written += self._second.stats.bytes_written
             self.stats.n_reqs += self._second.stats.n_reqs
             self.stats.checksums.update(self._second.stats.checksums)
+        if "bytes" in native_out:
+            self.stats.bytes_written += native_out["bytes"]
+            self.stats.n_reqs += len(native_reqs)
+            self.stats.checksums.update(native_out["sums"])
         self.stats.t_done = time.monotonic()
         for r in res:
             if isinstance(r, BaseException):

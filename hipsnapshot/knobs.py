@@ -255,6 +255,36 @@ def get_state_dict_barriers() -> str:
     return {"1": "always", "true": "always", "0": "never", "false": "never"}.get(v, v)
 
 
+def native_drain_enabled() -> bool:
+    """Drain an async take's raw frozen blobs to the local FS in native
+    threads (engine/native_drain.py, csrc/hsdrain.hip)."""
+    return _get_bool("NATIVE_DRAIN", True)
+
+
+def get_drain_slot_bytes() -> int:
+    return max(1 << 20, _get_int("DRAIN_SLOT_BYTES", 32 << 20))
+
+
+def get_drain_slots() -> int:
+    """Pinned slots the native drain cycles through (slots x slot bytes of
+    pinned host memory while a drain runs, outside the memory budget)."""
+    return max(2, _get_int("DRAIN_SLOTS", 12))
+
+
+def get_drain_writers() -> int:
+    return max(1, _get_int("DRAIN_WRITERS", min(8, get_io_threads())))
+
+
+def async_device_codec() -> str:
+    """What an ``async_take`` with ``compression="hsz1"`` does with the device
+    state it froze in HBM: ``raw`` (default) drains it uncompressed -- the
+    encoder kernels would compete with the training step for the compute
+    units (+30 % step time while they run, profiles/overlap_iso/) -- or
+    ``same`` encodes it like a blocking take."""
+    v = str(_get("ASYNC_DEVICE_CODEC") or "raw").lower()
+    return v if v in ("raw", "same") else "raw"
+
+
 def plan_cache_enabled() -> bool:
     """Reuse a take's plan for the next take of the same device-resident
     tensors (``engine/plan_cache.py``)."""

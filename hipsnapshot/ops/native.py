@@ -16,6 +16,7 @@ runtime resolved for our library is the one torch already loaded (same SONAME
 from __future__ import annotations
 
 import ctypes
+import errno
 import logging
 import os
 import threading
@@ -259,6 +260,13 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p])
         _declare(lib, "hsg_mx8_dequantize", c_int,
                  [c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p])
+        _declare(lib, "hsg_drain_start", c_void_p,
+                 [c_int, c_int, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64),
+                  ctypes.POINTER(c_char_p), c_uint64, c_int, c_int, c_int, c_int,
+                  ctypes.POINTER(c_int)])
+        _declare(lib, "hsg_drain_wait", c_int,
+                 [c_void_p, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64), c_char_p])
+        _declare(lib, "hsg_drain_pending", c_int, [c_void_p])
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
@@ -711,6 +719,47 @@ def mx8_dequantize(dev: int, q: torch.Tensor, scales: torch.Tensor, dst: torch.T
     assert q.numel() >= n and scales.numel() >= (n + 31) // 32
     _check(lib.hsg_mx8_dequantize(dev, q.data_ptr(), scales.data_ptr(), n, dst.data_ptr(),
                                   dtype_code(dst.dtype), stream_handle), "hsg_mx8_dequantize")
+
+
+class NativeDrain:
+    """``hsg_drain_start`` / ``hsg_drain_wait`` (csrc/hsdrain.hip): device
+    byte ranges -> files, entirely in native threads (SDMA copies through
+    pinned slots, pwrite, optional fdatasync and GPU hs64 hashing)."""
+
+    def __init__(self, dev: int, blobs: Sequence[Tuple[int, int, str]], slot_bytes: int,
+                 nslots: int, nwriters: int, fsync: bool, hash_blobs: bool,
+                 max_hash_grid: int) -> None:
+        lib = require_gpu_lib()
+        n = len(blobs)
+        self.n = n
+        self._srcs = (c_uint64 * max(n, 1))(*[b[0] for b in blobs])
+        self._sizes = (c_uint64 * max(n, 1))(*[b[1] for b in blobs])
+        self._paths = (c_char_p * max(n, 1))(*[os.fsencode(b[2]) for b in blobs])
+        err = c_int(0)
+        flags = (1 if fsync else 0) | (2 if hash_blobs else 0)
+        self._h = lib.hsg_drain_start(dev, n, self._srcs, self._sizes, self._paths,
+                                      slot_bytes, nslots, nwriters, flags, max_hash_grid,
+                                      ctypes.byref(err))
+        if not self._h:
+            raise HipError(f"hsg_drain_start failed ({err.value})")
+
+    def pending(self) -> int:
+        return require_gpu_lib().hsg_drain_pending(self._h) if self._h else 0
+
+    def wait(self) -> Tuple[List[int], int]:
+        """Blocks (GIL released); returns (hs64 partial sums, bytes written)."""
+        lib = require_gpu_lib()
+        sums = (c_uint64 * max(self.n, 1))()
+        written = c_uint64(0)
+        msg = ctypes.create_string_buffer(256)
+        h, self._h = self._h, None
+        r = lib.hsg_drain_wait(h, sums, ctypes.byref(written), msg)
+        if r != 0:
+            text = msg.value.decode(errors="replace")
+            if r < 0 and -r in errno.errorcode:
+                raise OSError(-r, text)
+            raise HipError(f"native drain failed ({r}): {text}")
+        return list(sums[: self.n]), int(written.value)
 
 
 # ---- managed memory -------------------------------------------------------------

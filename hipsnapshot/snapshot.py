@@ -364,6 +364,11 @@ class Snapshot:
         from .io.compression import plan_compression, resolve
 
         comp = resolve(compression)
+        if is_async and comp != "none" and knobs.async_device_codec() == "raw" \
+                and knobs.async_hbm_staging_enabled():
+            # the frozen device state drains raw: encoding it would run the
+            # codec kernels on the compute units beside the training step
+            comp = "none"
         rank = comm.get_rank()
         # plan reuse (engine/plan_cache.py): device-resident leaves whose plan
         # from an earlier take still holds are not planned again

@@ -101,6 +101,14 @@ class FSStoragePlugin(StoragePlugin):
     def _abs(self, path: str) -> str:
         return os.path.join(self.root, path)
 
+    def native_drain_root(self):
+        """(root, fsync) when an async take's frozen blobs may be written by
+        the native drain (engine/native_drain.py): plain buffered files;
+        O_DIRECT blobs keep the engine's aligned-write path."""
+        if self.direct_io:
+            return None
+        return self.root, self.fsync
+
     # -- StoragePlugin -------------------------------------------------------
 
     async def write(self, write_io: WriteIO) -> None:

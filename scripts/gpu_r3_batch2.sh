@@ -10,10 +10,7 @@ mkdir -p $O/fp8 bench_tmp
 echo "== mesh probe"
 timeout -k 10 150 python scripts/mesh_backend_probe.py > $O/mesh_probe.log 2>&1; echo "mesh probe rc=$?"
 grep -E "full ok|nccl|gloo" $O/mesh_probe.log | sort | uniq | head -20
-echo "== mx8 / fp8 GPU tests"
-timeout -k 10 300 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
-    -k "mx8 or fp8" > $O/fp8_tests.log 2>&1 || { echo FP8_TESTS_FAIL; grep -E "FAIL|Error|assert" $O/fp8_tests.log | head -20; exit 1; }
-tail -1 $O/fp8_tests.log
+echo "== (mx8 / fp8 tests ran in the full suite)"
 echo "== fp8 kernels host-timed"
 timeout -k 10 120 python scripts/fp8_kernels_bench.py > $O/fp8/host_timed.jsonl 2>&1 || { echo BENCH_FAIL; tail $O/fp8/host_timed.jsonl; exit 1; }
 cat $O/fp8/host_timed.jsonl

@@ -1022,3 +1022,101 @@ def test_gpu_compressed_restore_with_split_head_read(gpu, tmp_path, monkeypatch,
     torch.cuda.synchronize()
     for k, v in ref.items():
         assert torch.equal(sd[k], v), k
+
+
+# ---- native drain of an async take (csrc/hsdrain.hip) ---------------------------
+
+def _drain_state(gpu):
+    torch.manual_seed(11)
+    big = torch.randn(3000, 4099, device=gpu)                        # own blob, 49 MB
+    col = torch.randn(2048, 3000, device=gpu, dtype=torch.bfloat16)[:, 7:2007]  # strided view
+    small = [torch.randn(1000 + 37 * i, device=gpu, dtype=torch.bfloat16) for i in range(40)]
+    odd = torch.randint(0, 255, (12345,), dtype=torch.uint8, device=gpu)  # slab gap after it
+    return StateDict(big=big, col=col, small=small, odd=odd, step=3)
+
+
+def _blob_files(root):
+    out = {}
+    for r, _, fs in os.walk(root):
+        for f in fs:
+            p = os.path.join(r, f)
+            rel = os.path.relpath(p, root)
+            if not rel.startswith("."):
+                out[rel] = open(p, "rb").read()
+    return out
+
+
+@pytest.mark.parametrize("fsync", [False, True])
+def test_native_drain_matches_python_drain(gpu, tmp_path, fsync, monkeypatch):
+    """The native drain writes byte-identical blobs (slab gaps zero, strided
+    views packed) to the Python drain, records the same hs64 checksums,
+    is consistent under in-place updates right after async_take, and is
+    actually the path that ran."""
+    from hipsnapshot.engine import native_drain
+    from hipsnapshot.verify import verify_snapshot
+
+    calls = []
+    orig = native_drain.drain
+    monkeypatch.setattr(native_drain, "drain",
+                        lambda reqs, st: calls.append(len(reqs)) or orig(reqs, st))
+    sd = _drain_state(gpu)
+    ref = {k: (v.clone() if torch.is_tensor(v) else [t.clone() for t in v]
+               if isinstance(v, list) else v) for k, v in sd.items()}
+    opts = {"fsync": fsync}
+    p_nat = str(tmp_path / "native")
+    pending = Snapshot.async_take(p_nat, {"sd": sd}, storage_options=opts)
+    sd["big"].add_(1.0)  # after the freeze on the same stream
+    for t in sd["small"]:
+        t.zero_()
+    pending.wait()
+    assert calls and calls[0] >= 3, calls
+    with override_knob("NATIVE_DRAIN", "0"):
+        for k, v in ref.items():  # same values for the Python drain
+            if torch.is_tensor(v):
+                sd[k].copy_(v)
+            elif isinstance(v, list):
+                for a, b in zip(sd[k], v):
+                    a.copy_(b)
+        p_py = str(tmp_path / "python")
+        Snapshot.async_take(p_py, {"sd": sd}, storage_options=opts).wait()
+    assert len(calls) == 1  # the knob disabled it
+    a, b = _blob_files(p_nat), _blob_files(p_py)
+    assert a.keys() == b.keys() and a == b
+    import json
+    ca = json.load(open(os.path.join(p_nat, ".snapshot_checksums", "0")))["blobs"]
+    cb = json.load(open(os.path.join(p_py, ".snapshot_checksums", "0")))["blobs"]
+    assert ca == cb and len(ca) == len(a)
+    assert verify_snapshot(p_nat).ok
+    out = StateDict(big=torch.zeros_like(ref["big"]), col=torch.zeros_like(ref["col"]),
+                    small=[torch.zeros_like(t) for t in ref["small"]],
+                    odd=torch.zeros_like(ref["odd"]), step=0)
+    Snapshot(p_nat).restore({"sd": out})
+    assert torch.equal(out["big"], ref["big"]) and torch.equal(out["col"], ref["col"])
+    assert torch.equal(out["odd"], ref["odd"]) and out["step"] == 3
+    for x, y in zip(out["small"], ref["small"]):
+        assert torch.equal(x, y)
+
+
+def test_native_drain_rewrite_trims_and_async_codec_policy(gpu, tmp_path):
+    """An async take into a path whose files are larger (an earlier take of a
+    bigger state) leaves exactly the new bytes; compression='hsz1' async
+    takes drain the frozen device state raw by default (natively) and encode
+    with HIPSNAPSHOT_ASYNC_DEVICE_CODEC=same."""
+    p = str(tmp_path / "s")
+    w = torch.randn(4096, 1024, device=gpu)
+    with override_slab_size_threshold_bytes(1 << 20):  # w is its own blob
+        Snapshot.take(p, {"sd": StateDict(w=torch.randn(8192, 1024, device=gpu))})
+        size_before = os.path.getsize(os.path.join(p, "0", "sd", "w"))
+        Snapshot.async_take(p, {"sd": StateDict(w=w)}, compression="hsz1").wait()
+    assert os.path.getsize(os.path.join(p, "0", "sd", "w")) == w.numel() * 4 < size_before
+    e = Snapshot(p).get_manifest()["0/sd/w"]
+    assert getattr(e, "codec", None) is None
+    got = torch.zeros_like(w)
+    Snapshot(p).restore({"sd": StateDict(w=got)})
+    assert torch.equal(got, w)
+    with override_knob("ASYNC_DEVICE_CODEC", "same"):
+        Snapshot.async_take(p + "_c", {"sd": StateDict(w=w)}, compression="hsz1").wait()
+    assert Snapshot(p + "_c").get_manifest()["0/sd/w"].codec is not None
+    got.zero_()
+    Snapshot(p + "_c").restore({"sd": StateDict(w=got)})
+    assert torch.equal(got, w)

@@ -178,7 +178,8 @@ def test_quantize_fp8_cpu(tmp_path):
                   quantize=["sd/w"])
     man = Snapshot(str(tmp_path / "s")).get_manifest()
     assert man["0/sd/w"].serializer == "hipsnapshot_fp8_block"
-    assert man["0/sd/w"].quant["block"] == 128
+    assert man["0/sd/w"].quant["block"] == 32  # MX layout (E8M0 scale per 32)
+    assert man["0/sd/w"].quant["format"] == "fp8_e4m3fn_mx"
     out = StateDict(w=torch.zeros(300, 70), i=torch.zeros(5, dtype=torch.int64))
     Snapshot(str(tmp_path / "s")).restore({"sd": out})
     rel = (out["w"] - w).abs().max() / w.abs().max()
