@@ -123,7 +123,27 @@ def _with_adamw(model):
 
 
 def _full(v):
-    return v.full_tensor() if hasattr(v, "full_tensor") else v
+    if not hasattr(v, "full_tensor"):
+        return v
+    if not v.is_cuda:
+        return v.full_tensor()
+    # HIP tensors: a 1-D mesh over the whole world gets a "cuda:nccl" group
+    # from DeviceMesh even under a gloo default group, and RCCL refuses
+    # several ranks on one GPU -- assemble the full tensor from every rank's
+    # local boxes over the (gloo) default group instead.  (On the CPU the
+    # same boxes are checked against full_tensor() in _save_worker.)
+    import torch.distributed as dist
+
+    from hipsnapshot.io.sharded import local_boxes
+
+    mine = [(b.offsets, b.sizes, b.tensor.cpu()) for b in local_boxes(v)]
+    every = [None] * dist.get_world_size()
+    dist.all_gather_object(every, mine)
+    out = torch.zeros(tuple(v.shape), dtype=v.dtype)
+    for boxes in every:
+        for o, sz, t in boxes:
+            out[tuple(slice(a, a + n) for a, n in zip(o, sz))] = t
+    return out
 
 
 def _flat_state(model, opt):
@@ -168,7 +188,7 @@ def _save_worker(tmp: str, device: str = "cpu"):
     assert "_StridedShard" in kinds, kinds
     # every box the write path sees is where full_tensor() says it is
     for k, v in model.state_dict().items():
-        full = v.full_tensor()
+        full = _full(v).to(v.device) if v.is_cuda else v.full_tensor()
         for b in local_boxes(v, for_write=True):
             sl = tuple(slice(o, o + s) for o, s in zip(b.offsets, b.sizes))
             assert torch.equal(full[sl], b.tensor), k
