@@ -292,6 +292,106 @@ __device__ void copy_strided_cast(const CopyDesc& d, int64_t begin, int64_t end)
   }
 }
 
+// Contiguous -> contiguous cast between f16 / bf16 / f32 (the restore of an
+// fp32 checkpoint into a bf16 model, and back): 8 elements per lane per step
+// with 16-B vector loads and stores, same conversions as store_from_f32(
+// load_as_f32()) (bit-identical to torch's copy_).  Unaligned tiles and the
+// tail take the scalar path.
+template <int DT>
+__device__ __forceinline__ void load8_f32(const char* p, float* f) {
+  if constexpr (DT == kF32) {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[0];
+    const uint4 b = reinterpret_cast<const uint4*>(p)[1];
+    f[0] = __uint_as_float(a.x); f[1] = __uint_as_float(a.y);
+    f[2] = __uint_as_float(a.z); f[3] = __uint_as_float(a.w);
+    f[4] = __uint_as_float(b.x); f[5] = __uint_as_float(b.y);
+    f[6] = __uint_as_float(b.z); f[7] = __uint_as_float(b.w);
+  } else {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[0];
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint16_t lo = static_cast<uint16_t>(w[i] & 0xffffu);
+      const uint16_t hi = static_cast<uint16_t>(w[i] >> 16);
+      if constexpr (DT == kBF16) {
+        f[2 * i] = bf16_to_f32(lo);
+        f[2 * i + 1] = bf16_to_f32(hi);
+      } else {
+        _Float16 x, y;
+        __builtin_memcpy(&x, &lo, 2);
+        __builtin_memcpy(&y, &hi, 2);
+        f[2 * i] = static_cast<float>(x);
+        f[2 * i + 1] = static_cast<float>(y);
+      }
+    }
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void store8_f32(char* p, const float* f) {
+  if constexpr (DT == kF32) {
+    reinterpret_cast<uint4*>(p)[0] = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]),
+                                                __float_as_uint(f[2]), __float_as_uint(f[3]));
+    reinterpret_cast<uint4*>(p)[1] = make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]),
+                                                __float_as_uint(f[6]), __float_as_uint(f[7]));
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint16_t lo, hi;
+      if constexpr (DT == kBF16) {
+        lo = f32_to_bf16(f[2 * i]);
+        hi = f32_to_bf16(f[2 * i + 1]);
+      } else {
+        const _Float16 a = static_cast<_Float16>(f[2 * i]);
+        const _Float16 b = static_cast<_Float16>(f[2 * i + 1]);
+        __builtin_memcpy(&lo, &a, 2);
+        __builtin_memcpy(&hi, &b, 2);
+      }
+      w[i] = uint32_t(lo) | (uint32_t(hi) << 16);
+    }
+    reinterpret_cast<uint4*>(p)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+template <int SD, int DD>
+__device__ void copy_contig_cast(const CopyDesc& d, int64_t begin, int64_t end) {
+  constexpr int SES = (SD == kF32) ? 4 : 2;
+  constexpr int DES = (DD == kF32) ? 4 : 2;
+  const char* s = d.src + begin * SES;
+  char* o = d.dst + begin * DES;
+  const int64_t n = end - begin;
+  int64_t done = 0;
+  if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(o)) & 15) == 0) {
+    const int64_t nv = n / 8;
+    for (int64_t i = threadIdx.x; i < nv; i += kBlock) {
+      float f[8];
+      load8_f32<SD>(s + i * 8 * SES, f);
+      store8_f32<DD>(o + i * 8 * DES, f);
+    }
+    done = nv * 8;
+  }
+  for (int64_t j = done + threadIdx.x; j < n; j += kBlock)
+    store_from_f32(o + j * DES, DD, load_as_f32(s + j * SES, SD));
+}
+
+template <int ND>
+__device__ __forceinline__ bool try_contig_cast(const CopyDesc& d, int64_t b, int64_t e) {
+  if constexpr (ND != 1) {
+    return false;
+  } else {
+    if (d.src_strides[0] != 1 || d.dst_strides[0] != 1) return false;
+    const int sd = d.src_dtype, dd = d.dst_dtype;
+#define HS_CAST_CASE(S, D) \
+    if (sd == S && dd == D) { copy_contig_cast<S, D>(d, b, e); return true; }
+    HS_CAST_CASE(kF32, kBF16) HS_CAST_CASE(kBF16, kF32)
+    HS_CAST_CASE(kF32, kF16) HS_CAST_CASE(kF16, kF32)
+    HS_CAST_CASE(kBF16, kF16) HS_CAST_CASE(kF16, kBF16)
+#undef HS_CAST_CASE
+    return false;
+  }
+}
+
 template <int ND>
 __device__ __forceinline__ void copy_tile_nd(const CopyDesc& d, int64_t b, int64_t e) {
   if (d.src_dtype == d.dst_dtype || d.src_dtype < kF16) {
@@ -302,7 +402,7 @@ __device__ __forceinline__ void copy_tile_nd(const CopyDesc& d, int64_t b, int64
       case 8: copy_strided_same<ND, 8>(d, b, e); break;
       default: copy_strided_same<ND, 16>(d, b, e); break;
     }
-  } else {
+  } else if (!try_contig_cast<ND>(d, b, e)) {
     copy_strided_cast<ND>(d, b, e);
   }
 }

@@ -106,6 +106,27 @@ def test_scatter_cast_vs_torch(gpu, src_dtype, dst_dtype):
     assert big[:10].abs().sum() == 0 and big[:, :50].abs().sum() == 0
 
 
+@pytest.mark.parametrize("src_dtype", [torch.float32, torch.bfloat16, torch.float16], ids=str)
+@pytest.mark.parametrize("dst_dtype", [torch.float32, torch.bfloat16, torch.float16], ids=str)
+@pytest.mark.parametrize("n,off", [(1, 0), (7, 1), (4096 + 5, 0), (3 << 20, 3), ((1 << 22) + 1, 8)])
+def test_contiguous_cast_vs_torch(gpu, src_dtype, dst_dtype, n, off):
+    """Contiguous casts take the vectorized 8-per-lane path when 16-B aligned
+    (off = 0 / 8 elements) and the scalar path otherwise: bit-identical to
+    torch's copy_ either way."""
+    torch.manual_seed(6)
+    src_all = (torch.randn(n + off, device=gpu, dtype=torch.float64) * 300).to(src_dtype)
+    src = src_all[off:]
+    dst_all = torch.zeros(n + off, dtype=dst_dtype, device=gpu)
+    dst = dst_all[off:]
+    b = native.CopyBatch()
+    b.add(src.data_ptr(), src_dtype, [1], dst.data_ptr(), dst_dtype, [1], [n],
+          src.element_size())
+    _launch(b)
+    ref = src.to(dst_dtype)
+    assert torch.equal(dst, ref), (dst.float() - ref.float()).abs().max()
+    assert not dst_all[:off].any()
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("n", [1, 127, 128, 1000, 1 << 20])
 @pytest.mark.parametrize("vpt", [2, 8])
