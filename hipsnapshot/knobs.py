@@ -255,6 +255,22 @@ def get_state_dict_barriers() -> str:
     return {"1": "always", "true": "always", "0": "never", "false": "never"}.get(v, v)
 
 
+def rebalance_enabled() -> bool:
+    """Move whole blobs from heavily to lightly loaded ranks over xGMI before
+    a blocking take stages (parallel/rebalance.py).  Off by default."""
+    return _get_bool("REBALANCE", False)
+
+
+def rebalance_host() -> bool:
+    """Let the rebalancer move host (CPU) blobs too (gloo tests)."""
+    return _get_bool("REBALANCE_HOST", False)
+
+
+def rebalance_min_gain() -> float:
+    """Stop once the load spread is below this fraction of the mean."""
+    return float(_get("REBALANCE_MIN_GAIN") or 0.1)
+
+
 def native_drain_enabled() -> bool:
     """Drain an async take's raw frozen blobs to the local FS in native
     threads (engine/native_drain.py, csrc/hsdrain.hip)."""

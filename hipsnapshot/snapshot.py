@@ -466,6 +466,13 @@ class Snapshot:
                 freeze_device_state(write_reqs)
             deferred = [wr for wr in write_reqs if is_deferrable(wr)]
             write_reqs = [wr for wr in write_reqs if not is_deferrable(wr)]
+        if not is_async and comm.get_world_size() > 1 and knobs.rebalance_enabled():
+            # uneven device loads: move whole blobs to idle ranks over xGMI
+            # (a collective: before the background metadata gather starts)
+            from .parallel.rebalance import rebalance
+
+            with timeline.span("rebalance"):
+                write_reqs = rebalance(write_reqs, comm)
         # largest first: the writes still running after the last D2H -- the
         # take's tail -- are then the small ones (slabs), not a 100 MB chunk
         write_reqs.sort(key=lambda wr: wr.buffer_stager.get_staging_cost_bytes(), reverse=True)

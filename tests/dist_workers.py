@@ -470,3 +470,35 @@ def state_dict_barriers():
         n_coll = len(calls)
     # commit barriers only vs + one per app-state key (4 keys)
     assert n_coll - n_local == 4, (n_local, n_coll)
+
+
+def rebalance_take(path: str):
+    """Rank 0 owns most of the bytes; with rebalancing, its blobs are written
+    by the idle ranks (their checksum files list them), the manifest is
+    unchanged and every rank restores bitwise."""
+    import json
+
+    from hipsnapshot.knobs import override_knob, override_slab_size_threshold_bytes
+    from hipsnapshot.verify import verify_snapshot
+
+    rank, ws = dist.get_rank(), dist.get_world_size()
+    torch.manual_seed(rank)
+    n = 8 if rank == 0 else 1
+    sd = StateDict(**{f"t{i}": torch.randn(64 * 1024 + 7 * i) for i in range(n)}, r=rank)
+    with override_knob("REBALANCE", "1"), override_knob("REBALANCE_HOST", "1"), \
+            override_slab_size_threshold_bytes(1024):
+        Snapshot.take(path, {"sd": sd})
+    dist.barrier()
+    if rank == 0:
+        assert verify_snapshot(path).ok
+        written = {}
+        for r in range(ws):
+            doc = json.load(open(os.path.join(path, ".snapshot_checksums", str(r))))
+            written[r] = set(doc["blobs"])
+        moved = [p for r in range(1, ws) for p in written[r] if p.startswith("0/")]
+        assert moved, written  # idle ranks wrote some of rank 0's blobs
+    out = StateDict(**{f"t{i}": torch.zeros(64 * 1024 + 7 * i) for i in range(n)}, r=-1)
+    Snapshot(path).restore({"sd": out})
+    assert out["r"] == rank
+    for i in range(n):
+        assert torch.equal(out[f"t{i}"], sd[f"t{i}"]), i

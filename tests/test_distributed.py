@@ -94,3 +94,20 @@ def test_async_take_metadata_through_store(tmp_path):
 
 def test_state_dict_barriers_only_when_needed():
     run_distributed(W.state_dict_barriers, 2)
+
+
+def test_write_load_rebalancing(tmp_path):
+    run_distributed(W.rebalance_take, 3, str(tmp_path / "rb"))
+
+
+def test_rebalance_plan_math():
+    from hipsnapshot.parallel.rebalance import plan_moves
+
+    cands = [[(i, 100, f"a{i}") for i in range(8)], [], [(0, 50, "c0")]]
+    moves = plan_moves([800, 0, 50], cands, 0.1, 12)
+    loads = [800, 0, 50]
+    for src, _i, dst, n, _p in moves:
+        loads[src] -= n
+        loads[dst] += n
+    assert max(loads) - min(loads) <= 100 and loads[0] <= 350, (moves, loads)
+    assert plan_moves([100, 100], [[(0, 10, "x")], []], 0.1, 4) == []
