@@ -486,6 +486,22 @@ def cpu_tensor_bytes(t: torch.Tensor, copy: bool) -> StagedBuffer:
     return StagedBuffer(mv, keepalive=t)
 
 
+def _add_members_zero_gaps(batch, members, base: int, dev: int) -> None:
+    """Slab members at their offsets, and zeros in the alignment gaps between
+    them (same launch): a slab's padding never carries stale HBM bytes, and
+    every drain path writes identical blobs."""
+    from .hbm_staging import _zeros
+
+    zero = None
+    end = 0
+    for t, off in sorted(members, key=lambda m: m[1]):
+        if off > end:
+            zero = zero or _zeros(dev).data_ptr()
+            batch.add_bytes(zero, base + end, off - end)
+        batch.add_tensor(t, base + off)
+        end = max(end, off + t.numel() * t.element_size())
+
+
 def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int,
                    producers: Sequence[int], via_device_slab: bool = True,
                    codec: Optional[dict] = None) -> StagedBuffer:
@@ -517,8 +533,7 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
                 slab = None
         base = slab.data_ptr() if slab is not None else pb.ptr
         batch = native.CopyBatch()
-        for t, off in members:
-            batch.add_tensor(t, base + off)
+        _add_members_zero_gaps(batch, members, base, dev)
         keep = batch.launch(dev, stream, sync=False)
         if slab is not None:
             hs = None
@@ -550,9 +565,10 @@ def _gather_encoded(members, total_bytes: int, producers, codec: dict) -> Staged
         native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
     t1 = time.perf_counter()
     try:
-        slab = torch.zeros(total_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+        # uninitialised: the gather launch writes the members AND zeros into
+        # the alignment gaps (no separate zero-fill pass over the slab)
+        slab = torch.empty(total_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
         timeline.add("slab_join", "stage", t0, t1)
-        timeline.add("slab_zeros", "stage", t1, time.perf_counter())
     except torch.cuda.OutOfMemoryError:
         # no HBM for the slab: gather into host memory, encode on the CPU
         raw = gather_to_host(members, total_bytes, producers, via_device_slab=False)
@@ -560,12 +576,11 @@ def _gather_encoded(members, total_bytes: int, producers, codec: dict) -> Staged
             return _encode_host_bytes(raw.addr, total_bytes, codec)
         finally:
             raw.release()
-    # the slab comes from torch's allocator on the current stream: make the
-    # copy stream wait for its zero-fill (padding bytes are encoded too)
+    # the slab comes from torch's allocator on the current stream: order the
+    # copy stream after it (padding bytes are encoded too: zeroed below)
     _join_current_stream(dev, slot)
     batch = native.CopyBatch()
-    for t, off in members:
-        batch.add_tensor(t, slab.data_ptr() + off)
+    _add_members_zero_gaps(batch, members, slab.data_ptr(), dev)
     keep = batch.launch(dev, stream, sync=False)
     try:
         return _encode_device_to_host(dev, slot, slab, codec)
