@@ -830,25 +830,62 @@ __device__ __forceinline__ float hada(int k, int c) {
   return (__popc(k & c) & 1) ? -1.f : 1.f;
 }
 
+// Half-row operand layout: lane (r, h) owns X[r][16h .. 16h + 15] -- 32 B
+// (bf16/f16) or 64 B (f32) contiguous in memory, loaded with 16-B vector
+// loads -- and MFMA step t contracts k = t (h = 0 lanes) and k = 16 + t
+// (h = 1 lanes): the accumulation order is k = 0, 16, 1, 17, ..., 15, 31
+// (``ops/quant.py`` HADAMARD_K_ORDER; the torch reference sums in the same
+// order, so the blobs stay bit-identical).
+template <int DT>
+__device__ __forceinline__ void load_half_row(const char* src, int64_t e0, int64_t n, float* x) {
+  constexpr int ES = (DT == kF32) ? 4 : 2;
+  if (e0 + 16 <= n && ((reinterpret_cast<uintptr_t>(src + e0 * ES) & 15) == 0)) {
+    const uint4* v = reinterpret_cast<const uint4*>(src + e0 * ES);
+    if constexpr (ES == 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 w = v[q];
+        x[4 * q] = __uint_as_float(w.x);
+        x[4 * q + 1] = __uint_as_float(w.y);
+        x[4 * q + 2] = __uint_as_float(w.z);
+        x[4 * q + 3] = __uint_as_float(w.w);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint4 w = v[q];
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          x[8 * q + 2 * i] = mx_unpack<DT>(ws[i], 0);
+          x[8 * q + 2 * i + 1] = mx_unpack<DT>(ws[i], 1);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      x[t] = (e0 + t < n) ? load_as_f32(src + (e0 + t) * ES, DT) : 0.f;
+  }
+}
+
+template <int DT>
 __global__ void __launch_bounds__(kBlock)
-hs_fp8_hadamard_quant(const char* __restrict__ src, int32_t src_dtype, int64_t n, int64_t n_pad,
+hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
                       uint8_t* __restrict__ out, float* __restrict__ scales) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int ses = (src_dtype == kF32) ? 4 : 2;
   const int64_t ntiles = (n_pad + 1023) / 1024;
   const int64_t nblocks = (n_pad + 127) / 128;
   const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
   for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
-    const int64_t rowbase = (tile * 32 + r) * 32;  // flat index of X[row r][0]
+    float x[16];
+    load_half_row<DT>(src, (tile * 32 + r) * 32 + 16 * h, n, x);
     floatx16 acc = {};
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int64_t e = rowbase + 2 * t + h;
-      const float a = (e < n) ? load_as_f32(src + e * ses, src_dtype) : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, hada(2 * t + h, r), acc, 0, 0, 0);
-    }
+    for (int t = 0; t < 16; ++t)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[t], hada(16 * h + t, r), acc, 0, 0, 0);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       float amax = fmaxf(fmaxf(fabsf(acc[4 * g4]), fabsf(acc[4 * g4 + 1])),
@@ -880,14 +917,19 @@ hs_fp8_hadamard_dequant(const uint8_t* __restrict__ q, const float* __restrict__
   const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
   for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
     const int64_t grow = tile * 32 + r;  // global group (row) index
-    const int64_t rowbase = grow * 32;
-    const float s = (rowbase < n_pad) ? scales[rowbase / 128] : 0.f;
+    const int64_t e0 = grow * 32 + 16 * h;
+    const float s = (grow * 32 < n_pad) ? scales[(grow * 32) / 128] : 0.f;
+    // the lane's 16 fp8 codes: one 16-B load (n_pad is a multiple of 32)
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (e0 + 16 <= n_pad) {
+      const uint4 v = *reinterpret_cast<const uint4*>(q + e0);
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    }
     floatx16 acc = {};
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      const int64_t e = rowbase + 2 * t + h;
-      const float y = (e < n_pad) ? __builtin_amdgcn_cvt_f32_fp8(static_cast<int>(q[e]), 0) * s : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(y, hada(2 * t + h, r), acc, 0, 0, 0);
+      const float y = fp8_byte_to_f32(w[t >> 2], t & 3) * s;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(y, hada(16 * h + t, r), acc, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1569,9 +1611,16 @@ int hsg_fp8_hadamard_quantize(int dev, const void* src, int src_dtype, int64_t n
   const int64_t n_pad = (n + 31) / 32 * 32;
   const int64_t ntiles = (n_pad + 1023) / 1024;
   const int grid = static_cast<int>(std::min<int64_t>((ntiles + 3) / 4, 256 * 8));
-  hipLaunchKernelGGL(hs_fp8_hadamard_quant, dim3(grid), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const char*>(src), src_dtype,
-                     n, n_pad, static_cast<uint8_t*>(out), static_cast<float*>(scales));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const char* sp = static_cast<const char*>(src);
+  uint8_t* op = static_cast<uint8_t*>(out);
+  float* sc = static_cast<float*>(scales);
+  switch (src_dtype) {
+    case kBF16: hipLaunchKernelGGL(hs_fp8_hadamard_quant<kBF16>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
+    case kF16: hipLaunchKernelGGL(hs_fp8_hadamard_quant<kF16>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
+    case kF32: hipLaunchKernelGGL(hs_fp8_hadamard_quant<kF32>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
+    default: snprintf(g_err, sizeof(g_err), "unsupported hadamard source dtype %d", src_dtype); return -1002;
+  }
   HS_CHECK(hipGetLastError());
   return 0;
 }

@@ -210,11 +210,18 @@ def hadamard_matrix(n: int = GROUP, device=None) -> torch.Tensor:
     return 1.0 - 2.0 * parity.float()
 
 
+# k order of the GPU kernels' MFMA chain: step t contracts k = t (lanes of
+# half 0) then k = 16 + t (half 1), the layout that lets each lane load its
+# 16 elements of a row with 16-B vector loads (hs_fp8_hadamard_*)
+HADAMARD_K_ORDER = [k for t in range(GROUP // 2) for k in (t, GROUP // 2 + t)]
+
+
 def _rotate_sequential(rows: torch.Tensor) -> torch.Tensor:
-    """rows[R, 32] @ H with a k-ordered fp32 FMA chain (= MFMA f32 semantics)."""
+    """rows[R, 32] @ H with a k-ordered fp32 FMA chain (= MFMA f32 semantics,
+    in ``HADAMARD_K_ORDER``)."""
     h = hadamard_matrix(GROUP, rows.device)
     acc = torch.zeros_like(rows)
-    for k in range(GROUP):
+    for k in HADAMARD_K_ORDER:
         acc = acc + rows[:, k:k + 1] * h[k][None, :]  # x * +-1 is exact: one rounding
     return acc
 
