@@ -110,6 +110,11 @@ def main() -> None:
             take()
     sib = None
     if args.host_siblings > 0:
+        # this host runs world ranks: size I/O threads as a real W-rank job
+        # would (the take's first collective sets the same hint)
+        from hipsnapshot import knobs
+
+        knobs.set_local_ranks_hint(args.host_siblings + 1)
         sizes = [os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(path)
                  for f in fs if not f.startswith(".")]
         sib = _Siblings(args.host_siblings, sizes, root, bool(args.sibling_dma_pass))
@@ -204,7 +209,7 @@ def main() -> None:
     dist.destroy_process_group()
 
 
-def _sibling_main(i: int, sizes, root: str, dma_pass: bool, go, done) -> None:
+def _sibling_main(i: int, sizes, root: str, dma_pass: bool, go, done, hint: int) -> None:
     """One sibling rank's host work per take (no GPU): a write pass over its
     staging memory (the D2H DMA's DRAM writes), then every blob through the
     native FS engine."""
@@ -214,8 +219,11 @@ def _sibling_main(i: int, sizes, root: str, dma_pass: bool, go, done) -> None:
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__)))))
+    from hipsnapshot import knobs
     from hipsnapshot.io_types import WriteIO
     from hipsnapshot.storage.fs import FSStoragePlugin
+
+    knobs.set_local_ranks_hint(hint)  # I/O threads of one of `hint` ranks on this host
 
     buf = np.ones(max(sizes), dtype=np.uint8)  # touched: resident like the pinned pool
     staging = np.empty(sum(sizes), dtype=np.uint8)
@@ -256,7 +264,8 @@ class _Siblings:
         self.go_qs = [ctx.Queue() for _ in range(k)]
         self.done = ctx.Queue()
         self.procs = [ctx.Process(target=_sibling_main,
-                                  args=(i, sizes, root, dma_pass, self.go_qs[i], self.done))
+                                  args=(i, sizes, root, dma_pass, self.go_qs[i], self.done,
+                                        k + 1))
                       for i in range(k)]
         for p in self.procs:
             p.start()
