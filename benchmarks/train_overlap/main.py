@@ -54,6 +54,9 @@ def main() -> None:
     ap.add_argument("--baseline-steps", type=int, default=10)
     ap.add_argument("--window-steps", type=int, default=12,
                     help="train_time_lost_ms covers at least this many steps after async_take")
+    ap.add_argument("--gap-steps", type=int, default=0,
+                    help="training steps between one checkpoint's commit and the next "
+                         "async_take (the page cache writes the previous one back meanwhile)")
     ap.add_argument("--checkpoints", type=int, default=1,
                     help="async_takes back to back (each starts when the previous one has "
                          "committed) inside ONE measured window: enough steps overlap a "
@@ -173,12 +176,15 @@ def main() -> None:
         dist.all_reduce(f, op=dist.ReduceOp.MIN)
         return bool(f.item())
 
+    gap = []  # steps between checkpoints (no drain running)
     t0 = time.perf_counter()
     while True:
         if all_done(pending):
             if pending is not None:
                 pending.wait()
                 drains.append(time.perf_counter() - t_ck)
+                if taken < k_total:
+                    gap += [step() for _ in range(args.gap_steps)]
             if taken == k_total:
                 break
             if taken == k_total - 1:  # the restore check compares with this state
@@ -203,7 +209,7 @@ def main() -> None:
         step()
         extra += 1
     lost = ((time.perf_counter() - t0) - clone_s
-            - (len(during) + extra) * base_ms / 1e3) / k_total
+            - (len(during) + len(gap) + extra) * base_ms / 1e3) / k_total
     # every rank must finish its loop before collectives resume
     unblock = max_over_ranks(unblock, dev)
     drain = max_over_ranks(drain, dev)
@@ -238,8 +244,13 @@ def main() -> None:
           "steps_during_drain": n_during, "step_ms_during_drain_mean": round(mean_ms, 2),
           "step_ms_during_drain_median": round(med_ms, 2),
           "step_ms_during_drain_max": round(max_ms, 2),
+          "step_ms_during_drain_each": [round(x * 1e3, 1) for x in during],
           "slowdown_during_drain": round(mean_ms / base_ms - 1.0, 4) if during else None,
-          "window_steps": len(during) + extra, "train_time_lost_ms": round(lost * 1e3, 1),
+          "gap_steps": args.gap_steps,
+          "step_ms_between_checkpoints_median": round(statistics.median(gap) * 1e3, 2)
+          if gap else None,
+          "window_steps": len(during) + len(gap) + extra,
+          "train_time_lost_ms": round(lost * 1e3, 1),
           "train_time_lost_vs_sync_take": round(lost / sync_s, 3),
           "restore_bitwise_ok": bool(okt.item()), "stored_bytes": stored,
           "data": "synthetic tokens, random init"})
