@@ -54,6 +54,10 @@ def main() -> None:
     ap.add_argument("--baseline-steps", type=int, default=10)
     ap.add_argument("--window-steps", type=int, default=12,
                     help="train_time_lost_ms covers at least this many steps after async_take")
+    ap.add_argument("--warm-async", type=int, default=1,
+                    help="async_takes (waited for) before the measured window: the first "
+                         "one of a job allocates its HBM arena and pinned drain slots, a "
+                         "one-time cost reported as cold_async_* ")
     ap.add_argument("--gap-steps", type=int, default=0,
                     help="training steps between one checkpoint's commit and the next "
                          "async_take (the page cache writes the previous one back meanwhile)")
@@ -157,6 +161,16 @@ def main() -> None:
     if args.storage == "fs" and rank == 0:
         shutil.rmtree(f"{root}/sync", ignore_errors=True)  # keep the disk footprint to one copy
 
+    cold = []
+    for _ in range(args.warm_async):
+        sync(dev)
+        tw = time.perf_counter()
+        p = Snapshot.async_take(f"{root}/async", app, storage_options=opts,
+                                compression=args.compression)
+        tu = time.perf_counter() - tw
+        p.wait()
+        sync(dev)
+        cold.append((tu, time.perf_counter() - tw))
     # async takes while training continues: --checkpoints of them back to
     # back, each starting at the first step boundary after the previous one
     # committed (same path: a rewrite, as a ring of checkpoints would do)
@@ -239,6 +253,8 @@ def main() -> None:
           "baseline_step_ms": round(base_ms, 2), "sync_take_s": round(sync_s, 3),
           "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 2), "async_drain_s": round(drain, 3),
+          "cold_async_unblock_ms": [round(c[0] * 1e3, 1) for c in cold],
+          "cold_async_total_s": [round(c[1], 3) for c in cold],
           "checkpoints": k_total, "async_unblock_ms_each": [round(u * 1e3, 2) for u in unblocks],
           "async_drain_s_each": [round(d, 3) for d in drains],
           "steps_during_drain": n_during, "step_ms_during_drain_mean": round(mean_ms, 2),
