@@ -9,6 +9,7 @@ import sys as _sys
 
 import torch as _torch  # noqa: F401  (load torch's HIP runtime before our .so)
 
+from .engine.hbm_staging import release_hbm_arena
 from .snapshot import PendingSnapshot, Snapshot
 from .stateful import AppState, RNGState, StateDict, Stateful
 from .version import __hipsnapshot_version__, __version__
@@ -39,6 +40,7 @@ __all__ = [
     "StateDict",
     "RNGState",
     "AppState",
+    "release_hbm_arena",
     "__version__",
     "__hipsnapshot_version__",
 ]

@@ -125,7 +125,9 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
         # for the arena too (the allocator releases them and retries when a
         # fresh allocation does not fit) -- a trainer's cache is often tens of GB
         cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-        room = min(free + max(cached, 0) - knobs.hbm_staging_reserve_bytes(), cap)
+        kept = _kept.get(dev)
+        kept_bytes = kept[0].numel() if kept is not None and not kept[1] else 0
+        room = min(free + max(cached, 0) + kept_bytes - knobs.hbm_staging_reserve_bytes(), cap)
         want = sum(r[0] for r in reqs)
         chosen, total = [], 0
         for r in reqs:
@@ -148,12 +150,51 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
     return frozen
 
 
+# Arena kept between async takes (HIPSNAPSHOT_HBM_ARENA_KEEP): device ->
+# [tensor, busy].  A training loop frees and re-allocates activations between
+# checkpoints; a 48 GB arena handed back to torch's caching allocator gets
+# split up by them, and the next take's torch.empty then goes through
+# hipMalloc -- or frees cached blocks first -- right while a training step is
+# queued (a ~200 ms step stall measured on Llama-3-8B + AdamW,
+# profiles/r3/overlap/).  Kept, the next take reuses it as it is.
+_kept: Dict[int, list] = {}
+
+
+def _arena(dev: int, total: int) -> torch.Tensor:
+    k = _kept.get(dev)
+    if k is not None and not k[1] and k[0].numel() >= total:
+        k[1] = True
+        return k[0][:max(total, 1)]
+    arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
+    if knobs.hbm_arena_keep() and (k is None or not k[1]):
+        _kept[dev] = [arena, True]  # (a smaller idle one is dropped)
+    return arena
+
+
+def arena_done(arenas) -> None:
+    """The drain of these arenas finished: a kept arena may be reused."""
+    for a in arenas:
+        for k in _kept.values():
+            if k[1] and a.data_ptr() == k[0].data_ptr():
+                k[1] = False
+
+
+def release_hbm_arena() -> int:
+    """Drop the idle kept arenas (back to torch's caching allocator); returns
+    the bytes released.  Busy ones (a drain still running) are kept."""
+    freed = 0
+    for dev in list(_kept):
+        if not _kept[dev][1]:
+            freed += _kept.pop(dev)[0].numel()
+    return freed
+
+
 def _freeze(dev: int, chosen, total: int) -> None:
     _retire_launches()
     stream = torch.cuda.current_stream(dev)
     with torch.cuda.device(dev):
         with timeline.span("freeze_alloc", bytes=total):
-            arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
+            arena = _arena(dev, total)
         batch = native.CopyBatch()
         base = arena.data_ptr()
         zero = _zeros(dev).data_ptr()

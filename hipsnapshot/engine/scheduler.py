@@ -515,8 +515,16 @@ class DeferredIOWork:
                     await asyncio.get_running_loop().run_in_executor(
                         aux_pool(), native_drain.drain, native_reqs, self.storage)
 
-        res = await asyncio.gather(self.first.complete(), run_deferred(), run_native(),
-                                   return_exceptions=True)
+        try:
+            res = await asyncio.gather(self.first.complete(), run_deferred(), run_native(),
+                                       return_exceptions=True)
+        finally:
+            # every reader of the frozen arena is done: a kept arena is free
+            from .hbm_staging import arena_done
+
+            arena_done({id(a): a for a in (getattr(wr.buffer_stager, "frozen_region",
+                                                   (None,))[0] for wr in self.deferred)
+                        if a is not None}.values())
         if self._second is not None:
             self.stats.bytes_written += self._second.stats.bytes_written
             self.stats.n_reqs += self._second.stats.n_reqs

@@ -271,6 +271,12 @@ def rebalance_min_gain() -> float:
     return float(_get("REBALANCE_MIN_GAIN") or 0.1)
 
 
+def hbm_arena_keep() -> bool:
+    """Keep the async-take HBM arena allocated between takes and reuse it
+    (``hipsnapshot.release_hbm_arena()`` frees it).  Default on."""
+    return _get_bool("HBM_ARENA_KEEP", True)
+
+
 def native_drain_enabled() -> bool:
     """Drain an async take's raw frozen blobs to the local FS in native
     threads (engine/native_drain.py, csrc/hsdrain.hip)."""

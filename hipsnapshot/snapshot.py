@@ -279,6 +279,11 @@ class Snapshot:
                                                compression, progress=progress)
         except BaseException as e:
             _release_plan(progress)
+            from .engine.hbm_staging import arena_done
+
+            # no drain will read the arena this take froze into: a kept one
+            # is free for later takes (stream-ordered after this freeze)
+            arena_done(progress.get("arenas", []))
             if progress.get("collectives_done"):
                 # peers that staged successfully are already in (or about to
                 # start) their commit threads: fail their barrier now instead
@@ -464,6 +469,10 @@ class Snapshot:
 
             with timeline.span("hbm_freeze"):
                 freeze_device_state(write_reqs)
+            if progress is not None:
+                progress["arenas"] = list({
+                    id(r[0]): r[0] for r in (getattr(wr.buffer_stager, "frozen_region", None)
+                                             for wr in write_reqs) if r is not None}.values())
             deferred = [wr for wr in write_reqs if is_deferrable(wr)]
             write_reqs = [wr for wr in write_reqs if not is_deferrable(wr)]
         if not is_async and comm.get_world_size() > 1 and knobs.rebalance_enabled():

@@ -1161,3 +1161,33 @@ def test_native_drain_rewrite_trims_and_async_codec_policy(gpu, tmp_path):
     got.zero_()
     Snapshot(p + "_c").restore({"sd": StateDict(w=got)})
     assert torch.equal(got, w)
+
+
+def test_kept_hbm_arena_reused_and_never_shared(gpu, tmp_path):
+    """The async-take arena is kept between takes and reused once its drain
+    finished; a take that starts while a drain still reads it gets its own;
+    every snapshot holds its own values; release_hbm_arena frees it."""
+    from hipsnapshot import release_hbm_arena
+    from hipsnapshot.engine import hbm_staging
+
+    release_hbm_arena()
+    w = torch.randn(4096, 4096, device=gpu)
+    refs = []
+    Snapshot.async_take(str(tmp_path / "a0"), {"sd": StateDict(w=w)}).wait()
+    refs.append(w.clone())
+    first = hbm_staging._kept[0][0].data_ptr()
+    w.add_(1.0)
+    p1 = Snapshot.async_take(str(tmp_path / "a1"), {"sd": StateDict(w=w)})
+    refs.append(w.clone())
+    assert hbm_staging._kept[0][0].data_ptr() == first and hbm_staging._kept[0][1]
+    w.add_(1.0)  # a second take while the first drain may still run
+    p2 = Snapshot.async_take(str(tmp_path / "a2"), {"sd": StateDict(w=w)})
+    refs.append(w.clone())
+    p1.wait()
+    p2.wait()
+    assert not hbm_staging._kept[0][1]
+    for i, ref in enumerate(refs):
+        got = torch.zeros_like(w)
+        Snapshot(str(tmp_path / f"a{i}")).restore({"sd": StateDict(w=got)})
+        assert torch.equal(got, ref), i
+    assert release_hbm_arena() >= w.numel() * 4 and not hbm_staging._kept
