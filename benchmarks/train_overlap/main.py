@@ -119,7 +119,7 @@ def main() -> None:
         step()
     sync(dev)
     base = [step() for _ in range(args.baseline_steps)]
-    base_ms = max_over_ranks(statistics.median(base), dev) * 1e3
+    base_ms = max_over_ranks(statistics.median(base), dev) * 1e3  # provisional (log only)
     ckpt_bytes = sum(_local(p).numel() * _local(p).element_size() for p in model.parameters())
     for st in opt.state.values():
         for v in st.values():
@@ -191,6 +191,10 @@ def main() -> None:
         return bool(f.item())
 
     gap = []  # steps between checkpoints (no drain running)
+    from hipsnapshot.utils.tracing import GcWatch
+
+    gcw = GcWatch().start()
+    unblock_gc = []
     t0 = time.perf_counter()
     while True:
         if all_done(pending):
@@ -210,6 +214,7 @@ def main() -> None:
             pending = Snapshot.async_take(f"{root}/async", app, storage_options=opts,
                                           compression=args.compression)
             unblocks.append(time.perf_counter() - t_ck)
+            unblock_gc.append(gcw.ms_between(t_ck, t_ck + unblocks[-1]))
             taken += 1
         during.append(step())
     drain = statistics.mean(drains)
@@ -222,8 +227,17 @@ def main() -> None:
     while len(during) + extra < args.window_steps:
         step()
         extra += 1
-    lost = ((time.perf_counter() - t0) - clone_s
-            - (len(during) + len(gap) + extra) * base_ms / 1e3) / k_total
+    window_s = time.perf_counter() - t0
+    gc_window_ms = gcw.ms_between(t0, t0 + window_s)
+    gcw.stop()
+    # the step-time baseline: median of EVERY step no drain overlapped (before
+    # the first checkpoint, between checkpoints and after the window), so
+    # clock / thermal drift over the run does not count as checkpoint cost
+    post = [step() for _ in range(args.baseline_steps)]
+    base_ms = max_over_ranks(statistics.median(base + gap + post), dev) * 1e3
+    base_pre_ms = max_over_ranks(statistics.median(base), dev) * 1e3
+    base_post_ms = max_over_ranks(statistics.median(post), dev) * 1e3
+    lost = (window_s - clone_s - (len(during) + len(gap) + extra) * base_ms / 1e3) / k_total
     # every rank must finish its loop before collectives resume
     unblock = max_over_ranks(unblock, dev)
     drain = max_over_ranks(drain, dev)
@@ -250,7 +264,10 @@ def main() -> None:
           "compression": args.compression, "master_dtype": args.master_dtype,
           "switch_interval_ms": sys.getswitchinterval() * 1e3, "step_sync": args.step_sync,
           "checkpoint_bytes": ckpt_bytes,
-          "baseline_step_ms": round(base_ms, 2), "sync_take_s": round(sync_s, 3),
+          "baseline_step_ms": round(base_ms, 2), "baseline_step_ms_pre": round(base_pre_ms, 2),
+          "baseline_step_ms_post": round(base_post_ms, 2),
+          "async_unblock_gc_ms_each": [round(g, 1) for g in unblock_gc],
+          "gc_ms_in_window": round(gc_window_ms, 1), "sync_take_s": round(sync_s, 3),
           "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 2), "async_drain_s": round(drain, 3),
           "cold_async_unblock_ms": [round(c[0] * 1e3, 1) for c in cold],
