@@ -41,6 +41,26 @@ from hipsnapshot import Snapshot  # noqa: E402
 from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama  # noqa: E402
 
 
+def _cgroup_cpu() -> dict:
+    """cgroup v2 CPU accounting of this job (throttling = CFS quota stalls:
+    every thread of the cgroup waits for the next period)."""
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                out[k] = int(v)
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            out["max"] = f.read().strip()
+    except OSError:
+        pass
+    import resource
+
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    out["proc_cpu_s"] = ru.ru_utime + ru.ru_stime
+    return out
+
+
 def _local(t):
     return t._local_tensor if hasattr(t, "_local_tensor") else t
 
@@ -99,8 +119,16 @@ def main() -> None:
     opt = torch.optim.AdamW(model.parameters(), lr=1e-5, foreach=True)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
 
+    from hipsnapshot.utils.tracing import timeline
+
     def step() -> float:
         t0 = time.perf_counter()
+        try:
+            return _step(t0)
+        finally:
+            timeline.add("train_step", "train", t0, time.perf_counter())
+
+    def _step(t0: float) -> float:
         tok = torch.randint(0, cfg.vocab_size, (args.batch, args.seq + 1), device=dev,
                             generator=gen)
         logits = model(tok[:, :-1])
@@ -179,6 +207,7 @@ def main() -> None:
     k_total = max(1, args.checkpoints)
     pending, taken, t_ck = None, 0, 0.0
     during, unblocks, drains = [], [], []
+    during_k, gap_k = [], []  # per checkpoint: steps during its drain / after it
     ref, clone_s = None, 0.0
     def all_done(p) -> bool:
         """``p.done()`` agreed across ranks (a step runs FSDP collectives:
@@ -195,6 +224,7 @@ def main() -> None:
 
     gcw = GcWatch().start()
     unblock_gc = []
+    cg0 = _cgroup_cpu()
     t0 = time.perf_counter()
     while True:
         if all_done(pending):
@@ -202,7 +232,8 @@ def main() -> None:
                 pending.wait()
                 drains.append(time.perf_counter() - t_ck)
                 if taken < k_total:
-                    gap += [step() for _ in range(args.gap_steps)]
+                    gap_k.append([step() for _ in range(args.gap_steps)])
+                    gap += gap_k[-1]
             if taken == k_total:
                 break
             if taken == k_total - 1:  # the restore check compares with this state
@@ -215,8 +246,10 @@ def main() -> None:
                                           compression=args.compression)
             unblocks.append(time.perf_counter() - t_ck)
             unblock_gc.append(gcw.ms_between(t_ck, t_ck + unblocks[-1]))
+            during_k.append([])
             taken += 1
         during.append(step())
+        during_k[-1].append(during[-1])
     drain = statistics.mean(drains)
     unblock = statistics.median(unblocks)
     # training time lost to the checkpoints: wall time from the first
@@ -228,6 +261,12 @@ def main() -> None:
         step()
         extra += 1
     window_s = time.perf_counter() - t0
+    cg1 = _cgroup_cpu()
+    cgroup = {"cpu_max": cg1.get("max"), "window_s": round(window_s, 3),
+              "process_cpu_s": round(cg1["proc_cpu_s"] - cg0["proc_cpu_s"], 2)}
+    for k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+        if k in cg0 and k in cg1:
+            cgroup[k] = cg1[k] - cg0[k]
     gc_window_ms = gcw.ms_between(t0, t0 + window_s)
     gcw.stop()
     # the step-time baseline: median of EVERY step no drain overlapped (before
@@ -237,6 +276,19 @@ def main() -> None:
     base_ms = max_over_ranks(statistics.median(base + gap + post), dev) * 1e3
     base_pre_ms = max_over_ranks(statistics.median(base), dev) * 1e3
     base_post_ms = max_over_ranks(statistics.median(post), dev) * 1e3
+    # the same cost against a LOCAL baseline: each checkpoint's drain steps vs
+    # the no-drain steps right before and after it (the box's step time drifts
+    # by up to 10 % over a run with clocks and temperature; adjacent steps
+    # share the regime)
+    lost_local, slow_local = [], []
+    for k in range(k_total):
+        before = gap_k[k - 1] if k > 0 else base
+        after = gap_k[k] if k < len(gap_k) else post
+        loc = statistics.median(before + after)
+        d = during_k[k]
+        lost_local.append(unblocks[k] + sum(d) - len(d) * loc)
+        slow_local.append(statistics.median(d) / loc - 1.0 if d else 0.0)
+    lost_local_ms = max_over_ranks(statistics.mean(lost_local), dev) * 1e3
     lost = (window_s - clone_s - (len(during) + len(gap) + extra) * base_ms / 1e3) / k_total
     # every rank must finish its loop before collectives resume
     unblock = max_over_ranks(unblock, dev)
@@ -267,7 +319,7 @@ def main() -> None:
           "baseline_step_ms": round(base_ms, 2), "baseline_step_ms_pre": round(base_pre_ms, 2),
           "baseline_step_ms_post": round(base_post_ms, 2),
           "async_unblock_gc_ms_each": [round(g, 1) for g in unblock_gc],
-          "gc_ms_in_window": round(gc_window_ms, 1), "sync_take_s": round(sync_s, 3),
+          "gc_ms_in_window": round(gc_window_ms, 1), "cgroup_cpu_in_window": cgroup, "sync_take_s": round(sync_s, 3),
           "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 2), "async_drain_s": round(drain, 3),
           "cold_async_unblock_ms": [round(c[0] * 1e3, 1) for c in cold],
@@ -285,6 +337,10 @@ def main() -> None:
           "window_steps": len(during) + len(gap) + extra,
           "train_time_lost_ms": round(lost * 1e3, 1),
           "train_time_lost_vs_sync_take": round(lost / sync_s, 3),
+          "train_time_lost_local_ms": round(lost_local_ms, 1),
+          "train_time_lost_local_vs_sync_take": round(lost_local_ms / 1e3 / sync_s, 3),
+          "train_time_lost_local_ms_each": [round(x * 1e3, 1) for x in lost_local],
+          "slowdown_local_median_each": [round(x, 4) for x in slow_local],
           "restore_bitwise_ok": bool(okt.item()), "stored_bytes": stored,
           "data": "synthetic tokens, random init"})
     sync(dev)

@@ -14,8 +14,9 @@
 //                  device->host copy (ROCr copy engine, no CUs), queue it;
 //   wait thread    waits the copies in submission order, hands chunks to
 //                  the writers;
-//   writers        pwrite() chunks at their file offsets (page cache), return
-//                  slots; the last chunk of a blob trims the file to size,
+//   writers        pwrite() chunks at their file offsets (page cache, or
+//                  O_DIRECT straight from the pinned slot), return slots;
+//                  the last chunk of a blob trims the file to size,
 //                  optionally fdatasync()s it and closes it.
 //
 // No Python runs until the caller collects the result: the trainer keeps the
@@ -27,7 +28,9 @@
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <sys/types.h>
 #include <unistd.h>
 
@@ -63,6 +66,21 @@ constexpr int kDrainHashSlot = 1001;
 constexpr int kHashLag = 256;         // results collected this many blobs behind
 constexpr int kFlagSync = 1;
 constexpr int kFlagHash = 2;
+constexpr int kFlagDirect = 4;  // O_DIRECT: the engines' slots go to the device, no CPU copy
+constexpr uint64_t kDirectAlign = 4096;
+constexpr int kNiceShift = 8;  // flags bits 8..15: nice increment of the drain threads
+
+// Lower this thread's CPU priority by `inc` (Linux: per-thread nice).  The
+// drain's threads then yield a shared core to the trainer's launch thread
+// instead of taking half of it; an unprivileged process may always do this.
+void lower_priority(int inc) {
+  if (inc <= 0) return;
+  const pid_t tid = static_cast<pid_t>(syscall(SYS_gettid));
+  errno = 0;
+  const int cur = getpriority(PRIO_PROCESS, tid);
+  if (errno != 0) return;
+  setpriority(PRIO_PROCESS, tid, std::min(cur + inc, 19));
+}
 
 int mkdirs(const std::string& path) {
   // parent directories of `path`
@@ -79,6 +97,7 @@ struct Blob {
   uint64_t nbytes;
   std::string path;
   int fd = -1;
+  bool direct = false;
   std::atomic<int> chunks_left{0};
   uint64_t sum = 0;
   int hash_handle = -1;
@@ -138,6 +157,7 @@ void close_blob(Job* j, Blob& b) {
 }
 
 void dma_thread(Job* j) {
+  lower_priority((j->flags >> kNiceShift) & 0xff);
   void* stream = hsg_copy_stream(j->dev, kDrainCopySlot);
   int hashed = 0, collected = 0;
   const int nb = static_cast<int>(j->blobs.size());
@@ -152,7 +172,11 @@ void dma_thread(Job* j) {
   for (int i = 0; i < nb && !j->err.load(); ++i) {
     Blob& b = j->blobs[i];
     int r = mkdirs(b.path);
-    if (r == 0) {
+    if (r == 0 && (j->flags & kFlagDirect)) {
+      b.fd = open(b.path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC | O_DIRECT, 0644);
+      b.direct = b.fd >= 0;  // EINVAL: the filesystem has no O_DIRECT (tmpfs)
+    }
+    if (r == 0 && b.fd < 0) {
       b.fd = open(b.path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
       if (b.fd < 0) r = -errno;
     }
@@ -210,6 +234,7 @@ void dma_thread(Job* j) {
 }
 
 void wait_thread(Job* j) {
+  lower_priority((j->flags >> kNiceShift) & 0xff);
   for (;;) {
     Chunk c;
     {
@@ -236,6 +261,7 @@ void wait_thread(Job* j) {
 }
 
 void writer_thread(Job* j) {
+  lower_priority((j->flags >> kNiceShift) & 0xff);
   for (;;) {
     Chunk c;
     {
@@ -248,17 +274,25 @@ void writer_thread(Job* j) {
     Blob& b = j->blobs[c.blob];
     if (!j->err.load()) {
       const char* p = static_cast<const char*>(j->slots[c.slot]);
+      // O_DIRECT writes whole 4 KiB blocks: the tail chunk is padded with
+      // slot bytes past its end, which the blob's final ftruncate drops
+      const uint64_t len = b.direct ? (c.n + kDirectAlign - 1) / kDirectAlign * kDirectAlign : c.n;
       uint64_t done = 0;
-      while (done < c.n) {
-        const ssize_t w = pwrite(b.fd, p + done, c.n - done, off_t(c.off + done));
+      while (done < len) {
+        const ssize_t w = pwrite(b.fd, p + done, len - done, off_t(c.off + done));
         if (w < 0) {
           if (errno == EINTR) continue;
+          if (errno == EINVAL && b.direct) {
+            // the device wants a larger alignment: continue buffered
+            const int fl = fcntl(b.fd, F_GETFL);
+            if (fl >= 0 && fcntl(b.fd, F_SETFL, fl & ~O_DIRECT) == 0) continue;
+          }
           j->fail(-errno, "pwrite", b.path);
           break;
         }
         done += uint64_t(w);
       }
-      j->bytes_written.fetch_add(done);
+      j->bytes_written.fetch_add(std::min(done, c.n));
     }
     {
       std::lock_guard<std::mutex> g(j->mu);
@@ -280,7 +314,10 @@ extern "C" {
 // sizes[i]) -> file paths[i] (created with parent directories, overwritten
 // in place, trimmed to size).  `nslots` pinned slots of `slot_bytes` move
 // the data; `nwriters` threads write it.  flags: 1 = fdatasync every file,
-// 2 = hs64 hash every blob on the GPU (narrow grid `max_hash_grid`).
+// 2 = hs64 hash every blob on the GPU (narrow grid `max_hash_grid`), 4 =
+// O_DIRECT files (the pinned slots go to the device with no CPU copy and no
+// page cache; buffered where the filesystem refuses it), bits 8..15 = nice
+// increment of every drain thread.
 // Returns a handle (> 0) for hsg_drain_wait, or 0 with *err set.
 void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* sizes,
                       const char* const* paths, uint64_t slot_bytes, int nslots, int nwriters,
@@ -294,7 +331,8 @@ void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* size
   j->dev = dev;
   j->flags = flags;
   j->max_hash_grid = max_hash_grid;
-  j->slot_bytes = std::max<uint64_t>(slot_bytes, 1 << 20);
+  j->slot_bytes = (std::max<uint64_t>(slot_bytes, 1 << 20) + kDirectAlign - 1) / kDirectAlign *
+                  kDirectAlign;
   j->blobs = std::vector<Blob>(n);
   for (int i = 0; i < n; ++i) {
     j->blobs[i].src = srcs[i];
@@ -313,6 +351,7 @@ void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* size
     }
     j->slots.push_back(p);
     j->free_slots.push_back(s);
+    if (reinterpret_cast<uintptr_t>(p) % kDirectAlign) j->flags &= ~kFlagDirect;
   }
   j->threads.emplace_back(dma_thread, j);
   j->threads.emplace_back(wait_thread, j);

@@ -6,8 +6,8 @@ pinned slots -> ``pwrite``, per-blob hs64 hashes on the GPU, optional
 fdatasync -- in native threads, so the training loop keeps the GIL and the
 compute units while a checkpoint drains.  Eligible: a raw blob (no HSZ1
 codec, buffer-protocol serializer) whose bytes sit contiguously in the arena
-(``frozen_region``, engine/hbm_staging.py), written by the FS plugin without
-O_DIRECT.  Everything else drains through the Python pipeline as before.
+(``frozen_region``, engine/hbm_staging.py), written by the FS plugin
+(buffered, or O_DIRECT straight from the pinned slots).  Everything else drains through the Python pipeline as before.
 
 Reference counterpart: `/root/reference/torchsnapshot/snapshot.py:891-933`
 (the commit thread draining pending storage I/O) and
@@ -64,7 +64,7 @@ def split(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[List[WriteReq],
 def drain(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[Dict[str, int], int]:
     """Write every request's frozen region to its file; returns ({blob path:
     hs64}, bytes written).  Blocks (call it off the event loop)."""
-    root, fsync = _root(storage)
+    root, fsync, direct = _root(storage)
     by_dev: Dict[int, List[WriteReq]] = {}
     for wr in reqs:
         arena = wr.buffer_stager.frozen_region[0]
@@ -84,7 +84,8 @@ def drain(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[Dict[str, int],
             blobs.append((arena.data_ptr() + off, nbytes, os.path.join(root, wr.path)))
         job = native.NativeDrain(dev, blobs, knobs.get_drain_slot_bytes(),
                                  knobs.get_drain_slots(), knobs.get_drain_writers(), fsync,
-                                 want_sums, knobs.get_hash_grid())
+                                 want_sums, knobs.get_hash_grid(), knobs.get_drain_nice(),
+                                 direct)
         partial, written = job.wait()
         total += written
         if want_sums:

@@ -22,6 +22,17 @@ MI355X-specific knobs:
 * ``HIPSNAPSHOT_HBM_STAGING_RESERVE_BYTES`` (8 GiB) -- HBM left free for training.
 * ``HIPSNAPSHOT_HBM_STAGING_MAX_BYTES`` (unlimited) -- cap on the async-take HBM
   arena; requests beyond it are host-staged before ``async_take`` returns.
+* ``HIPSNAPSHOT_HBM_ARENA_KEEP`` (1) -- keep the async-take HBM arena between
+  takes (``hipsnapshot.release_hbm_arena()`` frees it).
+* ``HIPSNAPSHOT_NATIVE_DRAIN`` (1) -- drain raw frozen blobs to local files in
+  C++ threads (``csrc/hsdrain.hip``); ``HIPSNAPSHOT_DRAIN_SLOT_BYTES`` (32 MiB),
+  ``_DRAIN_SLOTS`` (12), ``_DRAIN_WRITERS`` (min(8, io threads)),
+  ``_DRAIN_NICE`` (10: nice increment of its threads), ``_DRAIN_DIRECT_IO`` (0:
+  O_DIRECT files, no page-cache copy).
+* ``HIPSNAPSHOT_ASYNC_DEVICE_CODEC`` (raw) -- ``same``: an async take encodes
+  its frozen device state like a blocking take.
+* ``HIPSNAPSHOT_REBALANCE`` (0) -- move whole blobs from loaded ranks to idle
+  ones over xGMI before a sync take writes (``parallel/rebalance.py``).
 * ``HIPSNAPSHOT_SLAB_ALIGN`` (256) -- byte alignment of slab members.
 * ``HIPSNAPSHOT_TRUST_OBJECTS`` (0) -- allow full unpickling of ``object``
   entries written by OTHER tools (our own writes are trusted by the reader).
@@ -295,6 +306,19 @@ def get_drain_slots() -> int:
 
 def get_drain_writers() -> int:
     return max(1, _get_int("DRAIN_WRITERS", min(8, get_io_threads())))
+
+
+def get_drain_nice() -> int:
+    """Nice increment of the native drain's threads (0-19, default 10): they
+    yield a shared core to the training loop's launch thread."""
+    return max(0, min(19, _get_int("DRAIN_NICE", 10)))
+
+
+def drain_direct_io() -> bool:
+    """O_DIRECT files for the native drain of an async take: no CPU copy into
+    the page cache (and none of its cache / memory-bandwidth pressure on the
+    training process), at the storage device's write rate."""
+    return _get_bool("DRAIN_DIRECT_IO", False)
 
 
 def async_device_codec() -> str:

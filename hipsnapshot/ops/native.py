@@ -728,7 +728,7 @@ class NativeDrain:
 
     def __init__(self, dev: int, blobs: Sequence[Tuple[int, int, str]], slot_bytes: int,
                  nslots: int, nwriters: int, fsync: bool, hash_blobs: bool,
-                 max_hash_grid: int) -> None:
+                 max_hash_grid: int, nice: int = 0, direct: bool = False) -> None:
         lib = require_gpu_lib()
         n = len(blobs)
         self.n = n
@@ -736,7 +736,8 @@ class NativeDrain:
         self._sizes = (c_uint64 * max(n, 1))(*[b[1] for b in blobs])
         self._paths = (c_char_p * max(n, 1))(*[os.fsencode(b[2]) for b in blobs])
         err = c_int(0)
-        flags = (1 if fsync else 0) | (2 if hash_blobs else 0)
+        flags = (1 if fsync else 0) | (2 if hash_blobs else 0) | (4 if direct else 0) | \
+            (max(0, min(nice, 19)) << 8)
         self._h = lib.hsg_drain_start(dev, n, self._srcs, self._sizes, self._paths,
                                       slot_bytes, nslots, nwriters, flags, max_hash_grid,
                                       ctypes.byref(err))

@@ -102,12 +102,10 @@ class FSStoragePlugin(StoragePlugin):
         return os.path.join(self.root, path)
 
     def native_drain_root(self):
-        """(root, fsync) when an async take's frozen blobs may be written by
-        the native drain (engine/native_drain.py): plain buffered files;
-        O_DIRECT blobs keep the engine's aligned-write path."""
-        if self.direct_io:
-            return None
-        return self.root, self.fsync
+        """(root, fsync, O_DIRECT) for the native drain of an async take's
+        frozen blobs (engine/native_drain.py).  O_DIRECT when this plugin
+        writes O_DIRECT or ``HIPSNAPSHOT_DRAIN_DIRECT_IO`` asks for it."""
+        return self.root, self.fsync, self.direct_io or knobs.drain_direct_io()
 
     # -- StoragePlugin -------------------------------------------------------
 

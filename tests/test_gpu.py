@@ -1075,14 +1075,49 @@ def _blob_files(root):
     return out
 
 
-@pytest.mark.parametrize("fsync", [False, True])
-def test_native_drain_matches_python_drain(gpu, tmp_path, fsync, monkeypatch):
+def _odirect_dir(tmp_path):
+    """A directory whose filesystem takes O_DIRECT (tmpfs does not)."""
+    import shutil
+    import uuid
+
+    for d in (tmp_path, os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                     ".odirect_tmp", uuid.uuid4().hex)):
+        os.makedirs(d, exist_ok=True)
+        try:
+            fd = os.open(os.path.join(d, "probe"), os.O_WRONLY | os.O_CREAT | os.O_DIRECT)
+            os.close(fd)
+            os.unlink(os.path.join(d, "probe"))
+            return str(d), (lambda: None) if d == tmp_path else (lambda: shutil.rmtree(d))
+        except OSError:
+            continue
+    pytest.skip("no filesystem with O_DIRECT")
+
+
+@pytest.mark.parametrize("fsync,direct", [(False, False), (True, False), (False, True)])
+def test_native_drain_matches_python_drain(gpu, tmp_path, fsync, direct, monkeypatch):
     """The native drain writes byte-identical blobs (slab gaps zero, strided
-    views packed) to the Python drain, records the same hs64 checksums,
+    views packed) to the Python drain -- buffered, fdatasync'd or O_DIRECT
+    (tail blocks padded, then trimmed) -- records the same hs64 checksums,
     is consistent under in-place updates right after async_take, and is
     actually the path that ran."""
     from hipsnapshot.engine import native_drain
     from hipsnapshot.verify import verify_snapshot
+
+    cleanup = lambda: None  # noqa: E731
+    if direct:
+        tmp_path, cleanup = _odirect_dir(tmp_path)
+        import pathlib
+
+        tmp_path = pathlib.Path(tmp_path)
+        monkeypatch.setenv("HIPSNAPSHOT_DRAIN_DIRECT_IO", "1")
+    try:
+        _native_vs_python_drain(gpu, tmp_path, fsync, monkeypatch, native_drain,
+                                verify_snapshot)
+    finally:
+        cleanup()
+
+
+def _native_vs_python_drain(gpu, tmp_path, fsync, monkeypatch, native_drain, verify_snapshot):
 
     calls = []
     orig = native_drain.drain
