@@ -241,7 +241,19 @@ def store(key: tuple, resident: Dict[str, Any], object_entries: Dict[str, Entry]
             return None  # an async take still drains with it: keep that one
         _plans[key] = plan
         stats["stores"] += 1
+    global _stored_since_collect
+    _stored_since_collect = True
     return plan
+
+
+_stored_since_collect = False
+
+
+def take_stored_flag() -> bool:
+    """True once after a take stored a new plan (see ``tracing.paused_gc``)."""
+    global _stored_since_collect
+    f, _stored_since_collect = _stored_since_collect, False
+    return f
 
 
 _watched: set = set()  # ids of app-state objects with a finalizer

@@ -31,6 +31,8 @@ MI355X-specific knobs:
   O_DIRECT files, no page-cache copy).
 * ``HIPSNAPSHOT_ASYNC_DEVICE_CODEC`` (raw) -- ``same``: an async take encodes
   its frozen device state like a blocking take.
+* ``HIPSNAPSHOT_GC_AFTER_PLAN`` (1) -- one full Python GC pass at the end of a
+  take that built a new take plan, not in a later take or training step.
 * ``HIPSNAPSHOT_REBALANCE`` (0) -- move whole blobs from loaded ranks to idle
   ones over xGMI before a sync take writes (``parallel/rebalance.py``).
 * ``HIPSNAPSHOT_SLAB_ALIGN`` (256) -- byte alignment of slab members.
@@ -312,6 +314,12 @@ def get_drain_nice() -> int:
     """Nice increment of the native drain's threads (0-19, default 10): they
     yield a shared core to the training loop's launch thread."""
     return max(0, min(19, _get_int("DRAIN_NICE", 10)))
+
+
+def gc_after_plan() -> bool:
+    """One full Python GC pass at the end of a take that built a new take
+    plan (utils/tracing.paused_gc)."""
+    return _get_bool("GC_AFTER_PLAN", True)
 
 
 def drain_direct_io() -> bool:

@@ -207,7 +207,17 @@ def paused_gc():
     requests, futures); in a training process with a large heap that triggers
     generation-2 collections costing 10-100 ms each in the middle of a take
     (measured: parsing an 8-rank manifest 129 ms with GC vs 16 ms without).
-    Garbage created meanwhile is collected after the section."""
+    Garbage created meanwhile is collected after the section.
+
+    A take that built (and cached) a new take plan ends with one full
+    collection (``HIPSNAPSHOT_GC_AFTER_PLAN``, default on).  The plan's
+    objects are long-lived; CPython runs a full pass once the objects that
+    survived into the oldest generation since the last full pass reach 25 %
+    of those counted by it, and a training loop allocates almost nothing
+    else, so that pass (160-200 ms with Llama-3-8B + AdamW loaded,
+    profiles/r3/overlap/) would otherwise fall into the NEXT take's unblock
+    or a training step.  Collecting at the end of the plan-building take puts
+    the one-time cost where the first take's other one-time costs are."""
     import gc
     import sys
 
@@ -226,3 +236,8 @@ def paused_gc():
             sys.setswitchinterval(prev)
         if was:
             gc.enable()
+            from ..engine import plan_cache
+
+            if plan_cache.take_stored_flag() and knobs.gc_after_plan():
+                with timeline.span("gc_after_plan"):
+                    gc.collect()

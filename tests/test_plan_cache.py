@@ -257,3 +257,30 @@ def test_failed_planning_releases_reused_plan(tmp_path, resident, monkeypatch, i
     for k, v in ref.items():
         if isinstance(v, torch.Tensor):
             assert torch.equal(got[k], v), k
+
+
+@pytest.mark.parametrize("is_async", [False, True])
+def test_plan_building_take_collects_once(tmp_path, resident, monkeypatch, is_async):
+    """The take that stores a new plan ends with ONE full GC pass; takes
+    that reuse it run none (the pass would otherwise land in a later take's
+    unblock or a training step); the knob turns it off."""
+    calls = []
+    real = gc.collect
+    monkeypatch.setattr(gc, "collect", lambda *a, **k: calls.append(a) or real(*a, **k))
+    sd = _state(resident)
+
+    def take(i):
+        if is_async:
+            Snapshot.async_take(str(tmp_path / f"s{i}"), {"sd": sd}).wait()
+        else:
+            Snapshot.take(str(tmp_path / f"s{i}"), {"sd": sd})
+
+    take(0)
+    assert plan_cache.stats["stores"] == 1 and len(calls) == 1
+    take(1)
+    take(2)
+    assert plan_cache.stats["hits"] == 2 and len(calls) == 1
+    plan_cache.clear()
+    with override_knob("GC_AFTER_PLAN", "0"):
+        take(3)
+    assert plan_cache.stats["stores"] == 2 and len(calls) == 1
