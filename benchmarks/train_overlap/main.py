@@ -208,6 +208,7 @@ def main() -> None:
     pending, taken, t_ck = None, 0, 0.0
     during, unblocks, drains = [], [], []
     during_k, gap_k = [], []  # per checkpoint: steps during its drain / after it
+    drain_stats = []  # per checkpoint: the native drain's phase seconds
     ref, clone_s = None, 0.0
     def all_done(p) -> bool:
         """``p.done()`` agreed across ranks (a step runs FSDP collectives:
@@ -231,6 +232,9 @@ def main() -> None:
             if pending is not None:
                 pending.wait()
                 drains.append(time.perf_counter() - t_ck)
+                from hipsnapshot.engine import native_drain
+
+                drain_stats.append(dict(native_drain.last_stats))
                 if taken < k_total:
                     gap_k.append([step() for _ in range(args.gap_steps)])
                     gap += gap_k[-1]
@@ -326,6 +330,7 @@ def main() -> None:
           "cold_async_total_s": [round(c[1], 3) for c in cold],
           "checkpoints": k_total, "async_unblock_ms_each": [round(u * 1e3, 2) for u in unblocks],
           "async_drain_s_each": [round(d, 3) for d in drains],
+          "native_drain_stats_each": drain_stats,
           "steps_during_drain": n_during, "step_ms_during_drain_mean": round(mean_ms, 2),
           "step_ms_during_drain_median": round(med_ms, 2),
           "step_ms_during_drain_max": round(max_ms, 2),

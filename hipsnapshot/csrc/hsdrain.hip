@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <condition_variable>
 #include <cstdint>
@@ -52,6 +53,7 @@ int hsg_sdma_d2h_submit(int dev, void* dst, const void* src, uint64_t n, void* s
                         uint64_t* handle);
 int hsg_sdma_wait(uint64_t handle);
 void* hsg_copy_stream(int dev, int slot);
+int hsg_stream_priority(int dev, int slot, int high);
 int hsg_hash64(int dev, int slot, int after_slot, const void* p, uint64_t n,
                uint64_t first_word, int max_grid, int* handle);
 int hsg_hash64_result(int dev, int slot, int handle, uint64_t* out);
@@ -62,11 +64,13 @@ int hsg_pinned_release(void* p);
 namespace {
 
 constexpr int kDrainCopySlot = 1000;  // idle stream the SDMA submits order after
-constexpr int kDrainHashSlot = 1001;
+constexpr int kDrainHashSlot = 1001;     // high priority
+constexpr int kDrainHashSlotLow = 1002;  // default priority (kFlagHashLowPrio)
 constexpr int kHashLag = 256;         // results collected this many blobs behind
 constexpr int kFlagSync = 1;
 constexpr int kFlagHash = 2;
-constexpr int kFlagDirect = 4;  // O_DIRECT: the engines' slots go to the device, no CPU copy
+constexpr int kFlagDirect = 4;
+constexpr int kFlagHashLowPrio = 8;  // keep the hash stream at default priority  // O_DIRECT: the engines' slots go to the device, no CPU copy
 constexpr uint64_t kDirectAlign = 4096;
 constexpr int kNiceShift = 8;  // flags bits 8..15: nice increment of the drain threads
 
@@ -111,7 +115,30 @@ struct Chunk {
   uint64_t handle;
 };
 
+// Where a drain's time goes (seconds, summed over the threads doing it):
+// returned by hsg_drain_wait for the bench / timeline.
+enum Stat {
+  kSlotWait,     // dma thread waiting for a free pinned slot (writers behind)
+  kHashCollect,  // dma thread waiting for hash results
+  kHashLaunch,   // dma thread launching hashes
+  kSubmit,       // dma thread submitting SDMA copies
+  kSdmaWait,     // wait thread waiting for copies (engines behind)
+  kPwrite,       // writers in pwrite
+  kClose,        // writers trimming / syncing / closing files
+  kOpen,         // dma thread creating directories and opening files
+  kWall,
+  kNumStats
+};
+
+uint64_t now_ns() {
+  return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
+      std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
 struct Job {
+  std::atomic<uint64_t> ns[kNumStats] = {};
+  uint64_t t_start = 0;
+  void add(Stat k, uint64_t t0) { ns[k].fetch_add(now_ns() - t0); }
   int dev;
   int flags;
   int max_hash_grid;
@@ -147,6 +174,7 @@ struct Job {
 
 void close_blob(Job* j, Blob& b) {
   if (b.fd < 0) return;
+  const uint64_t t0 = now_ns();
   struct stat st;
   if (fstat(b.fd, &st) == 0 && uint64_t(st.st_size) != b.nbytes) {
     if (ftruncate(b.fd, off_t(b.nbytes)) != 0) j->fail(-errno, "ftruncate", b.path);
@@ -154,23 +182,31 @@ void close_blob(Job* j, Blob& b) {
   if ((j->flags & kFlagSync) && fdatasync(b.fd) != 0) j->fail(-errno, "fdatasync", b.path);
   close(b.fd);
   b.fd = -1;
+  j->add(kClose, t0);
 }
 
 void dma_thread(Job* j) {
   lower_priority((j->flags >> kNiceShift) & 0xff);
+  // hashes run at high stream priority: a narrow grid that must not wait
+  // for a training step's workgroups to drain (hsg_stream_priority)
+  const int hash_slot = (j->flags & kFlagHashLowPrio) ? kDrainHashSlotLow : kDrainHashSlot;
+  if (hash_slot == kDrainHashSlot) hsg_stream_priority(j->dev, kDrainHashSlot, 1);
   void* stream = hsg_copy_stream(j->dev, kDrainCopySlot);
   int hashed = 0, collected = 0;
   const int nb = static_cast<int>(j->blobs.size());
   auto collect = [&](int upto) {
+    const uint64_t t0 = now_ns();
     for (; collected < upto && collected < hashed; ++collected) {
       Blob& b = j->blobs[collected];
       if (b.hash_handle < 0) continue;
-      if (hsg_hash64_result(j->dev, kDrainHashSlot, b.hash_handle, &b.sum) != 0)
+      if (hsg_hash64_result(j->dev, hash_slot, b.hash_handle, &b.sum) != 0)
         j->fail(-EIO, "hash result", b.path);
     }
+    j->add(kHashCollect, t0);
   };
   for (int i = 0; i < nb && !j->err.load(); ++i) {
     Blob& b = j->blobs[i];
+    uint64_t t0 = now_ns();
     int r = mkdirs(b.path);
     if (r == 0 && (j->flags & kFlagDirect)) {
       b.fd = open(b.path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC | O_DIRECT, 0644);
@@ -180,17 +216,20 @@ void dma_thread(Job* j) {
       b.fd = open(b.path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
       if (b.fd < 0) r = -errno;
     }
+    j->add(kOpen, t0);
     if (r != 0) {
       j->fail(r, "open", b.path);
       break;
     }
+    t0 = now_ns();
     if (j->flags & kFlagHash) {
-      if (hsg_hash64(j->dev, kDrainHashSlot, -1, reinterpret_cast<const void*>(b.src),
+      if (hsg_hash64(j->dev, hash_slot, -1, reinterpret_cast<const void*>(b.src),
                      b.nbytes, 0, j->max_hash_grid, &b.hash_handle) != 0) {
         j->fail(-EIO, "hash launch", b.path);
         break;
       }
     }
+    j->add(kHashLaunch, t0);
     hashed = i + 1;
     collect(hashed - kHashLag);
     const uint64_t nchunks = b.nbytes ? (b.nbytes + j->slot_bytes - 1) / j->slot_bytes : 0;
@@ -202,6 +241,7 @@ void dma_thread(Job* j) {
     }
     for (uint64_t c = 0; c < nchunks && !j->err.load(); ++c) {
       int slot;
+      uint64_t tw = now_ns();
       {
         std::unique_lock<std::mutex> lk(j->mu);
         j->cv.wait(lk, [&] { return !j->free_slots.empty() || j->err.load(); });
@@ -209,11 +249,14 @@ void dma_thread(Job* j) {
         slot = j->free_slots.back();
         j->free_slots.pop_back();
       }
+      j->add(kSlotWait, tw);
+      tw = now_ns();
       const uint64_t off = c * j->slot_bytes;
       const uint64_t n = std::min(j->slot_bytes, b.nbytes - off);
       uint64_t h = 0;
       r = hsg_sdma_d2h_submit(j->dev, j->slots[slot], reinterpret_cast<const void*>(b.src + off),
                               n, stream, &h);
+      j->add(kSubmit, tw);
       if (r != 0) {
         j->fail(-EIO, "sdma submit", b.path);
         break;
@@ -246,7 +289,9 @@ void wait_thread(Job* j) {
     }
     // every submitted copy is waited for, even after an error: the engine
     // must be done with a slot before it is reused or freed
+    const uint64_t t0 = now_ns();
     if (hsg_sdma_wait(c.handle) != 0) j->fail(-EIO, "sdma copy", j->blobs[c.blob].path);
+    j->add(kSdmaWait, t0);
     {
       std::lock_guard<std::mutex> g(j->mu);
       j->to_write.push_back(c);
@@ -278,6 +323,7 @@ void writer_thread(Job* j) {
       // slot bytes past its end, which the blob's final ftruncate drops
       const uint64_t len = b.direct ? (c.n + kDirectAlign - 1) / kDirectAlign * kDirectAlign : c.n;
       uint64_t done = 0;
+      const uint64_t t0 = now_ns();
       while (done < len) {
         const ssize_t w = pwrite(b.fd, p + done, len - done, off_t(c.off + done));
         if (w < 0) {
@@ -292,6 +338,7 @@ void writer_thread(Job* j) {
         }
         done += uint64_t(w);
       }
+      j->add(kPwrite, t0);
       j->bytes_written.fetch_add(std::min(done, c.n));
     }
     {
@@ -316,7 +363,8 @@ extern "C" {
 // the data; `nwriters` threads write it.  flags: 1 = fdatasync every file,
 // 2 = hs64 hash every blob on the GPU (narrow grid `max_hash_grid`), 4 =
 // O_DIRECT files (the pinned slots go to the device with no CPU copy and no
-// page cache; buffered where the filesystem refuses it), bits 8..15 = nice
+// page cache; buffered where the filesystem refuses it), 8 = hash stream at
+// default instead of high priority, bits 8..15 = nice
 // increment of every drain thread.
 // Returns a handle (> 0) for hsg_drain_wait, or 0 with *err set.
 void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* sizes,
@@ -353,6 +401,7 @@ void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* size
     j->free_slots.push_back(s);
     if (reinterpret_cast<uintptr_t>(p) % kDirectAlign) j->flags &= ~kFlagDirect;
   }
+  j->t_start = now_ns();
   j->threads.emplace_back(dma_thread, j);
   j->threads.emplace_back(wait_thread, j);
   for (int w = 0; w < std::max(nwriters, 1); ++w) j->threads.emplace_back(writer_thread, j);
@@ -362,10 +411,15 @@ void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* size
 // Wait for the drain (blocking; Python calls it without the GIL).  Returns 0
 // or the first error (negative errno); `sums` (n entries, may be null)
 // receives each blob's hs64 partial sum; `msg` (>= 256 bytes, may be null)
-// the error text.  Frees the job: call exactly once per handle.
-int hsg_drain_wait(void* handle, uint64_t* sums, uint64_t* bytes_written, char* msg) {
+// the error text; `stats` (kNumStats doubles, may be null) the seconds per
+// Stat.  Frees the job: call exactly once per handle.
+int hsg_drain_wait(void* handle, uint64_t* sums, uint64_t* bytes_written, char* msg,
+                   double* stats) {
   Job* j = static_cast<Job*>(handle);
   for (auto& t : j->threads) t.join();
+  j->add(kWall, j->t_start);
+  if (stats)
+    for (int k = 0; k < kNumStats; ++k) stats[k] = 1e-9 * double(j->ns[k].load());
   for (auto& b : j->blobs)
     if (b.fd >= 0) close(b.fd);
   for (void* p : j->slots) hsg_pinned_release(p);

@@ -1041,6 +1041,8 @@ std::mutex g_stream_mu;
 std::map<StreamKey, hipStream_t> g_streams;
 std::map<StreamKey, hipEvent_t> g_events;
 
+std::map<StreamKey, int> g_stream_prio;  // slots created with a priority (hsg_stream_priority)
+
 int get_stream(int dev, int slot, hipStream_t* out, hipEvent_t* ev) {
   std::lock_guard<std::mutex> g(g_stream_mu);
   StreamKey k{dev, slot};
@@ -1050,7 +1052,11 @@ int get_stream(int dev, int slot, hipStream_t* out, hipEvent_t* ev) {
     // default priority: lowest-priority copy streams made a concurrent
     // training step 45 % slower instead of 18 % (profiles/overlap/priority.md)
     hipStream_t s;
-    HS_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    auto pr = g_stream_prio.find(k);
+    if (pr != g_stream_prio.end())
+      HS_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pr->second));
+    else
+      HS_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     hipEvent_t e;
     HS_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     g_streams[k] = s;
@@ -1439,6 +1445,24 @@ int hsg_hash64_result(int dev, int slot, int handle, uint64_t* out) {
                           hipMemcpyDeviceToHost, s));
   HS_CHECK(hipStreamSynchronize(s));
   *out = h->host[handle];
+  return 0;
+}
+
+// Create stream (dev, slot) at the device's highest priority (high != 0)
+// when it is first used.  The native drain's hash stream: its tiny hs64
+// launches and 8-byte read-backs otherwise queue behind a saturating
+// training step's workgroups -- a GEMM loop on another stream cut a drain
+// with hashing from 36 to 13.5 GB/s, without hashing it kept 35.6 GB/s
+// (scripts/drain_contention_probe.py, profiles/r3/drain_probe/).  Returns
+// 1 if the stream already existed (its priority is unchanged).
+int hsg_stream_priority(int dev, int slot, int high) {
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  StreamKey k{dev, slot};
+  if (g_streams.count(k)) return 1;
+  int least = 0, greatest = 0;
+  HS_CHECK(hipSetDevice(dev));
+  HS_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  g_stream_prio[k] = high ? greatest : least;
   return 0;
 }
 

@@ -29,6 +29,9 @@ from ..utils.tracing import timeline
 logger = logging.getLogger(__name__)
 
 
+last_stats: Dict[str, float] = {}  # the last drain's phase seconds (NativeDrain.STATS)
+
+
 def _root(storage: StoragePlugin):
     fn = getattr(storage, "native_drain_root", None)
     return fn() if fn is not None else None
@@ -91,5 +94,8 @@ def drain(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[Dict[str, int],
         if want_sums:
             for wr, (_p, n, _path), s in zip(wrs, blobs, partial):
                 sums[wr.path] = checksum.finish(s, n)
-        timeline.add("native_drain", "io", t0, time.perf_counter(), n=len(wrs), bytes=written)
+        timeline.add("native_drain", "io", t0, time.perf_counter(), n=len(wrs), bytes=written,
+                     **job.stats)
+        last_stats.clear()
+        last_stats.update(job.stats, blobs=len(wrs), bytes=written)
     return sums, total

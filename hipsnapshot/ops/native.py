@@ -265,7 +265,8 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                   ctypes.POINTER(c_char_p), c_uint64, c_int, c_int, c_int, c_int,
                   ctypes.POINTER(c_int)])
         _declare(lib, "hsg_drain_wait", c_int,
-                 [c_void_p, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64), c_char_p])
+                 [c_void_p, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64), c_char_p,
+                  ctypes.POINTER(ctypes.c_double)])
         _declare(lib, "hsg_drain_pending", c_int, [c_void_p])
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
@@ -728,7 +729,8 @@ class NativeDrain:
 
     def __init__(self, dev: int, blobs: Sequence[Tuple[int, int, str]], slot_bytes: int,
                  nslots: int, nwriters: int, fsync: bool, hash_blobs: bool,
-                 max_hash_grid: int, nice: int = 0, direct: bool = False) -> None:
+                 max_hash_grid: int, nice: int = 0, direct: bool = False,
+                 hash_high_priority: bool = True) -> None:
         lib = require_gpu_lib()
         n = len(blobs)
         self.n = n
@@ -737,6 +739,7 @@ class NativeDrain:
         self._paths = (c_char_p * max(n, 1))(*[os.fsencode(b[2]) for b in blobs])
         err = c_int(0)
         flags = (1 if fsync else 0) | (2 if hash_blobs else 0) | (4 if direct else 0) | \
+            (0 if hash_high_priority else 8) | \
             (max(0, min(nice, 19)) << 8)
         self._h = lib.hsg_drain_start(dev, n, self._srcs, self._sizes, self._paths,
                                       slot_bytes, nslots, nwriters, flags, max_hash_grid,
@@ -747,14 +750,20 @@ class NativeDrain:
     def pending(self) -> int:
         return require_gpu_lib().hsg_drain_pending(self._h) if self._h else 0
 
+    STATS = ("slot_wait", "hash_collect", "hash_launch", "sdma_submit", "sdma_wait", "pwrite",
+             "close", "open", "wall")
+
     def wait(self) -> Tuple[List[int], int]:
-        """Blocks (GIL released); returns (hs64 partial sums, bytes written)."""
+        """Blocks (GIL released); returns (hs64 partial sums, bytes written).
+        ``self.stats``: seconds per phase (summed over the threads in it)."""
         lib = require_gpu_lib()
         sums = (c_uint64 * max(self.n, 1))()
         written = c_uint64(0)
         msg = ctypes.create_string_buffer(256)
+        st = (ctypes.c_double * len(self.STATS))()
         h, self._h = self._h, None
-        r = lib.hsg_drain_wait(h, sums, ctypes.byref(written), msg)
+        r = lib.hsg_drain_wait(h, sums, ctypes.byref(written), msg, st)
+        self.stats = {k: round(v, 4) for k, v in zip(self.STATS, st)}
         if r != 0:
             text = msg.value.decode(errors="replace")
             if r < 0 and -r in errno.errorcode:

@@ -59,7 +59,7 @@ def main() -> None:
                 gemms[0] += 8
                 s.synchronize()
 
-    def run(hash_blobs: bool, load: bool) -> dict:
+    def run(hash_blobs: bool, load: bool, high: bool = True) -> dict:
         shutil.rmtree(args.dir, ignore_errors=True)
         os.makedirs(args.dir, exist_ok=True)
         th = None
@@ -71,7 +71,8 @@ def main() -> None:
             time.sleep(0.5)
         g0 = gemms[0]
         t0 = time.perf_counter()
-        job = native.NativeDrain(0, blobs, 32 << 20, 12, 8, False, hash_blobs, 16, nice=10)
+        job = native.NativeDrain(0, blobs, 32 << 20, 12, 8, False, hash_blobs, 16, nice=10,
+                                 hash_high_priority=high)
         _, written = job.wait()
         dt = time.perf_counter() - t0
         g1 = gemms[0]
@@ -79,15 +80,16 @@ def main() -> None:
             stop.set()
             th.join()
         flops = 2 * args.gemm ** 3 * (g1 - g0) / dt
-        return {"hash": hash_blobs, "gemm_load": load, "s": round(dt, 3),
+        return {"hash": hash_blobs, "hash_stream_high_prio": high if hash_blobs else None,
+                "gemm_load": load, "s": round(dt, 3), "phases": job.stats,
                 "GBps": round(written / dt / 1e9, 2),
                 "gemm_TFLOPs_during": round(flops / 1e12, 1) if load else None}
 
     out = []
     for load in (False, True):
-        for h in (False, True):
-            run(h, load)  # warm (files exist: in-place overwrite as in the bench)
-            out.append(run(h, load))
+        for h, high in ((False, True), (True, False), (True, True)):
+            run(h, load, high)  # warm (files exist: in-place overwrite as in the bench)
+            out.append(run(h, load, high))
             print(json.dumps(out[-1]), flush=True)
     # the GEMM loop alone
     stop.clear()
