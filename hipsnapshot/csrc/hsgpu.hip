@@ -533,17 +533,20 @@ hs_fp8_quant(const char* __restrict__ src, int32_t src_dtype, int64_t n,
       amax = fmaxf(amax, fabsf(v[j]));
     }
     amax = wave_max(amax);
-    // correctly rounded division everywhere (no reciprocal-multiply): the
-    // payload is bit-identical to the fp32 torch reference of the same rule
+    // two correctly rounded divisions per BLOCK (scale, then its reciprocal)
+    // and one multiply per element -- the torch reference (ops/quant.py
+    // _scale_and_quant) applies the same rule, so payloads are bit-identical;
+    // a division per element made this kernel VALU-bound (profiles/pmc_r2)
     const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
+    const float inv = 1.f / scale;
     if (lane == 0) scales[b] = scale;
     uint32_t words[(VPT + 3) / 4];
 #pragma unroll
     for (int w = 0; w < (VPT + 3) / 4; ++w) {
-      float a0 = fminf(fmaxf(v[4 * w + 0] / scale, -kFp8Max), kFp8Max);
-      float a1 = (4 * w + 1 < VPT) ? fminf(fmaxf(v[4 * w + 1] / scale, -kFp8Max), kFp8Max) : 0.f;
-      float a2 = (4 * w + 2 < VPT) ? fminf(fmaxf(v[4 * w + 2] / scale, -kFp8Max), kFp8Max) : 0.f;
-      float a3 = (4 * w + 3 < VPT) ? fminf(fmaxf(v[4 * w + 3] / scale, -kFp8Max), kFp8Max) : 0.f;
+      float a0 = fminf(fmaxf(v[4 * w + 0] * inv, -kFp8Max), kFp8Max);
+      float a1 = (4 * w + 1 < VPT) ? fminf(fmaxf(v[4 * w + 1] * inv, -kFp8Max), kFp8Max) : 0.f;
+      float a2 = (4 * w + 2 < VPT) ? fminf(fmaxf(v[4 * w + 2] * inv, -kFp8Max), kFp8Max) : 0.f;
+      float a3 = (4 * w + 3 < VPT) ? fminf(fmaxf(v[4 * w + 3] * inv, -kFp8Max), kFp8Max) : 0.f;
       int word = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
       word = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, word, true);
       words[w] = static_cast<uint32_t>(word);
@@ -893,15 +896,27 @@ hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
       const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
+      const float inv = 1.f / scale;
       const int64_t blk = tile * 8 + 2 * g4 + h;
       if (r == 0 && blk < nblocks) scales[blk] = scale;
+      float v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = q + 8 * g4 + 4 * h;
-        const int64_t e = (tile * 32 + row) * 32 + r;
-        const float v = fminf(fmaxf(acc[4 * g4 + q] / scale, -kFp8Max), kFp8Max);
-        if (e < n_pad) out[e] = static_cast<uint8_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
-      }
+      for (int q = 0; q < 4; ++q) v[q] = fminf(fmaxf(acc[4 * g4 + q] * inv, -kFp8Max), kFp8Max);
+      // byte q of `w` = row q + 8 g4 + 4 h, column r.  A 4x4 byte transpose
+      // over each quad of lanes (two DPP quad-perm exchanges + v_perm_b32)
+      // leaves lane r with row (r & 3) + 8 g4 + 4 h, columns (r & ~3) .. +3:
+      // one 4-B store per lane, 256 contiguous bytes per wave instruction,
+      // instead of 4 one-byte stores.
+      uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false));
+      w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], static_cast<int>(w), true));
+      uint32_t o = static_cast<uint32_t>(
+          __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0xB1, 0xF, 0xF, false));  // lane ^ 1
+      w = __builtin_amdgcn_perm(o, w, (r & 1) ? 0x03070105u : 0x06020400u);
+      o = static_cast<uint32_t>(
+          __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0x4E, 0xF, 0xF, false));  // lane ^ 2
+      w = __builtin_amdgcn_perm(o, w, (r & 2) ? 0x03020706u : 0x05040100u);
+      const int64_t row0 = (tile * 32 + (r & 3) + 8 * g4 + 4 * h) * 32;
+      if (row0 < n_pad) *reinterpret_cast<uint32_t*>(out + row0 + (r & ~3)) = w;
     }
   }
 }
@@ -1685,6 +1700,44 @@ void* hsg_managed_alloc(int dev, uint64_t n) {
 
 int hsg_managed_free(void* p) {
   HS_CHECK(hipFree(p));
+  return 0;
+}
+
+// ---- device memory shared with the drain helper process ---------------------
+//
+// The async-take arena is a block of torch's caching allocator, i.e. some
+// offset inside one hipMalloc allocation.  Export the allocation (IPC handle,
+// dmabuf-backed on this driver) plus the offset of `p` in it; the helper
+// (csrc/hsdrain_helper.cpp) maps the allocation once and keeps the mapping
+// while the arena is kept between takes.
+
+int hsg_ipc_export(const void* p, void* handle_out, uint64_t* offset, uint64_t* alloc_bytes) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  HS_CHECK(hipMemGetAddressRange(&base, &size, const_cast<void*>(p)));
+  hipIpcMemHandle_t h;
+  HS_CHECK(hipIpcGetMemHandle(&h, base));
+  std::memcpy(handle_out, &h, sizeof(h));
+  *offset = static_cast<uint64_t>(static_cast<const char*>(p) - static_cast<char*>(base));
+  *alloc_bytes = size;
+  return 0;
+}
+
+int hsg_ipc_handle_bytes() { return static_cast<int>(sizeof(hipIpcMemHandle_t)); }
+
+void* hsg_ipc_open(int dev, const void* handle) {
+  hipError_t se = hipSetDevice(dev);
+  if (se != hipSuccess) { set_err("hipSetDevice", se); return nullptr; }
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  void* p = nullptr;
+  hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) { set_err("hipIpcOpenMemHandle", e); return nullptr; }
+  return p;
+}
+
+int hsg_ipc_close(void* p) {
+  HS_CHECK(hipIpcCloseMemHandle(p));
   return 0;
 }
 

@@ -160,15 +160,31 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
 _kept: Dict[int, list] = {}
 
 
+def _drop_kept(t: torch.Tensor) -> None:
+    from . import drain_process
+
+    drain_process.forget_arena(t.data_ptr())  # the drain helper unmaps it
+
+
 def _arena(dev: int, total: int) -> torch.Tensor:
     k = _kept.get(dev)
     if k is not None and not k[1] and k[0].numel() >= total:
         k[1] = True
         return k[0][:max(total, 1)]
+    if k is not None and not k[1]:
+        _drop_kept(k[0])  # a smaller idle one is dropped
+        del _kept[dev]
+        k = None
     arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
-    if knobs.hbm_arena_keep() and (k is None or not k[1]):
-        _kept[dev] = [arena, True]  # (a smaller idle one is dropped)
+    if knobs.hbm_arena_keep() and k is None:
+        _kept[dev] = [arena, True]
     return arena
+
+
+def is_kept(arena: torch.Tensor) -> bool:
+    """Is ``arena`` (or a view at its start) the kept arena of its device?"""
+    k = _kept.get(arena.device.index if arena.device.index is not None else 0)
+    return k is not None and k[0].data_ptr() == arena.data_ptr()
 
 
 def arena_done(arenas) -> None:
@@ -185,7 +201,9 @@ def release_hbm_arena() -> int:
     freed = 0
     for dev in list(_kept):
         if not _kept[dev][1]:
-            freed += _kept.pop(dev)[0].numel()
+            t = _kept.pop(dev)[0]
+            _drop_kept(t)
+            freed += t.numel()
     return freed
 
 

@@ -64,6 +64,31 @@ def split(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[List[WriteReq],
     return nat, py
 
 
+def _run(dev: int, wrs: List[WriteReq], blobs, fsync: bool, want_sums: bool, direct: bool):
+    """One device's drain: in the helper process (HIPSNAPSHOT_DRAIN_PROCESS)
+    when it can take it, else in this process's native threads.  Returns
+    (hs64 partial sums, bytes written, stats, "helper" | "in_process")."""
+    args = (knobs.get_drain_slot_bytes(), knobs.get_drain_slots(), knobs.get_drain_writers())
+    flags = native.NativeDrain.flags(fsync, want_sums, direct, True, knobs.get_drain_nice())
+    arenas = {id(wr.buffer_stager.frozen_region[0]): wr.buffer_stager.frozen_region[0]
+              for wr in wrs}
+    if knobs.drain_process() and len({a.data_ptr() for a in arenas.values()}) == 1:
+        from . import drain_process
+        from .hbm_staging import is_kept
+
+        arena = next(iter(arenas.values()))
+        base = arena.data_ptr()
+        res = drain_process.drain(dev, base, is_kept(arena),
+                                  [(p - base, n, path) for p, n, path in blobs], *args, flags,
+                                  knobs.get_hash_grid())
+        if res is not None:
+            return (*res, "helper")
+    job = native.NativeDrain(dev, blobs, *args, fsync, want_sums, knobs.get_hash_grid(),
+                             knobs.get_drain_nice(), direct)
+    partial, written = job.wait()
+    return partial, written, job.stats, "in_process"
+
+
 def drain(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[Dict[str, int], int]:
     """Write every request's frozen region to its file; returns ({blob path:
     hs64}, bytes written).  Blocks (call it off the event loop)."""
@@ -85,17 +110,13 @@ def drain(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[Dict[str, int],
         for wr in wrs:
             arena, off, nbytes = wr.buffer_stager.frozen_region
             blobs.append((arena.data_ptr() + off, nbytes, os.path.join(root, wr.path)))
-        job = native.NativeDrain(dev, blobs, knobs.get_drain_slot_bytes(),
-                                 knobs.get_drain_slots(), knobs.get_drain_writers(), fsync,
-                                 want_sums, knobs.get_hash_grid(), knobs.get_drain_nice(),
-                                 direct)
-        partial, written = job.wait()
+        partial, written, stats, where = _run(dev, wrs, blobs, fsync, want_sums, direct)
         total += written
         if want_sums:
             for wr, (_p, n, _path), s in zip(wrs, blobs, partial):
                 sums[wr.path] = checksum.finish(s, n)
         timeline.add("native_drain", "io", t0, time.perf_counter(), n=len(wrs), bytes=written,
-                     **job.stats)
+                     where=where, **stats)
         last_stats.clear()
-        last_stats.update(job.stats, blobs=len(wrs), bytes=written)
+        last_stats.update(stats, blobs=len(wrs), bytes=written, where=where)
     return sums, total

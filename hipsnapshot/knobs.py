@@ -28,7 +28,8 @@ MI355X-specific knobs:
   C++ threads (``csrc/hsdrain.hip``); ``HIPSNAPSHOT_DRAIN_SLOT_BYTES`` (32 MiB),
   ``_DRAIN_SLOTS`` (12), ``_DRAIN_WRITERS`` (min(8, io threads)),
   ``_DRAIN_NICE`` (10: nice increment of its threads), ``_DRAIN_DIRECT_IO`` (0:
-  O_DIRECT files, no page-cache copy).
+  O_DIRECT files, no page-cache copy); ``_DRAIN_PROCESS`` (0: run that drain in a
+  helper process that maps the arena over IPC, ``engine/drain_process.py``).
 * ``HIPSNAPSHOT_ASYNC_DEVICE_CODEC`` (raw) -- ``same``: an async take encodes
   its frozen device state like a blocking take.
 * ``HIPSNAPSHOT_GC_AFTER_PLAN`` (1) -- one full Python GC pass at the end of a
@@ -314,6 +315,13 @@ def get_drain_nice() -> int:
     """Nice increment of the native drain's threads (0-19, default 10): they
     yield a shared core to the training loop's launch thread."""
     return max(0, min(19, _get_int("DRAIN_NICE", 10)))
+
+
+def drain_process() -> bool:
+    """Run the native drain in a helper process (csrc/hsdrain_helper.cpp)
+    that maps the frozen arena through a HIP IPC handle: the trainer's
+    process then runs no drain thread, runtime call or page-cache copy."""
+    return _get_bool("DRAIN_PROCESS", False)
 
 
 def gc_after_plan() -> bool:

@@ -269,6 +269,9 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                   ctypes.POINTER(ctypes.c_double)])
         _declare(lib, "hsg_drain_pending", c_int, [c_void_p])
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
+        _declare(lib, "hsg_ipc_export", c_int,
+                 [c_void_p, c_void_p, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)])
+        _declare(lib, "hsg_ipc_handle_bytes", c_int, [])
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
         _declare(lib, "hsg_hsz_last_error", c_char_p, [])
@@ -738,14 +741,18 @@ class NativeDrain:
         self._sizes = (c_uint64 * max(n, 1))(*[b[1] for b in blobs])
         self._paths = (c_char_p * max(n, 1))(*[os.fsencode(b[2]) for b in blobs])
         err = c_int(0)
-        flags = (1 if fsync else 0) | (2 if hash_blobs else 0) | (4 if direct else 0) | \
-            (0 if hash_high_priority else 8) | \
-            (max(0, min(nice, 19)) << 8)
+        flags = self.flags(fsync, hash_blobs, direct, hash_high_priority, nice)
         self._h = lib.hsg_drain_start(dev, n, self._srcs, self._sizes, self._paths,
                                       slot_bytes, nslots, nwriters, flags, max_hash_grid,
                                       ctypes.byref(err))
         if not self._h:
             raise HipError(f"hsg_drain_start failed ({err.value})")
+
+    @staticmethod
+    def flags(fsync: bool, hash_blobs: bool, direct: bool, hash_high_priority: bool,
+              nice: int) -> int:
+        return (1 if fsync else 0) | (2 if hash_blobs else 0) | (4 if direct else 0) | \
+            (0 if hash_high_priority else 8) | (max(0, min(nice, 19)) << 8)
 
     def pending(self) -> int:
         return require_gpu_lib().hsg_drain_pending(self._h) if self._h else 0
@@ -770,6 +777,31 @@ class NativeDrain:
                 raise OSError(-r, text)
             raise HipError(f"native drain failed ({r}): {text}")
         return list(sums[: self.n]), int(written.value)
+
+
+def ipc_export(ptr: int) -> Tuple[bytes, int, int]:
+    """(IPC handle of the hipMalloc allocation holding ``ptr``, offset of
+    ``ptr`` in it, allocation bytes) -- for the drain helper process."""
+    lib = require_gpu_lib()
+    hb = ctypes.create_string_buffer(int(lib.hsg_ipc_handle_bytes()))
+    off = c_uint64(0)
+    size = c_uint64(0)
+    _check(lib.hsg_ipc_export(ptr, hb, ctypes.byref(off), ctypes.byref(size)), "hsg_ipc_export")
+    return hb.raw, int(off.value), int(size.value)
+
+
+def hip_runtime_path() -> Optional[str]:
+    """Path of the libamdhip64 this process has loaded (torch's), so a helper
+    process can load the very same runtime."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6 and os.path.basename(parts[5]).startswith("libamdhip64.so"):
+                    return parts[5]
+    except OSError:
+        pass
+    return None
 
 
 # ---- managed memory -------------------------------------------------------------

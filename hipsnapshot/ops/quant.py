@@ -135,7 +135,9 @@ def _scale_and_quant(blocks: torch.Tensor):
     # tensor/tensor division (correctly rounded; a Python-scalar divisor is
     # lowered to a reciprocal multiply by torch and differs by 1 ulp)
     scale = torch.where(amax > 0, amax / torch.full_like(amax, FP8_MAX), torch.ones_like(amax))
-    q = (blocks / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    # one reciprocal per block, one multiply per element (the kernels' rule)
+    inv = torch.ones_like(scale) / scale
+    q = (blocks * inv[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
     return q, scale
 
 
