@@ -8,9 +8,11 @@ random init, synthetic) to local storage, committed (metadata written after
 every rank finished).  The total model is fixed as N grows -> strong scaling;
 ``value`` is the whole-job GB/s = model bytes / step time (max over ranks).
 
-After the timed steps, ``async_take`` is run ``--async-iters`` times and its
-time-to-unblock (max over ranks, median over the iterations) is reported in
-``time_to_unblock_ms`` (every iteration in ``time_to_unblock_ms_each``); then
+After the timed steps, ``async_take`` is run ``--async-warmup`` times untimed
+(the first async take of a state builds its plan: ``cold_time_to_unblock_ms``)
+and then ``--async-iters`` times; its time-to-unblock (max over ranks, median
+over the iterations) is reported in ``time_to_unblock_ms`` (every iteration in
+``time_to_unblock_ms_each``); then
 every local shard is zeroed, restored, and compared bitwise to a copy.
 
 Blobs are written with the lossless HSZ1 codec by default (``--compression``):
@@ -77,6 +79,10 @@ def main() -> None:
     ap.add_argument("--model", default="llama3_8b", choices=["llama3_8b", "llama3_70b", "tiny"])
     ap.add_argument("--path", default=None)
     ap.add_argument("--async-iters", type=int, default=3)
+    ap.add_argument("--async-warmup", type=int, default=1,
+                    help="untimed async_takes before the timed ones (the first builds the "
+                         "async take plan and runs the one full GC pass that follows a plan "
+                         "build); their unblock is reported as cold_time_to_unblock_ms")
     ap.add_argument("--no-restore-check", action="store_true")
     ap.add_argument("--raw-steps", type=int, default=3,
                     help="after the headline, also time this many takes with raw "
@@ -197,6 +203,18 @@ def main() -> None:
     # that stream's busy time between events recorded before and after the
     # call (event-timed), unblock_incl_freeze_ms the host time until the
     # stream is free again -- what a trainer whose next kernel waits sees.
+    cold_unblock = []
+    for i in range(args.async_warmup):
+        barrier_sync()
+        ts = time.perf_counter()
+        pending = Snapshot.async_take(path + "_async", app_state, storage_options=opts,
+                                      compression=args.compression)
+        tu = time.perf_counter() - ts
+        pending.wait()
+        u = torch.tensor([tu], dtype=torch.float64, device=dev)
+        dist.all_reduce(u, op=dist.ReduceOp.MAX)
+        cold_unblock.append(float(u.item()) * 1e3)
+        log(f"async warmup {i}: unblock {cold_unblock[-1]:.1f} ms")
     unblock = []
     drain = []
     freeze = []
@@ -381,6 +399,8 @@ def main() -> None:
             # median over the async iterations (each value listed below)
             "time_to_unblock_ms": round(statistics.median(unblock), 2) if unblock else None,
             "time_to_unblock_ms_each": [round(u, 2) for u in unblock],
+            "cold_time_to_unblock_ms": [round(u, 2) for u in cold_unblock],
+            "async_warmup": args.async_warmup,
             "freeze_gpu_ms": round(statistics.median(freeze), 3) if freeze else None,
             "freeze_gpu_ms_each": [round(f, 3) for f in freeze],
             "unblock_incl_freeze_ms": round(statistics.median(unblock_gpu), 2)

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--uvm", action="store_true")
     ap.add_argument("--sharding", default="row", choices=["row", "column", "table"])
+    ap.add_argument("--uvm-place", default=None, choices=["host", "device"],
+                    help="advise + prefetch the UVM tables to host DRAM or HBM first")
     ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
     args = ap.parse_args()
     rank, ws, dev = init_dist()
@@ -42,6 +44,18 @@ def main():
     model = DLRM([rows] * args.tables, dim=args.dim, device=dev, mesh=mesh, uvm=args.uvm,
                  sharding=args.sharding)
     nbytes = sum(p.numel() * 4 for p in model.parameters())
+    residency = None
+    if args.uvm:
+        from hipsnapshot.ops.uvm import is_uvm_tensor, place, residency as uvm_residency
+
+        locals_ = [t for t in (getattr(p, "_local_tensor", p) for p in model.parameters())
+                   if is_uvm_tensor(t)]
+        if args.uvm_place:
+            for t in locals_:
+                if t.numel():
+                    place(t, args.uvm_place)
+            torch.cuda.synchronize()
+        residency = sorted({uvm_residency(t) for t in locals_ if t.numel()})
     log(f"DLRM: {args.tables} tables x {rows} rows x {args.dim} (uvm={args.uvm}, "
         f"{args.sharding}-wise), "
         f"{nbytes / 1e9:.2f} GB")
@@ -56,15 +70,39 @@ def main():
         sync(dev)
     sync_s = max_over_ranks(t.s, dev)
     sync(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     with Timer() as tu:
         pending = Snapshot.async_take(root + "/async", {"model": model})
+    e1.record()
+    e1.synchronize()
+    freeze_ms = e0.elapsed_time(e1)  # the trainer stream's busy time (HBM freeze)
     unblock = max_over_ranks(tu.s, dev)
     pending.wait()
     sync(dev)
+    restore_s = None
+    if os.environ.get("DLRM_RESTORE", "1") == "1":
+        refs = [getattr(p, "_local_tensor", p).clone() for p in model.parameters()]
+        for p in model.parameters():
+            getattr(p, "_local_tensor", p).zero_()
+        sync(dev)
+        with Timer() as tr:
+            Snapshot(root + "/sync").restore({"model": model})
+            sync(dev)
+        restore_s = max_over_ranks(tr.s, dev)
+        ok = all(torch.equal(r, getattr(p, "_local_tensor", p))
+                 for r, p in zip(refs, model.parameters()))
+        del refs
+    else:
+        ok = None
     emit({"bench": "dlrm_uvm" if args.uvm else "dlrm_hbm", "sharding": args.sharding,
           "world_size": ws, "bytes": nbytes,
           "sync_take_s": round(sync_s, 3), "sync_GBps": round(nbytes / sync_s / 1e9, 2),
-          "async_unblock_ms": round(unblock * 1e3, 1)})
+          "async_unblock_ms": round(unblock * 1e3, 1), "freeze_gpu_ms": round(freeze_ms, 2),
+          "uvm_residency": residency, "uvm_place": args.uvm_place,
+          "restore_s": round(restore_s, 3) if restore_s else None,
+          "restore_GBps": round(nbytes / restore_s / 1e9, 2) if restore_s else None,
+          "restore_bitwise_ok": ok})
     if rank == 0:
         shutil.rmtree(root, ignore_errors=True)
     dist.destroy_process_group()

@@ -811,6 +811,100 @@ hs_mx8_dequant(const uint8_t* __restrict__ q, const uint8_t* __restrict__ scales
 }
 
 // ---------------------------------------------------------------------------
+// Blockwise fp8 (f32 scale per BLK elements, format "fp8_e4m3fn_block") in the
+// streaming layout of hs_mx8_quant: lane l of a wave reads 16 contiguous bytes
+// (EPL elements) of a 1 KiB wave segment, U = 4 segments in flight per lane,
+// a block spans LPB = BLK / EPL adjacent lanes (amax: log2(LPB) xor shuffles),
+// and each lane stores its EPL fp8 codes with one vector store.  Same numerics
+// as hs_fp8_quant: scale = amax / 448 (1 if amax == 0), q = cvt(clamp(x * (1 /
+// scale))).  hs_fp8_quant (one block per wave, two 2-B loads per lane) ran at
+// 1.9 TB/s: too little in flight per wave.
+// ---------------------------------------------------------------------------
+
+template <int DT, int BLK>
+__global__ void __launch_bounds__(kBlock)
+hs_fp8_quant_v(const char* __restrict__ src, int64_t n, uint8_t* __restrict__ out,
+               float* __restrict__ scales) {
+  constexpr int ES = (DT == kF32) ? 4 : 2;
+  constexpr int EPL = 16 / ES;
+  constexpr int LPB = BLK / EPL;
+  static_assert(LPB >= 1 && LPB <= 64 && (64 % LPB) == 0, "block must fit a wave");
+  constexpr int U = 4;
+  constexpr int64_t kChunk = 64LL * EPL * U;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  const int64_t nchunks = (n + kChunk - 1) / kChunk;
+  for (int64_t c = wave0; c < nchunks; c += nwaves) {
+    const int64_t base = c * kChunk;
+    const bool full = base + kChunk <= n;
+    uint4 raw[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e0 = base + (int64_t(u) * 64 + lane) * EPL;
+      if (full) {
+        const mx_u32x4 t =
+            __builtin_nontemporal_load(reinterpret_cast<const mx_u32x4*>(src + e0 * ES));
+        raw[u] = make_uint4(t.x, t.y, t.z, t.w);
+      } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int j = 0; j < EPL; ++j) {
+          if (e0 + j >= n) break;
+          uint32_t bits;
+          if constexpr (ES == 4) bits = *reinterpret_cast<const uint32_t*>(src + (e0 + j) * 4);
+          else bits = *reinterpret_cast<const uint16_t*>(src + (e0 + j) * 2);
+          w[(j * ES) >> 2] |= bits << (((j * ES) & 3) * 8);
+        }
+        raw[u] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t ws[4] = {raw[u].x, raw[u].y, raw[u].z, raw[u].w};
+      float v[EPL];
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) {
+        if constexpr (ES == 4) v[j] = __uint_as_float(ws[j]);
+        else v[j] = mx_unpack<DT>(ws[j >> 1], j & 1);
+      }
+      float amax = 0.f;
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) amax = fmaxf(amax, fabsf(v[j]));
+#pragma unroll
+      for (int o = 1; o < LPB; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+      const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
+      const float inv = 1.f / scale;
+      const int64_t e0 = base + (int64_t(u) * 64 + lane) * EPL;
+      if ((lane % LPB) == 0 && e0 < n) scales[e0 / BLK] = scale;
+      uint32_t q[EPL / 4];
+#pragma unroll
+      for (int w = 0; w < EPL / 4; ++w) {
+        int word = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4 * w] * inv, -kFp8Max), kFp8Max),
+                                                   fminf(fmaxf(v[4 * w + 1] * inv, -kFp8Max), kFp8Max),
+                                                   0, false);
+        word = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4 * w + 2] * inv, -kFp8Max), kFp8Max),
+                                               fminf(fmaxf(v[4 * w + 3] * inv, -kFp8Max), kFp8Max),
+                                               word, true);
+        q[w] = static_cast<uint32_t>(word);
+      }
+      if (full) {
+        if constexpr (EPL == 8) {
+          mx_u32x2 t;
+          t.x = q[0];
+          t.y = q[1];
+          __builtin_nontemporal_store(t, reinterpret_cast<mx_u32x2*>(out + e0));
+        } else {
+          __builtin_nontemporal_store(q[0], reinterpret_cast<uint32_t*>(out + e0));
+        }
+      } else {
+        for (int j = 0; j < EPL && e0 + j < n; ++j)
+          out[e0 + j] = static_cast<uint8_t>(q[j >> 2] >> (8 * (j & 3)));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Hadamard-rotated fp8 (MFMA).  The flat tensor is viewed as rows of 32
 // ("groups"); every group is rotated by the 32x32 Sylvester Hadamard matrix H
 // (entries +-1, H*H = 32 I) before blockwise e4m3 quantization, which spreads
@@ -1562,6 +1656,33 @@ int hsg_fp8_quantize(int dev, const void* src, int src_dtype, int64_t n, void* o
   const char* sp = static_cast<const char*>(src);
   uint8_t* op = static_cast<uint8_t*>(out);
   float* sc = static_cast<float*>(scales);
+  // streaming kernel: 16-B aligned source, 8-B aligned payload, a block
+  // within one wave (bf16/f16 blocks of 128..512, f32 of 128..256)
+  const bool aligned = (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
+                       (reinterpret_cast<uintptr_t>(out) % 8) == 0;
+  if (aligned && (src_dtype == kBF16 || src_dtype == kF16 || src_dtype == kF32)) {
+    const int epl = src_dtype == kF32 ? 4 : 8;
+    const int64_t chunk = 64LL * epl * 4;
+    const int vgrid = static_cast<int>(std::max<int64_t>(
+        1, std::min<int64_t>((n + chunk - 1) / chunk / waves_per_wg + 1, 256 * 16)));
+#define HS_FP8V(DT, B)                                                                     \
+  hipLaunchKernelGGL((hs_fp8_quant_v<DT, B>), dim3(vgrid), dim3(kBlock), 0, s, sp, n, op, sc); \
+  HS_CHECK(hipGetLastError());                                                             \
+  return 0
+    if (src_dtype == kBF16) {
+      if (vpt == 2) { HS_FP8V(kBF16, 128); }
+      if (vpt == 4) { HS_FP8V(kBF16, 256); }
+      if (vpt == 8) { HS_FP8V(kBF16, 512); }
+    } else if (src_dtype == kF16) {
+      if (vpt == 2) { HS_FP8V(kF16, 128); }
+      if (vpt == 4) { HS_FP8V(kF16, 256); }
+      if (vpt == 8) { HS_FP8V(kF16, 512); }
+    } else {
+      if (vpt == 2) { HS_FP8V(kF32, 128); }
+      if (vpt == 4) { HS_FP8V(kF32, 256); }
+    }
+#undef HS_FP8V
+  }
   switch (vpt) {
     case 2: hipLaunchKernelGGL(hs_fp8_quant<2>, dim3(grid), dim3(kBlock), 0, s, sp, src_dtype, n, op, sc); break;
     case 4: hipLaunchKernelGGL(hs_fp8_quant<4>, dim3(grid), dim3(kBlock), 0, s, sp, src_dtype, n, op, sc); break;
@@ -1700,6 +1821,35 @@ void* hsg_managed_alloc(int dev, uint64_t n) {
 
 int hsg_managed_free(void* p) {
   HS_CHECK(hipFree(p));
+  return 0;
+}
+
+// Advised placement of a managed range: *preferred / *last_prefetch get a
+// device index, -1 (hipCpuDeviceId: host DRAM) or -2 (never set).
+int hsg_managed_location(const void* p, uint64_t n, int* preferred, int* last_prefetch) {
+  int v = -2;
+  if (hipMemRangeGetAttribute(&v, sizeof(v), hipMemRangeAttributePreferredLocation,
+                              const_cast<void*>(p), n) != hipSuccess) {
+    (void)hipGetLastError();
+    v = -2;
+  }
+  *preferred = v;
+  v = -2;
+  if (hipMemRangeGetAttribute(&v, sizeof(v), hipMemRangeAttributeLastPrefetchLocation,
+                              const_cast<void*>(p), n) != hipSuccess) {
+    (void)hipGetLastError();
+    v = -2;
+  }
+  *last_prefetch = v;
+  return 0;
+}
+
+// Place a managed range: preferred location `loc` (device index, or -1 for
+// host DRAM) and an asynchronous prefetch there on `stream`.
+int hsg_managed_place(int dev, const void* p, uint64_t n, int loc, void* stream) {
+  HS_CHECK(hipSetDevice(dev));
+  HS_CHECK(hipMemAdvise(p, n, hipMemAdviseSetPreferredLocation, loc));
+  HS_CHECK(hipMemPrefetchAsync(p, n, loc, static_cast<hipStream_t>(stream)));
   return 0;
 }
 

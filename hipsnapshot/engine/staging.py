@@ -267,15 +267,47 @@ def _elem_strides_ok(t: torch.Tensor) -> bool:
     return t.dim() <= native.MAX_DIMS
 
 
+def host_resident_managed(t: torch.Tensor) -> bool:
+    """A managed (UVM) tensor whose pages live in host DRAM (``ops.uvm``)."""
+    from ..ops import uvm
+
+    return uvm.residency(t) == "host"
+
+
+def managed_host_view(t: torch.Tensor, producer: Optional[int]) -> StagedBuffer:
+    """The bytes of a contiguous host-resident managed tensor, in place: the
+    writer ``pwrite``s straight from the UVM pages (one DRAM read, no DMA
+    over PCIe and back, no pinned copy) and hashes them on the host.  Waits
+    for the producer stream first (kernels queued before the take may still
+    write the table).  Only for blocking takes: the view aliases live memory.
+    Restores read into the same view (``TensorBufferConsumer.get_read_dest``)."""
+    if producer is not None:
+        native.sync_stream_handle(producer)
+    else:
+        torch.cuda.current_stream(t.device).synchronize()
+    nbytes = t.numel() * t.element_size()
+    import ctypes
+
+    mv = memoryview((ctypes.c_char * nbytes).from_address(t.data_ptr())).cast("B")
+    return StagedBuffer(mv, addr=t.data_ptr(), keepalive=t)
+
+
 def d2h_tensor(t: torch.Tensor, producer: Optional[int],
-               codec: Optional[dict] = None) -> StagedBuffer:
+               codec: Optional[dict] = None, alias_ok: bool = False) -> StagedBuffer:
     """Copy a CUDA tensor's logical bytes (C order) into a pinned block.
 
     With ``codec`` (HSZ1 info dict) the bytes are compressed on the GPU first
-    and only the encoded blob crosses PCIe.
+    and only the encoded blob crosses PCIe.  ``alias_ok`` (blocking takes): a
+    contiguous managed tensor in host DRAM is handed out in place
+    (``managed_host_view``) instead of copied.
     """
     if codec is not None:
         return _d2h_encoded(t, producer, codec)
+    if alias_ok and t.is_contiguous() and t.numel() and host_resident_managed(t):
+        t_s = time.perf_counter()
+        staged = managed_host_view(t, producer)
+        timeline.add("uvm_host_view", "d2h", t_s, time.perf_counter(), bytes=staged.nbytes)
+        return staged
     nbytes = t.numel() * t.element_size()
     pb, staged = _pinned_staged(nbytes)
     if nbytes == 0:

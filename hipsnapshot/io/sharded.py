@@ -387,8 +387,29 @@ class ShardedTensorBufferConsumer(BufferConsumer):
                      and all(r.dst.is_cuda for r in regions) and len(regions) > 0
                      and len({r.dst.device for r in regions}) == 1)
         self.producer = staging.producer_stream_handle(regions[0].dst) if self._gpu else None
+        self._direct = False
+
+    def _whole_piece_dst(self, nbytes: int) -> Optional[torch.Tensor]:
+        """The one contiguous destination view the saved piece maps onto 1:1
+        (same layout on restore), else None."""
+        if not self._gpu or len(self.regions) != 1:
+            return None
+        r = self.regions[0]
+        if any(so != 0 or ln != self.entry.shape[d] for d, so, _do, ln in r.narrows):
+            return None
+        dst = _narrow_dst(r.dst, r.narrows)
+        if (not dst.is_contiguous() or dst.dtype != string_to_dtype(self.entry.dtype)
+                or dst.numel() * dst.element_size() != nbytes
+                or nbytes != tensor_nbytes_from_entry(self.entry)):
+            return None
+        return dst
 
     def get_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
+        dst = self._whole_piece_dst(nbytes)
+        if dst is not None and nbytes and staging.host_resident_managed(dst):
+            # UVM table pages in host DRAM: read the file straight into them
+            self._direct = True
+            return staging.managed_host_view(dst, self.producer)
         if self._gpu:
             from ..ops import native
 
@@ -400,6 +421,8 @@ class ShardedTensorBufferConsumer(BufferConsumer):
         return self.get_read_dest(nbytes)
 
     async def consume_buffer(self, buf, executor: Optional[Executor] = None) -> None:
+        if self._direct:
+            return  # read straight into the destination
         await run_in_executor(executor, self._consume_sync, buf)
 
     def _consume_sync(self, buf) -> None:

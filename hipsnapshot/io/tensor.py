@@ -270,7 +270,9 @@ class TensorBufferStager(BufferStager):
     def _d2h(self, t: torch.Tensor):
         if self.wait_event is not None:
             self.wait_event.synchronize()
-        return staging.d2h_tensor(t, self.producer, codec=self.codec)
+        # a blocking take may write host-resident UVM pages in place
+        return staging.d2h_tensor(t, self.producer, codec=self.codec,
+                                  alias_ok=not self.is_async_snapshot)
 
     def get_staging_cost_bytes(self) -> int:
         n = tensor_nbytes_from_entry(self.entry)
@@ -339,6 +341,12 @@ class TensorBufferConsumer(BufferConsumer):
             if dest is not None:
                 self._direct = True
                 return dest
+        if (t.is_cuda and t.is_contiguous() and t.dtype == string_to_dtype(self.entry.dtype)
+                and nbytes == self._nbytes() and list(t.shape) == list(self.entry.shape)
+                and nbytes and staging.host_resident_managed(t)):
+            # UVM pages in host DRAM: read the file straight into them
+            self._direct = True
+            return staging.managed_host_view(t, self.producer)
         if t.is_cuda:
             from ..ops import native
 

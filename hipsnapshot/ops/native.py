@@ -272,6 +272,9 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_ipc_export", c_int,
                  [c_void_p, c_void_p, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_ipc_handle_bytes", c_int, [])
+        _declare(lib, "hsg_managed_location", c_int,
+                 [c_void_p, c_uint64, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
+        _declare(lib, "hsg_managed_place", c_int, [c_int, c_void_p, c_uint64, c_int, c_void_p])
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
         _declare(lib, "hsg_hsz_last_error", c_char_p, [])
@@ -777,6 +780,22 @@ class NativeDrain:
                 raise OSError(-r, text)
             raise HipError(f"native drain failed ({r}): {text}")
         return list(sums[: self.n]), int(written.value)
+
+
+def managed_location(ptr: int, nbytes: int) -> Tuple[int, int]:
+    """(preferred, last prefetch) location of a managed range: device index,
+    -1 = host DRAM, -2 = never advised / prefetched."""
+    lib = require_gpu_lib()
+    a, b = c_int(-2), c_int(-2)
+    lib.hsg_managed_location(ptr, nbytes, ctypes.byref(a), ctypes.byref(b))
+    return int(a.value), int(b.value)
+
+
+def managed_place(dev: int, ptr: int, nbytes: int, loc: int, stream_handle: int) -> None:
+    """Advise ``loc`` (device index or -1 = host) as the preferred location of
+    a managed range and prefetch it there on ``stream_handle``."""
+    _check(require_gpu_lib().hsg_managed_place(dev, ptr, nbytes, loc, stream_handle or None),
+           "hsg_managed_place")
 
 
 def ipc_export(ptr: int) -> Tuple[bytes, int, int]:

@@ -31,6 +31,37 @@ def is_uvm_tensor(t: torch.Tensor) -> bool:
     return native.is_managed_ptr(ptr)
 
 
+def residency(t: torch.Tensor) -> str:
+    """Where a managed tensor's pages live: ``"host"`` / ``"device"`` when
+    advised or prefetched (``place``); never-placed pages are in host DRAM
+    unless XNACK migrates them (``HIPSNAPSHOT_UVM_ASSUME_HOST``), else
+    ``"unknown"``.  Not a managed tensor: ``"not_managed"`` (the range query
+    is only valid on managed memory)."""
+    if not is_uvm_tensor(t):
+        return "not_managed"
+    ptr = t.untyped_storage().data_ptr()
+    nbytes = max(t.untyped_storage().nbytes(), 1)
+    pref, last = native.managed_location(ptr, nbytes)
+    loc = last if last != -2 else pref
+    if loc == -2:
+        from .. import knobs
+
+        return "host" if knobs.uvm_assume_host() else "unknown"
+    return "host" if loc == -1 else "device"
+
+
+def place(t: torch.Tensor, where: str) -> None:
+    """Advise + prefetch a managed tensor's pages to host DRAM (``"host"``,
+    TorchRec's UVM tables larger than HBM) or to its GPU (``"device"``);
+    asynchronous on the current stream."""
+    if where not in ("host", "device"):
+        raise ValueError(f"where must be 'host' or 'device' (got {where!r})")
+    dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    native.managed_place(dev, t.untyped_storage().data_ptr(),
+                         max(t.untyped_storage().nbytes(), 1), -1 if where == "host" else dev,
+                         int(torch.cuda.current_stream(dev).cuda_stream))
+
+
 def uvm_to_cpu(t: torch.Tensor) -> torch.Tensor:
     return t.detach().cpu()
 

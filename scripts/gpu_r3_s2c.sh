@@ -1,17 +1,16 @@
 #!/bin/bash
-# Session 2, call A: drain-helper GPU tests, full GPU suite, smoke, headline
-# bench; the fp8 kernels (host-timed, rocprofv3 kernel stats, FETCH/WRITE
-# counters) after the reciprocal-scale + packed-store change; UVM residency probe.
+# Session 2, call C: fp8 / UVM / drain-helper GPU tests, the streaming block
+# fp8 quantizer (host-timed + rocprofv3 stats + FETCH/WRITE counters), DLRM
+# UVM tables never placed / placed in host DRAM / placed in HBM, bench.py.
 set -o pipefail
 export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
 REPO=$PWD
-O=$PWD/gpurun_out/s2a
+O=$PWD/gpurun_out/s2c
 mkdir -p $O bench_tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -v -m gpu -k "drain_process or native_drain" \
-    --timeout 120 --timeout-method thread > $O/pytest_helper.log 2>&1 \
-    || { echo PYTEST_HELPER_FAIL; tail -40 $O/pytest_helper.log; exit 1; }
-tail -2 $O/pytest_helper.log
-TESTS=1 STEPS=10 bash scripts/gpu_check.sh || exit 1
+timeout -k 10 400 python -u -m pytest tests/test_gpu.py -x -v -m gpu -k "fp8 or mx8 or uvm or drain_process" \
+    --timeout 120 --timeout-method thread > $O/pytest_sub.log 2>&1 \
+    || { echo PYTEST_FAIL; tail -40 $O/pytest_sub.log; exit 1; }
+tail -2 $O/pytest_sub.log
 timeout -k 10 120 python scripts/fp8_kernels_bench.py > $O/fp8_host_timed.jsonl 2>&1 \
     || { echo FP8_BENCH_FAIL; tail $O/fp8_host_timed.jsonl; exit 1; }
 grep kernel $O/fp8_host_timed.jsonl
@@ -26,15 +25,15 @@ for pass in FETCH_SIZE WRITE_SIZE; do
       > $O/fp8_pmc_$tag.log 2>&1 || { echo PMC_FAIL $tag; tail -20 $O/fp8_pmc_$tag.log; exit 1; }
 done
 cd $REPO
-timeout -k 10 180 python scripts/uvm_residency_probe.py > $O/uvm_probe.jsonl 2> $O/uvm_probe.err \
-    || { echo UVM_PROBE_FAIL; tail -20 $O/uvm_probe.err; exit 1; }
-cat $O/uvm_probe.jsonl
 for pl in default host device; do
   extra=""; [ $pl != default ] && extra="--uvm-place $pl"
   timeout -k 10 300 python benchmarks/dlrm_uvm/main.py --total-gb 8 --uvm $extra > $O/dlrm_uvm_$pl.json 2> $O/dlrm_uvm_$pl.err \
       || { echo DLRM_FAIL $pl; tail -20 $O/dlrm_uvm_$pl.err; exit 1; }
   tail -1 $O/dlrm_uvm_$pl.json
 done
+timeout -k 10 300 python bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err \
+    || { echo BENCH_FAIL; tail -30 $O/bench.err; exit 1; }
+cat $O/bench.json; grep -E "async" $O/bench.err
 df -h /dev/shm /tmp $PWD | cat
 free -g | cat
 rm -rf bench_tmp

@@ -128,13 +128,18 @@ def test_contiguous_cast_vs_torch(gpu, src_dtype, dst_dtype, n, off):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("n", [1, 127, 128, 1000, 1 << 20])
-@pytest.mark.parametrize("vpt", [2, 8])
-def test_fp8_quant_dequant_vs_reference(gpu, dtype, n, vpt):
+@pytest.mark.parametrize("n", [1, 127, 128, 1000, 1 << 20, (1 << 20) + 77])
+@pytest.mark.parametrize("vpt", [2, 4, 8])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_fp8_quant_dequant_vs_reference(gpu, dtype, n, vpt, offset):
+    """Streaming (hs_fp8_quant_v: aligned source, block within a wave) and
+    one-block-per-wave (hs_fp8_quant: misaligned ``offset`` views, f32 blocks
+    of 512) quantizers are bit-identical to the torch reference."""
     from hipsnapshot.ops.quant import dequantize_reference, quantize_reference
 
     torch.manual_seed(2)
-    x = (torch.randn(n, device=gpu) * torch.logspace(-3, 3, n, device=gpu)).to(dtype)
+    x = (torch.randn(n + offset, device=gpu)
+         * torch.logspace(-3, 3, n + offset, device=gpu)).to(dtype)[offset:]
     block = 64 * vpt
     nblocks = (n + block - 1) // block
     q = torch.empty(n, dtype=torch.uint8, device=gpu)
@@ -401,6 +406,56 @@ def test_uvm_managed_tensor(gpu, tmp_path):
     Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(t=out)})
     torch.cuda.synchronize()
     assert torch.equal(out, t)
+
+
+@pytest.mark.parametrize("where", ["host", "device", None])
+def test_uvm_placed_save_restore(gpu, tmp_path, where, monkeypatch):
+    """Managed tables placed in host DRAM are written in place by a blocking
+    take (no DMA, no pinned copy), copied by an async take (it must not alias
+    live memory), and both restore bitwise with verified checksums; tables
+    placed in HBM keep the DMA path.  The take waits for kernels still
+    writing the table."""
+    from hipsnapshot.engine import staging
+    from hipsnapshot.ops.uvm import new_managed_tensor, place, residency
+    from hipsnapshot.verify import verify_snapshot
+
+    from hipsnapshot import knobs
+
+    t = new_managed_tensor([4096, 1024], torch.float32, 0)
+    if where is not None:
+        place(t, where)
+    torch.cuda.synchronize()
+    # never-placed pages are in host DRAM unless XNACK migrates them
+    host = where == "host" or (where is None and knobs.uvm_assume_host())
+    assert residency(t) == ("host" if host else where or "unknown")
+    views = []
+    real = staging.managed_host_view
+    monkeypatch.setattr(staging, "managed_host_view",
+                        lambda x, p: views.append(x.numel()) or real(x, p))
+    with override_slab_size_threshold_bytes(1 << 20):  # t is its own blob
+        t.normal_()
+        ref = t.clone()
+        Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(t=t)})  # normal_ may still run
+        assert views == ([t.numel()] if host else [])
+        pending = Snapshot.async_take(str(tmp_path / "a"), {"sd": StateDict(t=t)})
+        t.add_(1.0)  # after the async take's capture
+        pending.wait()
+    assert len(views) == (1 if host else 0)
+    out_m = new_managed_tensor([4096, 1024], torch.float32, 0)
+    if where is not None:
+        place(out_m, where)
+    for p in ("s", "a"):
+        assert verify_snapshot(str(tmp_path / p)).ok
+        out = torch.zeros_like(ref)
+        Snapshot(str(tmp_path / p)).restore({"sd": StateDict(t=out)})
+        assert torch.equal(out, ref), p
+        # into placed UVM pages: host DRAM ones are read into in place
+        out_m.zero_()
+        n = len(views)
+        Snapshot(str(tmp_path / p)).restore({"sd": StateDict(t=out_m)})
+        torch.cuda.synchronize()
+        assert torch.equal(out_m, ref), p
+        assert len(views) == n + (1 if host else 0)
 
 
 def _fsdp_gpu_worker(path):
