@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--uvm-place", default=None, choices=["host", "device"],
                     help="advise + prefetch the UVM tables to host DRAM or HBM first")
     ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--single-path", action="store_true",
+                    help="every take rewrites ONE snapshot path (100 GB runs: one copy on storage)")
     args = ap.parse_args()
     rank, ws, dev = init_dist()
     from torch.distributed.device_mesh import init_device_mesh
@@ -63,17 +65,24 @@ def main():
     if rank == 0:
         shutil.rmtree(root, ignore_errors=True)
     sync(dev)
-    Snapshot.take(root + "/warm", {"model": model})
+    p_warm, p_sync, p_async = ((root + "/ckpt",) * 3 if args.single_path
+                               else (root + "/warm", root + "/sync", root + "/async"))
+    Snapshot.take(p_warm, {"model": model})
     sync(dev)
     with Timer() as t:
-        Snapshot.take(root + "/sync", {"model": model})
+        Snapshot.take(p_sync, {"model": model})
         sync(dev)
     sync_s = max_over_ranks(t.s, dev)
+    sync(dev)
+    # the first async_take of a state builds its plan: untimed, reported as cold
+    with Timer() as tc:
+        Snapshot.async_take(p_async, {"model": model}).wait()
+    cold_s = max_over_ranks(tc.s, dev)
     sync(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     with Timer() as tu:
-        pending = Snapshot.async_take(root + "/async", {"model": model})
+        pending = Snapshot.async_take(p_async, {"model": model})
     e1.record()
     e1.synchronize()
     freeze_ms = e0.elapsed_time(e1)  # the trainer stream's busy time (HBM freeze)
@@ -82,12 +91,13 @@ def main():
     sync(dev)
     restore_s = None
     if os.environ.get("DLRM_RESTORE", "1") == "1":
-        refs = [getattr(p, "_local_tensor", p).clone() for p in model.parameters()]
-        for p in model.parameters():
-            getattr(p, "_local_tensor", p).zero_()
+        refs = [getattr(p, "_local_tensor", p).detach().clone() for p in model.parameters()]
+        with torch.no_grad():
+            for p in model.parameters():
+                getattr(p, "_local_tensor", p).zero_()
         sync(dev)
         with Timer() as tr:
-            Snapshot(root + "/sync").restore({"model": model})
+            Snapshot(p_sync).restore({"model": model})
             sync(dev)
         restore_s = max_over_ranks(tr.s, dev)
         ok = all(torch.equal(r, getattr(p, "_local_tensor", p))
@@ -99,6 +109,7 @@ def main():
           "world_size": ws, "bytes": nbytes,
           "sync_take_s": round(sync_s, 3), "sync_GBps": round(nbytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 1), "freeze_gpu_ms": round(freeze_ms, 2),
+          "cold_async_total_s": round(cold_s, 3), "single_path": args.single_path,
           "uvm_residency": residency, "uvm_place": args.uvm_place,
           "restore_s": round(restore_s, 3) if restore_s else None,
           "restore_GBps": round(nbytes / restore_s / 1e9, 2) if restore_s else None,

@@ -810,6 +810,61 @@ hs_mx8_dequant(const uint8_t* __restrict__ q, const uint8_t* __restrict__ scales
   }
 }
 
+// Blockwise fp8 restore in the same streaming layout (hs_mx8_dequant's):
+// lane l reads EPL = 16 / dst-element-size codes and writes 16 B, U = 4 in
+// flight; x = f32(q) * scale[e / BLK] (the scale is per lane: BLK % EPL == 0).
+template <int DT, int BLK>
+__global__ void __launch_bounds__(kBlock)
+hs_fp8_dequant_v(const uint8_t* __restrict__ q, const float* __restrict__ scales, int64_t n,
+                 char* __restrict__ dst) {
+  constexpr int DES = (DT == kF32) ? 4 : (DT == kF64 ? 8 : 2);
+  constexpr int EPL = 16 / DES;
+  constexpr int U = 4;
+  constexpr int64_t kChunk = 64LL * EPL * U;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  const int64_t nchunks = (n + kChunk - 1) / kChunk;
+  for (int64_t c = wave0; c < nchunks; c += nwaves) {
+    const int64_t base = c * kChunk;
+    const bool full = base + kChunk <= n;
+    uint32_t raw[U][(EPL + 3) / 4];
+    float sc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e0 = base + (int64_t(u) * 64 + lane) * EPL;
+      if (full) {
+        if constexpr (EPL == 8) {
+          const uint2 t = *reinterpret_cast<const uint2*>(q + e0);
+          raw[u][0] = t.x;
+          raw[u][1] = t.y;
+        } else if constexpr (EPL == 4) {
+          raw[u][0] = *reinterpret_cast<const uint32_t*>(q + e0);
+        } else {
+          raw[u][0] = *reinterpret_cast<const uint16_t*>(q + e0);
+        }
+      } else {
+        for (int w = 0; w < (EPL + 3) / 4; ++w) raw[u][w] = 0;
+        for (int j = 0; j < EPL && e0 + j < n; ++j)
+          raw[u][j >> 2] |= uint32_t(q[e0 + j]) << (8 * (j & 3));
+      }
+      sc[u] = e0 < n ? scales[e0 / BLK] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e0 = base + (int64_t(u) * 64 + lane) * EPL;
+      float f[EPL];
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) f[j] = fp8_byte_to_f32(raw[u][j >> 2], j & 3) * sc[u];
+      if (full) {
+        mx_store<DT>(dst + e0 * DES, f);
+      } else {
+        for (int j = 0; j < EPL && e0 + j < n; ++j) store_from_f32(dst + (e0 + j) * DES, DT, f[j]);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Blockwise fp8 (f32 scale per BLK elements, format "fp8_e4m3fn_block") in the
 // streaming layout of hs_mx8_quant: lane l of a wave reads 16 contiguous bytes
@@ -966,6 +1021,65 @@ __device__ __forceinline__ void load_half_row(const char* src, int64_t e0, int64
   }
 }
 
+// The same half row as raw 16-B words (2 for bf16/f16, 4 for f32): what the
+// Hadamard quantizer prefetches for its next tile (half the registers of the
+// converted floats); ok = false -> tail / misaligned, load_half_row at use.
+template <int DT>
+struct HalfRowRaw {
+  uint4 v[(DT == kF32) ? 4 : 2];
+  bool ok;
+};
+
+template <int DT>
+__device__ __forceinline__ void load_half_row_raw(const char* src, int64_t e0, int64_t n,
+                                                  HalfRowRaw<DT>& r) {
+  constexpr int ES = (DT == kF32) ? 4 : 2;
+  r.ok = e0 + 16 <= n && ((reinterpret_cast<uintptr_t>(src + e0 * ES) & 15) == 0);
+  if (r.ok) {
+    const uint4* v = reinterpret_cast<const uint4*>(src + e0 * ES);
+#pragma unroll
+    for (int q = 0; q < ((DT == kF32) ? 4 : 2); ++q) r.v[q] = v[q];
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void half_row_floats(const char* src, int64_t e0, int64_t n,
+                                                const HalfRowRaw<DT>& r, float* x) {
+  if (!r.ok) {
+    load_half_row<DT>(src, e0, n, x);
+    return;
+  }
+  if constexpr (DT == kF32) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      x[4 * q] = __uint_as_float(r.v[q].x);
+      x[4 * q + 1] = __uint_as_float(r.v[q].y);
+      x[4 * q + 2] = __uint_as_float(r.v[q].z);
+      x[4 * q + 3] = __uint_as_float(r.v[q].w);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t ws[4] = {r.v[q].x, r.v[q].y, r.v[q].z, r.v[q].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[8 * q + 2 * i] = mx_unpack<DT>(ws[i], 0);
+        x[8 * q + 2 * i + 1] = mx_unpack<DT>(ws[i], 1);
+      }
+    }
+  }
+}
+
+// max over the 32 lanes of a wave half: quad xor-1 / xor-2 and the 8- and
+// 16-lane mirrors on DPP (no LDS traffic), one ds_bpermute for lane ^ 16
+__device__ __forceinline__ float max_over_32(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false)));
+  return fmaxf(v, __shfl_xor(v, 16, 64));
+}
+
 template <int DT>
 __global__ void __launch_bounds__(kBlock)
 hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
@@ -976,9 +1090,17 @@ hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
   const int64_t nblocks = (n_pad + 127) / 128;
   const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  // software-pipelined: the next tile's half rows are loaded before this
+  // tile's MFMA chain, so every wave keeps HBM reads in flight while the
+  // matrix pipe works
+  HalfRowRaw<DT> raw;
+  raw.ok = false;
+  if (wave0 < ntiles) load_half_row_raw<DT>(src, (wave0 * 32 + r) * 32 + 16 * h, n, raw);
   for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
     float x[16];
-    load_half_row<DT>(src, (tile * 32 + r) * 32 + 16 * h, n, x);
+    half_row_floats<DT>(src, (tile * 32 + r) * 32 + 16 * h, n, raw, x);
+    const int64_t next = tile + nwaves;
+    if (next < ntiles) load_half_row_raw<DT>(src, (next * 32 + r) * 32 + 16 * h, n, raw);
     floatx16 acc = {};
 #pragma unroll
     for (int t = 0; t < 16; ++t)
@@ -987,8 +1109,7 @@ hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
     for (int g4 = 0; g4 < 4; ++g4) {
       float amax = fmaxf(fmaxf(fabsf(acc[4 * g4]), fabsf(acc[4 * g4 + 1])),
                          fmaxf(fabsf(acc[4 * g4 + 2]), fabsf(acc[4 * g4 + 3])));
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+      amax = max_over_32(amax);
       const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
       const float inv = 1.f / scale;
       const int64_t blk = tile * 8 + 2 * g4 + h;
@@ -1704,6 +1825,30 @@ int hsg_fp8_dequantize(int dev, const void* q, const void* scales, int64_t n, vo
   const uint8_t* qp = static_cast<const uint8_t*>(q);
   const float* sc = static_cast<const float*>(scales);
   char* dp = static_cast<char*>(dst);
+  // streaming kernel: 8-B aligned codes, 16-B aligned destination
+  if ((reinterpret_cast<uintptr_t>(q) % 8) == 0 && (reinterpret_cast<uintptr_t>(dst) % 16) == 0 &&
+      (vpt == 2 || vpt == 4 || vpt == 8 || vpt == 16) &&
+      (dst_dtype == kBF16 || dst_dtype == kF16 || dst_dtype == kF32 || dst_dtype == kF64)) {
+    const int64_t epl = (dst_dtype == kF32) ? 4 : (dst_dtype == kF64 ? 2 : 8);
+    const int64_t waves = (n + 64 * epl * 4 - 1) / (64 * epl * 4);
+    const int vgrid = static_cast<int>(std::min<int64_t>((waves + 3) / 4, 256 * 16));
+#define HS_FP8DV(DT)                                                                          \
+  switch (vpt) {                                                                              \
+    case 2: hipLaunchKernelGGL((hs_fp8_dequant_v<DT, 128>), dim3(vgrid), dim3(kBlock), 0, s, qp, sc, n, dp); break; \
+    case 4: hipLaunchKernelGGL((hs_fp8_dequant_v<DT, 256>), dim3(vgrid), dim3(kBlock), 0, s, qp, sc, n, dp); break; \
+    case 8: hipLaunchKernelGGL((hs_fp8_dequant_v<DT, 512>), dim3(vgrid), dim3(kBlock), 0, s, qp, sc, n, dp); break; \
+    default: hipLaunchKernelGGL((hs_fp8_dequant_v<DT, 1024>), dim3(vgrid), dim3(kBlock), 0, s, qp, sc, n, dp); break; \
+  }
+    switch (dst_dtype) {
+      case kBF16: HS_FP8DV(kBF16); break;
+      case kF16: HS_FP8DV(kF16); break;
+      case kF32: HS_FP8DV(kF32); break;
+      default: HS_FP8DV(kF64); break;
+    }
+#undef HS_FP8DV
+    HS_CHECK(hipGetLastError());
+    return 0;
+  }
   switch (vpt) {
     case 2: hipLaunchKernelGGL(hs_fp8_dequant<2>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;
     case 4: hipLaunchKernelGGL(hs_fp8_dequant<4>, dim3(grid), dim3(kBlock), 0, s, qp, sc, n, dp, dst_dtype); break;

@@ -630,7 +630,8 @@ def h2d_into(dst: torch.Tensor, host_addr: int, nbytes: int, src_dtype: torch.dt
     """
     dev = device_of(dst)
     slot = copy_slot()
-    if dst.dtype == src_dtype and dst.is_contiguous() and list(dst.shape) == list(src_shape):
+    if dst.dtype == src_dtype and dst.is_contiguous() and list(dst.shape) == list(src_shape) \
+            and not _is_managed(dst):
         native.memcpy(dev, slot, dst.data_ptr(), host_addr, nbytes, native.H2D, producer,
                       sync=True)
         return
@@ -659,12 +660,15 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
     # Regions whose source bytes are one contiguous range and whose destination
     # is a contiguous tensor of the same dtype/shape go host -> destination with
     # one DMA each (no scratch, no kernel: the common FSDP/DTensor restore).
+    # Managed (UVM) destinations take the scratch + kernel path: a host ->
+    # managed DMA ran at 4.8 GB/s into HBM-resident pages (profiles/r3/s2/),
+    # the kernel writes them at HBM rate.
     kernel_regions = []
     for region in regions:
         src_dtype, src_shape, off, narrows, dst = region
         rng = _contiguous_src_range(src_dtype, src_shape, off, narrows)
         if (rng is not None and dst.dtype == src_dtype and dst.is_contiguous()
-                and dst.numel() * dst.element_size() == rng[1]):
+                and dst.numel() * dst.element_size() == rng[1] and not _is_managed(dst)):
             native.memcpy(dev, slot, dst.data_ptr(), host_addr + rng[0], rng[1], native.H2D,
                           None, sync=False)
         else:

@@ -56,3 +56,16 @@ def test_forget_arena_queues_unmap():
     finally:
         drain_process._mapped.clear()
         drain_process._to_close.clear()
+
+
+def test_helper_unavailable_falls_back(monkeypatch, tmp_path):
+    """No helper binary: drain() returns None (the caller drains in process)
+    and the failure is remembered instead of retried on every take."""
+    monkeypatch.setattr(drain_process, "_helper", None)
+    monkeypatch.setattr(drain_process, "_start_failed", None)
+    monkeypatch.setattr(_build, "DRAIN_HELPER", str(tmp_path / "missing_helper"))
+    if native.hip_runtime_path() is None:
+        pytest.skip("no HIP runtime loaded by torch")
+    assert not drain_process.available()
+    assert "not built" in drain_process._start_failed
+    assert drain_process.drain(0, 0, False, [], 1 << 20, 2, 1, 0, 8) is None
