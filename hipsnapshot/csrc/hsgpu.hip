@@ -1021,55 +1021,6 @@ __device__ __forceinline__ void load_half_row(const char* src, int64_t e0, int64
   }
 }
 
-// The same half row as raw 16-B words (2 for bf16/f16, 4 for f32): what the
-// Hadamard quantizer prefetches for its next tile (half the registers of the
-// converted floats); ok = false -> tail / misaligned, load_half_row at use.
-template <int DT>
-struct HalfRowRaw {
-  uint4 v[(DT == kF32) ? 4 : 2];
-  bool ok;
-};
-
-template <int DT>
-__device__ __forceinline__ void load_half_row_raw(const char* src, int64_t e0, int64_t n,
-                                                  HalfRowRaw<DT>& r) {
-  constexpr int ES = (DT == kF32) ? 4 : 2;
-  r.ok = e0 + 16 <= n && ((reinterpret_cast<uintptr_t>(src + e0 * ES) & 15) == 0);
-  if (r.ok) {
-    const uint4* v = reinterpret_cast<const uint4*>(src + e0 * ES);
-#pragma unroll
-    for (int q = 0; q < ((DT == kF32) ? 4 : 2); ++q) r.v[q] = v[q];
-  }
-}
-
-template <int DT>
-__device__ __forceinline__ void half_row_floats(const char* src, int64_t e0, int64_t n,
-                                                const HalfRowRaw<DT>& r, float* x) {
-  if (!r.ok) {
-    load_half_row<DT>(src, e0, n, x);
-    return;
-  }
-  if constexpr (DT == kF32) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      x[4 * q] = __uint_as_float(r.v[q].x);
-      x[4 * q + 1] = __uint_as_float(r.v[q].y);
-      x[4 * q + 2] = __uint_as_float(r.v[q].z);
-      x[4 * q + 3] = __uint_as_float(r.v[q].w);
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const uint32_t ws[4] = {r.v[q].x, r.v[q].y, r.v[q].z, r.v[q].w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        x[8 * q + 2 * i] = mx_unpack<DT>(ws[i], 0);
-        x[8 * q + 2 * i + 1] = mx_unpack<DT>(ws[i], 1);
-      }
-    }
-  }
-}
-
 // max over the 32 lanes of a wave half: quad xor-1 / xor-2 and the 8- and
 // 16-lane mirrors on DPP (no LDS traffic), one ds_bpermute for lane ^ 16
 __device__ __forceinline__ float max_over_32(float v) {
@@ -1090,17 +1041,11 @@ hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
   const int64_t nblocks = (n_pad + 127) / 128;
   const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
-  // software-pipelined: the next tile's half rows are loaded before this
-  // tile's MFMA chain, so every wave keeps HBM reads in flight while the
-  // matrix pipe works
-  HalfRowRaw<DT> raw;
-  raw.ok = false;
-  if (wave0 < ntiles) load_half_row_raw<DT>(src, (wave0 * 32 + r) * 32 + 16 * h, n, raw);
+  // (prefetching the next tile's half rows before the MFMA chain was tried:
+  // 100 VGPRs instead of 48, no faster -- profiles/r3/s2/fp8_host_timed_callE.jsonl)
   for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
     float x[16];
-    half_row_floats<DT>(src, (tile * 32 + r) * 32 + 16 * h, n, raw, x);
-    const int64_t next = tile + nwaves;
-    if (next < ntiles) load_half_row_raw<DT>(src, (next * 32 + r) * 32 + 16 * h, n, raw);
+    load_half_row<DT>(src, (tile * 32 + r) * 32 + 16 * h, n, x);
     floatx16 acc = {};
 #pragma unroll
     for (int t = 0; t < 16; ++t)
