@@ -28,7 +28,7 @@ MI355X-specific knobs:
   C++ threads (``csrc/hsdrain.hip``); ``HIPSNAPSHOT_DRAIN_SLOT_BYTES`` (32 MiB),
   ``_DRAIN_SLOTS`` (12), ``_DRAIN_WRITERS`` (min(8, io threads)),
   ``_DRAIN_NICE`` (10: nice increment of its threads), ``_DRAIN_DIRECT_IO`` (0:
-  O_DIRECT files, no page-cache copy); ``_DRAIN_PROCESS`` (1: run that drain in a
+  O_DIRECT files, no page-cache copy); ``_DRAIN_PROCESS`` (0: run that drain in a
   helper process that maps the arena over IPC, ``engine/drain_process.py``).
 * ``HIPSNAPSHOT_ASYNC_DEVICE_CODEC`` (raw) -- ``same``: an async take encodes
   its frozen device state like a blocking take.
@@ -325,10 +325,11 @@ def drain_process() -> bool:
     """Run the native drain in a helper process (csrc/hsdrain_helper.cpp)
     that maps the frozen arena through a HIP IPC handle: the trainer's
     process then runs no drain thread, runtime call or page-cache copy.
-    Default on: Llama-3-8B + AdamW at seq 512 drained 48 GB in 1.3-2.5 s
+    Opt-in (a bench.py run hung with it, under investigation): Llama-3-8B +
+    AdamW at seq 512 drained 48 GB in 1.3-2.5 s
     instead of 2.5-4.0 s and lost 0.21-0.33x a blocking take per checkpoint
     instead of 0.41-0.58x (profiles/r3/s2/overlap/)."""
-    return _get_bool("DRAIN_PROCESS", True)
+    return _get_bool("DRAIN_PROCESS", False)
 
 
 def uvm_assume_host() -> bool:
