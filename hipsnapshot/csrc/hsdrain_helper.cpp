@@ -32,7 +32,8 @@
 //                 i32 nslots, i32 nwriters, i32 flags, i32 max_hash_grid,
 //                 u32 close_after, u32 n, n x {u64 offset, u64 nbytes,
 //                 u32 plen, char path[plen]}
-//       reply:    i32 rc, u64 written, u32 n, u64 sums[n], u32 nstats,
+//       replies:  i32 mapped (0, or -10000: the arena could not be mapped),
+//                 then i32 rc, u64 written, u32 n, u64 sums[n], u32 nstats,
 //                 f64 stats[nstats], f64 map_s, u32 mlen, char msg[mlen]
 //     op 2 CLOSE: u32 hlen, u8 handle[hlen]        reply: i32 rc
 //     op 3 PING:                                   reply: i32 0, i32 pid
@@ -45,6 +46,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -63,12 +65,15 @@ using drain_wait_t = int (*)(void*, uint64_t*, uint64_t*, char*, double*);
 using ipc_open_t = void* (*)(int, const void*);
 using ipc_close_t = int (*)(void*);
 using last_error_t = const char* (*)();
+using init_device_t = int (*)(int);
 
 drain_start_t drain_start;
 drain_wait_t drain_wait;
 ipc_open_t ipc_open;
 ipc_close_t ipc_close;
 last_error_t last_error;
+init_device_t init_device;
+int g_ready_dev = -1;  // device whose runtime context is up
 
 bool read_all(void* p, size_t n) {
   char* c = static_cast<char*>(p);
@@ -135,6 +140,15 @@ void unmap(const std::string& handle) {
   g_maps.erase(it);
 }
 
+bool g_debug = false;  // HIPSNAPSHOT_DRAIN_HELPER_DEBUG: stage markers on stderr
+
+void dbg(const char* what) {
+  if (g_debug) {
+    fprintf(stderr, "hsdrain_helper[%d]: %s\n", static_cast<int>(getpid()), what);
+    fflush(stderr);
+  }
+}
+
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -153,9 +167,20 @@ bool do_drain(Out* out) {
   for (uint32_t i = 0; i < n; ++i)
     if (!get(&offs[i]) || !get(&sizes[i]) || !get_string(&paths[i])) return false;
 
+  if (g_ready_dev != dev) {
+    dbg("drain: runtime init");
+    if (init_device(dev) == 0) g_ready_dev = dev;
+    dbg("drain: runtime ready");
+  }
+  dbg("drain: mapping the arena");
   const double t0 = now_s();
   void* base = mapping(dev, handle);
   const double map_s = now_s() - t0;
+  dbg(base ? "drain: mapped, starting" : "drain: mapping failed");
+  // interim reply: the mapping outcome, before the (long) drain runs -- the
+  // trainer bounds this wait separately and drains in process on a stall
+  out->put(static_cast<int32_t>(base ? 0 : -10000));
+  if (!out->flush()) return false;
   int32_t rc = 0;
   uint64_t written = 0;
   std::vector<uint64_t> sums(n, 0);
@@ -179,7 +204,9 @@ bool do_drain(Out* out) {
       snprintf(msg, sizeof(msg), "drain helper: hsg_drain_start failed (%d): %s", err,
                last_error());
     } else {
+      dbg("drain: started, waiting");
       rc = drain_wait(job, sums.data(), &written, msg, stats);
+      dbg("drain: done");
     }
   }
   if (close_after) unmap(handle);
@@ -206,6 +233,8 @@ bool sym(void* lib, const char* name, F* fn) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  g_debug = getenv("HIPSNAPSHOT_DRAIN_HELPER_DEBUG") != nullptr;
+  dbg("started");
   if (argc < 3) {
     fprintf(stderr, "usage: hsdrain_helper <libamdhip64 path> <_hsgpu.so path>\n");
     return 2;
@@ -214,6 +243,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "hsdrain_helper: %s\n", dlerror());
     return 2;
   }
+  dbg("HIP runtime loaded");
   void* lib = dlopen(argv[2], RTLD_NOW);
   if (!lib) {
     fprintf(stderr, "hsdrain_helper: %s\n", dlerror());
@@ -221,8 +251,9 @@ int main(int argc, char** argv) {
   }
   if (!sym(lib, "hsg_drain_start", &drain_start) || !sym(lib, "hsg_drain_wait", &drain_wait) ||
       !sym(lib, "hsg_ipc_open", &ipc_open) || !sym(lib, "hsg_ipc_close", &ipc_close) ||
-      !sym(lib, "hsg_last_error", &last_error))
+      !sym(lib, "hsg_last_error", &last_error) || !sym(lib, "hsg_init_device", &init_device))
     return 2;
+  dbg("libraries loaded, serving");
   Out out;
   for (;;) {
     uint32_t magic = 0, op = 0;

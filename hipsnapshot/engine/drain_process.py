@@ -35,9 +35,11 @@ import atexit
 import errno
 import logging
 import os
+import select
 import struct
 import subprocess
 import threading
+import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from .. import _build
@@ -50,6 +52,10 @@ _OP_DRAIN, _OP_CLOSE, _OP_PING = 1, 2, 3
 
 class DrainHelperError(RuntimeError):
     """The helper process could not run a drain (it died or refused the job)."""
+
+
+class DrainHelperMapTimeout(DrainHelperError):
+    """The helper did not report the arena mapping in time (nothing drained)."""
 
 
 class DrainHelper:
@@ -71,7 +77,7 @@ class DrainHelper:
         self._w = self.proc.stdin.fileno()
         self._r = self.proc.stdout.fileno()
         self._send(struct.pack("=II", _MAGIC, _OP_PING))
-        rc, pid = struct.unpack("=ii", self._recv(8))
+        rc, pid = struct.unpack("=ii", self._recv(8, timeout=60.0))
         if rc != 0 or pid != self.proc.pid:
             raise DrainHelperError(f"drain helper handshake failed ({rc}, {pid})")
 
@@ -85,10 +91,32 @@ class DrainHelper:
         except OSError as e:
             raise DrainHelperError(f"drain helper is gone ({e})") from e
 
-    def _recv(self, n: int) -> bytes:
+    def _recv(self, n: int, timeout: Optional[float] = None, poke=None) -> bytes:
+        """``n`` reply bytes.  The helper's liveness is checked every few
+        seconds; ``timeout`` (s) bounds the whole wait (None = the drain
+        timeout knob)."""
+        from .. import knobs
+
+        limit = knobs.drain_helper_timeout_s() if timeout is None else timeout
+        t_end = time.monotonic() + limit if limit > 0 else None
         parts, left = [], n
         while left:
-            b = os.read(self._r, left)  # releases the GIL while it blocks
+            while True:
+                slot = 5.0 if poke is None else 0.05
+                wait = slot if t_end is None else min(slot, t_end - time.monotonic())
+                if wait <= 0:
+                    self.proc.kill()
+                    cls = DrainHelperMapTimeout if timeout is not None else DrainHelperError
+                    raise cls(f"drain helper did not answer within {limit:.0f} s (killed)")
+                ready, _, _ = select.select([self._r], [], [], wait)
+                if ready:
+                    break
+                if poke is not None:
+                    poke()
+                if self.proc.poll() is not None:
+                    raise DrainHelperError(
+                        f"drain helper exited (status {self.proc.returncode})")
+            b = os.read(self._r, left)  # the GIL is released while select waits
             if not b:
                 code = self.proc.poll()
                 raise DrainHelperError(f"drain helper exited (status {code})")
@@ -116,6 +144,16 @@ class DrainHelper:
             parts.append(struct.pack("=QQI", off, n, len(p)))
             parts.append(p)
         self._send(b"".join(parts))
+        from .. import knobs
+
+        poke = None
+        if knobs.drain_helper_poke():
+            from ..ops import native
+
+            lib = native.require_gpu_lib()
+            poke = lambda: lib.hsg_runtime_poke(dev)  # noqa: E731
+        (mapped,) = struct.unpack("=i", self._recv(4, timeout=knobs.drain_helper_map_timeout_s(),
+                                                   poke=poke))
         rc, written, n = struct.unpack("=iQI", self._recv(16))
         sums = list(struct.unpack(f"={n}Q", self._recv(8 * n))) if n else []
         (nstats,) = struct.unpack("=I", self._recv(4))
@@ -196,6 +234,16 @@ def drain(dev: int, arena_ptr: int, kept: bool, blobs: Sequence[Tuple[int, int, 
             rc, written, sums, stats, map_s, msg = helper.drain(
                 dev, handle, [(base_off + off, n, p) for off, n, p in blobs], slot_bytes,
                 nslots, nwriters, flags, max_hash_grid, close_after=not kept)
+        except DrainHelperMapTimeout as e:
+            # the arena could not be mapped in time: drain in process, now and
+            # for the rest of this process
+            logger.warning(f"{e}; draining in process from now on")
+            globals()["_start_failed"] = str(e)
+            dead, _helper = _helper, None
+            _mapped.clear()
+            _to_close.clear()
+            dead.shutdown()
+            return None
         except DrainHelperError:
             dead, _helper = _helper, None
             _mapped.clear()

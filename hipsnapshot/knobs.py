@@ -325,8 +325,10 @@ def drain_process() -> bool:
     """Run the native drain in a helper process (csrc/hsdrain_helper.cpp)
     that maps the frozen arena through a HIP IPC handle: the trainer's
     process then runs no drain thread, runtime call or page-cache copy.
-    Opt-in (a bench.py run hung with it, under investigation): Llama-3-8B +
-    AdamW at seq 512 drained 48 GB in 1.3-2.5 s
+    Opt-in: in bench.py's process the helper's hipIpcOpenMemHandle spins
+    (cause not found; a 30 s mapping timeout then drains in process, see
+    drain_helper_map_timeout_s).  Where it maps, Llama-3-8B + AdamW at seq 512
+    drained 48 GB in 1.3-2.5 s
     instead of 2.5-4.0 s and lost 0.21-0.33x a blocking take per checkpoint
     instead of 0.41-0.58x (profiles/r3/s2/overlap/)."""
     return _get_bool("DRAIN_PROCESS", False)
@@ -339,6 +341,25 @@ def uvm_assume_host() -> bool:
     a never-placed table reads at 57 GB/s from a kernel (PCIe), 3.9 TB/s once
     prefetched to the GPU (profiles/r3/uvm/)."""
     return _get_bool("UVM_ASSUME_HOST", os.environ.get("HSA_XNACK", "0") != "1")
+
+
+def drain_helper_timeout_s() -> float:
+    """Longest wait for one drain helper reply (s, 0 = unbounded); a helper
+    that does not answer in time is killed and the take's commit fails."""
+    return float(_get("DRAIN_HELPER_TIMEOUT_S") or 1800)
+
+
+def drain_helper_map_timeout_s() -> float:
+    """Longest wait for the drain helper to map an arena (s); on a stall the
+    helper is stopped and this process drains in process from then on."""
+    return float(_get("DRAIN_HELPER_MAP_TIMEOUT_S") or 30)
+
+
+def drain_helper_poke() -> bool:
+    """While the drain helper maps an arena, make a runtime call every 50 ms
+    in this process (diagnostic for a mapping that stalls while the trainer
+    is idle)."""
+    return _get_bool("DRAIN_HELPER_POKE", False)
 
 
 def gc_after_plan() -> bool:
