@@ -301,6 +301,46 @@ int hsg_sdma_d2h_submit(int dev, void* dst, const void* src, uint64_t n, void* s
   return 0;
 }
 
+// One system-scope release on `stream` (writes back the L2s), for a caller
+// that then submits many copies of memory nothing writes any more: the
+// async-take drain of a frozen arena.  Per-copy release events (above) cost
+// an event create/record/sync/destroy each -- ~1.3 ms per 32 MiB chunk when
+// the trainer's launches contend for the same runtime (profiles/r3/s2/overlap).
+int hsg_sdma_release(int dev, void* stream) {
+  if (hipSetDevice(dev) != hipSuccess) return -2;
+  hipEvent_t ev;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToSystem) != hipSuccess)
+    return -3;
+  hipError_t e = hipEventRecord(ev, static_cast<hipStream_t>(stream));
+  if (e == hipSuccess) e = hipEventSynchronize(ev);
+  hipEventDestroy(ev);
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "release event: %s", hipGetErrorString(e));
+    return -4;
+  }
+  return 0;
+}
+
+// hsg_sdma_d2h_submit without the per-copy release (after hsg_sdma_release).
+int hsg_sdma_d2h_submit_released(int dev, void* dst, const void* src, uint64_t n,
+                                 uint64_t* handle) {
+  *handle = 0;
+  DevInfo* d = dev_info(dev);
+  if (!d) return -1;
+  if (n == 0) return 0;
+  hsa_signal_t s = take_signal();
+  if (s.handle == 0) return -5;
+  g_api.signal_store(s, 1);
+  const hsa_status_t st = g_api.async_copy(dst, d->cpu, src, d->gpu, n, 0, nullptr, s);
+  if (st != HSA_STATUS_SUCCESS) {
+    give_signal(s);
+    snprintf(g_err, sizeof(g_err), "hsa_amd_memory_async_copy: status 0x%x", unsigned(st));
+    return -6;
+  }
+  *handle = s.handle;
+  return 0;
+}
+
 // Wait for a copy submitted by hsg_sdma_d2h_submit; 0 = done, < 0 = the
 // engine reported an error (the copy did not complete).  handle 0: no-op.
 int hsg_sdma_wait(uint64_t handle) {

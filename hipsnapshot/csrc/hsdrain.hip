@@ -52,6 +52,9 @@ extern "C" {
 int hsg_sdma_d2h_submit(int dev, void* dst, const void* src, uint64_t n, void* stream,
                         uint64_t* handle);
 int hsg_sdma_wait(uint64_t handle);
+int hsg_sdma_release(int dev, void* stream);
+int hsg_sdma_d2h_submit_released(int dev, void* dst, const void* src, uint64_t n,
+                                 uint64_t* handle);
 void* hsg_copy_stream(int dev, int slot);
 int hsg_stream_priority(int dev, int slot, int high);
 int hsg_hash64(int dev, int slot, int after_slot, const void* p, uint64_t n,
@@ -192,6 +195,13 @@ void dma_thread(Job* j) {
   const int hash_slot = (j->flags & kFlagHashLowPrio) ? kDrainHashSlotLow : kDrainHashSlot;
   if (hash_slot == kDrainHashSlot) hsg_stream_priority(j->dev, kDrainHashSlot, 1);
   void* stream = hsg_copy_stream(j->dev, kDrainCopySlot);
+  // the arena is frozen (the caller waited for the freeze): ONE system-scope
+  // release makes it visible to the copy engines, no per-chunk event
+  {
+    const uint64_t t0 = now_ns();
+    if (hsg_sdma_release(j->dev, stream) != 0) j->fail(-EIO, "release", "");
+    j->add(kSubmit, t0);
+  }
   int hashed = 0, collected = 0;
   const int nb = static_cast<int>(j->blobs.size());
   auto collect = [&](int upto) {
@@ -254,8 +264,8 @@ void dma_thread(Job* j) {
       const uint64_t off = c * j->slot_bytes;
       const uint64_t n = std::min(j->slot_bytes, b.nbytes - off);
       uint64_t h = 0;
-      r = hsg_sdma_d2h_submit(j->dev, j->slots[slot], reinterpret_cast<const void*>(b.src + off),
-                              n, stream, &h);
+      r = hsg_sdma_d2h_submit_released(j->dev, j->slots[slot],
+                                       reinterpret_cast<const void*>(b.src + off), n, &h);
       j->add(kSubmit, tw);
       if (r != 0) {
         j->fail(-EIO, "sdma submit", b.path);
