@@ -71,6 +71,12 @@ def _default_dir() -> str:
     return "hipsnapshot_bench"
 
 
+def _drain_stats():
+    from hipsnapshot.engine import native_drain
+
+    return dict(native_drain.last_stats) or None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -406,6 +412,8 @@ def main() -> None:
             "unblock_incl_freeze_ms": round(statistics.median(unblock_gpu), 2)
             if unblock_gpu else None,
             "async_iters": args.async_iters,
+            # rank 0's last native drain, seconds per phase (summed over its threads)
+            "async_drain_stats": _drain_stats(),
             "async_total_ms": round(statistics.median(drain), 2) if drain else None,
             "restore_bitwise_ok": restore_ok,
             "restore_GBps": round(restore_gbps, 2) if restore_gbps else None,

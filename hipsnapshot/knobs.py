@@ -25,8 +25,8 @@ MI355X-specific knobs:
 * ``HIPSNAPSHOT_HBM_ARENA_KEEP`` (1) -- keep the async-take HBM arena between
   takes (``hipsnapshot.release_hbm_arena()`` frees it).
 * ``HIPSNAPSHOT_NATIVE_DRAIN`` (1) -- drain raw frozen blobs to local files in
-  C++ threads (``csrc/hsdrain.hip``); ``HIPSNAPSHOT_DRAIN_SLOT_BYTES`` (32 MiB),
-  ``_DRAIN_SLOTS`` (12), ``_DRAIN_WRITERS`` (min(8, io threads)),
+  C++ threads (``csrc/hsdrain.hip``); ``HIPSNAPSHOT_DRAIN_SLOT_BYTES`` (64 MiB),
+  ``_DRAIN_SLOTS`` (16), ``_DRAIN_WRITERS`` (min(16, io threads)),
   ``_DRAIN_NICE`` (10: nice increment of its threads), ``_DRAIN_DIRECT_IO`` (0:
   O_DIRECT files, no page-cache copy); ``_DRAIN_PROCESS`` (0: run that drain in a
   helper process that maps the arena over IPC, ``engine/drain_process.py``).
@@ -301,18 +301,22 @@ def native_drain_enabled() -> bool:
     return _get_bool("NATIVE_DRAIN", True)
 
 
+# native drain sizing: 16 writers x 16 slots of 64 MiB drain the 16 GB
+# Llama-3-8B arena at the PCIe rate with an idle trainer (307 ms, was 380-475
+# ms with 8 x 12 x 32 MiB) and lose no more training time at seq 512
+# (profiles/r3/s2/drain_sizing/)
 def get_drain_slot_bytes() -> int:
-    return max(1 << 20, _get_int("DRAIN_SLOT_BYTES", 32 << 20))
+    return max(1 << 20, _get_int("DRAIN_SLOT_BYTES", 64 << 20))
 
 
 def get_drain_slots() -> int:
     """Pinned slots the native drain cycles through (slots x slot bytes of
     pinned host memory while a drain runs, outside the memory budget)."""
-    return max(2, _get_int("DRAIN_SLOTS", 12))
+    return max(2, _get_int("DRAIN_SLOTS", 16))
 
 
 def get_drain_writers() -> int:
-    return max(1, _get_int("DRAIN_WRITERS", min(8, get_io_threads())))
+    return max(1, _get_int("DRAIN_WRITERS", min(16, get_io_threads())))
 
 
 def get_drain_nice() -> int:
