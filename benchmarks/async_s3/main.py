@@ -40,6 +40,10 @@ def main():
     ap.add_argument("--concurrency", type=int, default=16)
     ap.add_argument("--part-mb", type=int, default=32)
     ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--share-of", type=int, default=None,
+                    help="save ONE rank's share of the model at this world size (each "
+                         "parameter's dim-0 shard as a DTensor, as benchmarks/rank_share "
+                         "builds it): BASELINE config 5's Llama-3-70B share on one GPU")
     args = ap.parse_args()
     rank, ws, dev = init_dist()
     from torch.distributed.device_mesh import init_device_mesh
@@ -48,8 +52,32 @@ def main():
     if args.layers:
         cfg.n_layers = args.layers
     mesh = init_device_mesh(dev.type, (ws,))
-    model = build_fsdp_llama(cfg, dev, torch.bfloat16, mesh=mesh)
-    nbytes = sum(p._local_tensor.numel() * 2 for p in model.parameters())
+    if args.share_of:
+        from torch.distributed.tensor import DTensor, Shard
+
+        from hipsnapshot import StateDict
+        from hipsnapshot.models.llama import Llama
+
+        with torch.device("meta"):
+            meta = Llama(cfg)
+        gen = torch.Generator(device=dev).manual_seed(0)
+        params = {}
+        for name, p in meta.named_parameters():
+            rows = -(-p.shape[0] // args.share_of)
+            local = (torch.randn((rows,) + tuple(p.shape[1:]), device=dev, generator=gen)
+                     * 0.02).to(torch.bfloat16)
+            params[name] = DTensor.from_local(local, mesh, [Shard(0)], run_check=False)
+        del meta
+        model = StateDict(**params)
+        tensors = list(params.values())
+    else:
+        model = build_fsdp_llama(cfg, dev, torch.bfloat16, mesh=mesh)
+        tensors = None
+    # after a restore, compare what the state holds NOW (a StateDict's entries
+    # may be re-pointed by load_state_dict)
+    local_of = ((lambda: list(model.values())) if tensors is not None
+                else (lambda: list(model.parameters())))
+    nbytes = sum(p._local_tensor.numel() * 2 for p in local_of())
     t = torch.tensor([nbytes], dtype=torch.int64, device=dev)
     dist.all_reduce(t)
     total_bytes = int(t.item())
@@ -76,21 +104,23 @@ def main():
         res["write_GBps"].append(round(total_bytes / tw / 1e9, 2))
         log(f"async_take {i}: unblock {tu * 1e3:.1f} ms, committed after {tw:.2f} s "
             f"({total_bytes / tw / 1e9:.2f} GB/s)")
-        refs = [p._local_tensor.clone() for p in model.parameters()]
-        for p in model.parameters():
-            p._local_tensor.zero_()
+        refs = [p._local_tensor.detach().clone() for p in local_of()]
+        with torch.no_grad():
+            for p in local_of():
+                p._local_tensor.zero_()
         sync(dev)
         t0 = time.perf_counter()
         Snapshot(path, storage_options=opts).restore(app)
         sync(dev)
         tr = max_over_ranks(time.perf_counter() - t0, dev)
         res["restore_GBps"].append(round(total_bytes / tr / 1e9, 2))
-        ok = ok and all(torch.equal(r, p._local_tensor) for r, p in zip(refs, model.parameters()))
+        ok = ok and all(torch.equal(r, p._local_tensor) for r, p in zip(refs, local_of()))
         del refs
         log(f"restore {i}: {tr:.2f} s ({total_bytes / tr / 1e9:.2f} GB/s) bitwise ok={ok}")
     flag = torch.tensor([int(ok)], device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     emit({"bench": "async_take_s3", "model": args.model, "layers": cfg.n_layers,
+          "share_of": args.share_of,
           "world_size": ws, "bytes": total_bytes, "compression": args.compression,
           "server": "fake S3, own process, loopback", "concurrency": args.concurrency,
           "part_mb": args.part_mb, **res, "restore_bitwise_ok": bool(flag.item())})
