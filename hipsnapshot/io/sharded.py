@@ -410,6 +410,9 @@ class ShardedTensorBufferConsumer(BufferConsumer):
             # UVM table pages in host DRAM: read the file straight into them
             self._direct = True
             return staging.managed_host_view(dst, self.producer)
+        return self._pinned_dest(nbytes)
+
+    def _pinned_dest(self, nbytes: int) -> Optional[StagedBuffer]:
         if self._gpu:
             from ..ops import native
 
@@ -418,7 +421,8 @@ class ShardedTensorBufferConsumer(BufferConsumer):
         return None
 
     def get_compressed_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
-        return self.get_read_dest(nbytes)
+        # encoded bytes are never the destination's bytes: no direct read
+        return self._pinned_dest(nbytes)
 
     async def consume_buffer(self, buf, executor: Optional[Executor] = None) -> None:
         if self._direct:
