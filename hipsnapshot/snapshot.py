@@ -251,9 +251,13 @@ class Snapshot:
         committed regardless.
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.async_take")
-        with paused_gc():
+        deferred_gc: list = []
+        with paused_gc(deferred_gc):
             pending = cls._async_take(path, app_state, pg, replicated, storage_options,
                                       _custom_tensor_prepare_func, quantize, compression)
+        # a new plan's one full GC pass runs in the commit thread after the
+        # drain, not on the unblock path (utils/tracing.paused_gc)
+        pending._gc_after = bool(deferred_gc)
         # the commit thread starts draining only now: its staging workers would
         # otherwise hold the GIL while this thread is still on its way out
         pending._go.set()
@@ -977,6 +981,7 @@ class PendingSnapshot:
         self._storage_options = storage_options
         self.stats: Dict[str, float] = {}
         self._go = threading.Event()  # set by async_take once it is returning
+        self._gc_after = False  # run the new plan's full GC pass after the commit
         store = get_or_create_store(comm) if comm.get_world_size() > 1 else None
         self.thread = threading.Thread(
             target=self._complete_snapshot, name="hipsnapshot-commit",
@@ -1042,6 +1047,11 @@ class PendingSnapshot:
                 storage.sync_close(event_loop)
             finally:
                 event_loop.close()
+            if self._gc_after:
+                import gc
+
+                with timeline.span("gc_after_plan"):
+                    gc.collect()
         self._done = True
 
     def wait(self) -> Snapshot:

@@ -199,7 +199,7 @@ class GcWatch:
 
 
 @contextlib.contextmanager
-def paused_gc():
+def paused_gc(defer_plan_gc: Optional[list] = None):
     """Suspend Python's cyclic GC for a bounded critical section (and, with
     ``HIPSNAPSHOT_GIL_SWITCH_US``, shorten the GIL switch interval for it).
 
@@ -217,7 +217,12 @@ def paused_gc():
     else, so that pass (160-200 ms with Llama-3-8B + AdamW loaded,
     profiles/r3/overlap/) would otherwise fall into the NEXT take's unblock
     or a training step.  Collecting at the end of the plan-building take puts
-    the one-time cost where the first take's other one-time costs are."""
+    the one-time cost where the first take's other one-time costs are.
+
+    ``defer_plan_gc`` (a list): instead of collecting, append True to it --
+    ``async_take`` runs that pass in its commit thread once the drain is done,
+    off the unblock path (while a GPU-bound training step waits on the
+    device with the GIL released)."""
     import gc
     import sys
 
@@ -239,5 +244,8 @@ def paused_gc():
             from ..engine import plan_cache
 
             if plan_cache.take_stored_flag() and knobs.gc_after_plan():
-                with timeline.span("gc_after_plan"):
-                    gc.collect()
+                if defer_plan_gc is not None:
+                    defer_plan_gc.append(True)
+                else:
+                    with timeline.span("gc_after_plan"):
+                        gc.collect()
