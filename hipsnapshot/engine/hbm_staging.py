@@ -34,7 +34,7 @@ from __future__ import annotations
 
 import logging
 from collections import defaultdict
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -102,24 +102,64 @@ def _zeros(dev: int) -> torch.Tensor:
     return z
 
 
-def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
-    """Returns {device: arena_bytes} for the devices that were (partly) frozen."""
-    if not native.gpu_available():
-        return {}
-    by_dev = defaultdict(list)  # device -> [(region bytes, member offsets, blob bytes, wr, sts)]
+def _layout(write_reqs: List[WriteReq]) -> Dict[int, list]:
+    """device -> [(region bytes, member offsets, blob bytes, wr, stagers)]."""
+    by_dev = defaultdict(list)
     for wr in write_reqs:
-        # a previous take's region (reused plan) never carries over
-        wr.buffer_stager.__dict__.pop("frozen_region", None)
-        wr.buffer_stager.__dict__.pop("frozen_event", None)
         sts = _cuda_sources(wr)
         if not sts:
             continue
         t = sts[0].tensor
         dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
         by_dev[dev].append((*_region(wr, sts), wr, sts))
+    return by_dev
+
+
+def _plan_layout(write_reqs: List[WriteReq], plan) -> Dict[int, list]:
+    """The layout of a reused take plan's requests is the same every take
+    (same tensors, same slabs): computed once and kept on the plan.  Requests
+    outside the plan (host tensors, objects) are scanned as usual."""
+    cache = getattr(plan, "freeze_layout", None)
+    if cache is None:
+        ids = {id(wr) for wr in plan.write_reqs}
+        cache = plan.freeze_layout = {"ids": ids, "layout": _layout(plan.write_reqs),
+                                      "launch": {}}
+    ids = cache["ids"]
+    extra = _layout([wr for wr in write_reqs if id(wr) not in ids])
+    if not extra:
+        return cache["layout"]
+    merged = defaultdict(list, {d: list(v) for d, v in cache["layout"].items()})
+    for d, v in extra.items():
+        merged[d].extend(v)
+    return merged
+
+
+def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]:
+    """Returns {device: arena_bytes} for the devices that were (partly) frozen.
+    ``plan``: the reused take plan the requests come from (layout and the
+    freeze launch's descriptor table are cached on it)."""
+    if not native.gpu_available():
+        return {}
+    for wr in write_reqs:
+        # a previous take's region (reused plan) never carries over
+        wr.buffer_stager.__dict__.pop("frozen_region", None)
+        wr.buffer_stager.__dict__.pop("frozen_event", None)
+    by_dev = _plan_layout(write_reqs, plan) if plan is not None else _layout(write_reqs)
+    launch_cache = plan.freeze_layout["launch"] if plan is not None else None
     frozen = {}
     cap = knobs.hbm_staging_max_bytes()
     for dev, reqs in by_dev.items():
+        want = sum(r[0] for r in reqs)
+        kept = _kept.get(dev)
+        if kept is not None and not kept[1] and kept[0].numel() >= want and want <= cap:
+            # the idle kept arena holds everything: no room estimate needed
+            try:
+                _freeze(dev, reqs, want, launch_cache)
+            except torch.cuda.OutOfMemoryError:
+                logger.info(f"HBM staging on cuda:{dev}: arena of {want} B not allocatable")
+                continue
+            frozen[dev] = want
+            continue
         free, _ = torch.cuda.mem_get_info(dev)
         # blocks torch's caching allocator holds but does not use are free
         # for the arena too (the allocator releases them and retries when a
@@ -141,7 +181,7 @@ def freeze_device_state(write_reqs: List[WriteReq]) -> Dict[int, int]:
             logger.info(f"HBM staging on cuda:{dev}: {total} of {want} B frozen, the rest "
                         "is staged to host before async_take returns")
         try:
-            _freeze(dev, chosen, total)
+            _freeze(dev, chosen, total, launch_cache if len(chosen) == len(reqs) else None)
         except torch.cuda.OutOfMemoryError:
             # fragmentation: the estimate above was optimistic -> host path
             logger.info(f"HBM staging on cuda:{dev}: arena of {total} B not allocatable")
@@ -217,29 +257,45 @@ def release_hbm_arena() -> int:
     return freed
 
 
-def _freeze(dev: int, chosen, total: int) -> None:
+def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -> None:
     _retire_launches()
     stream = torch.cuda.current_stream(dev)
     with torch.cuda.device(dev):
         with timeline.span("freeze_alloc", bytes=total):
             arena = _arena(dev, total)
-        batch = native.CopyBatch()
         base = arena.data_ptr()
-        zero = _zeros(dev).data_ptr()
-        placed = []  # (stager, arena offset)
-        off = 0
-        for region, moffs, blob, wr, sts in chosen:
-            end = 0
-            for st, mo in zip(sts, moffs):
-                if mo > end:  # slab gap: zeros, as the slab gather writes them
-                    batch.add_bytes(zero, base + off + end, mo - end)
-                t = st.tensor.detach()
-                if t.numel():
-                    batch.add_tensor(t, base + off + mo)
-                placed.append((st, off + mo))
-                end = mo + t.numel() * t.element_size()
-            wr.buffer_stager.frozen_region = (arena, off, blob)
-            off += region
+        # a reused plan into the same arena launches the very same copies:
+        # keep the packed descriptor table (sources = the plan's tensors,
+        # unchanged by construction of plan reuse; destinations = this arena)
+        key = (dev, base, total, len(chosen))
+        hit = launch_cache.get(dev) if launch_cache is not None else None
+        if hit is not None and hit[0] == key:
+            arr, placed, regions = hit[1], hit[2], hit[3]
+            for (wr, off, blob) in regions:
+                wr.buffer_stager.frozen_region = (arena, off, blob)
+        else:
+            batch = native.CopyBatch()
+            zero = _zeros(dev).data_ptr()
+            placed = []  # (stager, arena offset)
+            regions = []  # (write request, arena offset, blob bytes)
+            off = 0
+            for region, moffs, blob, wr, sts in chosen:
+                end = 0
+                for st, mo in zip(sts, moffs):
+                    if mo > end:  # slab gap: zeros, as the slab gather writes them
+                        batch.add_bytes(zero, base + off + end, mo - end)
+                    t = st.tensor.detach()
+                    if t.numel():
+                        batch.add_tensor(t, base + off + mo)
+                    placed.append((st, off + mo))
+                    end = mo + t.numel() * t.element_size()
+                wr.buffer_stager.frozen_region = (arena, off, blob)
+                regions.append((wr, off, blob))
+                off += region
+            with timeline.span("copy_pack", n=len(batch)):
+                arr = batch.pack()
+            if launch_cache is not None:
+                launch_cache[dev] = (key, arr, placed, regions)
         sts_all = [st for st, _ in placed]
         # producers may differ from the current stream: order after them
         for p in {st.producer for st in sts_all if st.producer is not None}:
@@ -249,7 +305,7 @@ def _freeze(dev: int, chosen, total: int) -> None:
                           else torch.cuda.ExternalStream(p))
                 stream.wait_event(ev)
         with timeline.span("freeze_launch", n=len(sts_all)):
-            keep = batch.launch(dev, int(stream.cuda_stream), sync=False)
+            keep = native.launch_packed(arr, dev, int(stream.cuda_stream), sync=False)
         done = torch.cuda.Event()
         done.record(stream)
     _live_launches.append((keep, done))

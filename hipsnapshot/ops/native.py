@@ -633,29 +633,40 @@ class CopyBatch:
             return None
         from ..utils.tracing import timeline
 
-        lib = require_gpu_lib()
         with timeline.span("copy_pack", n=len(self.rows)):
             arr = self.pack()
-            ws_bytes = int(lib.hsg_copy_workspace_bytes(arr.ctypes.data, len(arr)))
-        with timeline.span("copy_stage_alloc", bytes=ws_bytes):
-            stage = PinnedBuffer(ws_bytes)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
-        cur = torch.cuda.current_stream(dev)
-        if int(cur.cuda_stream) != int(stream_handle):
-            # ``ws`` comes from torch's caching allocator in the CURRENT
-            # stream's order: its block may have been freed a moment ago by
-            # another thread (the trainer) with kernels still queued on that
-            # stream.  The launch stream must not write it before they ran.
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            torch.cuda.ExternalStream(int(stream_handle), device=f"cuda:{dev}").wait_event(ev)
-        rc = lib.hsg_copy_nd(dev, arr.ctypes.data, len(arr), ws.data_ptr(), ws_bytes,
-                             stage.ptr, stream_handle, 1 if sync else 0)
-        _check(rc, "hsg_copy_nd")
-        if sync:
-            stage.release()
-            return None
-        return (stage, ws)
+        return launch_packed(arr, dev, stream_handle, sync)
+
+
+def launch_packed(arr: np.ndarray, dev: int, stream_handle: int, sync: bool = True):
+    """``CopyBatch.launch`` of an already packed descriptor table (a caller
+    that launches the same copies again -- the async-take freeze of a reused
+    take plan -- keeps the table instead of rebuilding it)."""
+    if not len(arr):
+        return None
+    from ..utils.tracing import timeline
+
+    lib = require_gpu_lib()
+    ws_bytes = int(lib.hsg_copy_workspace_bytes(arr.ctypes.data, len(arr)))
+    with timeline.span("copy_stage_alloc", bytes=ws_bytes):
+        stage = PinnedBuffer(ws_bytes)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+    cur = torch.cuda.current_stream(dev)
+    if int(cur.cuda_stream) != int(stream_handle):
+        # ``ws`` comes from torch's caching allocator in the CURRENT
+        # stream's order: its block may have been freed a moment ago by
+        # another thread (the trainer) with kernels still queued on that
+        # stream.  The launch stream must not write it before they ran.
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        torch.cuda.ExternalStream(int(stream_handle), device=f"cuda:{dev}").wait_event(ev)
+    rc = lib.hsg_copy_nd(dev, arr.ctypes.data, len(arr), ws.data_ptr(), ws_bytes,
+                         stage.ptr, stream_handle, 1 if sync else 0)
+    _check(rc, "hsg_copy_nd")
+    if sync:
+        stage.release()
+        return None
+    return (stage, ws)
 
 
 def tensor_copy_descriptor(batch: CopyBatch, src: torch.Tensor, dst: torch.Tensor) -> None:

@@ -347,8 +347,8 @@ def test_async_take_partial_hbm_freeze(gpu, tmp_path):
     seen = {}
     orig = hbm_staging.freeze_device_state
 
-    def spy(write_reqs):
-        out = orig(write_reqs)
+    def spy(write_reqs, plan=None):
+        out = orig(write_reqs, plan)
         seen["frozen"] = out
         seen["kinds"] = [(type(wr.buffer_stager).__name__, hbm_staging.is_deferrable(wr))
                          for wr in write_reqs]
