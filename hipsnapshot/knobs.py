@@ -26,7 +26,7 @@ MI355X-specific knobs:
   takes (``hipsnapshot.release_hbm_arena()`` frees it).
 * ``HIPSNAPSHOT_NATIVE_DRAIN`` (1) -- drain raw frozen blobs to local files in
   C++ threads (``csrc/hsdrain.hip``); ``HIPSNAPSHOT_DRAIN_SLOT_BYTES`` (64 MiB),
-  ``_DRAIN_SLOTS`` (16), ``_DRAIN_WRITERS`` (min(16, io threads)),
+  ``_DRAIN_SLOTS`` (16), ``_DRAIN_WRITERS`` (min(16, io threads, half the rank's CPU share)),
   ``_DRAIN_NICE`` (10: nice increment of its threads), ``_DRAIN_DIRECT_IO`` (0:
   O_DIRECT files, no page-cache copy); ``_DRAIN_PROCESS`` (0: run that drain in a
   helper process that maps the arena over IPC, ``engine/drain_process.py``).
@@ -303,8 +303,10 @@ def native_drain_enabled() -> bool:
 
 # native drain sizing: 16 writers x 16 slots of 64 MiB drain the 16 GB
 # Llama-3-8B arena at the PCIe rate with an idle trainer (307 ms, was 380-475
-# ms with 8 x 12 x 32 MiB) and lose no more training time at seq 512
-# (profiles/r3/s2/drain_sizing/)
+# ms with 8 x 12 x 32 MiB; profiles/r3/s2/drain_sizing/).  The writers stay
+# within half of this rank's CPU share: a drain runs next to a training
+# loop, and writer threads that use up a cgroup CPU quota stall the
+# trainer's thread with them (8 writers on the 16-CPU box).
 def get_drain_slot_bytes() -> int:
     return max(1 << 20, _get_int("DRAIN_SLOT_BYTES", 64 << 20))
 
@@ -316,7 +318,8 @@ def get_drain_slots() -> int:
 
 
 def get_drain_writers() -> int:
-    return max(1, _get_int("DRAIN_WRITERS", min(16, get_io_threads())))
+    share = available_cpus() // max(_local_ranks_hint[0], 1)
+    return max(1, _get_int("DRAIN_WRITERS", min(16, get_io_threads(), max(2, share // 2))))
 
 
 def get_drain_nice() -> int:
