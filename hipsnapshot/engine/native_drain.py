@@ -69,7 +69,8 @@ def _run(dev: int, wrs: List[WriteReq], blobs, fsync: bool, want_sums: bool, dir
     when it can take it, else in this process's native threads.  Returns
     (hs64 partial sums, bytes written, stats, "helper" | "in_process")."""
     args = (knobs.get_drain_slot_bytes(), knobs.get_drain_slots(), knobs.get_drain_writers())
-    flags = native.NativeDrain.flags(fsync, want_sums, direct, True, knobs.get_drain_nice())
+    flags = native.NativeDrain.flags(fsync, want_sums, direct, knobs.drain_hash_high_priority(),
+                                     knobs.get_drain_nice())
     arenas = {id(wr.buffer_stager.frozen_region[0]): wr.buffer_stager.frozen_region[0]
               for wr in wrs}
     if knobs.drain_process() and len({a.data_ptr() for a in arenas.values()}) == 1:
@@ -84,7 +85,7 @@ def _run(dev: int, wrs: List[WriteReq], blobs, fsync: bool, want_sums: bool, dir
         if res is not None:
             return (*res, "helper")
     job = native.NativeDrain(dev, blobs, *args, fsync, want_sums, knobs.get_hash_grid(),
-                             knobs.get_drain_nice(), direct)
+                             knobs.get_drain_nice(), direct, knobs.drain_hash_high_priority())
     partial, written = job.wait()
     return partial, written, job.stats, "in_process"
 

@@ -350,6 +350,13 @@ def uvm_assume_host() -> bool:
     return _get_bool("UVM_ASSUME_HOST", os.environ.get("HSA_XNACK", "0") != "1")
 
 
+def drain_hash_high_priority() -> bool:
+    """The native drain's hs64 launches run on a high-priority stream
+    (default): at normal priority a training step's GEMMs starved them
+    (profiles/r3/drain_probe/)."""
+    return _get_bool("DRAIN_HASH_HIGH_PRIORITY", True)
+
+
 def drain_helper_timeout_s() -> float:
     """Longest wait for one drain helper reply (s, 0 = unbounded); a helper
     that does not answer in time is killed and the take's commit fails."""
