@@ -218,7 +218,7 @@ def drain(dev: int, arena_ptr: int, kept: bool, blobs: Sequence[Tuple[int, int, 
     stats) or None when the helper cannot take the job (run it in process)."""
     from ..ops import native
 
-    global _helper
+    global _helper, _start_failed
     with _lock:
         helper = _get()
         if helper is None:
@@ -238,7 +238,7 @@ def drain(dev: int, arena_ptr: int, kept: bool, blobs: Sequence[Tuple[int, int, 
             # the arena could not be mapped in time: drain in process, now and
             # for the rest of this process
             logger.warning(f"{e}; draining in process from now on")
-            globals()["_start_failed"] = str(e)
+            _start_failed = str(e)
             dead, _helper = _helper, None
             _mapped.clear()
             _to_close.clear()
@@ -254,7 +254,7 @@ def drain(dev: int, arena_ptr: int, kept: bool, blobs: Sequence[Tuple[int, int, 
             # mapping refused (IPC unsupported here): in process from now on
             logger.warning(f"drain helper: {msg}; draining in process")
             _helper = None
-            globals()["_start_failed"] = msg
+            _start_failed = msg
             helper.shutdown()
             return None
         if kept:
