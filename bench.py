@@ -24,9 +24,11 @@ reported as ``raw_GBps``; ``--compression none`` makes raw blobs the headline.
 
 Self-audit keys next to the headline (each with its step count):
 
-* ``freeze_gpu_ms`` -- event-timed busy time of the trainer's stream during
-  ``async_take`` (the HBM freeze kernel), and ``unblock_incl_freeze_ms``: host
-  time until that stream is free again;
+* ``freeze_gpu_ms`` -- event-timed GPU time from the start of ``async_take``
+  to the end of the HBM freeze it enqueues on the trainer's stream (includes
+  the host planning before the launch); ``freeze_kernel_ms`` -- the freeze
+  launch alone; ``unblock_incl_freeze_ms``: host time until that stream is
+  free again;
 * ``fresh_path_GBps`` -- the same take into a NEW ``step_<i>/`` directory each
   time (fresh files, as a training loop writes them); the headline rewrites
   one path;
@@ -206,9 +208,10 @@ def main() -> None:
     # async_take: time-to-unblock
     # time_to_unblock: host time until async_take returns.  The HBM freeze
     # it enqueued on the trainer's stream runs after that: freeze_gpu_ms is
-    # that stream's busy time between events recorded before and after the
-    # call (event-timed), unblock_incl_freeze_ms the host time until the
-    # stream is free again -- what a trainer whose next kernel waits sees.
+    # the GPU time between events recorded before and after the call (the
+    # host planning before the launch included), freeze_kernel_ms the launch
+    # alone, unblock_incl_freeze_ms the host time until the stream is free
+    # again -- what a trainer whose next kernel waits sees.
     cold_unblock = []
     for i in range(args.async_warmup):
         barrier_sync()
@@ -224,7 +227,10 @@ def main() -> None:
     unblock = []
     drain = []
     freeze = []
+    freeze_kernel = []
     unblock_gpu = []
+    from hipsnapshot.engine.hbm_staging import last_freeze_ms
+
     for i in range(args.async_iters):
         barrier_sync()
         e0 = torch.cuda.Event(enable_timing=True)
@@ -240,13 +246,15 @@ def main() -> None:
         pending.wait()
         torch.cuda.synchronize()
         td = time.perf_counter() - ts
-        u = torch.tensor([tu, td, e0.elapsed_time(e1) / 1e3, tg], dtype=torch.float64,
+        fk = last_freeze_ms(gpu_index) or 0.0
+        u = torch.tensor([tu, td, e0.elapsed_time(e1) / 1e3, tg, fk / 1e3], dtype=torch.float64,
                          device=dev)
         dist.all_reduce(u, op=dist.ReduceOp.MAX)
         unblock.append(float(u[0].item()) * 1e3)
         drain.append(float(u[1].item()) * 1e3)
         freeze.append(float(u[2].item()) * 1e3)
         unblock_gpu.append(float(u[3].item()) * 1e3)
+        freeze_kernel.append(float(u[4].item()) * 1e3)
         log(f"async {i}: unblock {unblock[-1]:.1f} ms (stream free at {unblock_gpu[-1]:.1f} ms, "
             f"freeze kernel {freeze[-1]:.2f} ms), total {drain[-1]:.1f} ms")
 
@@ -409,6 +417,9 @@ def main() -> None:
             "async_warmup": args.async_warmup,
             "freeze_gpu_ms": round(statistics.median(freeze), 3) if freeze else None,
             "freeze_gpu_ms_each": [round(f, 3) for f in freeze],
+            # the freeze launch alone (events around it inside async_take)
+            "freeze_kernel_ms": round(statistics.median(freeze_kernel), 3) if freeze_kernel
+            else None,
             "unblock_incl_freeze_ms": round(statistics.median(unblock_gpu), 2)
             if unblock_gpu else None,
             "async_iters": args.async_iters,

@@ -200,6 +200,20 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
 _kept: Dict[int, list] = {}
 
 
+# device -> (event before, event after) the last freeze launch
+_last_freeze: Dict[int, tuple] = {}
+
+
+def last_freeze_ms(dev: int = 0) -> Optional[float]:
+    """GPU time of the last async-take freeze launch on ``dev`` (waits for
+    it): what the trainer's stream spends on the copy itself."""
+    ev = _last_freeze.get(dev)
+    if ev is None:
+        return None
+    ev[1].synchronize()
+    return float(ev[0].elapsed_time(ev[1]))
+
+
 def _drop_kept(t: torch.Tensor) -> None:
     from . import drain_process
 
@@ -304,10 +318,13 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
                 ev.record(torch.cuda.default_stream(dev) if p == 0
                           else torch.cuda.ExternalStream(p))
                 stream.wait_event(ev)
+        t_start = torch.cuda.Event(enable_timing=True)
+        t_start.record(stream)
         with timeline.span("freeze_launch", n=len(sts_all)):
             keep = native.launch_packed(arr, dev, int(stream.cuda_stream), sync=False)
-        done = torch.cuda.Event()
+        done = torch.cuda.Event(enable_timing=True)
         done.record(stream)
+        _last_freeze[dev] = (t_start, done)
     _live_launches.append((keep, done))
     done_keep = (keep, done)
     for st, o in placed:
