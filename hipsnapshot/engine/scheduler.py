@@ -224,7 +224,9 @@ class PendingIOWork:
                 await asyncio.gather(*self.io_tasks, return_exceptions=True)
             done = True
         finally:
-            if done:
+            if self.executor is None:
+                pass  # nothing was staged (empty_write_work)
+            elif done:
                 _release_pool(self.executor, reusable=True)
             else:  # cancelled while waiting: tasks may still run
                 self.executor.shutdown(wait=True)
@@ -237,6 +239,15 @@ class PendingIOWork:
 
     def sync_complete(self, event_loop: asyncio.AbstractEventLoop) -> None:
         run_sync(event_loop, self.complete())
+
+
+def empty_write_work(memory_budget_bytes: int) -> PendingIOWork:
+    """The ``PendingIOWork`` of an empty request list, without a pipeline (an
+    async take whose every write was frozen in HBM stages nothing before it
+    returns; starting the pipeline for nothing cost ~0.3 ms of its unblock)."""
+    stats = PipelineStats()
+    stats.n_reqs = 0
+    return PendingIOWork(set(), None, stats, [], MemoryGate(memory_budget_bytes))
 
 
 async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,

@@ -518,8 +518,13 @@ class Snapshot:
                 # async: whatever was not frozen in HBM is copied from the
                 # LIVE tensors -- every such copy (and its hash) must have
                 # finished before async_take returns and training resumes
-                pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop,
-                                                  wait_copies=is_async)
+                if write_reqs or not is_async:
+                    pending = sync_execute_write_reqs(write_reqs, storage, budget, rank, loop,
+                                                      wait_copies=is_async)
+                else:
+                    from .engine.scheduler import empty_write_work
+
+                    pending = empty_write_work(budget)
         except BaseException:
             if gather is not None:
                 gather.join_quietly()  # the staging error is the one to report
