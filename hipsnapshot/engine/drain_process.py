@@ -203,11 +203,23 @@ def available() -> bool:
 
 
 def forget_arena(ptr: int) -> None:
-    """A kept arena is being dropped: unmap it in the helper before its next
-    job (never blocks: a drain may hold the pipe for seconds)."""
+    """A kept arena is being dropped: unmap it in the helper now when the
+    helper is idle (its mapping would otherwise pin the memory), else before
+    its next job (never blocks: a drain may hold the pipe for seconds)."""
     h = _mapped.pop(ptr, None)
-    if h is not None:
-        _to_close.append(h)
+    if h is None:
+        return
+    _to_close.append(h)
+    if _lock.acquire(blocking=False):
+        try:
+            helper = _helper
+            if helper is not None and helper.pid_owner == os.getpid():
+                while _to_close:
+                    helper.close_handle(_to_close.pop())
+        except DrainHelperError as e:
+            logger.warning(f"drain helper: unmapping a released arena failed: {e}")
+        finally:
+            _lock.release()
 
 
 def drain(dev: int, arena_ptr: int, kept: bool, blobs: Sequence[Tuple[int, int, str]],

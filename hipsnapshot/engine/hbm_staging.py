@@ -33,6 +33,7 @@ scales with the bytes that did NOT fit, instead of falling back wholesale.
 from __future__ import annotations
 
 import logging
+import weakref
 from collections import defaultdict
 from typing import Dict, List, Optional, Tuple
 
@@ -214,9 +215,31 @@ def last_freeze_ms(dev: int = 0) -> Optional[float]:
     return float(ev[0].elapsed_time(ev[1]))
 
 
+# arena data_ptr -> the stagers whose frozen_at / frozen_region view it (a
+# reused take plan keeps its stagers, and with them the arena, alive)
+_holders: Dict[int, "weakref.WeakSet"] = {}
+
+
+def _unpin(ptr: int) -> None:
+    """Clear every stager reference into the arena at ``ptr`` (its drain is
+    over): dropping the kept arena then really frees it."""
+    for st in list(_holders.pop(ptr, ())):
+        fa = st.__dict__.get("frozen_at")
+        if fa is not None and fa[0].data_ptr() == ptr:
+            st.frozen_at = None
+            st.frozen = False
+            st.wait_event = None
+            st.__dict__.pop("arena_keepalive", None)
+        fr = st.__dict__.get("frozen_region")
+        if fr is not None and fr[0].data_ptr() == ptr:
+            st.__dict__.pop("frozen_region", None)
+            st.__dict__.pop("frozen_event", None)
+
+
 def _drop_kept(t: torch.Tensor) -> None:
     from . import drain_process
 
+    _unpin(t.data_ptr())
     drain_process.forget_arena(t.data_ptr())  # the drain helper unmaps it
 
 
@@ -327,6 +350,10 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
         _last_freeze[dev] = (t_start, done)
     _live_launches.append((keep, done))
     done_keep = (keep, done)
+    if is_kept(arena):
+        holders = _holders.setdefault(base, weakref.WeakSet())
+        holders.update(st for st, _ in placed)
+        holders.update(r[0].buffer_stager for r in regions)
     for st, o in placed:
         st.frozen_at = (arena, o)  # _source() views the arena from now on
         st.producer = None  # ordering is carried by wait_event

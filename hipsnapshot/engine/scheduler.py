@@ -509,6 +509,7 @@ class DeferredIOWork:
 
         native_reqs, py_reqs = native_drain.split(self.deferred, self.storage)
         native_out: Dict[str, Any] = {}
+        native_fut: List[Any] = []  # the native drain's executor future
 
         async def run_deferred() -> None:
             if not py_reqs:
@@ -522,14 +523,21 @@ class DeferredIOWork:
             # one native call for every raw frozen blob: no Python (and no
             # GIL) between the arena and the files while the trainer runs
             if native_reqs:
-                native_out["sums"], native_out["bytes"] = \
-                    await asyncio.get_running_loop().run_in_executor(
-                        aux_pool(), native_drain.drain, native_reqs, self.storage)
+                cf = aux_pool().submit(native_drain.drain, native_reqs, self.storage)
+                native_fut.append(cf)
+                native_out["sums"], native_out["bytes"] = await asyncio.wrap_future(cf)
 
         try:
             res = await asyncio.gather(self.first.complete(), run_deferred(), run_native(),
                                        return_exceptions=True)
         finally:
+            # a cancelled wait does not stop the native drain thread: it
+            # still reads the arena, which is only free once it returned
+            for cf in native_fut:
+                try:
+                    cf.result()
+                except BaseException:  # noqa: BLE001 -- reported through ``res``
+                    pass
             # every reader of the frozen arena is done: a kept arena is free
             from .hbm_staging import arena_done
 

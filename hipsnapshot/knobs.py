@@ -36,7 +36,7 @@ MI355X-specific knobs:
   take that built a new take plan, not in a later take or training step.
 * ``HIPSNAPSHOT_REBALANCE`` (0) -- move whole blobs from loaded ranks to idle
   ones over xGMI before a sync take writes (``parallel/rebalance.py``).
-* ``HIPSNAPSHOT_UVM_ASSUME_HOST`` (1 unless ``HSA_XNACK=1``) -- managed tensors
+* ``HIPSNAPSHOT_UVM_ASSUME_HOST`` (1 unless the device runs with XNACK on) -- managed tensors
   never placed with ``ops.uvm.place`` are host-resident: blocking takes write
   host-resident UVM pages in place and restores read into them, instead of
   copying them over PCIe and back.
@@ -47,6 +47,7 @@ MI355X-specific knobs:
 
 from __future__ import annotations
 
+import functools
 import math
 import os
 from contextlib import contextmanager
@@ -341,13 +342,40 @@ def drain_process() -> bool:
     return _get_bool("DRAIN_PROCESS", False)
 
 
+def _arch_features(arch_name: str) -> dict:
+    """``gfx950:sramecc+:xnack-`` -> {"sramecc": "+", "xnack": "-"}."""
+    feats = {}
+    for f in arch_name.split(":")[1:]:
+        if f and f[-1] in "+-":
+            feats[f[:-1]] = f[-1]
+    return feats
+
+
+@functools.lru_cache(maxsize=None)
+def device_xnack_enabled(index: int = 0) -> bool:
+    """Whether the HIP device runs with XNACK (retryable page faults) on, read
+    from the device itself (``hipDeviceProp.gcnArchName`` feature suffix), not
+    from the environment.  False without a GPU."""
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            return False
+        name = torch.cuda.get_device_properties(index).gcnArchName
+    except Exception:  # noqa: BLE001 -- no device / old torch: XNACK unknown = off
+        return False
+    return _arch_features(name).get("xnack") == "+"
+
+
 def uvm_assume_host() -> bool:
     """Managed (UVM) tensors that were never advised / prefetched are in host
-    DRAM (blocking takes write them in place).  Default: unless XNACK is on
-    (HSA_XNACK=1), where pages migrate to the GPU that touches them.  Measured:
-    a never-placed table reads at 57 GB/s from a kernel (PCIe), 3.9 TB/s once
-    prefetched to the GPU (profiles/r3/uvm/)."""
-    return _get_bool("UVM_ASSUME_HOST", os.environ.get("HSA_XNACK", "0") != "1")
+    DRAM (blocking takes write them in place).  Default: unless the device runs
+    with XNACK on (``device_xnack_enabled``), where pages migrate to the GPU that
+    touches them.  Measured: a never-placed table reads at 57 GB/s from a kernel
+    (PCIe), 3.9 TB/s once prefetched to the GPU (profiles/r3/uvm/)."""
+    if _get("UVM_ASSUME_HOST") is not None:
+        return _get_bool("UVM_ASSUME_HOST", True)
+    return not device_xnack_enabled()
 
 
 def drain_hash_high_priority() -> bool:

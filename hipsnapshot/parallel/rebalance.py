@@ -124,8 +124,12 @@ class ReceivedBlobStager(BufferStager):
         return self.buf.numel()
 
 
-def _blob_bytes(wr: WriteReq) -> torch.Tensor:
-    """The blob's exact bytes as one contiguous uint8 tensor on its device."""
+def _blob_bytes(wr: WriteReq) -> Tuple[torch.Tensor, object]:
+    """The blob's exact bytes as one contiguous uint8 tensor on its device,
+    plus the keepalive of the gather launch that fills it (its pinned
+    descriptor stage and device workspace): hold it until the stream has
+    passed the launch, or a later launch reuses the stage block and the
+    gather reads ITS descriptors."""
     from ..io.batcher import GPUBatchedBufferStager
     from ..ops import native
 
@@ -138,11 +142,11 @@ def _blob_bytes(wr: WriteReq) -> torch.Tensor:
             t = m._source_view().detach()
             if t.numel():
                 batch.add_tensor(t, out.data_ptr() + lo)
-        batch.launch(dev.index or 0, int(torch.cuda.current_stream(dev).cuda_stream),
-                     sync=False)
-        return out
+        keep = batch.launch(dev.index or 0, int(torch.cuda.current_stream(dev).cuda_stream),
+                            sync=False)
+        return out, keep
     t = st._source().contiguous()
-    return t.reshape(-1).view(torch.uint8)
+    return t.reshape(-1).view(torch.uint8), None
 
 
 def rebalance(write_reqs: List[WriteReq], comm: Comm) -> List[WriteReq]:
@@ -168,12 +172,14 @@ def rebalance(write_reqs: List[WriteReq], comm: Comm) -> List[WriteReq]:
     rank = comm.get_rank()
     logger.info(f"rebalance: {len(moves)} blob(s), "
                 f"{sum(m[3] for m in moves) / 1e9:.2f} GB over xGMI")
-    ops, keep, outgoing, incoming = [], [], set(), []
+    ops, keep, launches, outgoing, incoming = [], [], [], set(), []
     pg = comm.pg
     for src, idx, dst, n, path in moves:
         if rank == src:
-            buf = _blob_bytes(write_reqs[idx])
+            buf, ka = _blob_bytes(write_reqs[idx])
             keep.append(buf)
+            if ka is not None:
+                launches.append(ka)
             outgoing.add(idx)
             ops.append(dist.P2POp(dist.isend, buf, dist.get_global_rank(pg, dst)
                                   if pg is not dist.group.WORLD else dst, group=pg))
@@ -184,6 +190,12 @@ def rebalance(write_reqs: List[WriteReq], comm: Comm) -> List[WriteReq]:
             incoming.append((path, buf))
             ops.append(dist.P2POp(dist.irecv, buf, dist.get_global_rank(pg, src)
                                   if pg is not dist.group.WORLD else src, group=pg))
+    if keep and any(b.is_cuda for b in keep):
+        # every gather launch (and the producers queued before it on this
+        # stream) must be done before a send reads its buffer and before its
+        # pinned descriptor stage goes back to the pool
+        torch.cuda.current_stream().synchronize()
+    launches.clear()
     if ops:
         if "nccl" in str(comm.backend()):
             works = dist.batch_isend_irecv(ops)  # one NCCL group: no ordering deadlock

@@ -141,8 +141,14 @@ def _state_dict_is_local(stateful: Any) -> bool:
 
     from .stateful import StateDict
 
-    if isinstance(stateful, (StateDict, RNGState, torch.optim.Optimizer)):
+    if isinstance(stateful, RNGState):
         return True
+    # a subclass that overrides state_dict (a sharded optimizer that gathers)
+    # keeps the per-key barrier
+    if isinstance(stateful, StateDict):
+        return type(stateful).state_dict is StateDict.state_dict
+    if isinstance(stateful, torch.optim.Optimizer):
+        return type(stateful).state_dict is torch.optim.Optimizer.state_dict
     if isinstance(stateful, nn.Module) and type(stateful).state_dict is nn.Module.state_dict:
         hit = _module_local.get(stateful)
         if hit is not None:
@@ -1030,13 +1036,23 @@ class PendingSnapshot:
                 # the metadata exchange happens here, through the store (not a
                 # collective): every rank publishes its part before it
                 # arrives at the commit barrier; rank 0 assembles them after
-                with timeline.span("manifest_payload", "commit"):
-                    payload = Snapshot._metadata_payload(metadata.manifest, metadata.plan)
-                    if store is None:
-                        metadata = Snapshot._assemble_metadata([payload], world_size)
-                    else:
-                        store.set(_manifest_key(path, nonce, rank), _encode_payload(*payload))
-                        metadata = None
+                try:
+                    with timeline.span("manifest_payload", "commit"):
+                        payload = Snapshot._metadata_payload(metadata.manifest, metadata.plan)
+                        if store is None:
+                            metadata = Snapshot._assemble_metadata([payload], world_size)
+                        else:
+                            store.set(_manifest_key(path, nonce, rank),
+                                      _encode_payload(*payload))
+                            metadata = None
+                except BaseException:
+                    # the drain must still be awaited (its threads read the
+                    # frozen arena and use this event loop) before failing
+                    try:
+                        pending_io_work.sync_complete(event_loop)
+                    except Exception:  # noqa: BLE001 -- the first error is reported
+                        pass
+                    raise
             pending_io_work.sync_complete(event_loop)
             _write_checksums(storage, event_loop, rank, world_size,
                              pending_io_work.stats.checksums)

@@ -1338,4 +1338,46 @@ def test_kept_hbm_arena_reused_and_never_shared(gpu, tmp_path):
         got = torch.zeros_like(w)
         Snapshot(str(tmp_path / f"a{i}")).restore({"sd": StateDict(w=got)})
         assert torch.equal(got, ref), i
-    assert release_hbm_arena() >= w.numel() * 4 and not hbm_staging._kept
+    del p1, p2, got
+    import gc
+
+    gc.collect()
+    torch.cuda.synchronize()
+    before = torch.cuda.memory_allocated(gpu)
+    freed = release_hbm_arena()
+    assert freed >= w.numel() * 4 and not hbm_staging._kept
+    # the memory really goes back: no cached plan's stager pins the arena
+    assert before - torch.cuda.memory_allocated(gpu) >= freed, (before, freed)
+
+
+def test_rebalance_blob_bytes_two_slabs_busy_stream(gpu):
+    """Two device slabs gathered for xGMI moves off one rank while the stream
+    is still busy: each launch's descriptor stage must stay alive until the
+    stream passes it, so both buffers hold exactly their members' bytes."""
+    from hipsnapshot.io.batcher import GPUBatchedBufferStager, batch_write_requests
+    from hipsnapshot.io.preparer import prepare_write
+    from hipsnapshot.parallel.rebalance import _blob_bytes
+
+    torch.manual_seed(0)
+    ts = [torch.randn(4096 + 13 * i, device=gpu) for i in range(12)]
+    entries, wrs = [], []
+    for i, t in enumerate(ts):
+        e, w = prepare_write(t, f"sd/t{i}", rank=0, replicated=False)
+        entries.append(e)
+        wrs += w
+    _, out = batch_write_requests(entries, wrs, slab_size_threshold_bytes=4 * 4096 * 4)
+    slabs = [w for w in out if isinstance(w.buffer_stager, GPUBatchedBufferStager)]
+    assert len(slabs) >= 2
+    a = torch.randn(2048, 2048, device=gpu)
+    for _ in range(20):  # queue work ahead of the gathers
+        a = a @ a
+        a /= a.norm()
+    got = [_blob_bytes(w) for w in slabs]
+    torch.cuda.current_stream().synchronize()
+    for w, (buf, _keep) in zip(slabs, got):
+        st = w.buffer_stager
+        want = torch.zeros(st.total, dtype=torch.uint8, device=gpu)
+        for (lo, hi), m in st.members:
+            src = m._source_view().reshape(-1).view(torch.uint8)
+            want[lo:lo + src.numel()] = src
+        assert torch.equal(buf, want)
