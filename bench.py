@@ -32,13 +32,26 @@ Self-audit keys next to the headline (each with its step count):
 * ``fresh_path_GBps`` -- the same take into a NEW ``step_<i>/`` directory each
   time (fresh files, as a training loop writes them); the headline rewrites
   one path;
-* ``vs_baseline_same_config`` -- the reference's own published config (DDP,
-  200 x 100 MB fp32 params = 20 GB, replicated, raw blobs) timed in the same
-  run, vs its 13.91 s (1 GPU) / 3.38 s (8 GPUs).  ``vs_baseline`` divides the
-  headline by the same reference number, i.e. it mixes configs.
+* ``vs_baseline`` (= ``vs_baseline_same_config``) -- the reference's own
+  published config (DDP, 200 x 100 MB fp32 params = 20 GB, replicated, raw
+  blobs) timed in the same run, vs its 13.91 s (1 GPU) / 3.38 s (8 GPUs);
+  null at 2 and 4 GPUs, where the reference publishes nothing.
 
-Launch: ``python bench.py`` (1 GPU) or
-``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
+BASELINE configs 2 and 3 run in the same command:
+
+* ``ddp_llama_*`` -- Llama-3-8B under DDP, bf16, ``replicated=["**"]``: the
+  partitioner splits the replicated state so each rank writes ~1/N of the
+  bytes (raw blobs), restore checked bitwise through per-parameter hashes;
+* ``elastic_*`` (N >= 2, N even) -- the FSDP checkpoint written by the N
+  ranks above restored into N/2 ranks (a fresh FSDP2 model on an N/2 mesh of
+  a ``dist.new_group``), every shard checked bitwise against hashes of the
+  N-rank shards it was cut from.
+
+Launch: ``python bench.py --gpus N`` starts N ranks itself (one process per
+GPU, the parent never touches the GPU) and forwards rank 0's JSON line; a
+failing or hung rank fails the whole run.  Under torchrun
+(``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N``)
+WORLD_SIZE must equal ``--gpus``.
 """
 
 from __future__ import annotations
@@ -47,14 +60,16 @@ import argparse
 import json
 import os
 import shutil
+import signal
 import socket
-import sys
 import statistics
+import subprocess
+import sys
+import threading
 import time
 
 # published reference numbers: DDP 20 GB save on p4d.24xlarge,
 # local FS -- 1 GPU 13.91 s (1.44 GB/s), 1 node x 8 GPUs 3.38 s (5.92 GB/s)
-BASELINE_GBPS = {1: 20.0 / 13.91, 8: 20.0 / 3.38}
 REF_DDP_S = {1: 13.91, 8: 3.38}  # the same DDP 20 GB config, seconds per save
 
 
@@ -77,6 +92,139 @@ def _drain_stats():
     from hipsnapshot.engine import native_drain
 
     return dict(native_drain.last_stats) or None
+
+
+def _hash_tensor(t, dev: int) -> int:
+    """hs64 of a contiguous device tensor's bytes (the blob-checksum kernel)."""
+    import torch
+
+    from hipsnapshot.ops import checksum
+
+    n = t.numel() * t.element_size()
+    if n == 0:
+        return 0
+    assert t.is_contiguous()
+    torch.cuda.synchronize()
+    h = checksum.device_hash_start(dev, 0, t.data_ptr(), n)
+    return checksum.device_hash_result(dev, 0, h, n)
+
+
+def _shard_hashes(model, dev: int) -> dict:
+    """{param: (global row offset, rows, hs64)} of this rank's FSDP shards."""
+    from torch.distributed.tensor._utils import compute_local_shape_and_global_offset
+
+    out = {}
+    for name, p in model.named_parameters():
+        loc = p._local_tensor
+        _, off = compute_local_shape_and_global_offset(p.shape, p.device_mesh, p.placements)
+        rows = int(loc.shape[0]) if loc.dim() else 0
+        out[name] = (int(off[0]) if len(off) else 0, rows, _hash_tensor(loc, dev))
+    return out
+
+
+def _check_resharded(model, old: list, dev: int) -> list:
+    """Compare every restored shard, piece by piece, with the hashes of the
+    shards it was cut from (``old``: every saving rank's ``_shard_hashes``).
+    Returns the mismatches."""
+    from torch.distributed.tensor._utils import compute_local_shape_and_global_offset
+
+    bad = []
+    for name, p in model.named_parameters():
+        loc = p._local_tensor
+        _, off = compute_local_shape_and_global_offset(p.shape, p.device_mesh, p.placements)
+        lo = int(off[0]) if len(off) else 0
+        rows = int(loc.shape[0]) if loc.dim() else 0
+        covered = 0
+        for o, n, h in sorted(r[name] for r in old):
+            if n == 0 or o + n <= lo or o >= lo + rows:
+                continue
+            if o < lo or o + n > lo + rows:  # N -> N/2 of Shard(0): whole pieces
+                bad.append((name, "piece straddles the new shard"))
+                continue
+            covered += n
+            if _hash_tensor(loc.narrow(0, o - lo, n), dev) != h:
+                bad.append((name, o))
+        if covered != rows:
+            bad.append((name, f"{covered} of {rows} rows covered"))
+    return bad
+
+
+def _selftest_hook(rank: int) -> None:
+    """``HIPSNAPSHOT_BENCH_SELFTEST`` (launcher tests on CPU, before any
+    torch import): ``ok`` -- rank 0 prints a JSON line, every rank exits 0;
+    ``fail:<r>`` -- rank r exits 3 at once, the others block as a rank stuck
+    in the rendezvous would."""
+    mode = os.environ.get("HIPSNAPSHOT_BENCH_SELFTEST")
+    if not mode:
+        return
+    if mode == "ok":
+        if rank == 0:
+            print(json.dumps({"metric": "selftest", "n_gpus": int(os.environ["WORLD_SIZE"])}),
+                  flush=True)
+        sys.exit(0)
+    if mode.startswith("fail:") and rank == int(mode.split(":")[1]):
+        sys.exit(3)
+    time.sleep(3600)
+    sys.exit(0)
+
+
+def _launch_ranks(n: int, argv: list, timeout_s: float) -> int:
+    """Start ``n`` ranks of this script (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*
+    set, one process group each) and forward rank 0's stdout.  The first rank
+    to fail, or the timeout, ends every rank; returns the exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+            stdout=subprocess.PIPE if r == 0 else None, start_new_session=True))
+
+    def pump() -> None:
+        for line in iter(procs[0].stdout.readline, b""):
+            sys.stdout.write(line.decode(errors="replace"))
+            sys.stdout.flush()
+
+    out = threading.Thread(target=pump, daemon=True)
+    out.start()
+
+    def kill_all() -> None:
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, sig)
+                    except ProcessLookupError:
+                        pass
+            t_end = time.monotonic() + 10
+            while time.monotonic() < t_end and any(p.poll() is None for p in procs):
+                time.sleep(0.1)
+
+    deadline = time.monotonic() + timeout_s
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, rc = bad[0]
+                print(f"bench launcher: rank {r} exited with {rc}; stopping every rank",
+                      file=sys.stderr, flush=True)
+                break
+            if all(c == 0 for c in codes):
+                break
+            if time.monotonic() > deadline:
+                print(f"bench launcher: timed out after {timeout_s:.0f} s; stopping every rank",
+                      file=sys.stderr, flush=True)
+                rc = 124
+                break
+            time.sleep(0.2)
+    finally:
+        kill_all()
+        out.join(timeout=5)
+    return rc
 
 
 def main() -> None:
@@ -112,12 +260,30 @@ def main() -> None:
                     help="hsz1 (default) = lossless GPU-side exponent-nibble compression of "
                          "the bf16 blobs, restore verified bitwise; none = raw blobs "
                          "(reference-compatible format)")
+    ap.add_argument("--ddp-llama-steps", type=int, default=2,
+                    help="BASELINE config 2: timed takes of the model under DDP, bf16, "
+                         "replicated=['**'] (partitioned across ranks, raw blobs) (0 = skip)")
+    ap.add_argument("--ddp-llama-layers", type=int, default=None,
+                    help="layers of the DDP model (default: all; a gloo rehearsal of 8 ranks "
+                         "on one GPU cannot hold 8 replicas + DDP buckets of Llama-3-8B)")
+    ap.add_argument("--elastic-iters", type=int, default=1,
+                    help="BASELINE config 3 (N >= 2, N even): restores of the N-rank FSDP "
+                         "checkpoint into N/2 ranks, each checked bitwise (0 = skip)")
+    ap.add_argument("--launch-timeout", type=float, default=3600.0,
+                    help="self-launched ranks (--gpus N > 1 without torchrun): seconds before "
+                         "every rank is stopped and the run fails")
     args = ap.parse_args()
+
+    torchrun = "RANK" in os.environ and "WORLD_SIZE" in os.environ
+    if not torchrun and args.gpus > 1:
+        # one process per GPU; this parent never initialises the GPU
+        sys.exit(_launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
+    if torchrun:
+        _selftest_hook(int(os.environ["RANK"]))
 
     import torch
     import torch.distributed as dist
 
-    torchrun = "RANK" in os.environ and "WORLD_SIZE" in os.environ
     if not torchrun:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
@@ -126,8 +292,8 @@ def main() -> None:
     world = int(os.environ["WORLD_SIZE"])
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using WORLD_SIZE",
-              file=sys.stderr)
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE is {world}", file=sys.stderr)
+        sys.exit(2)
     # --backend gloo rehearses the multi-rank path with several ranks sharing
     # one GPU (RCCL refuses that); the measured numbers are then NOT scaling data
     gpu_index = local_rank % max(torch.cuda.device_count(), 1)
@@ -147,6 +313,7 @@ def main() -> None:
 
     from hipsnapshot import Snapshot
     from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+    from hipsnapshot.snapshot import TakeStats
     from hipsnapshot.ops import native
 
     native.require_gpu_lib()  # the HIP data plane must be the one running
@@ -191,10 +358,13 @@ def main() -> None:
     gcw = GcWatch().start()  # Python GC time inside the timed regions (reported)
     barrier_sync()
     t0 = time.perf_counter()
+    my_step_s = []  # this rank's own take times (no barrier inside a step)
     for i in range(args.steps):
         ts = time.perf_counter()
         Snapshot.take(path, app_state, storage_options=opts, compression=args.compression)
-        log(f"step {i}: {time.perf_counter() - ts:.3f}s")
+        my_step_s.append(time.perf_counter() - ts)
+        log(f"step {i}: {my_step_s[-1]:.3f}s")
+    my_stored = int(TakeStats.last.get("bytes", 0))
     barrier_sync()
     t_end = time.perf_counter()
     elapsed = t_end - t0
@@ -204,6 +374,11 @@ def main() -> None:
     elapsed = float(e.item())
     ms_per_step = elapsed / args.steps * 1e3
     gbps = total_bytes / (ms_per_step / 1e3) / 1e9
+    # per-rank view: mean take time and stored bytes of every rank
+    per_rank = [None] * world
+    dist.all_gather_object(per_rank, (statistics.mean(my_step_s) * 1e3, my_stored))
+    rank_take_ms = sorted(r[0] for r in per_rank)
+    rank_stored = [r[1] for r in per_rank]
 
     # async_take: time-to-unblock
     # time_to_unblock: host time until async_take returns.  The HBM freeze
@@ -302,6 +477,54 @@ def main() -> None:
         log(f"restore: {restore_s:.3f}s ({restore_gbps:.2f} GB/s) ok={restore_ok} "
             f"each {restore_each} GB/s")
 
+    # BASELINE config 3: the N-rank FSDP checkpoint restored into N/2 ranks
+    elastic = {}
+    if args.elastic_iters > 0 and world >= 2 and world % 2 == 0:
+        from torch.distributed.device_mesh import DeviceMesh
+
+        from hipsnapshot import release_hbm_arena
+
+        release_hbm_arena()
+        mine = _shard_hashes(model, gpu_index)
+        old = [None] * world
+        dist.all_gather_object(old, mine)
+        half = world // 2
+        sub = dist.new_group(list(range(half)))
+        submesh = DeviceMesh("cuda", list(range(half)))  # every rank constructs it
+        times, bad = [], []
+        if rank < half:
+            model2 = build_fsdp_llama(cfg, dev, torch.bfloat16, mesh=submesh)
+            for _ in range(args.elastic_iters):
+                for p in model2.parameters():
+                    p._local_tensor.zero_()
+                torch.cuda.synchronize()
+                dist.barrier(group=sub)
+                tr = time.perf_counter()
+                Snapshot(path, pg=sub).restore({"model": model2})
+                torch.cuda.synchronize()
+                dist.barrier(group=sub)
+                times.append(time.perf_counter() - tr)
+                bad += _check_resharded(model2, old, gpu_index)
+            for n_, what in bad[:5]:
+                print(f"rank {rank}: elastic restore mismatch in {n_}: {what}", file=sys.stderr)
+            del model2
+            torch.cuda.empty_cache()
+        res = torch.tensor([max(times) if times else 0.0, float(bool(bad))],
+                           dtype=torch.float64, device=dev)
+        dist.all_reduce(res, op=dist.ReduceOp.MAX)
+        each = [None] * world
+        dist.all_gather_object(each, times)
+        per_iter = [max(e[i] for e in each[:half]) for i in range(len(each[0]))]
+        elastic = {
+            "elastic_from_ranks": world, "elastic_to_ranks": half,
+            "elastic_restore_s": round(statistics.median(per_iter), 3),
+            "elastic_restore_GBps": round(total_bytes / statistics.median(per_iter) / 1e9, 2),
+            "elastic_restore_GBps_each": [round(total_bytes / t / 1e9, 2) for t in per_iter],
+            "elastic_bitwise_ok": not bool(res[1].item()),
+        }
+        log(f"elastic restore {world} -> {half} ranks: {elastic}")
+        dist.barrier()
+
     # the same save with raw, reference-format blobs (no HSZ1): what the
     # headline would be without the codec, measured in the same process
     raw_gbps = None
@@ -388,7 +611,78 @@ def main() -> None:
         if rank == 0:
             shutil.rmtree(dpath, ignore_errors=True)
 
-    base = BASELINE_GBPS.get(world)
+    # BASELINE config 2: the model under DDP, bf16, replicated=["**"]: the
+    # partitioner spreads the replicated state over the ranks' writers
+    ddp_llama = {}
+    if args.ddp_llama_steps > 0:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+
+        from hipsnapshot import release_hbm_arena
+        from hipsnapshot.models.llama import Llama, init_weights_
+
+        release_hbm_arena()
+        dcfg = {"llama3_8b": LlamaConfig.llama3_8b, "llama3_70b": LlamaConfig.llama3_70b,
+                "tiny": LlamaConfig.tiny}[args.model]()
+        if args.ddp_llama_layers:
+            dcfg.n_layers = args.ddp_llama_layers
+        with torch.device("meta"):
+            dm = Llama(dcfg).to(torch.bfloat16)
+        dm.to_empty(device=dev)
+        init_weights_(dm, std=0.02)
+        ddp = DDP(dm, device_ids=[gpu_index])  # broadcasts rank 0's weights
+        dbytes = sum(p.numel() * p.element_size() for p in dm.parameters())
+        dpath = os.path.join(root, "ddp_llama")
+        dapp = {"model": ddp}
+        Snapshot.take(dpath, dapp, replicated=["**"], storage_options=opts, compression="none")
+        d_each, d_mine = [], []
+        for _ in range(args.ddp_llama_steps):
+            barrier_sync()
+            tf = time.perf_counter()
+            Snapshot.take(dpath, dapp, replicated=["**"], storage_options=opts,
+                          compression="none")
+            d_mine.append(time.perf_counter() - tf)
+            barrier_sync()
+            e = torch.tensor([time.perf_counter() - tf], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            d_each.append(float(e.item()))
+        d_written = int(TakeStats.last.get("bytes", 0))
+        # bitwise restore check through per-parameter hashes
+        before = {n: _hash_tensor(p.data, gpu_index) for n, p in dm.named_parameters()}
+        for p in dm.parameters():
+            p.data.zero_()
+        barrier_sync()
+        tr = time.perf_counter()
+        Snapshot(dpath).restore(dapp)
+        barrier_sync()
+        d_restore = time.perf_counter() - tr
+        dbad = [n for n, p in dm.named_parameters() if _hash_tensor(p.data, gpu_index) != before[n]]
+        for n in dbad[:5]:
+            print(f"rank {rank}: DDP restore mismatch in {n}", file=sys.stderr)
+        per = [None] * world
+        dist.all_gather_object(per, (d_written, statistics.mean(d_mine) * 1e3, d_restore,
+                                     len(dbad)))
+        d_s = statistics.median(d_each)
+        wr = [r[0] for r in per]
+        ddp_llama = {
+            "ddp_llama_GBps": round(dbytes / d_s / 1e9, 2),
+            "ddp_llama_s": round(d_s, 3),
+            "ddp_llama_s_each": [round(x, 3) for x in d_each],
+            "ddp_llama_bytes": dbytes,
+            "ddp_llama_layers": dcfg.n_layers,
+            "ddp_llama_rank_written_bytes": wr,
+            "ddp_llama_rank_written_max_over_mean": round(max(wr) / (sum(wr) / world), 3)
+            if sum(wr) else None,
+            "ddp_llama_rank_take_ms": [round(r[1], 1) for r in per],
+            "ddp_llama_restore_GBps": round(dbytes / max(r[2] for r in per) / 1e9, 2),
+            "ddp_llama_restore_bitwise_ok": all(r[3] == 0 for r in per),
+        }
+        log(f"DDP Llama partitioned save: {ddp_llama}")
+        del ddp, dm, dapp
+        torch.cuda.empty_cache()
+        if rank == 0:
+            shutil.rmtree(dpath, ignore_errors=True)
+        dist.barrier()
+
     if rank == 0:
         out = {
             "metric": "checkpoint save GB/s + time-to-unblock, Llama-3-8B FSDP",
@@ -400,7 +694,10 @@ def main() -> None:
             "ms_per_step": round(ms_per_step, 2),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": round(gbps / base, 3) if base else None,
+            # same config only (the reference's DDP 20 GB, timed below): null
+            # where the reference publishes no number (2 and 4 GPUs)
+            "vs_baseline": round(REF_DDP_S[world] / ddp_s, 2)
+            if ddp_s and world in REF_DDP_S else None,
             "dtype": "bf16",
             "data": "synthetic (random-init weights)",
             "config": {"model": {"llama3_8b": "Llama-3-8B", "llama3_70b": "Llama-3-70B",
@@ -410,6 +707,12 @@ def main() -> None:
                        "checkpoint_bytes": total_bytes,
                        "storage": "local fs" + (" fsync" if args.fsync else ""),
                        "compression": args.compression},
+            "world_size": dist.get_world_size(),
+            "backend": str(dist.get_backend()),
+            "rank_take_ms": {"max": round(rank_take_ms[-1], 2),
+                             "median": round(statistics.median(rank_take_ms), 2),
+                             "min": round(rank_take_ms[0], 2)},
+            "rank_stored_bytes": rank_stored,
             # median over the async iterations (each value listed below)
             "time_to_unblock_ms": round(statistics.median(unblock), 2) if unblock else None,
             "time_to_unblock_ms_each": [round(u, 2) for u in unblock],
@@ -450,6 +753,8 @@ def main() -> None:
             if ddp_s and world in REF_DDP_S else None,
             "baseline_note": "reference DDP 20GB save, p4d: 1 GPU 1.44 GB/s, 8 GPU 5.92 GB/s; "
                              "no published number for 2/4 GPUs",
+            **ddp_llama,
+            **elastic,
         }
         print(json.dumps(out), flush=True)
     dist.barrier()
