@@ -18,8 +18,6 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 HSIO_SO = os.path.join(PKG_DIR, "_hsio.so")
 HSGPU_SO = os.path.join(PKG_DIR, "_hsgpu.so")
-# drain helper process (csrc/hsdrain_helper.cpp): plain C++, dlopens _hsgpu.so
-DRAIN_HELPER = os.path.join(PKG_DIR, "_hsdrain_helper")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 GPU_ARCH = os.environ.get("HIPSNAPSHOT_GPU_ARCH", "gfx950")
 
@@ -66,23 +64,12 @@ def build_hsgpu(force: bool = False) -> str:
     return HSGPU_SO
 
 
-def build_drain_helper(force: bool = False) -> str:
-    srcs = [os.path.join(CSRC, "hsdrain_helper.cpp")]
-    if force or _stale(DRAIN_HELPER, srcs):
-        cxx = shutil.which("g++") or shutil.which("c++") or os.path.join(ROCM, "llvm/bin/clang++")
-        _atomic_build(DRAIN_HELPER, lambda out: [cxx, "-O2", "-std=c++17", "-Wall", "-o", out]
-                      + srcs + ["-ldl"])
-    return DRAIN_HELPER
-
-
 def build_all(force: bool = False) -> None:
     build_hsio(force)
     build_hsgpu(force)
-    build_drain_helper(force)
 
 
 if __name__ == "__main__":
     build_all(force="--force" in sys.argv)
     print(HSIO_SO)
     print(HSGPU_SO)
-    print(DRAIN_HELPER)

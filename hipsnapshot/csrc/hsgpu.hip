@@ -1943,78 +1943,4 @@ int hsg_managed_place(int dev, const void* p, uint64_t n, int loc, void* stream)
   return 0;
 }
 
-// ---- device memory shared with the drain helper process ---------------------
-//
-// The async-take arena is a block of torch's caching allocator, i.e. some
-// offset inside one hipMalloc allocation.  Export the allocation (IPC handle,
-// dmabuf-backed on this driver) plus the offset of `p` in it; the helper
-// (csrc/hsdrain_helper.cpp) maps the allocation once and keeps the mapping
-// while the arena is kept between takes.
-
-int hsg_ipc_export(const void* p, void* handle_out, uint64_t* offset, uint64_t* alloc_bytes) {
-  hipDeviceptr_t base = nullptr;
-  size_t size = 0;
-  HS_CHECK(hipMemGetAddressRange(&base, &size, const_cast<void*>(p)));
-  hipIpcMemHandle_t h;
-  HS_CHECK(hipIpcGetMemHandle(&h, base));
-  std::memcpy(handle_out, &h, sizeof(h));
-  *offset = static_cast<uint64_t>(static_cast<const char*>(p) - static_cast<char*>(base));
-  *alloc_bytes = size;
-  return 0;
-}
-
-int hsg_ipc_handle_bytes() { return static_cast<int>(sizeof(hipIpcMemHandle_t)); }
-
-// A dedicated device allocation for the async-take arena when the drain
-// helper maps it: one hipMalloc, exported whole, instead of a block inside a
-// torch caching-allocator segment (mapping such a segment in the helper
-// spun for > 60 s in bench.py, profiles/r3/s2/).
-void* hsg_device_alloc(int dev, uint64_t n) {
-  if (hipSetDevice(dev) != hipSuccess) return nullptr;
-  void* p = nullptr;
-  hipError_t e = hipMalloc(&p, n);
-  if (e != hipSuccess) { set_err("hipMalloc", e); return nullptr; }
-  return p;
-}
-
-int hsg_device_free(int dev, void* p) {
-  HS_CHECK(hipSetDevice(dev));
-  HS_CHECK(hipFree(p));
-  return 0;
-}
-
-// A cheap runtime round trip (null-stream query): the trainer makes it while
-// it waits for the drain helper to map an arena.
-int hsg_runtime_poke(int dev) {
-  HS_CHECK(hipSetDevice(dev));
-  const hipError_t e = hipStreamQuery(nullptr);
-  if (e != hipSuccess && e != hipErrorNotReady) { set_err("hipStreamQuery", e); return -1; }
-  (void)hipGetLastError();
-  return 0;
-}
-
-// Runtime init for `dev` in this process (context creation), separately
-// from the first IPC open, so a helper can report which of the two stalls.
-int hsg_init_device(int dev) {
-  HS_CHECK(hipSetDevice(dev));
-  HS_CHECK(hipFree(nullptr));
-  return 0;
-}
-
-void* hsg_ipc_open(int dev, const void* handle) {
-  hipError_t se = hipSetDevice(dev);
-  if (se != hipSuccess) { set_err("hipSetDevice", se); return nullptr; }
-  hipIpcMemHandle_t h;
-  std::memcpy(&h, handle, sizeof(h));
-  void* p = nullptr;
-  hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-  if (e != hipSuccess) { set_err("hipIpcOpenMemHandle", e); return nullptr; }
-  return p;
-}
-
-int hsg_ipc_close(void* p) {
-  HS_CHECK(hipIpcCloseMemHandle(p));
-  return 0;
-}
-
 }  // extern "C"

@@ -237,10 +237,7 @@ def _unpin(ptr: int) -> None:
 
 
 def _drop_kept(t: torch.Tensor) -> None:
-    from . import drain_process
-
     _unpin(t.data_ptr())
-    drain_process.forget_arena(t.data_ptr())  # the drain helper unmaps it
 
 
 def _arena(dev: int, total: int) -> torch.Tensor:
@@ -252,17 +249,7 @@ def _arena(dev: int, total: int) -> torch.Tensor:
         _drop_kept(k[0])  # a smaller idle one is dropped
         del _kept[dev]
         k = None
-    if knobs.drain_process():
-        # its own allocation: the drain helper maps exactly this, once.  The
-        # room estimate counts torch's cached blocks; hand them back first
-        # when hipMalloc does not find the space otherwise
-        try:
-            arena = native.device_tensor(dev, total)
-        except torch.cuda.OutOfMemoryError:
-            torch.cuda.empty_cache()
-            arena = native.device_tensor(dev, total)
-    else:
-        arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
+    arena = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{dev}")
     if knobs.hbm_arena_keep() and k is None:
         _kept[dev] = [arena, True]
     return arena

@@ -65,25 +65,9 @@ def split(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[List[WriteReq],
 
 
 def _run(dev: int, wrs: List[WriteReq], blobs, fsync: bool, want_sums: bool, direct: bool):
-    """One device's drain: in the helper process (HIPSNAPSHOT_DRAIN_PROCESS)
-    when it can take it, else in this process's native threads.  Returns
-    (hs64 partial sums, bytes written, stats, "helper" | "in_process")."""
+    """One device's drain in this process's native threads.  Returns (hs64
+    partial sums, bytes written, stats, "in_process")."""
     args = (knobs.get_drain_slot_bytes(), knobs.get_drain_slots(), knobs.get_drain_writers())
-    flags = native.NativeDrain.flags(fsync, want_sums, direct, knobs.drain_hash_high_priority(),
-                                     knobs.get_drain_nice())
-    arenas = {id(wr.buffer_stager.frozen_region[0]): wr.buffer_stager.frozen_region[0]
-              for wr in wrs}
-    if knobs.drain_process() and len({a.data_ptr() for a in arenas.values()}) == 1:
-        from . import drain_process
-        from .hbm_staging import is_kept
-
-        arena = next(iter(arenas.values()))
-        base = arena.data_ptr()
-        res = drain_process.drain(dev, base, is_kept(arena),
-                                  [(p - base, n, path) for p, n, path in blobs], *args, flags,
-                                  knobs.get_hash_grid())
-        if res is not None:
-            return (*res, "helper")
     job = native.NativeDrain(dev, blobs, *args, fsync, want_sums, knobs.get_hash_grid(),
                              knobs.get_drain_nice(), direct, knobs.drain_hash_high_priority())
     partial, written = job.wait()

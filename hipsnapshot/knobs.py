@@ -28,8 +28,7 @@ MI355X-specific knobs:
   C++ threads (``csrc/hsdrain.hip``); ``HIPSNAPSHOT_DRAIN_SLOT_BYTES`` (64 MiB),
   ``_DRAIN_SLOTS`` (16), ``_DRAIN_WRITERS`` (min(16, io threads, half the rank's CPU share)),
   ``_DRAIN_NICE`` (10: nice increment of its threads), ``_DRAIN_DIRECT_IO`` (0:
-  O_DIRECT files, no page-cache copy); ``_DRAIN_PROCESS`` (0: run that drain in a
-  helper process that maps the arena over IPC, ``engine/drain_process.py``).
+  O_DIRECT files, no page-cache copy).
 * ``HIPSNAPSHOT_ASYNC_DEVICE_CODEC`` (raw) -- ``same``: an async take encodes
   its frozen device state like a blocking take.
 * ``HIPSNAPSHOT_GC_AFTER_PLAN`` (1) -- one full Python GC pass at the end of a
@@ -329,19 +328,6 @@ def get_drain_nice() -> int:
     return max(0, min(19, _get_int("DRAIN_NICE", 10)))
 
 
-def drain_process() -> bool:
-    """Run the native drain in a helper process (csrc/hsdrain_helper.cpp)
-    that maps the frozen arena through a HIP IPC handle: the trainer's
-    process then runs no drain thread, runtime call or page-cache copy.
-    Opt-in: in bench.py's process the helper's hipIpcOpenMemHandle spins
-    (cause not found; a 30 s mapping timeout then drains in process, see
-    drain_helper_map_timeout_s).  Where it maps, Llama-3-8B + AdamW at seq 512
-    drained 48 GB in 1.3-2.5 s
-    instead of 2.5-4.0 s and lost 0.21-0.33x a blocking take per checkpoint
-    instead of 0.41-0.58x (profiles/r3/s2/overlap/)."""
-    return _get_bool("DRAIN_PROCESS", False)
-
-
 def _arch_features(arch_name: str) -> dict:
     """``gfx950:sramecc+:xnack-`` -> {"sramecc": "+", "xnack": "-"}."""
     feats = {}
@@ -383,25 +369,6 @@ def drain_hash_high_priority() -> bool:
     (default): at normal priority a training step's GEMMs starved them
     (profiles/r3/drain_probe/)."""
     return _get_bool("DRAIN_HASH_HIGH_PRIORITY", True)
-
-
-def drain_helper_timeout_s() -> float:
-    """Longest wait for one drain helper reply (s, 0 = unbounded); a helper
-    that does not answer in time is killed and the take's commit fails."""
-    return float(_get("DRAIN_HELPER_TIMEOUT_S") or 1800)
-
-
-def drain_helper_map_timeout_s() -> float:
-    """Longest wait for the drain helper to map an arena (s); on a stall the
-    helper is stopped and this process drains in process from then on."""
-    return float(_get("DRAIN_HELPER_MAP_TIMEOUT_S") or 30)
-
-
-def drain_helper_poke() -> bool:
-    """While the drain helper maps an arena, make a runtime call every 50 ms
-    in this process (diagnostic for a mapping that stalls while the trainer
-    is idle)."""
-    return _get_bool("DRAIN_HELPER_POKE", False)
 
 
 def gc_after_plan() -> bool:

@@ -269,12 +269,6 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                   ctypes.POINTER(ctypes.c_double)])
         _declare(lib, "hsg_drain_pending", c_int, [c_void_p])
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
-        _declare(lib, "hsg_ipc_export", c_int,
-                 [c_void_p, c_void_p, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)])
-        _declare(lib, "hsg_ipc_handle_bytes", c_int, [])
-        _declare(lib, "hsg_device_alloc", c_void_p, [c_int, c_uint64])
-        _declare(lib, "hsg_runtime_poke", c_int, [c_int])
-        _declare(lib, "hsg_device_free", c_int, [c_int, c_void_p])
         _declare(lib, "hsg_managed_location", c_int,
                  [c_void_p, c_uint64, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
         _declare(lib, "hsg_managed_place", c_int, [c_int, c_void_p, c_uint64, c_int, c_void_p])
@@ -812,43 +806,8 @@ def managed_place(dev: int, ptr: int, nbytes: int, loc: int, stream_handle: int)
            "hsg_managed_place")
 
 
-def device_tensor(dev: int, nbytes: int) -> torch.Tensor:
-    """A uint8 CUDA tensor over its own ``hipMalloc`` (outside torch's caching
-    allocator), freed with ``hipFree`` when the tensor's storage dies."""
-    import weakref
-
-    lib = require_gpu_lib()
-    ptr = lib.hsg_device_alloc(dev, max(nbytes, 1))
-    if not ptr:
-        raise torch.cuda.OutOfMemoryError(
-            f"hipMalloc({nbytes}) failed: {lib.hsg_last_error().decode()}")
-
-    class _Holder:
-        pass
-
-    holder = _Holder()
-    holder.__cuda_array_interface__ = {"shape": (max(nbytes, 1),), "typestr": "|u1",
-                                       "data": (ptr, False), "version": 3, "strides": None}
-    with torch.cuda.device(dev):
-        t = torch.as_tensor(holder, device=f"cuda:{dev}")
-    weakref.finalize(t.untyped_storage(), lib.hsg_device_free, dev, ptr)
-    return t
-
-
-def ipc_export(ptr: int) -> Tuple[bytes, int, int]:
-    """(IPC handle of the hipMalloc allocation holding ``ptr``, offset of
-    ``ptr`` in it, allocation bytes) -- for the drain helper process."""
-    lib = require_gpu_lib()
-    hb = ctypes.create_string_buffer(int(lib.hsg_ipc_handle_bytes()))
-    off = c_uint64(0)
-    size = c_uint64(0)
-    _check(lib.hsg_ipc_export(ptr, hb, ctypes.byref(off), ctypes.byref(size)), "hsg_ipc_export")
-    return hb.raw, int(off.value), int(size.value)
-
-
 def hip_runtime_path() -> Optional[str]:
-    """Path of the libamdhip64 this process has loaded (torch's), so a helper
-    process can load the very same runtime."""
+    """Path of the libamdhip64 this process has loaded (torch's)."""
     try:
         with open("/proc/self/maps") as f:
             for line in f:

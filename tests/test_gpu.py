@@ -1228,64 +1228,6 @@ def _native_vs_python_drain(gpu, tmp_path, fsync, monkeypatch, native_drain, ver
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("direct", [False, True])
-def test_drain_process_matches_python_drain(gpu, tmp_path, direct, monkeypatch):
-    """HIPSNAPSHOT_DRAIN_PROCESS=1: the drain runs in the helper process
-    (csrc/hsdrain_helper.cpp) on the arena mapped through a HIP IPC handle,
-    and writes byte-identical blobs and checksums to the Python drain."""
-    from hipsnapshot.engine import drain_process, native_drain
-    from hipsnapshot.verify import verify_snapshot
-
-    monkeypatch.setenv("HIPSNAPSHOT_DRAIN_PROCESS", "1")
-    cleanup = lambda: None  # noqa: E731
-    if direct:
-        tmp_path, cleanup = _odirect_dir(tmp_path)
-        import pathlib
-
-        tmp_path = pathlib.Path(tmp_path)
-        monkeypatch.setenv("HIPSNAPSHOT_DRAIN_DIRECT_IO", "1")
-    try:
-        _native_vs_python_drain(gpu, tmp_path, False, monkeypatch, native_drain,
-                                verify_snapshot)
-    finally:
-        cleanup()
-    assert native_drain.last_stats.get("where") == "helper", native_drain.last_stats
-    assert drain_process.available()
-
-
-def test_drain_process_kept_arena_mapping(gpu, tmp_path, monkeypatch):
-    """The helper maps a kept arena once and reuses the mapping; dropping the
-    arena (release_hbm_arena) unmaps it before the next job, and the next
-    take's new arena drains the right bytes."""
-    from hipsnapshot import release_hbm_arena
-    from hipsnapshot.engine import drain_process, hbm_staging, native_drain
-
-    monkeypatch.setenv("HIPSNAPSHOT_DRAIN_PROCESS", "1")
-    release_hbm_arena()
-    w = torch.randn(2048, 4096, device=gpu)
-    refs, maps = [], []
-    for i in range(3):
-        Snapshot.async_take(str(tmp_path / f"a{i}"), {"sd": StateDict(w=w)}).wait()
-        assert native_drain.last_stats["where"] == "helper"
-        maps.append(native_drain.last_stats["ipc_map"])
-        refs.append(w.clone())
-        w.mul_(-0.5)
-    kept = hbm_staging._kept[0][0].data_ptr()
-    assert kept in drain_process._mapped
-    assert release_hbm_arena() > 0 and kept not in drain_process._mapped
-    assert len(drain_process._to_close) == 1
-    Snapshot.async_take(str(tmp_path / "a3"), {"sd": StateDict(w=w)}).wait()
-    refs.append(w.clone())
-    assert not drain_process._to_close
-    for i, ref in enumerate(refs):
-        got = torch.zeros_like(w)
-        Snapshot(str(tmp_path / f"a{i}")).restore({"sd": StateDict(w=got)})
-        assert torch.equal(got, ref), i
-    # takes 2 and 3 found the arena mapped (a map is a lookup, not an IPC open)
-    assert maps[1] < 0.01 and maps[2] < 0.01, maps
-    release_hbm_arena()
-
-
 def test_native_drain_rewrite_trims_and_async_codec_policy(gpu, tmp_path):
     """An async take into a path whose files are larger (an earlier take of a
     bigger state) leaves exactly the new bytes; compression='hsz1' async
