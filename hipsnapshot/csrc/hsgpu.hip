@@ -1081,6 +1081,97 @@ hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
   }
 }
 
+// 16-bit inputs (bf16 / f16): the same rotation on the 16-bit MFMA,
+// v_mfma_f32_32x32x16_{bf16,f16}: K = 16 per instruction, so a 32x32 tile
+// takes 2 MFMAs instead of 16 f32 ones (~64 matrix-pipe cycles per KiB of
+// output instead of ~256, which no longer hide under the tile's HBM traffic).
+// The +-1 entries and the 16-bit inputs are exact; the products are summed
+// inside the MFMA in fp32, in the hardware's own order, so a result can differ
+// from the k-ordered fp32 reference in its last bit (tests bound the fp8 codes).
+// Operand maps (CDNA guide 3, 32x32x16): lane l, r = l&31, h = l>>5 holds
+//   A[row r][k = 8h + j], B[k = 8h + j][col r], j = 0..7, per K-step s (+16 s)
+// i.e. the A fragment of step s is the 16 contiguous bytes X[r][16s + 8h ..+7]:
+// one 16-B load, and the two loads of a wave cover the tile's 2 KiB exactly.
+// C/D is the f32 form's map, so the epilogue is the one above.
+typedef short hs_i16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 hs_bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hs_f16x8 __attribute__((ext_vector_type(8)));
+
+template <int DT>
+__device__ __forceinline__ floatx16 mfma16(hs_i16x8 a, hs_i16x8 b, floatx16 c) {
+  if constexpr (DT == kBF16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(hs_bf16x8, a),
+                                                   __builtin_bit_cast(hs_bf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(hs_f16x8, a),
+                                                  __builtin_bit_cast(hs_f16x8, b), c, 0, 0, 0);
+}
+
+template <int DT>
+__device__ __forceinline__ hs_i16x8 load_a_frag(const char* src, int64_t e0, int64_t n) {
+  hs_i16x8 a;
+  if (e0 + 8 <= n && ((reinterpret_cast<uintptr_t>(src + e0 * 2) & 15) == 0)) {
+    const mx_u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const mx_u32x4*>(src + e0 * 2));
+    a = __builtin_bit_cast(hs_i16x8, t);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      a[j] = (e0 + j < n) ? *reinterpret_cast<const short*>(src + (e0 + j) * 2) : short(0);
+  }
+  return a;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kBlock)
+hs_fp8_hadamard_quant16(const char* __restrict__ src, int64_t n, int64_t n_pad,
+                        uint8_t* __restrict__ out, float* __restrict__ scales) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t ntiles = (n_pad + 1023) / 1024;
+  const int64_t nblocks = (n_pad + 127) / 128;
+  const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+  // B fragments: H[16 s + 8 h + j][r] as 16-bit +-1 (bf16 0x3F80/0xBF80, f16 0x3C00/0xBC00)
+  const short one = (DT == kBF16) ? short(0x3F80) : short(0x3C00);
+  hs_i16x8 b0, b1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    b0[j] = (__popc((8 * h + j) & r) & 1) ? short(one | 0x8000) : one;
+    b1[j] = (__popc((16 + 8 * h + j) & r) & 1) ? short(one | 0x8000) : one;
+  }
+  for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
+    const int64_t e0 = (tile * 32 + r) * 32 + 8 * h;
+    const hs_i16x8 a0 = load_a_frag<DT>(src, e0, n);
+    const hs_i16x8 a1 = load_a_frag<DT>(src, e0 + 16, n);
+    floatx16 acc = {};
+    acc = mfma16<DT>(a0, b0, acc);
+    acc = mfma16<DT>(a1, b1, acc);
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      float amax = fmaxf(fmaxf(fabsf(acc[4 * g4]), fabsf(acc[4 * g4 + 1])),
+                         fmaxf(fabsf(acc[4 * g4 + 2]), fabsf(acc[4 * g4 + 3])));
+      amax = max_over_32(amax);
+      const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
+      const float inv = 1.f / scale;
+      const int64_t blk = tile * 8 + 2 * g4 + h;
+      if (r == 0 && blk < nblocks) scales[blk] = scale;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = fminf(fmaxf(acc[4 * g4 + q] * inv, -kFp8Max), kFp8Max);
+      uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false));
+      w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], static_cast<int>(w), true));
+      uint32_t o = static_cast<uint32_t>(
+          __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0xB1, 0xF, 0xF, false));  // lane ^ 1
+      w = __builtin_amdgcn_perm(o, w, (r & 1) ? 0x03070105u : 0x06020400u);
+      o = static_cast<uint32_t>(
+          __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0x4E, 0xF, 0xF, false));  // lane ^ 2
+      w = __builtin_amdgcn_perm(o, w, (r & 2) ? 0x03020706u : 0x05040100u);
+      const int64_t row0 = (tile * 32 + (r & 3) + 8 * g4 + 4 * h) * 32;
+      if (row0 < n_pad) __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(out + row0 + (r & ~3)));
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kBlock)
 hs_fp8_hadamard_dequant(const uint8_t* __restrict__ q, const float* __restrict__ scales,
                         int64_t n, int64_t n_pad, char* __restrict__ dst, int32_t dst_dtype) {
@@ -1866,8 +1957,8 @@ int hsg_fp8_hadamard_quantize(int dev, const void* src, int src_dtype, int64_t n
   uint8_t* op = static_cast<uint8_t*>(out);
   float* sc = static_cast<float*>(scales);
   switch (src_dtype) {
-    case kBF16: hipLaunchKernelGGL(hs_fp8_hadamard_quant<kBF16>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
-    case kF16: hipLaunchKernelGGL(hs_fp8_hadamard_quant<kF16>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
+    case kBF16: hipLaunchKernelGGL(hs_fp8_hadamard_quant16<kBF16>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
+    case kF16: hipLaunchKernelGGL(hs_fp8_hadamard_quant16<kF16>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
     case kF32: hipLaunchKernelGGL(hs_fp8_hadamard_quant<kF32>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
     default: snprintf(g_err, sizeof(g_err), "unsupported hadamard source dtype %d", src_dtype); return -1002;
   }

@@ -17,9 +17,13 @@ tensor is cut into groups of 32 elements and each group is multiplied by the
 computes ``(Y' H) / 32``.  The rotation spreads outliers over the group; for
 e4m3 that only pays when a block's dynamic range exceeds the format's (see
 ``default_rotation``), so it is off by default.  On MI355X both directions run on the
-matrix cores (``v_mfma_f32_32x32x2_f32``, exact f32 k-ordered FMA chains) in
-``hs_fp8_hadamard_quant/dequant``; the torch references below use the same
-sequential k order, so GPU and CPU produce bit-identical blobs.
+matrix cores.  bf16 / f16 tensors are rotated by ``v_mfma_f32_32x32x16_{bf16,f16}``
+(``hs_fp8_hadamard_quant16``: 2 MFMAs per 1024 elements; the MFMA sums 16 exact
+products in its own order, so a code can differ from the fp32 reference by one
+fp8 ulp -- tests bound it); fp32 tensors and every dequantization use
+``v_mfma_f32_32x32x2_f32`` (exact f32 k-ordered FMA chains) in
+``hs_fp8_hadamard_quant/dequant``, bit-identical to the torch references below,
+which use the same sequential k order.
 
 rotation ``"none"`` (default): plain blockwise quantization (``hs_fp8_quant`` kernel:
 one wave per block, 64-lane xor-shuffle amax, ``v_cvt_pk_fp8_f32`` -- gfx950
