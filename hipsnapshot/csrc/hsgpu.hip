@@ -1400,7 +1400,7 @@ int hsg_device_count() {
 // device 57.5 GB/s), but the CPU side -- pread()s of a restore into the
 // block, pwrite()s of a take out of it -- runs ~1.5x faster on 2 MiB pages
 // (pread into hipHostMalloc memory 88 GB/s, into THP-backed memory 131 GB/s,
-// 16 threads; scripts/pinned_thp_probe.py, profiles/pinned/).  Registering
+// 16 threads; scripts/probes/pinned_thp_probe.py, profiles/pinned/).  Registering
 // pre-faulted huge pages costs ~2 ms per GiB, once per pool block.  Any
 // failure falls back to hipHostMalloc.  HIPSNAPSHOT_PINNED_THP=0 turns it off.
 
@@ -1663,7 +1663,7 @@ int hash_ring(int dev, HashRing** out) {
 //
 // `max_grid` bounds the launch (<= 0: whole chip).  A full-width hash reads
 // HBM at ~4 TB/s and slows concurrent SDMA reads of HBM by ~20 %
-// (scripts/hash_probe.py), while blobs only need hashing at the PCIe rate;
+// (scripts/probes/hash_probe.py), while blobs only need hashing at the PCIe rate;
 // the staging path therefore launches it narrow.
 int hsg_hash64(int dev, int slot, int after_slot, const void* p, uint64_t n,
                uint64_t first_word, int max_grid, int* handle) {
@@ -1719,7 +1719,7 @@ int hsg_hash64_result(int dev, int slot, int handle, uint64_t* out) {
 // launches and 8-byte read-backs otherwise queue behind a saturating
 // training step's workgroups -- a GEMM loop on another stream cut a drain
 // with hashing from 36 to 13.5 GB/s, without hashing it kept 35.6 GB/s
-// (scripts/drain_contention_probe.py, profiles/r3/drain_probe/).  Returns
+// (scripts/probes/drain_contention_probe.py, profiles/r3/drain_probe/).  Returns
 // 1 if the stream already existed (its priority is unchanged).
 int hsg_stream_priority(int dev, int slot, int high) {
   std::lock_guard<std::mutex> g(g_stream_mu);

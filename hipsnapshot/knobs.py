@@ -156,7 +156,7 @@ def get_io_threads() -> int:
     2 x (CPUs this process can use, ``available_cpus``) / (ranks on this
     host), within [4, 16].  Buffered writes scale with threads only up to the
     CPU share: 8 processes x 16 writer threads on 16 CPUs wrote 26 GB/s to
-    the page cache, 8 x 2 threads 108 GB/s (scripts/pagecache_write_probe.py,
+    the page cache, 8 x 2 threads 108 GB/s (scripts/probes/pagecache_write_probe.py,
     profiles/pagecache/)."""
     v = _get("IO_THREADS")
     if v is not None:
@@ -232,7 +232,7 @@ def checksum_enabled() -> bool:
 def get_hash_grid() -> int:
     """Workgroups of one blob-checksum launch (0 = whole chip).  Narrow by
     default: a full-width hash saturates HBM reads and slows the concurrent
-    SDMA copies (scripts/hash_probe.py); blobs only need hashing at PCIe rate."""
+    SDMA copies (scripts/probes/hash_probe.py); blobs only need hashing at PCIe rate."""
     return _get_int("HASH_GRID", 64)
 
 
