@@ -163,6 +163,48 @@ def _state_dict_is_local(stateful: Any) -> bool:
     return False
 
 
+# FSDP2's own load_state_dict hooks (torch/distributed/fsdp/_fully_shard/):
+# the pre-hook reshards (a no-op once ``state_dict`` ran for the restore
+# plan) and the post-hook re-points the sharded parameter at its local
+# tensor (a no-op when that tensor is the one restored in place)
+_NOOP_LOAD_HOOKS = ("FSDPParamGroup._register_state_dict_hooks.<locals>.to_sharded_hook",
+                    "FSDPParam.__init__.<locals>.<lambda>")
+_module_plain_load: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _plain_module_load(module: Any) -> bool:
+    """True when ``module.load_state_dict`` does nothing beyond copying each
+    state-dict tensor into the module's own tensor: nn.Module's own
+    load_state_dict / _load_from_state_dict / set_extra_state in every
+    submodule and no load hooks other than FSDP2's no-op ones.  Kept per
+    module like ``_module_local``."""
+    import torch.nn as nn
+
+    if not isinstance(module, nn.Module) or \
+            type(module).load_state_dict is not nn.Module.load_state_dict:
+        return False
+    hit = _module_plain_load.get(module)
+    if hit is not None:
+        return hit
+
+    def known(h) -> bool:
+        h = getattr(h, "hook", h)  # _WrappedHook of _register_load_state_dict_pre_hook
+        return getattr(h, "__module__", "").startswith("torch.distributed.fsdp._fully_shard") \
+            and getattr(h, "__qualname__", "") in _NOOP_LOAD_HOOKS
+
+    ok = True
+    for m in module.modules():
+        t = type(m)
+        if t._load_from_state_dict is not nn.Module._load_from_state_dict or \
+                t.set_extra_state is not nn.Module.set_extra_state or \
+                not all(known(h) for h in m._load_state_dict_pre_hooks.values()) or \
+                not all(known(h) for h in m._load_state_dict_post_hooks.values()):
+            ok = False
+            break
+    _module_plain_load[module] = ok
+    return ok
+
+
 _avail_mem = [0, -1e9]  # [bytes available, time.monotonic() of the reading]
 
 
@@ -585,8 +627,10 @@ class Snapshot:
             with timeline.span("state_dict_view"):
                 _, flat = flatten(_state_dict_view(stateful), prefix=key)
         with timeline.span("restore_filter"):
+            n_leaves = len(flat)
             flat = {k: v for k, v in flat.items()
                     if isinstance(v, torch.Tensor) or is_sharded(v)}
+            own = dict(flat) if len(flat) == n_leaves else None
             prefix = flat_prefix(key)
             manifest = {k: v for k, v in manifest.items()
                         if k == prefix or k.startswith(prefix + "/")}
@@ -613,7 +657,15 @@ class Snapshot:
         with timeline.span("read_pipeline", n=len(reads)):
             sync_execute_read_reqs(reads, storage, budget, comm.get_rank(), loop)
         with timeline.span("load_state_dict", n=len(futs)):
-            state_dict = inflate(containers, {k: f.obj for k, f in futs.items()}, prefix=key)
+            objs = {k: f.obj for k, f in futs.items()}
+            # every leaf was read into the module's own tensor: load_state_dict
+            # would only copy each tensor onto itself (FSDP2: ~9 ms of DTensor
+            # copy_ dispatch per Llama-3-8B restore), so it is skipped
+            if own is not None and len(objs) == len(own) and \
+                    all(objs.get(k) is v for k, v in own.items()) and \
+                    _plain_module_load(stateful):
+                return
+            state_dict = inflate(containers, objs, prefix=key)
             stateful.load_state_dict(state_dict)
 
     # ---------------------------------------------------------- inspection

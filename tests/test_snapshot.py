@@ -239,3 +239,47 @@ def test_run_sync_reraises_without_cycle():
         assert not [o for o in _cyclic_garbage(fail) if isinstance(o, BaseException)]
     finally:
         loop.close()
+
+
+def test_in_place_module_restore_skips_self_copy(tmp_path, monkeypatch):
+    """Every leaf read into the module's own tensor: load_state_dict would
+    copy each tensor onto itself, so it is skipped; a module that customises
+    loading (its own _load_from_state_dict, or a load hook) still gets it."""
+    import torch.nn as nn
+
+    calls = []
+    orig = nn.Module.load_state_dict
+
+    def spy(self, *a, **k):
+        calls.append(type(self).__name__)
+        return orig(self, *a, **k)
+
+    monkeypatch.setattr(nn.Module, "load_state_dict", spy)
+    import hipsnapshot.snapshot as snap_mod
+
+    monkeypatch.setattr(snap_mod, "_module_plain_load", snap_mod.weakref.WeakKeyDictionary())
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(8, 4), nn.ReLU(), nn.Linear(4, 2))
+    ref = {k: v.clone() for k, v in m.state_dict().items()}
+    Snapshot.take(str(tmp_path / "a"), {"m": m})
+    for p in m.parameters():
+        p.data.zero_()
+    Snapshot(str(tmp_path / "a")).restore({"m": m})
+    assert calls == []
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, ref[k]), k
+
+    class Custom(nn.Linear):
+        def _load_from_state_dict(self, *a, **k):
+            calls.append("custom")
+            return super()._load_from_state_dict(*a, **k)
+
+    c = Custom(8, 4)
+    cref = {k: v.clone() for k, v in c.state_dict().items()}
+    Snapshot.take(str(tmp_path / "b"), {"c": c})
+    for p in c.parameters():
+        p.data.zero_()
+    Snapshot(str(tmp_path / "b")).restore({"c": c})
+    assert calls == ["Custom", "custom"]
+    for k, v in c.state_dict().items():
+        assert torch.equal(v, cref[k]), k
