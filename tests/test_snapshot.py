@@ -283,3 +283,21 @@ def test_in_place_module_restore_skips_self_copy(tmp_path, monkeypatch):
     assert calls == ["Custom", "custom"]
     for k, v in c.state_dict().items():
         assert torch.equal(v, cref[k]), k
+
+
+def test_local_metadata_cache_follows_the_file(tmp_path):
+    """Two Snapshot objects of one committed local snapshot share the parsed
+    metadata; a new take into the path replaces the file and is re-read."""
+    import hipsnapshot.snapshot as snap_mod
+
+    p = str(tmp_path / "s")
+    Snapshot.take(p, {"sd": StateDict(a=torch.ones(3), n=1)})
+    m1 = Snapshot(p).metadata
+    assert Snapshot(p).metadata is m1
+    Snapshot.take(p, {"sd": StateDict(a=torch.ones(3), n=2, extra=torch.zeros(5))})
+    m2 = Snapshot(p).metadata
+    assert m2 is not m1 and "0/sd/extra" in m2.manifest
+    out = StateDict(a=torch.zeros(3), n=0, extra=torch.ones(5))
+    Snapshot(p).restore({"sd": out})
+    assert out["n"] == 2 and torch.equal(out["extra"], torch.zeros(5))
+    assert len(snap_mod._metadata_cache) <= 4
