@@ -1121,7 +1121,40 @@ __device__ __forceinline__ hs_i16x8 load_a_frag(const char* src, int64_t e0, int
   return a;
 }
 
-template <int DT>
+// Epilogue of one rotated tile: blockwise scales + e4m3 codes (see above).
+__device__ __forceinline__ void hadamard_tile_store(const floatx16& acc, int64_t tile, int r,
+                                                    int h, int64_t n_pad, int64_t nblocks,
+                                                    uint8_t* __restrict__ out,
+                                                    float* __restrict__ scales) {
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    float amax = fmaxf(fmaxf(fabsf(acc[4 * g4]), fabsf(acc[4 * g4 + 1])),
+                       fmaxf(fabsf(acc[4 * g4 + 2]), fabsf(acc[4 * g4 + 3])));
+    amax = max_over_32(amax);
+    const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
+    const float inv = 1.f / scale;
+    const int64_t blk = tile * 8 + 2 * g4 + h;
+    if (r == 0 && blk < nblocks) scales[blk] = scale;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = fminf(fmaxf(acc[4 * g4 + q] * inv, -kFp8Max), kFp8Max);
+    uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false));
+    w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], static_cast<int>(w), true));
+    uint32_t o = static_cast<uint32_t>(
+        __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0xB1, 0xF, 0xF, false));  // lane ^ 1
+    w = __builtin_amdgcn_perm(o, w, (r & 1) ? 0x03070105u : 0x06020400u);
+    o = static_cast<uint32_t>(
+        __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0x4E, 0xF, 0xF, false));  // lane ^ 2
+    w = __builtin_amdgcn_perm(o, w, (r & 2) ? 0x03020706u : 0x05040100u);
+    const int64_t row0 = (tile * 32 + (r & 3) + 8 * g4 + 4 * h) * 32;
+    if (row0 < n_pad) __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(out + row0 + (r & ~3)));
+  }
+}
+
+// U tiles per iteration (2 A-fragment loads each): 2U 16-B loads in flight
+// per lane before the first MFMA (one tile per iteration ran at 4.2 TB/s,
+// latency-bound with 2 loads in flight).
+template <int DT, int U>
 __global__ void __launch_bounds__(kBlock)
 hs_fp8_hadamard_quant16(const char* __restrict__ src, int64_t n, int64_t n_pad,
                         uint8_t* __restrict__ out, float* __restrict__ scales) {
@@ -1139,69 +1172,142 @@ hs_fp8_hadamard_quant16(const char* __restrict__ src, int64_t n, int64_t n_pad,
     b0[j] = (__popc((8 * h + j) & r) & 1) ? short(one | 0x8000) : one;
     b1[j] = (__popc((16 + 8 * h + j) & r) & 1) ? short(one | 0x8000) : one;
   }
-  for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
-    const int64_t e0 = (tile * 32 + r) * 32 + 8 * h;
-    const hs_i16x8 a0 = load_a_frag<DT>(src, e0, n);
-    const hs_i16x8 a1 = load_a_frag<DT>(src, e0 + 16, n);
-    floatx16 acc = {};
-    acc = mfma16<DT>(a0, b0, acc);
-    acc = mfma16<DT>(a1, b1, acc);
+  // wave-uniform fast path: every load of the U tiles in bounds and 16-B
+  // aligned -> 2U vector loads issued back to back (a per-load bounds branch
+  // made the compiler wait for each load before the next one)
+  const bool aligned = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+  for (int64_t t0 = wave0 * U; t0 < ntiles; t0 += nwaves * U) {
+    hs_i16x8 a[U][2];
+    if (aligned && (t0 + U) * 1024 <= n) {
+      const mx_u32x4* p = reinterpret_cast<const mx_u32x4*>(src) + ((t0 * 32 + r) * 32 + 8 * h) / 8;
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      float amax = fmaxf(fmaxf(fabsf(acc[4 * g4]), fabsf(acc[4 * g4 + 1])),
-                         fmaxf(fabsf(acc[4 * g4 + 2]), fabsf(acc[4 * g4 + 3])));
-      amax = max_over_32(amax);
-      const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
-      const float inv = 1.f / scale;
-      const int64_t blk = tile * 8 + 2 * g4 + h;
-      if (r == 0 && blk < nblocks) scales[blk] = scale;
-      float v[4];
+      for (int u = 0; u < U; ++u) {
+        a[u][0] = __builtin_bit_cast(hs_i16x8, __builtin_nontemporal_load(p + u * 128));
+        a[u][1] = __builtin_bit_cast(hs_i16x8, __builtin_nontemporal_load(p + u * 128 + 2));
+      }
+    } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = fminf(fmaxf(acc[4 * g4 + q] * inv, -kFp8Max), kFp8Max);
-      uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false));
-      w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], static_cast<int>(w), true));
-      uint32_t o = static_cast<uint32_t>(
-          __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0xB1, 0xF, 0xF, false));  // lane ^ 1
-      w = __builtin_amdgcn_perm(o, w, (r & 1) ? 0x03070105u : 0x06020400u);
-      o = static_cast<uint32_t>(
-          __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0x4E, 0xF, 0xF, false));  // lane ^ 2
-      w = __builtin_amdgcn_perm(o, w, (r & 2) ? 0x03020706u : 0x05040100u);
-      const int64_t row0 = (tile * 32 + (r & 3) + 8 * g4 + 4 * h) * 32;
-      if (row0 < n_pad) __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(out + row0 + (r & ~3)));
+      for (int u = 0; u < U; ++u) {
+        const int64_t e0 = ((t0 + u) * 32 + r) * 32 + 8 * h;  // past the end: zeros
+        a[u][0] = load_a_frag<DT>(src, e0, n);
+        a[u][1] = load_a_frag<DT>(src, e0 + 16, n);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t0 + u >= ntiles) break;
+      floatx16 acc = {};
+      acc = mfma16<DT>(a[u][0], b0, acc);
+      acc = mfma16<DT>(a[u][1], b1, acc);
+      hadamard_tile_store(acc, t0 + u, r, h, n_pad, nblocks, out, scales);
     }
   }
 }
 
+// Dequantization on the fp8 MFMA: X = (Q H) * s / 32 with Q the e4m3 codes,
+// v_mfma_f32_32x32x16_fp8_fp8 (2 per tile).  Every e4m3 value is a multiple
+// of 2^-9 below 448, so a row sum of 32 of them (|sum| < 2^14) is exact in
+// fp32 whatever order the MFMA adds in: the only rounding is the product with
+// the block scale (the /32 is exact) -- ``ops/quant.py`` computes the same,
+// so GPU and CPU restores of a blob are bit-identical.
+// Operands (lane l, r = l&31, h = l>>5): the lane's 16 contiguous codes of
+// row r, k = 16h .. 16h+15, are its A fragments of steps 0 and 1 (k = 16h +
+// 8s + j); B holds H[16h + 8s + j][r] (e4m3 +-1 = 0x38 / 0xB8).  C/D as the
+// quant kernels: register quad g4 = rows 8g4 + 4h + 0..3, column r, one block
+// scale.  16-bit destinations leave through a 4x4 lane-quad transpose (3 DPP
+// moves per quad) as 8-B stores, 256 contiguous bytes per wave instruction.
+typedef long hs_fp8x8;
+
+template <int DT>
+__device__ __forceinline__ uint32_t pack16(float lo, float hi) {
+  uint32_t a, b;
+  if constexpr (DT == kBF16) {
+    a = f32_to_bf16(lo);
+    b = f32_to_bf16(hi);
+  } else {
+    a = __builtin_bit_cast(uint16_t, static_cast<_Float16>(lo));
+    b = __builtin_bit_cast(uint16_t, static_cast<_Float16>(hi));
+  }
+  return a | (b << 16);
+}
+
+template <int DT, int U>
 __global__ void __launch_bounds__(kBlock)
-hs_fp8_hadamard_dequant(const uint8_t* __restrict__ q, const float* __restrict__ scales,
-                        int64_t n, int64_t n_pad, char* __restrict__ dst, int32_t dst_dtype) {
+hs_fp8_hadamard_dequant8(const uint8_t* __restrict__ q, const float* __restrict__ scales,
+                         int64_t n, int64_t n_pad, char* __restrict__ dst) {
+  constexpr int DES = (DT == kF32) ? 4 : (DT == kF64 ? 8 : 2);
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int des = (dst_dtype == kF32) ? 4 : (dst_dtype == kF64 ? 8 : 2);
   const int64_t ntiles = (n_pad + 1023) / 1024;
   const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
-  for (int64_t tile = wave0; tile < ntiles; tile += nwaves) {
-    const int64_t grow = tile * 32 + r;  // global group (row) index
-    const int64_t e0 = grow * 32 + 16 * h;
-    const float s = (grow * 32 < n_pad) ? scales[(grow * 32) / 128] : 0.f;
-    // the lane's 16 fp8 codes: one 16-B load (n_pad is a multiple of 32)
-    uint32_t w[4] = {0, 0, 0, 0};
-    if (e0 + 16 <= n_pad) {
-      const uint4 v = *reinterpret_cast<const uint4*>(q + e0);
-      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-    }
-    floatx16 acc = {};
+  hs_fp8x8 b0 = 0, b1 = 0;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const float y = fp8_byte_to_f32(w[t >> 2], t & 3) * s;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(y, hada(16 * h + t, r), acc, 0, 0, 0);
+  for (int j = 0; j < 8; ++j) {
+    b0 |= int64_t((__popc((16 * h + j) & r) & 1) ? 0xB8 : 0x38) << (8 * j);
+    b1 |= int64_t((__popc((16 * h + 8 + j) & r) & 1) ? 0xB8 : 0x38) << (8 * j);
+  }
+  const bool vec_out = (DES == 2) && (reinterpret_cast<uintptr_t>(dst) & 7) == 0;
+  for (int64_t t0 = wave0 * U; t0 < ntiles; t0 += nwaves * U) {
+    mx_u32x4 a[U];
+    float sc[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // q holds n_pad bytes (a multiple of 32)
+      const int64_t e0 = ((t0 + u) * 32 + r) * 32 + 16 * h;
+      a[u] = (e0 + 16 <= n_pad) ? __builtin_nontemporal_load(reinterpret_cast<const mx_u32x4*>(q + e0))
+                                : mx_u32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int64_t blk = (t0 + u) * 8 + 2 * g4 + h;
+        sc[u][g4] = (blk * 128 < n_pad) ? scales[blk] : 0.f;
+      }
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-      const int64_t e = (tile * 32 + row) * 32 + r;
-      if (e < n) store_from_f32(dst + e * des, dst_dtype, acc[i] * (1.f / 32.f));
+    for (int u = 0; u < U; ++u) {
+      const int64_t tile = t0 + u;
+      if (tile >= ntiles) break;
+      floatx16 acc = {};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(
+          static_cast<hs_fp8x8>(a[u].x | (uint64_t(a[u].y) << 32)), b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(
+          static_cast<hs_fp8x8>(a[u].z | (uint64_t(a[u].w) << 32)), b1, acc, 0, 0, 0);
+      if (vec_out && (tile + 1) * 1024 <= n) {
+        if constexpr (DES == 2) {
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const float s = sc[u][g4] * (1.f / 32.f);
+            // lane slot i = row 8 g4 + 4 h + i, column r (two 16-bit rows per word)
+            uint32_t A = pack16<DT>(acc[4 * g4] * s, acc[4 * g4 + 1] * s);
+            uint32_t B = pack16<DT>(acc[4 * g4 + 2] * s, acc[4 * g4 + 3] * s);
+            // stage 1 (lanes ^ 1): 2x2 transposes of 16-bit elements
+            const uint32_t A1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(A), 0xB1, 0xF, 0xF, false));
+            const uint32_t B1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(B), 0xB1, 0xF, 0xF, false));
+            if (r & 1) {
+              A = __builtin_amdgcn_perm(A, A1, 0x07060302u);  // (partner.hi, mine.hi)
+              B = __builtin_amdgcn_perm(B, B1, 0x07060302u);
+            } else {
+              A = __builtin_amdgcn_perm(A1, A, 0x05040100u);  // (mine.lo, partner.lo)
+              B = __builtin_amdgcn_perm(B1, B, 0x05040100u);
+            }
+            // stage 2 (lanes ^ 2): swap 32-bit words
+            const uint32_t X = (r & 2) ? A : B;
+            const uint32_t R = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(X), 0x4E, 0xF, 0xF, false));
+            if (r & 2) A = R; else B = R;
+            const int64_t row = tile * 32 + 8 * g4 + 4 * h + (r & 3);
+            mx_u32x2 w;
+            w.x = A;
+            w.y = B;
+            __builtin_nontemporal_store(w, reinterpret_cast<mx_u32x2*>(dst + (row * 32 + (r & ~3)) * 2));
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+          const int64_t e = (tile * 32 + row) * 32 + r;
+          if (e < n) store_from_f32(dst + e * DES, DT, acc[i] * (sc[u][i >> 2] * (1.f / 32.f)));
+        }
+      }
     }
   }
 }
@@ -1952,13 +2058,15 @@ int hsg_fp8_hadamard_quantize(int dev, const void* src, int src_dtype, int64_t n
   const int64_t n_pad = (n + 31) / 32 * 32;
   const int64_t ntiles = (n_pad + 1023) / 1024;
   const int grid = static_cast<int>(std::min<int64_t>((ntiles + 3) / 4, 256 * 8));
+  constexpr int kHadU = 2;
+  const int grid16 = static_cast<int>(std::min<int64_t>((ntiles + 4 * kHadU - 1) / (4 * kHadU), 256 * 8));
   hipStream_t st = static_cast<hipStream_t>(stream);
   const char* sp = static_cast<const char*>(src);
   uint8_t* op = static_cast<uint8_t*>(out);
   float* sc = static_cast<float*>(scales);
   switch (src_dtype) {
-    case kBF16: hipLaunchKernelGGL(hs_fp8_hadamard_quant16<kBF16>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
-    case kF16: hipLaunchKernelGGL(hs_fp8_hadamard_quant16<kF16>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
+    case kBF16: hipLaunchKernelGGL((hs_fp8_hadamard_quant16<kBF16, kHadU>), dim3(grid16), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
+    case kF16: hipLaunchKernelGGL((hs_fp8_hadamard_quant16<kF16, kHadU>), dim3(grid16), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
     case kF32: hipLaunchKernelGGL(hs_fp8_hadamard_quant<kF32>, dim3(grid), dim3(kBlock), 0, st, sp, n, n_pad, op, sc); break;
     default: snprintf(g_err, sizeof(g_err), "unsupported hadamard source dtype %d", src_dtype); return -1002;
   }
@@ -1972,11 +2080,19 @@ int hsg_fp8_hadamard_dequantize(int dev, const void* q, const void* scales, int6
   if (n <= 0) return 0;
   const int64_t n_pad = (n + 31) / 32 * 32;
   const int64_t ntiles = (n_pad + 1023) / 1024;
-  const int grid = static_cast<int>(std::min<int64_t>((ntiles + 3) / 4, 256 * 8));
-  hipLaunchKernelGGL(hs_fp8_hadamard_dequant, dim3(grid), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(q),
-                     static_cast<const float*>(scales), n, n_pad, static_cast<char*>(dst),
-                     dst_dtype);
+  constexpr int U = 2;
+  const int grid = static_cast<int>(std::min<int64_t>((ntiles + 4 * U - 1) / (4 * U), 256 * 8));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint8_t* qp = static_cast<const uint8_t*>(q);
+  const float* sp = static_cast<const float*>(scales);
+  char* dp = static_cast<char*>(dst);
+  switch (dst_dtype) {
+    case kBF16: hipLaunchKernelGGL((hs_fp8_hadamard_dequant8<kBF16, U>), dim3(grid), dim3(kBlock), 0, st, qp, sp, n, n_pad, dp); break;
+    case kF16: hipLaunchKernelGGL((hs_fp8_hadamard_dequant8<kF16, U>), dim3(grid), dim3(kBlock), 0, st, qp, sp, n, n_pad, dp); break;
+    case kF32: hipLaunchKernelGGL((hs_fp8_hadamard_dequant8<kF32, U>), dim3(grid), dim3(kBlock), 0, st, qp, sp, n, n_pad, dp); break;
+    case kF64: hipLaunchKernelGGL((hs_fp8_hadamard_dequant8<kF64, U>), dim3(grid), dim3(kBlock), 0, st, qp, sp, n, n_pad, dp); break;
+    default: snprintf(g_err, sizeof(g_err), "unsupported hadamard dest dtype %d", dst_dtype); return -1002;
+  }
   HS_CHECK(hipGetLastError());
   return 0;
 }

@@ -20,10 +20,11 @@ e4m3 that only pays when a block's dynamic range exceeds the format's (see
 matrix cores.  bf16 / f16 tensors are rotated by ``v_mfma_f32_32x32x16_{bf16,f16}``
 (``hs_fp8_hadamard_quant16``: 2 MFMAs per 1024 elements; the MFMA sums 16 exact
 products in its own order, so a code can differ from the fp32 reference by one
-fp8 ulp -- tests bound it); fp32 tensors and every dequantization use
-``v_mfma_f32_32x32x2_f32`` (exact f32 k-ordered FMA chains) in
-``hs_fp8_hadamard_quant/dequant``, bit-identical to the torch references below,
-which use the same sequential k order.
+fp8 ulp -- tests bound it); fp32 tensors use ``v_mfma_f32_32x32x2_f32``
+(exact f32 k-ordered FMA chains, ``hs_fp8_hadamard_quant``), bit-identical to
+the torch reference below, which uses the same sequential k order.  Every
+dequantization runs on ``v_mfma_f32_32x32x16_fp8_fp8`` (``hs_fp8_hadamard_dequant8``):
+the row sums of e4m3 codes are exact, so GPU and torch restores agree bit for bit.
 
 rotation ``"none"`` (default): plain blockwise quantization (``hs_fp8_quant`` kernel:
 one wave per block, 64-lane xor-shuffle amax, ``v_cvt_pk_fp8_f32`` -- gfx950
@@ -247,11 +248,16 @@ def hadamard_quantize_reference(x: torch.Tensor, block: int = 128):
 
 def hadamard_dequantize_reference(q: torch.Tensor, scale: torch.Tensor, n: int,
                                   dtype: torch.dtype, block: int = 128) -> torch.Tensor:
+    """x = (Q H) * (s / 32): the row sums of e4m3 codes are exact (multiples of
+    2^-9 below 2^14, computed in float64 and exact in fp32), then ONE fp32
+    rounding by the block scale -- the same arithmetic as the GPU kernel
+    (``hs_fp8_hadamard_dequant8``, fp8 MFMA), so both are bit-identical."""
     n_pad = q.numel()
-    y = q.float().reshape(-1)
-    s = scale.repeat_interleave(block)[:n_pad]
-    rows = (y * s).view(-1, GROUP)
-    x = _rotate_sequential(rows) * (1.0 / GROUP)
+    rows = q.float().reshape(-1, GROUP).double()
+    h = hadamard_matrix(GROUP, rows.device).double()
+    z = (rows @ h).float()  # exact
+    s = (scale.float() * (1.0 / GROUP)).repeat_interleave(block // GROUP)[:z.shape[0]]
+    x = z * s[:, None]
     return x.reshape(-1)[:n].to(dtype)
 
 

@@ -177,8 +177,9 @@ def test_fp8_hadamard_mfma_vs_reference(gpu, dtype, n):
     bf16 / f16 inputs (v_mfma_f32_32x32x16_{bf16,f16}: the MFMA sums 16
     exact products in its own order): scales within 2 fp32 ulps, every fp8
     code within one fp8 ulp, >= 99.9 % identical, and the round-trip error no
-    worse than the reference's.  Dequantization (fp32 MFMA) is bit-identical
-    to the reference on the kernel's own codes."""
+    worse than the reference's.  Dequantization (fp8 MFMA, exact row sums)
+    is bit-identical to the reference on the kernel's own codes, into every
+    float dtype."""
     from hipsnapshot.ops.quant import hadamard_dequantize_reference, hadamard_quantize_reference
 
     torch.manual_seed(4)
@@ -197,11 +198,13 @@ def test_fp8_hadamard_mfma_vs_reference(gpu, dtype, n):
     else:
         assert torch.allclose(sc, rs, rtol=2.0 ** -22, atol=0), ((sc - rs) / rs).abs().max()
         _assert_fp8_codes_close(q, rq)
-    out = torch.empty(n, dtype=dtype, device=gpu)
-    native.fp8_hadamard_dequantize(0, q, sc, out, stream)
-    ref = hadamard_dequantize_reference(q.view(torch.float8_e4m3fn), sc, n, dtype)
-    torch.cuda.synchronize()
-    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max()
+    for out_dtype in (dtype, torch.float64):
+        out = torch.empty(n, dtype=out_dtype, device=gpu)
+        native.fp8_hadamard_dequantize(0, q, sc, out, stream)
+        ref = hadamard_dequantize_reference(q.view(torch.float8_e4m3fn), sc, n, out_dtype)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (out_dtype, (out.float() - ref.float()).abs().max())
+    out = out.to(dtype)
     if dtype != torch.float32 and n >= 1000:
         rt_ref = hadamard_dequantize_reference(rq, rs, n, torch.float32)
         err_gpu = (out.float() - x.float()).norm()
