@@ -1204,19 +1204,32 @@ hs_fp8_hadamard_quant16(const char* __restrict__ src, int64_t n, int64_t n_pad,
   }
 }
 
-// Dequantization on the fp8 MFMA: X = (Q H) * s / 32 with Q the e4m3 codes,
-// v_mfma_f32_32x32x16_fp8_fp8 (2 per tile).  Every e4m3 value is a multiple
-// of 2^-9 below 448, so a row sum of 32 of them (|sum| < 2^14) is exact in
-// fp32 whatever order the MFMA adds in: the only rounding is the product with
-// the block scale (the /32 is exact) -- ``ops/quant.py`` computes the same,
-// so GPU and CPU restores of a blob are bit-identical.
+// Dequantization on the matrix cores: X = (Q H) * s / 32 with Q the e4m3
+// codes widened to bf16 (exact: 3 mantissa bits, exponents -9..8) and fed to
+// v_mfma_f32_32x32x16_bf16 (2 per tile).  Every e4m3 value is a multiple of
+// 2^-9 below 448, so a row sum of 32 of them (|sum| < 2^14) is exact in fp32
+// whatever order the MFMA adds in: the only rounding is the product with the
+// block scale (the /32 is exact) -- ``ops/quant.py`` computes the same, so GPU
+// and CPU restores of a blob are bit-identical.  (The fp8 MFMA,
+// v_mfma_f32_32x32x16_fp8_fp8, is not used: on a 65 613-element test its
+// sums differed from the exact ones in the last bit -- subnormal e4m3 inputs
+// are the suspect.)
 // Operands (lane l, r = l&31, h = l>>5): the lane's 16 contiguous codes of
 // row r, k = 16h .. 16h+15, are its A fragments of steps 0 and 1 (k = 16h +
-// 8s + j); B holds H[16h + 8s + j][r] (e4m3 +-1 = 0x38 / 0xB8).  C/D as the
-// quant kernels: register quad g4 = rows 8g4 + 4h + 0..3, column r, one block
-// scale.  16-bit destinations leave through a 4x4 lane-quad transpose (3 DPP
-// moves per quad) as 8-B stores, 256 contiguous bytes per wave instruction.
-typedef long hs_fp8x8;
+// 8s + j); B holds H[16h + 8s + j][r] (bf16 +-1).  C/D as the quant kernels:
+// register quad g4 = rows 8g4 + 4h + 0..3, column r, one block scale.
+// 16-bit destinations leave through a 4x4 lane-quad transpose (3 DPP moves
+// per quad) as 8-B stores, 256 contiguous bytes per wave instruction.
+// 8 e4m3 codes (two words) -> 8 bf16 (exact: the f32 value's upper half)
+__device__ __forceinline__ hs_i16x8 fp8x8_to_bf16x8(uint32_t w0, uint32_t w1) {
+  hs_i16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = static_cast<short>(__float_as_uint(fp8_byte_to_f32(w0, j)) >> 16);
+    o[4 + j] = static_cast<short>(__float_as_uint(fp8_byte_to_f32(w1, j)) >> 16);
+  }
+  return o;
+}
 
 template <int DT>
 __device__ __forceinline__ uint32_t pack16(float lo, float hi) {
@@ -1241,11 +1254,11 @@ hs_fp8_hadamard_dequant8(const uint8_t* __restrict__ q, const float* __restrict_
   const int64_t ntiles = (n_pad + 1023) / 1024;
   const int64_t wave0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
-  hs_fp8x8 b0 = 0, b1 = 0;
+  hs_i16x8 b0, b1;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    b0 |= int64_t((__popc((16 * h + j) & r) & 1) ? 0xB8 : 0x38) << (8 * j);
-    b1 |= int64_t((__popc((16 * h + 8 + j) & r) & 1) ? 0xB8 : 0x38) << (8 * j);
+    b0[j] = (__popc((16 * h + j) & r) & 1) ? short(0xBF80) : short(0x3F80);
+    b1[j] = (__popc((16 * h + 8 + j) & r) & 1) ? short(0xBF80) : short(0x3F80);
   }
   const bool vec_out = (DES == 2) && (reinterpret_cast<uintptr_t>(dst) & 7) == 0;
   for (int64_t t0 = wave0 * U; t0 < ntiles; t0 += nwaves * U) {
@@ -1267,10 +1280,8 @@ hs_fp8_hadamard_dequant8(const uint8_t* __restrict__ q, const float* __restrict_
       const int64_t tile = t0 + u;
       if (tile >= ntiles) break;
       floatx16 acc = {};
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(
-          static_cast<hs_fp8x8>(a[u].x | (uint64_t(a[u].y) << 32)), b0, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(
-          static_cast<hs_fp8x8>(a[u].z | (uint64_t(a[u].w) << 32)), b1, acc, 0, 0, 0);
+      acc = mfma16<kBF16>(fp8x8_to_bf16x8(a[u].x, a[u].y), b0, acc);
+      acc = mfma16<kBF16>(fp8x8_to_bf16x8(a[u].z, a[u].w), b1, acc);
       if (vec_out && (tile + 1) * 1024 <= n) {
         if constexpr (DES == 2) {
 #pragma unroll

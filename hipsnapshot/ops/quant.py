@@ -23,8 +23,9 @@ products in its own order, so a code can differ from the fp32 reference by one
 fp8 ulp -- tests bound it); fp32 tensors use ``v_mfma_f32_32x32x2_f32``
 (exact f32 k-ordered FMA chains, ``hs_fp8_hadamard_quant``), bit-identical to
 the torch reference below, which uses the same sequential k order.  Every
-dequantization runs on ``v_mfma_f32_32x32x16_fp8_fp8`` (``hs_fp8_hadamard_dequant8``):
-the row sums of e4m3 codes are exact, so GPU and torch restores agree bit for bit.
+dequantization runs on ``v_mfma_f32_32x32x16_bf16`` over the codes widened to
+bf16 (``hs_fp8_hadamard_dequant8``): the row sums of e4m3 values are exact, so
+GPU and torch restores agree bit for bit.
 
 rotation ``"none"`` (default): plain blockwise quantization (``hs_fp8_quant`` kernel:
 one wave per block, 64-lane xor-shuffle amax, ``v_cvt_pk_fp8_f32`` -- gfx950
@@ -251,7 +252,8 @@ def hadamard_dequantize_reference(q: torch.Tensor, scale: torch.Tensor, n: int,
     """x = (Q H) * (s / 32): the row sums of e4m3 codes are exact (multiples of
     2^-9 below 2^14, computed in float64 and exact in fp32), then ONE fp32
     rounding by the block scale -- the same arithmetic as the GPU kernel
-    (``hs_fp8_hadamard_dequant8``, fp8 MFMA), so both are bit-identical."""
+    (``hs_fp8_hadamard_dequant8``, bf16 MFMA on the widened codes), so both
+    are bit-identical."""
     n_pad = q.numel()
     rows = q.float().reshape(-1, GROUP).double()
     h = hadamard_matrix(GROUP, rows.device).double()

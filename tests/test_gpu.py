@@ -177,7 +177,8 @@ def test_fp8_hadamard_mfma_vs_reference(gpu, dtype, n):
     bf16 / f16 inputs (v_mfma_f32_32x32x16_{bf16,f16}: the MFMA sums 16
     exact products in its own order): scales within 2 fp32 ulps, every fp8
     code within one fp8 ulp, >= 99.9 % identical, and the round-trip error no
-    worse than the reference's.  Dequantization (fp8 MFMA, exact row sums)
+    worse than the reference's.  Dequantization (bf16 MFMA on the widened
+    codes, exact row sums)
     is bit-identical to the reference on the kernel's own codes, into every
     float dtype."""
     from hipsnapshot.ops.quant import hadamard_dequantize_reference, hadamard_quantize_reference
