@@ -134,7 +134,14 @@ __device__ __forceinline__ float load_as_f32(const char* p, int32_t dt) {
 
 __device__ __forceinline__ void store_from_f32(char* p, int32_t dt, float v) {
   switch (dt) {
-    case kF16: *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(v); break;
+    case kF16: {
+      // the empty asm pins v as an f32: otherwise a caller's f32 multiply and
+      // this fptrunc may be fused into one mixed-precision FMA (a single
+      // rounding to f16), which differs from torch's f32 -> f16 in rare ties
+      asm volatile("" : "+v"(v));
+      *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(v);
+      break;
+    }
     case kBF16: *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(v); break;
     case kF32: *reinterpret_cast<float*>(p) = v; break;
     default: *reinterpret_cast<double*>(p) = static_cast<double>(v); break;
@@ -1238,6 +1245,7 @@ __device__ __forceinline__ uint32_t pack16(float lo, float hi) {
     a = f32_to_bf16(lo);
     b = f32_to_bf16(hi);
   } else {
+    asm volatile("" : "+v"(lo), "+v"(hi));  // f32 products, then RNE (store_from_f32)
     a = __builtin_bit_cast(uint16_t, static_cast<_Float16>(lo));
     b = __builtin_bit_cast(uint16_t, static_cast<_Float16>(hi));
   }
