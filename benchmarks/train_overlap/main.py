@@ -288,7 +288,9 @@ def main() -> None:
     for k in range(k_total):
         before = gap_k[k - 1] if k > 0 else base
         after = gap_k[k] if k < len(gap_k) else post
-        loc = statistics.median(before + after)
+        # with --gap-steps 0 the checkpoints run back to back: no drain-free
+        # steps between them, the run's own baseline steps stand in
+        loc = statistics.median((before + after) or (base + post))
         d = during_k[k]
         lost_local.append(unblocks[k] + sum(d) - len(d) * loc)
         slow_local.append(statistics.median(d) / loc - 1.0 if d else 0.0)
