@@ -11,7 +11,7 @@ mkdir -p $HIPSNAPSHOT_BENCH_DIR
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 tr=/tmp/ovtrace_$$
 SEQ=${SEQ:-512}
-timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $tr -o ov \
+timeout -k 10 600 rocprofv3 --kernel-trace ${HIPTRACE:+--hip-runtime-trace} --output-format csv -d $tr -o ov \
     -- python3 benchmarks/train_overlap/main.py --seq $SEQ --checkpoints ${CKPT:-3} \
     --baseline-steps 8 ${ARGS:-} > $out/ov${SEQ}.json 2> $out/ov${SEQ}.err \
     || { echo OV_FAIL; grep -v "^frame" $out/ov${SEQ}.err | tail -30; exit 1; }

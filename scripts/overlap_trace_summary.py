@@ -48,18 +48,27 @@ def main() -> None:
     out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
     trainer, drain, markers = [], [], []
     with open(path, newline="") as f:
-        for row in csv.DictReader(f):
-            name = row["Kernel_Name"]
-            s, e = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
-            if ours(name):
-                if "hash64" in name:
-                    drain.append((s, e))
-                continue
-            trainer.append((s, e, name))
-            if "randint" in name or ("random_from_to" in name) or \
-                    ("distribution_elementwise" in name and "unsigned" in name.split("<")[1][:40]
-                     if "<" in name else False):
-                markers.append(s)
+        rows = list(csv.DictReader(f))
+    # the trainer's stream / thread: the ones its per-step randint ran on
+    mark = [r for r in rows if "random_from_to" in r["Kernel_Name"] or "randint" in r["Kernel_Name"]]
+    if not mark:
+        sys.exit("no per-step randint kernel found")
+    t_stream = max({r["Stream_Id"] for r in mark}, key=lambda x: sum(r["Stream_Id"] == x for r in mark))
+    t_thread = mark[-1]["Thread_Id"]
+    other = defaultdict(lambda: [0, 0])
+    for row in rows:
+        name = row["Kernel_Name"]
+        s, e = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+        if ours(name) or row["Stream_Id"] != t_stream:
+            if "hash64" in name:
+                drain.append((s, e))
+            k = name.split("(")[0][:80]
+            other[k][0] += 1
+            other[k][1] += e - s
+            continue
+        trainer.append((s, e, name))
+        if row in mark:
+            markers.append(s)
     markers.sort()
     drain.sort()
     windows = []
@@ -120,6 +129,53 @@ def main() -> None:
         res["kernel_time_growth_per_step_ms"] = [
             {"kernel": n[:120], "base_ms": round(db / 1e6, 3), "during_ms": round(dd / 1e6, 3),
              "growth_ms": round(g / 1e6, 3)} for g, n, db, dd in grow[:12]]
+    res["off_trainer_stream_kernels_ms"] = {k: {"n": v[0], "ms": round(v[1] / 1e6, 2)}
+                                            for k, v in sorted(other.items(),
+                                                               key=lambda x: -x[1][1])[:10]}
+    api_path = path.replace("kernel_trace.csv", "hip_api_trace.csv")
+    api = []
+    if api_path != path:
+        try:
+            with open(api_path, newline="") as f:
+                api = [r for r in csv.DictReader(f) if r.get("Thread_Id") == t_thread]
+        except OSError:
+            pass
+    fcol = next((k for k in (api[0] if api else {}) if k in ("Function", "Operation")), None)
+    if api:
+        # the trainer thread's HIP calls per step: time inside the runtime
+        # vs time between calls (Python, GIL, CPU share)
+        api.sort(key=lambda r: int(r["Start_Timestamp"]))
+        per = []
+        j = 0
+        for a, b in zip(markers, markers[1:]):
+            while j < len(api) and int(api[j]["Start_Timestamp"]) < a:
+                j += 1
+            k, inside, n, fn = j, 0, 0, defaultdict(lambda: [0, 0])
+            while k < len(api) and int(api[k]["Start_Timestamp"]) < b:
+                d_ = int(api[k]["End_Timestamp"]) - int(api[k]["Start_Timestamp"])
+                inside += d_
+                n += 1
+                f_ = fn[api[k][fcol] if fcol else "?"]
+                f_[0] += 1
+                f_[1] += d_
+                k += 1
+            during = any(s < b and e > a for s, e in windows)
+            per.append((during, inside, n, fn))
+        def agg(sel):
+            if not sel:
+                return None
+            fns = defaultdict(lambda: [0, 0])
+            for _, _, _, fn in sel:
+                for name, (c, t) in fn.items():
+                    fns[name][0] += c
+                    fns[name][1] += t
+            return {"in_runtime_ms": round(statistics.median(x[1] for x in sel) / 1e6, 3),
+                    "calls": int(statistics.median(x[2] for x in sel)),
+                    "top": {name: {"calls_per_step": round(c / len(sel), 1),
+                                   "us_per_call": round(t / c / 1e3, 2)}
+                            for name, (c, t) in sorted(fns.items(), key=lambda x: -x[1][1])[:6]}}
+        res["trainer_thread_hip_api"] = {"baseline": agg([x for x in per[2:] if not x[0]]),
+                                         "during_drain": agg([x for x in per if x[0]])}
     print(json.dumps(res, indent=1))
     if out_json:
         with open(out_json, "w") as f:

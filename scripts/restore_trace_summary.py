@@ -61,6 +61,8 @@ def main() -> None:
     copies = _rows(os.path.join(d, "**", "*memory_copy_trace.csv"))
     kernels = _rows(os.path.join(d, "**", "*kernel_trace.csv"))
     api = _rows(os.path.join(d, "**", "*hip_api_trace.csv"))
+    hdr = {"memory_copy": list(copies[0].keys()) if copies else None,
+           "hip_api": list(api[0].keys()) if api else None}
     h2d = []
     for r in copies:
         direction = (_col(r, "Direction", "Operation", "Kind") or "").upper()
@@ -68,16 +70,17 @@ def main() -> None:
             continue
         s, e = int(_col(r, "Start_Timestamp")), int(_col(r, "End_Timestamp"))
         nb = _col(r, "Size", "Bytes", "Copy_Bytes")
-        h2d.append((s, e, int(nb) if nb not in (None, "") else 0))
+        h2d.append((s, e, int(nb) if nb not in (None, "") else -1))
     h2d.sort()
-    big = [c for c in h2d if c[2] >= (1 << 20)]
+    # copies of >= 1 MiB (or, without a size column, of >= 20 us)
+    big = [c for c in h2d if c[2] >= (1 << 20) or (c[2] < 0 and c[1] - c[0] >= 20_000)]
     clusters = []
     for c in big:
         if clusters and c[0] - clusters[-1][-1][1] < 50_000_000:
             clusters[-1].append(c)
         else:
             clusters.append([c])
-    out = {"h2d_copies": len(h2d), "restore_windows": len(clusters)}
+    out = {"h2d_copies": len(h2d), "restore_windows": len(clusters), "columns": hdr}
     if not clusters:
         print(json.dumps(out, indent=1))
         return
@@ -86,7 +89,7 @@ def main() -> None:
     w1 = max(e for _, e, _ in last)
     in_w = [c for c in h2d if c[0] >= w0 - 5_000_000 and c[1] <= w1 + 5_000_000]
     busy, gaps = union([(s, e) for s, e, _ in in_w])
-    nbytes = sum(n for _, _, n in in_w)
+    nbytes = sum(max(n, 0) for _, _, n in in_w)
     out["last_restore"] = {
         "h2d_window_ms": round((w1 - w0) / 1e6, 2),
         "h2d_busy_ms": round(busy / 1e6, 2),
@@ -96,7 +99,8 @@ def main() -> None:
         "h2d_copies": len(in_w),
         "h2d_idle_gaps_over_0.3ms": [(round((a - w0) / 1e6, 2), round((b - a) / 1e6, 2))
                                      for a, b in gaps if b - a > 300_000],
-        "copy_ms_each": sorted((round((e - s) / 1e6, 2) for s, e, n in in_w if n >= (1 << 20)),
+        "copy_ms_each": sorted((round((e - s) / 1e6, 2) for s, e, n in in_w
+                                if n >= (1 << 20) or e - s >= 20_000),
                                reverse=True)[:12],
     }
     kt = defaultdict(lambda: [0, 0])
