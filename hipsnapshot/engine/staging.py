@@ -39,6 +39,7 @@ _tls = threading.local()
 _slot_lock = threading.Lock()
 _next_slot = [0]
 NUM_COPY_SLOTS = 4
+_HASH_SLOT_BASE = 64  # hash streams: slots 64.. (copy slots stay below)
 
 
 def mark_background_thread() -> None:
@@ -52,11 +53,16 @@ def mark_background_thread() -> None:
 
 
 def copy_slot() -> int:
-    """A copy-stream slot per OS thread (concurrent DMAs from executor threads)."""
+    """A copy-stream slot per OS thread (concurrent DMAs from executor threads):
+    at least as many slots as staging threads, so two threads never share a
+    stream (a stream sync would wait for the other thread's copies too)."""
     s = getattr(_tls, "slot", None)
     if s is None:
+        from .. import knobs
+
+        n = max(NUM_COPY_SLOTS, min(_HASH_SLOT_BASE, knobs.get_stage_threads()))
         with _slot_lock:
-            s = _next_slot[0] % NUM_COPY_SLOTS
+            s = _next_slot[0] % n
             _next_slot[0] += 1
         _tls.slot = s
     return s
@@ -64,7 +70,7 @@ def copy_slot() -> int:
 
 def hash_slot(slot: int) -> int:
     """The stream that hashes blobs beside copy slot ``slot``'s DMAs."""
-    return NUM_COPY_SLOTS + slot
+    return _HASH_SLOT_BASE + slot
 
 
 def device_of(t: torch.Tensor) -> int:
