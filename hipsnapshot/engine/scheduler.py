@@ -735,24 +735,30 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                 dest.release()
             in_use[0] -= cost
 
+    from . import staging
+
     clean = False
     try:
-        while pending or inflight:
-            while pending and len(inflight) < max_inflight:
-                cost = pending[0].buffer_consumer.get_consuming_cost_bytes()
-                if in_use[0] + cost > memory_budget_bytes and inflight:
-                    break
-                rr = pending.popleft()
-                in_use[0] += cost
-                inflight.add(asyncio.ensure_future(_one(rr, cost)))
-            done, inflight = await asyncio.wait(inflight, return_when=asyncio.FIRST_COMPLETED)
-            inflight = set(inflight)
-            for t in done:
-                if t.exception() is not None:
-                    failing.append(t.exception())
-                    # drain, do not cancel: see ``failing`` above
-                    await asyncio.gather(*inflight, return_exceptions=True)
-                    raise t.exception()
+        # consumers may leave their decode / scatter kernels running: the
+        # scope waits for them (and raises corrupt frames) at its end
+        with staging.deferred_device_work():
+            while pending or inflight:
+                while pending and len(inflight) < max_inflight:
+                    cost = pending[0].buffer_consumer.get_consuming_cost_bytes()
+                    if in_use[0] + cost > memory_budget_bytes and inflight:
+                        break
+                    rr = pending.popleft()
+                    in_use[0] += cost
+                    inflight.add(asyncio.ensure_future(_one(rr, cost)))
+                done, inflight = await asyncio.wait(inflight,
+                                                    return_when=asyncio.FIRST_COMPLETED)
+                inflight = set(inflight)
+                for t in done:
+                    if t.exception() is not None:
+                        failing.append(t.exception())
+                        # drain, do not cancel: see ``failing`` above
+                        await asyncio.gather(*inflight, return_exceptions=True)
+                        raise t.exception()
         clean = True
     finally:
         if clean:

@@ -25,7 +25,7 @@ from __future__ import annotations
 import threading
 import time
 from contextlib import contextmanager
-from typing import Iterator, List, Optional, Sequence, Tuple
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -71,6 +71,95 @@ def copy_slot() -> int:
 def hash_slot(slot: int) -> int:
     """The stream that hashes blobs beside copy slot ``slot``'s DMAs."""
     return _HASH_SLOT_BASE + slot
+
+
+_DECODE_SLOT_BASE = 32  # decode / scatter streams of the restore: slots 32..
+
+
+def decode_slot(slot: int) -> int:
+    """The stream that decodes / scatters what copy slot ``slot`` uploaded:
+    the copy stream then only carries H2D copies, so the next blob's upload
+    does not queue behind this one's kernels."""
+    return _DECODE_SLOT_BASE + slot
+
+
+_ext_streams: Dict[Tuple[int, int], "torch.cuda.ExternalStream"] = {}
+
+
+def _ext_stream(dev: int, slot: int) -> "torch.cuda.ExternalStream":
+    key = (dev, slot)
+    st = _ext_streams.get(key)
+    if st is None:
+        st = _ext_streams[key] = torch.cuda.ExternalStream(native.copy_stream(dev, slot),
+                                                           device=f"cuda:{dev}")
+    return st
+
+
+def _event_on(dev: int, slot: int) -> "torch.cuda.Event":
+    ev = torch.cuda.Event()
+    ev.record(_ext_stream(dev, slot))
+    return ev
+
+
+class _DeferredDeviceWork:
+    """Device work of one read pipeline that its consumers do not wait for:
+    a consumer returns once its H2D copies are done (its pinned buffer can go
+    back), while decode / scatter kernels keep running on the decode stream.
+    ``flush`` (end of the pipeline) waits for all of it, checks the decoders'
+    error words and releases what the kernels used."""
+
+    def __init__(self) -> None:
+        self.items: List[tuple] = []
+        self.lock = threading.Lock()
+
+    def add(self, done: "torch.cuda.Event", keep, err=None, what: str = "") -> None:
+        with self.lock:
+            self.items.append((done, keep, err, what))
+
+    def flush(self, raise_errors: bool = True) -> None:
+        first = None
+        with self.lock:
+            items, self.items = self.items, []
+        for done, keep, err, what in items:
+            done.synchronize()
+            if err is not None:
+                try:
+                    err.check(what)
+                except Exception as e:  # noqa: BLE001 -- the first one is raised
+                    first = first or e
+            if keep is not None and hasattr(keep[0], "release"):
+                keep[0].release()
+        if first is not None and raise_errors:
+            raise first
+
+
+_deferred_scopes: List[_DeferredDeviceWork] = []
+_deferred_lock = threading.Lock()
+
+
+@contextmanager
+def deferred_device_work() -> Iterator[_DeferredDeviceWork]:
+    """Scope of a read pipeline whose H2D consumers may leave their decode /
+    scatter kernels running; everything is waited for (and corrupt frames
+    raised) when the scope ends."""
+    scope = _DeferredDeviceWork()
+    with _deferred_lock:
+        _deferred_scopes.append(scope)
+    try:
+        yield scope
+    except BaseException:
+        with _deferred_lock:
+            _deferred_scopes.remove(scope)
+        scope.flush(raise_errors=False)
+        raise
+    with _deferred_lock:
+        _deferred_scopes.remove(scope)
+    scope.flush()
+
+
+def _current_deferred() -> Optional[_DeferredDeviceWork]:
+    with _deferred_lock:
+        return _deferred_scopes[-1] if _deferred_scopes else None
 
 
 def device_of(t: torch.Tensor) -> int:
@@ -686,8 +775,21 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
     _join_current_stream(dev, slot)
     native.memcpy(dev, slot, scratch.data_ptr(), host_addr, nbytes, native.H2D, None,
                   sync=False)
-    _copy_regions(scratch, kernel_regions, dev, slot)
-    del scratch
+    scope = _current_deferred()
+    if scope is None:
+        _copy_regions(scratch, kernel_regions, dev, slot)
+        return
+    # the copy kernel runs on the decode stream after the upload; this
+    # consumer only waits for the upload (its host buffer goes back)
+    h2d = _event_on(dev, slot)
+    dslot = decode_slot(slot)
+    native.memcpy(dev, dslot, 0, 0, 0, native.H2D, native.copy_stream(dev, slot), sync=False)
+    keep = _copy_regions(scratch, kernel_regions, dev, dslot, wait=False)
+    scratch.record_stream(_ext_stream(dev, dslot))
+    scope.add(_event_on(dev, dslot), keep)
+    t_w = time.perf_counter()
+    h2d.synchronize()
+    timeline.add("h2d_wait", "h2d", t_w, time.perf_counter(), bytes=nbytes)
 
 
 _elem_sizes: dict = {}
@@ -700,9 +802,11 @@ def _elem_size(dtype: torch.dtype) -> int:
     return es
 
 
-def _copy_regions(scratch: torch.Tensor, regions, dev: int, slot: int) -> None:
+def _copy_regions(scratch: torch.Tensor, regions, dev: int, slot: int, wait: bool = True):
     """ONE copy/cast launch from the device buffer ``scratch`` (region offsets
-    are relative to it) into every destination view, then a stream sync."""
+    are relative to it) into every destination view, then a stream sync.
+    ``wait=False``: no sync; returns the launch's keepalive (the caller holds
+    it until the stream passed the launch)."""
     t0 = time.perf_counter()
     batch = native.CopyBatch()
     fallbacks = []
@@ -733,6 +837,10 @@ def _copy_regions(scratch: torch.Tensor, regions, dev: int, slot: int) -> None:
     t1 = time.perf_counter()
     keep = batch.launch(dev, native.copy_stream(dev, slot), sync=False)
     t2 = time.perf_counter()
+    if not wait and not fallbacks:
+        timeline.add("regions_build", "h2d", t0, t1, n=len(regions))
+        timeline.add("regions_launch", "h2d", t1, t2)
+        return keep
     native.stream_sync(dev, slot)
     t3 = time.perf_counter()
     timeline.add("regions_build", "h2d", t0, t1, n=len(regions))
@@ -820,7 +928,15 @@ def _decode_span(span, regions, dev, slot, direct, enc, offs_pb, n_offs, c_n, lo
                       sync=False)
     native.memcpy(dev, slot, offs_dev.data_ptr(), offs_pb.ptr, 8 * n_offs, native.H2D, None,
                   sync=False)
-    stream = native.copy_stream(dev, slot)
+    scope = _current_deferred()
+    kslot = slot
+    if scope is not None:
+        # decode + scatter on the decode stream, after the uploads: the copy
+        # stream is free for the next blob's upload at once
+        h2d = _event_on(dev, slot)
+        kslot = decode_slot(slot)
+        native.memcpy(dev, kslot, 0, 0, 0, native.H2D, native.copy_stream(dev, slot), sync=False)
+    stream = native.copy_stream(dev, kslot)
     err = native.DecodeErrorWord()
     native.hsz_decode_gpu(dev, enc.data_ptr(), offs_dev.data_ptr(), first, last - first,
                           h.logical_size, h.elem_width, h.frame_bytes,
@@ -829,6 +945,19 @@ def _decode_span(span, regions, dev, slot, direct, enc, offs_pb, n_offs, c_n, lo
     t2 = time.perf_counter()
     timeline.add("dec_alloc", "h2d", t0, t1)
     timeline.add("dec_launch", "h2d", t1, t2)
+    if scope is not None:
+        keep = None
+        if direct is None:
+            keep = _copy_regions(out[span.lo - log_lo:], regions, dev, kslot, wait=False)
+        ext = _ext_stream(dev, kslot)
+        for t in (enc, offs_dev, out):
+            if t is not None:
+                t.record_stream(ext)
+        scope.add(_event_on(dev, kslot), keep, err, f"frames [{first}, {last})")
+        t_w = time.perf_counter()
+        h2d.synchronize()  # the encoded frames and offsets are on the device
+        timeline.add("h2d_wait", "h2d", t_w, time.perf_counter(), bytes=c_n)
+        return
     if direct is not None:
         native.stream_sync(dev, slot)
         timeline.add("dec_wait", "h2d", t2, time.perf_counter(), bytes=c_n)
