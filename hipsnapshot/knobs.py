@@ -364,6 +364,13 @@ def uvm_assume_host() -> bool:
     return not device_xnack_enabled()
 
 
+def drain_avoid_caller_core() -> bool:
+    """The native drain's threads keep off the physical core of the thread
+    that called ``async_take`` (utils/affinity.py): a launch-bound training
+    step loses issue slots to an SMT sibling busy with page-cache copies."""
+    return _get_bool("DRAIN_AVOID_CALLER_CORE", True)
+
+
 def drain_hash_high_priority() -> bool:
     """The native drain's hs64 launches run on a high-priority stream
     (default): at normal priority a training step's GEMMs starved them

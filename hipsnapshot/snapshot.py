@@ -314,6 +314,9 @@ class Snapshot:
         committed regardless.
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.async_take")
+        from .utils.affinity import note_caller_cpu
+
+        note_caller_cpu()  # the drain's threads keep off this thread's core
         deferred_gc: list = []
         with paused_gc(deferred_gc):
             pending = cls._async_take(path, app_state, pg, replicated, storage_options,

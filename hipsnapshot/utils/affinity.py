@@ -103,3 +103,88 @@ def describe(devices: List[int]) -> List[dict]:
         out.append({"device": d, "pci": gpu_pci_bus_id(d), "numa_node": node,
                     "node_cpus": len(node_cpus(node)) if node is not None else None})
     return out
+
+
+# ---- keeping background threads off the trainer's core -----------------------
+#
+# A launch-bound training step (seq 512 Llama-3-8B: ~8400 kernel launches per
+# 240 ms step from one Python thread) slows down whenever that thread shares
+# its physical core: an SMT sibling busy with a drain writer's page-cache
+# memcpy takes a large share of the core's issue slots.  ``async_take`` notes
+# the core its caller runs on; the native drain's threads are created with an
+# affinity mask that excludes that core's hardware threads
+# (``HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE``, default on).
+
+_caller_cpu: List[Optional[int]] = [None]
+
+
+def current_cpu() -> Optional[int]:
+    """The CPU the calling thread last ran on (/proc/thread-self/stat)."""
+    try:
+        with open("/proc/thread-self/stat") as f:
+            stat = f.read()
+        # fields after the command name "(...)": field 39 = processor
+        return int(stat.rsplit(")", 1)[1].split()[36])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+def core_siblings(cpu: int) -> Set[int]:
+    """The hardware threads of ``cpu``'s physical core (``cpu`` itself if
+    the topology is unknown)."""
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list") as f:
+            sib = _parse_cpulist(f.read())
+        return sib or {cpu}
+    except OSError:
+        return {cpu}
+
+
+def note_caller_cpu() -> None:
+    """Record the core the calling (training) thread runs on."""
+    _caller_cpu[0] = current_cpu()
+
+
+def mask_avoiding_caller() -> Optional[Set[int]]:
+    """This thread's allowed CPUs minus the noted caller's core, or None when
+    nothing was noted or too few CPUs would remain."""
+    cpu = _caller_cpu[0]
+    if cpu is None:
+        return None
+    try:
+        allowed = os.sched_getaffinity(0)
+    except OSError:
+        return None
+    rest = allowed - core_siblings(cpu)
+    if len(rest) < 2 or rest == allowed:
+        return None
+    return rest
+
+
+class threads_avoiding_caller:
+    """Context manager: threads created inside it (they inherit the creating
+    thread's mask) never run on the noted caller's core; the calling
+    thread's own mask is restored on exit."""
+
+    def __init__(self, enabled: bool = True) -> None:
+        self.enabled = enabled
+        self.prev: Optional[Set[int]] = None
+
+    def __enter__(self) -> "threads_avoiding_caller":
+        if not self.enabled:
+            return self
+        mask = mask_avoiding_caller()
+        if mask is not None:
+            try:
+                self.prev = os.sched_getaffinity(0)
+                os.sched_setaffinity(0, mask)
+            except OSError:
+                self.prev = None
+        return self
+
+    def __exit__(self, *exc) -> None:
+        if self.prev is not None:
+            try:
+                os.sched_setaffinity(0, self.prev)
+            except OSError:
+                pass

@@ -297,3 +297,31 @@ def test_plan_scope_caches_per_device_and_restores():
             staging._plan.streams[0] = 123
         assert staging._plan.streams == {}
     assert getattr(staging._plan, "streams", None) is None
+
+
+def test_drain_threads_avoid_the_callers_core():
+    """Threads created under threads_avoiding_caller inherit a mask without
+    the noted caller's core; the creating thread's mask is restored."""
+    import os
+    import threading
+
+    from hipsnapshot.utils import affinity
+
+    cpu = affinity.current_cpu()
+    assert cpu is not None and cpu in affinity.core_siblings(cpu)
+    before = os.sched_getaffinity(0)
+    affinity.note_caller_cpu()
+    seen = {}
+    with affinity.threads_avoiding_caller():
+        t = threading.Thread(target=lambda: seen.setdefault("mask", os.sched_getaffinity(0)))
+        t.start()
+        t.join()
+    assert os.sched_getaffinity(0) == before
+    expect = affinity.mask_avoiding_caller()
+    if expect is None:  # too few CPUs here: nothing is restricted
+        assert seen["mask"] == before
+    else:
+        assert seen["mask"] == expect
+        assert not (seen["mask"] & affinity.core_siblings(affinity._caller_cpu[0]))
+    with affinity.threads_avoiding_caller(enabled=False):
+        assert os.sched_getaffinity(0) == before
