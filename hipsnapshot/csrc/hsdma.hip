@@ -341,6 +341,43 @@ int hsg_sdma_d2h_submit_released(int dev, void* dst, const void* src, uint64_t n
   return 0;
 }
 
+// ---- host -> device into uncached device memory -----------------------------
+//
+// hipMemcpyAsync(HostToDevice) calls issued by several restore threads block
+// inside the HIP runtime for milliseconds each before the copy is submitted
+// (rocprofv3 --hip-runtime-trace, profiles/r4/restore_trace/): the PCIe link
+// idles meanwhile.  The SDMA engines take the same copy through ROCr with no
+// such stall.  An SDMA write into HBM is not ordered with the GPU's L2, so the
+// destination is memory the GPU never caches (hipDeviceMallocUncached): no L2
+// line of it can be stale when a kernel reads it after the copy, and no
+// system-scope acquire is needed.  The restore uploads encoded HSZ1 frames
+// there; the decode kernel reads them once.
+
+// Blocking pinned-host -> device copy of n bytes on an SDMA engine.  `dst`
+// must be uncached device memory (hsg_uncached_acquire); `src` pinned.
+int hsg_sdma_h2d(int dev, void* dst, const void* src, uint64_t n) {
+  DevInfo* d = dev_info(dev);
+  if (!d) return -1;
+  if (n == 0) return 0;
+  hsa_signal_t s = take_signal();
+  if (s.handle == 0) return -5;
+  g_api.signal_store(s, 1);
+  const hsa_status_t st = g_api.async_copy(dst, d->gpu, src, d->cpu, n, 0, nullptr, s);
+  if (st != HSA_STATUS_SUCCESS) {
+    give_signal(s);
+    snprintf(g_err, sizeof(g_err), "hsa_amd_memory_async_copy (h2d): status 0x%x", unsigned(st));
+    return -6;
+  }
+  const hsa_signal_value_t v =
+      g_api.signal_wait(s, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+  give_signal(s);
+  if (v < 0) {
+    snprintf(g_err, sizeof(g_err), "SDMA h2d copy reported an error (%ld)", long(v));
+    return -7;
+  }
+  return 0;
+}
+
 // Wait for a copy submitted by hsg_sdma_d2h_submit; 0 = done, < 0 = the
 // engine reported an error (the copy did not complete).  handle 0: no-op.
 int hsg_sdma_wait(uint64_t handle) {

@@ -1694,6 +1694,89 @@ uint64_t hsg_pinned_trim() {
 // torch stream; handle 0 = the legacy default stream).
 // kind: 0 = D2H, 1 = H2D, 2 = D2D.  If `sync` is nonzero the call blocks until
 // the copy is done (ctypes releases the GIL around it).
+// ---- uncached device blocks (SDMA upload targets, csrc/hsdma.hip) ----------
+//
+// hipDeviceMallocUncached memory, cached per device by size (best fit up to
+// 2x, 2 MiB granules): the restore's encoded frames are uploaded into it by
+// SDMA and read once by the decode kernel, never through a stale L2 line.
+struct UncachedPool {
+  std::mutex mu;
+  std::map<int, std::multimap<size_t, void*>> free_blocks;  // dev -> size -> block
+  std::unordered_map<void*, std::pair<int, size_t>> live;
+  size_t cached_bytes = 0;
+};
+UncachedPool g_upool;
+
+void* hsg_uncached_acquire(int dev, uint64_t nbytes) {
+  constexpr size_t kGranule = size_t(2) << 20;
+  const size_t want = (std::max<size_t>(nbytes, 1) + kGranule - 1) / kGranule * kGranule;
+  {
+    std::lock_guard<std::mutex> g(g_upool.mu);
+    auto& fl = g_upool.free_blocks[dev];
+    auto it = fl.lower_bound(want);
+    if (it != fl.end() && it->first <= 2 * want) {
+      void* p = it->second;
+      g_upool.live[p] = {dev, it->first};
+      fl.erase(it);
+      return p;
+    }
+  }
+  if (hipSetDevice(dev) != hipSuccess) return nullptr;
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, want, hipDeviceMallocUncached);
+  if (e != hipSuccess) {
+    // drop this device's idle blocks and retry once
+    std::vector<void*> drop;
+    {
+      std::lock_guard<std::mutex> g(g_upool.mu);
+      auto& fl = g_upool.free_blocks[dev];
+      for (auto& kv : fl) { drop.push_back(kv.second); g_upool.cached_bytes -= kv.first; }
+      fl.clear();
+    }
+    for (void* q : drop) (void)hipFree(q);
+    e = hipExtMallocWithFlags(&p, want, hipDeviceMallocUncached);
+    if (e != hipSuccess) {
+      set_err("hipExtMallocWithFlags(uncached)", e);
+      return nullptr;
+    }
+  }
+  std::lock_guard<std::mutex> g(g_upool.mu);
+  g_upool.live[p] = {dev, want};
+  g_upool.cached_bytes += want;
+  return p;
+}
+
+int hsg_uncached_release(void* p) {
+  std::lock_guard<std::mutex> g(g_upool.mu);
+  auto it = g_upool.live.find(p);
+  if (it == g_upool.live.end()) return -1;
+  g_upool.free_blocks[it->second.first].emplace(it->second.second, p);
+  g_upool.live.erase(it);
+  return 0;
+}
+
+// Free every idle uncached block; returns the bytes freed.
+uint64_t hsg_uncached_trim() {
+  std::vector<std::pair<int, void*>> drop;
+  uint64_t freed = 0;
+  {
+    std::lock_guard<std::mutex> g(g_upool.mu);
+    for (auto& dv : g_upool.free_blocks) {
+      for (auto& kv : dv.second) {
+        drop.emplace_back(dv.first, kv.second);
+        freed += kv.first;
+      }
+      dv.second.clear();
+    }
+    g_upool.cached_bytes -= freed;
+  }
+  for (auto& d : drop) {
+    (void)hipSetDevice(d.first);
+    (void)hipFree(d.second);
+  }
+  return freed;
+}
+
 int hsg_memcpy(int dev, int slot, void* dst, const void* src, uint64_t n, int kind,
                void* producer, int has_producer, int sync) {
   HS_CHECK(hipSetDevice(dev));

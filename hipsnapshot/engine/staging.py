@@ -113,8 +113,18 @@ class _DeferredDeviceWork:
         self.lock = threading.Lock()
 
     def add(self, done: "torch.cuda.Event", keep, err=None, what: str = "") -> None:
+        """``keep``: objects to release once ``done`` fired (``.release()``
+        is called on those that have it): a launch keepalive tuple, a list."""
+        if isinstance(keep, tuple):
+            keep = list(keep)  # (pinned descriptor stage, device workspace): both
         with self.lock:
-            self.items.append((done, keep, err, what))
+            self.items.append([done, keep or [], err, what])
+            # finished earlier items give their buffers back now, not at the
+            # end of the pipeline (uncached upload blocks, descriptor stages)
+            for it in self.items[:-1]:
+                if it[1] and it[0].query():
+                    _release_all(it[1])
+                    it[1] = []
 
     def flush(self, raise_errors: bool = True) -> None:
         first = None
@@ -127,10 +137,16 @@ class _DeferredDeviceWork:
                     err.check(what)
                 except Exception as e:  # noqa: BLE001 -- the first one is raised
                     first = first or e
-            if keep is not None and hasattr(keep[0], "release"):
-                keep[0].release()
+            _release_all(keep)
         if first is not None and raise_errors:
             raise first
+
+
+def _release_all(objs) -> None:
+    for o in objs:
+        rel = getattr(o, "release", None)
+        if rel is not None:
+            rel()
 
 
 _deferred_scopes: List[_DeferredDeviceWork] = []
@@ -886,7 +902,6 @@ def _scatter_compressed(span, regions, dev: int, producer: Optional[int] = None)
                 and dst.data_ptr() % 16 == 0):
             direct = dst
     t0 = time.perf_counter()
-    enc = torch.empty(c_n, dtype=torch.uint8, device=f"cuda:{dev}")
     # frame offsets go up from pinned memory: a pageable source would make
     # the async H2D wait for the encoded frames' copy queued before it
     n_offs = last - first + 1
@@ -894,6 +909,12 @@ def _scatter_compressed(span, regions, dev: int, producer: Optional[int] = None)
     offs = np.frombuffer(offs_pb.view, dtype=np.int64, count=n_offs)
     offs[:] = np.asarray(h.offsets[first:last + 1], dtype=np.int64) - c_lo
     try:
+        scope = _current_deferred()
+        if scope is not None and _sdma_uploads(dev):
+            _decode_span_sdma(span, regions, dev, slot, direct, offs_pb, n_offs, c_n, log_lo,
+                              log_n, first, last, t0, scope)
+            return
+        enc = torch.empty(c_n, dtype=torch.uint8, device=f"cuda:{dev}")
         _decode_span(span, regions, dev, slot, direct, enc, offs_pb, n_offs, c_n, log_lo, log_n,
                      first, last, t0)
     finally:
@@ -902,6 +923,75 @@ def _scatter_compressed(span, regions, dev: int, producer: Optional[int] = None)
             native.stream_sync(dev, slot)  # no-op normally; on errors: H2D done
         finally:
             offs_pb.release()
+
+
+_sdma_ok: Dict[int, bool] = {}
+
+
+def _sdma_uploads(dev: int) -> bool:
+    """Encoded frames go up on the SDMA engines (``HIPSNAPSHOT_H2D_ENGINE``,
+    default sdma, when ROCr reports an engine)."""
+    from .. import knobs
+
+    if knobs.get_h2d_engine() != "sdma":
+        return False
+    ok = _sdma_ok.get(dev)
+    if ok is None:
+        ok = _sdma_ok[dev] = native.sdma_engines(dev) > 0
+    return ok
+
+
+def _decode_span_sdma(span, regions, dev, slot, direct, offs_pb, n_offs, c_n, log_lo, log_n,
+                      first, last, t0, scope) -> None:
+    """Upload the encoded frames and their offsets on an SDMA engine into an
+    uncached device block (no HIP runtime copy call: those block for ms when
+    several threads upload, profiles/r4/restore_trace/), then leave decode +
+    scatter running on the decode stream; the block goes back once they ran."""
+    h = span.header
+    offs_at = (c_n + 15) // 16 * 16
+    ub = native.UncachedBlock(dev, offs_at + 8 * n_offs)
+    try:
+        out = None if direct is not None else torch.empty(log_n, dtype=torch.uint8,
+                                                         device=f"cuda:{dev}")
+        t1 = time.perf_counter()
+        native.sdma_h2d(dev, ub.ptr + offs_at, offs_pb.ptr, 8 * n_offs)
+        tail = span.tail
+        if tail is not None and 0 < tail.offset < c_n:
+            # the head's frames go up while the rest of the blob is being read
+            native.sdma_h2d(dev, ub.ptr, span.buf.addr, tail.offset)
+            t_w = time.perf_counter()
+            tail.wait()
+            timeline.add("tail_wait", "h2d", t_w, time.perf_counter())
+            native.sdma_h2d(dev, ub.ptr + tail.offset, span.buf.addr + tail.offset,
+                            c_n - tail.offset)
+        else:
+            span.wait_tail()
+            native.sdma_h2d(dev, ub.ptr, span.buf.addr, c_n)
+        t2 = time.perf_counter()
+        kslot = decode_slot(slot)
+        # after the destinations' producer (joined on the copy stream) and
+        # after the current stream (``out`` comes from its allocator)
+        native.memcpy(dev, kslot, 0, 0, 0, native.H2D, native.copy_stream(dev, slot), sync=False)
+        _join_current_stream(dev, kslot)
+        err = native.DecodeErrorWord()
+        native.hsz_decode_gpu(dev, ub.ptr, ub.ptr + offs_at, first, last - first,
+                              h.logical_size, h.elem_width, h.frame_bytes,
+                              (direct if direct is not None else out).data_ptr(),
+                              native.copy_stream(dev, kslot), err.addr)
+        keep = [ub]
+        if direct is None:
+            ck = _copy_regions(out[span.lo - log_lo:], regions, dev, kslot, wait=False)
+            if ck is not None:
+                keep.extend(ck)  # descriptor stage + device workspace
+            out.record_stream(_ext_stream(dev, kslot))
+    except BaseException:
+        native.stream_sync(dev, decode_slot(slot))
+        ub.release()
+        raise
+    scope.add(_event_on(dev, kslot), keep, err, f"frames [{first}, {last})")
+    timeline.add("dec_alloc", "h2d", t0, t1)
+    timeline.add("h2d_sdma", "h2d", t1, t2, bytes=c_n)
+    timeline.add("dec_launch", "h2d", t2, time.perf_counter())
 
 
 def _decode_span(span, regions, dev, slot, direct, enc, offs_pb, n_offs, c_n, log_lo, log_n,

@@ -192,6 +192,18 @@ def get_d2h_engine() -> str:
     return v
 
 
+def get_h2d_engine() -> str:
+    """Engine for a restore's uploads of encoded (HSZ1) frames: ``sdma`` (the
+    DMA engines through ROCr into uncached device memory, ``csrc/hsdma.hip``)
+    or ``hip`` (hipMemcpyAsync, whose calls block for milliseconds when
+    several threads upload; profiles/r4/restore_trace/).  Default sdma when
+    ROCr reports an engine."""
+    v = str(_get("H2D_ENGINE") or "sdma").strip().lower()
+    if v not in ("hip", "sdma"):
+        raise ValueError(f"HIPSNAPSHOT_H2D_ENGINE must be hip or sdma, not {v!r}")
+    return v
+
+
 def async_dma() -> bool:
     """Staging workers submit their SDMA copy and move on; the writer waits
     for it (engine/staging.py ``d2h_staged``)."""

@@ -281,6 +281,10 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_hash64_result", c_int, [c_int, c_int, c_int, ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_sdma_last_error", c_char_p, [])
         _declare(lib, "hsg_sdma_engines", c_int, [c_int])
+        _declare(lib, "hsg_sdma_h2d", c_int, [c_int, c_void_p, c_void_p, c_uint64])
+        _declare(lib, "hsg_uncached_acquire", c_void_p, [c_int, c_uint64])
+        _declare(lib, "hsg_uncached_release", c_int, [c_void_p])
+        _declare(lib, "hsg_uncached_trim", c_uint64, [])
         _declare(lib, "hsg_sdma_d2h", c_int,
                  [c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p])
         _declare(lib, "hsg_sdma_d2h_submit", c_int,
@@ -430,6 +434,50 @@ def sdma_d2h(dev: int, dst: int, src: int, nbytes: int, stream=None,
     if r != 0:
         msg = lib.hsg_sdma_last_error()
         raise HipError(f"hsg_sdma_d2h failed ({r}): {msg.decode() if msg else ''}")
+
+
+def sdma_h2d(dev: int, dst: int, src: int, nbytes: int) -> None:
+    """Blocking pinned-host -> device copy on an SDMA engine.  ``dst`` must be
+    an ``UncachedBlock`` (the GPU reads it without an L2, so the copy needs no
+    acquire before kernels read it)."""
+    lib = require_gpu_lib()
+    r = lib.hsg_sdma_h2d(dev, dst, src, nbytes)
+    if r != 0:
+        msg = lib.hsg_sdma_last_error()
+        raise HipError(f"hsg_sdma_h2d failed ({r}): {msg.decode() if msg else ''}")
+
+
+class UncachedBlock:
+    """Device memory the GPU never caches (hipDeviceMallocUncached), from a
+    per-device caching pool: the target of SDMA uploads."""
+
+    __slots__ = ("ptr", "dev", "nbytes", "_released", "__weakref__")
+
+    def __init__(self, dev: int, nbytes: int) -> None:
+        lib = require_gpu_lib()
+        ptr = lib.hsg_uncached_acquire(dev, max(int(nbytes), 1))
+        if not ptr:
+            raise torch.cuda.OutOfMemoryError(
+                f"uncached device allocation of {nbytes} bytes failed: "
+                f"{lib.hsg_last_error().decode()}")
+        self.ptr, self.dev, self.nbytes, self._released = ptr, dev, int(nbytes), False
+
+    def release(self) -> None:
+        if not self._released:
+            self._released = True
+            lib = _load_hsgpu()
+            if lib is not None:
+                lib.hsg_uncached_release(self.ptr)
+
+    def __del__(self) -> None:  # pragma: no cover - GC path
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+def uncached_trim() -> int:
+    return int(require_gpu_lib().hsg_uncached_trim())
 
 
 def sdma_d2h_submit(dev: int, dst: int, src: int, nbytes: int, stream=None) -> int:
