@@ -937,16 +937,44 @@ class CorruptBlobError(ValueError, RuntimeError):
 
 class DecodeErrorWord:
     """Pinned host word the GPU decoders flag corrupt HSZ1 frames in (the
-    device writes it through the host mapping; no extra copy or sync)."""
+    device writes it through the host mapping; no extra copy or sync).
+
+    Words come from pinned slabs of 1024 (one hipHostMalloc each, reused):
+    a restore creates one per blob, and a pinned allocation per blob cost
+    ~0.1 ms of HIP runtime time each (profiles/r4/restore_trace/)."""
+
+    _lock = threading.Lock()
+    _free: List[tuple] = []  # (slab tensor, index)
+    _SLAB = 1024
 
     def __init__(self) -> None:
         import torch
 
-        self._t = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        self.addr = self._t.data_ptr()
+        with DecodeErrorWord._lock:
+            if not DecodeErrorWord._free:
+                slab = torch.zeros(DecodeErrorWord._SLAB, dtype=torch.int32, pin_memory=True)
+                DecodeErrorWord._free.extend((slab, i) for i in range(DecodeErrorWord._SLAB))
+            self._slab, self._i = DecodeErrorWord._free.pop()
+        self._slab[self._i] = 0
+        self.addr = self._slab.data_ptr() + 4 * self._i
+        self._held = True
 
     def check(self, what: str) -> None:
         """Call after the decode's stream was synchronised."""
-        if int(self._t[0]) != 0:
+        bad = int(self._slab[self._i]) != 0
+        self.release()
+        if bad:
             raise CorruptBlobError(
                 f"corrupt HSZ1 blob: the GPU decoder rejected a frame of {what}")
+
+    def release(self) -> None:
+        if self._held:
+            self._held = False
+            with DecodeErrorWord._lock:
+                DecodeErrorWord._free.append((self._slab, self._i))
+
+    def __del__(self) -> None:  # pragma: no cover - GC path
+        try:
+            self.release()
+        except Exception:
+            pass
