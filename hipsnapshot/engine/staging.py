@@ -741,8 +741,9 @@ def h2d_into(dst: torch.Tensor, host_addr: int, nbytes: int, src_dtype: torch.dt
     """
     dev = device_of(dst)
     slot = copy_slot()
+    sdma = _current_deferred() is not None and nbytes >= _SDMA_MIN_BYTES and _sdma_uploads(dev)
     if dst.dtype == src_dtype and dst.is_contiguous() and list(dst.shape) == list(src_shape) \
-            and not _is_managed(dst):
+            and not _is_managed(dst) and not sdma:
         native.memcpy(dev, slot, dst.data_ptr(), host_addr, nbytes, native.H2D, producer,
                       sync=True)
         return
@@ -768,6 +769,12 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
     slot = copy_slot()
     # order after pending work on the destinations' stream (captured at plan time)
     native.memcpy(dev, slot, 0, 0, 0, native.H2D, producer, sync=False)
+    scope = _current_deferred()
+    if scope is not None and nbytes >= _SDMA_MIN_BYTES and _sdma_uploads(dev) and \
+            all(native.can_cast_on_device(r[0], r[4].dtype) and r[4].dim() <= native.MAX_DIMS
+                for r in regions):
+        _scatter_host_regions_sdma(host_addr, nbytes, regions, dev, slot, scope)
+        return
     # Regions whose source bytes are one contiguous range and whose destination
     # is a contiguous tensor of the same dtype/shape go host -> destination with
     # one DMA each (no scratch, no kernel: the common FSDP/DTensor restore).
@@ -791,7 +798,6 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
     _join_current_stream(dev, slot)
     native.memcpy(dev, slot, scratch.data_ptr(), host_addr, nbytes, native.H2D, None,
                   sync=False)
-    scope = _current_deferred()
     if scope is None:
         _copy_regions(scratch, kernel_regions, dev, slot)
         return
@@ -808,6 +814,35 @@ def _scatter_host_regions(host_addr: int, nbytes: int, regions, dev: int,
     timeline.add("h2d_wait", "h2d", t_w, time.perf_counter(), bytes=nbytes)
 
 
+# below this, one hipMemcpyAsync is cheaper than an uncached block + a kernel
+_SDMA_MIN_BYTES = 1 << 20
+
+
+def _scatter_host_regions_sdma(host_addr: int, nbytes: int, regions, dev: int, slot: int,
+                               scope) -> None:
+    """The whole buffer goes up on an SDMA engine into an uncached block (one
+    DMA instead of a HIP copy call per region; those calls block for ms when
+    several threads upload), then ONE copy kernel on the decode stream writes
+    every destination view; this consumer returns once the upload is done."""
+    ub = native.UncachedBlock(dev, nbytes)
+    try:
+        t0 = time.perf_counter()
+        native.sdma_h2d(dev, ub.ptr, host_addr, nbytes)
+        t1 = time.perf_counter()
+        dslot = decode_slot(slot)
+        native.memcpy(dev, dslot, 0, 0, 0, native.H2D, native.copy_stream(dev, slot), sync=False)
+        keep = [ub]
+        ck = _copy_regions(None, regions, dev, dslot, wait=False, base=ub.ptr)
+        if ck is not None:
+            keep.extend(ck)
+    except BaseException:
+        native.stream_sync(dev, decode_slot(slot))
+        ub.release()
+        raise
+    scope.add(_event_on(dev, dslot), keep)
+    timeline.add("h2d_sdma", "h2d", t0, t1, bytes=nbytes)
+
+
 _elem_sizes: dict = {}
 
 
@@ -818,7 +853,8 @@ def _elem_size(dtype: torch.dtype) -> int:
     return es
 
 
-def _copy_regions(scratch: torch.Tensor, regions, dev: int, slot: int, wait: bool = True):
+def _copy_regions(scratch: Optional[torch.Tensor], regions, dev: int, slot: int,
+                  wait: bool = True, base: Optional[int] = None):
     """ONE copy/cast launch from the device buffer ``scratch`` (region offsets
     are relative to it) into every destination view, then a stream sync.
     ``wait=False``: no sync; returns the launch's keepalive (the caller holds
@@ -826,7 +862,8 @@ def _copy_regions(scratch: torch.Tensor, regions, dev: int, slot: int, wait: boo
     t0 = time.perf_counter()
     batch = native.CopyBatch()
     fallbacks = []
-    base = scratch.data_ptr()
+    if base is None:
+        base = scratch.data_ptr()
     for src_dtype, src_shape, off, narrows, dst in regions:
         es = _elem_size(src_dtype)
         if native.can_cast_on_device(src_dtype, dst.dtype) and dst.dim() <= native.MAX_DIMS:
