@@ -376,11 +376,18 @@ def uvm_assume_host() -> bool:
     return not device_xnack_enabled()
 
 
-def drain_avoid_caller_core() -> bool:
-    """The native drain's threads keep off the physical core of the thread
-    that called ``async_take`` (utils/affinity.py): a launch-bound training
-    step loses issue slots to an SMT sibling busy with page-cache copies."""
-    return _get_bool("DRAIN_AVOID_CALLER_CORE", True)
+def drain_avoid_caller_core() -> str:
+    """Where the native drain's threads may NOT run, relative to the thread
+    that called ``async_take`` (utils/affinity.py): ``"core"`` (default) its
+    physical core -- a launch-bound training step loses issue slots to an SMT
+    sibling busy with page-cache copies; ``"l3"`` every CPU sharing its L3
+    (the writers' streaming copies then evict none of the trainer's cached
+    interpreter and allocator state); ``""`` anywhere is fine.  Env
+    ``DRAIN_AVOID_CALLER_CORE``: 0/1 or core/l3."""
+    v = (_get("DRAIN_AVOID_CALLER_CORE") or "core").strip().lower()
+    if v in ("0", "false", "no", "off", ""):
+        return ""
+    return "l3" if v == "l3" else "core"
 
 
 def drain_hash_high_priority() -> bool:

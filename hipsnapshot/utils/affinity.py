@@ -112,8 +112,9 @@ def describe(devices: List[int]) -> List[dict]:
 # its physical core: an SMT sibling busy with a drain writer's page-cache
 # memcpy takes a large share of the core's issue slots.  ``async_take`` notes
 # the core its caller runs on; the native drain's threads are created with an
-# affinity mask that excludes that core's hardware threads
-# (``HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE``, default on).
+# affinity mask that excludes that core's hardware threads, or every CPU of
+# its L3 domain (``HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE`` = core (default) / l3
+# / 0).
 
 _caller_cpu: List[Optional[int]] = [None]
 
@@ -140,21 +141,45 @@ def core_siblings(cpu: int) -> Set[int]:
         return {cpu}
 
 
+def l3_siblings(cpu: int) -> Set[int]:
+    """The CPUs sharing ``cpu``'s last-level (L3) cache: one CCD on EPYC
+    hosts (``cpu`` itself if the topology is unknown)."""
+    base = f"/sys/devices/system/cpu/cpu{cpu}/cache"
+    try:
+        for idx in sorted(os.listdir(base)):
+            if not idx.startswith("index"):
+                continue
+            with open(os.path.join(base, idx, "level")) as f:
+                if f.read().strip() != "3":
+                    continue
+            with open(os.path.join(base, idx, "shared_cpu_list")) as f:
+                return _parse_cpulist(f.read()) or {cpu}
+    except OSError:
+        pass
+    return {cpu}
+
+
 def note_caller_cpu() -> None:
     """Record the core the calling (training) thread runs on."""
     _caller_cpu[0] = current_cpu()
 
 
-def mask_avoiding_caller() -> Optional[Set[int]]:
-    """This thread's allowed CPUs minus the noted caller's core, or None when
-    nothing was noted or too few CPUs would remain."""
+def mask_avoiding_caller(mode: str = "core") -> Optional[Set[int]]:
+    """This thread's allowed CPUs minus the noted caller's core (``mode``
+    "core") or its whole L3 domain ("l3"; the core alone when fewer than 2
+    CPUs would remain), or None when nothing was noted or too few CPUs
+    would remain."""
     cpu = _caller_cpu[0]
-    if cpu is None:
+    if cpu is None or not mode:
         return None
     try:
         allowed = os.sched_getaffinity(0)
     except OSError:
         return None
+    if mode == "l3":
+        rest = allowed - l3_siblings(cpu) - core_siblings(cpu)
+        if len(rest) >= 2 and rest != allowed:
+            return rest
     rest = allowed - core_siblings(cpu)
     if len(rest) < 2 or rest == allowed:
         return None
@@ -166,14 +191,15 @@ class threads_avoiding_caller:
     thread's mask) never run on the noted caller's core; the calling
     thread's own mask is restored on exit."""
 
-    def __init__(self, enabled: bool = True) -> None:
-        self.enabled = enabled
+    def __init__(self, enabled=True) -> None:
+        # True / "core": the caller's core; "l3": its L3 domain; falsy: off
+        self.mode = "core" if enabled is True else (enabled or "")
         self.prev: Optional[Set[int]] = None
 
     def __enter__(self) -> "threads_avoiding_caller":
-        if not self.enabled:
+        if not self.mode:
             return self
-        mask = mask_avoiding_caller()
+        mask = mask_avoiding_caller(self.mode)
         if mask is not None:
             try:
                 self.prev = os.sched_getaffinity(0)

@@ -325,3 +325,22 @@ def test_drain_threads_avoid_the_callers_core():
         assert not (seen["mask"] & affinity.core_siblings(affinity._caller_cpu[0]))
     with affinity.threads_avoiding_caller(enabled=False):
         assert os.sched_getaffinity(0) == before
+    # "l3": the caller's whole L3 domain is excluded when enough CPUs remain
+    cpu = affinity._caller_cpu[0]
+    assert cpu in affinity.l3_siblings(cpu)
+    m = affinity.mask_avoiding_caller("l3")
+    if m is not None:
+        assert not (m & affinity.core_siblings(cpu))
+        if len(before - affinity.l3_siblings(cpu)) >= 2:
+            assert not (m & affinity.l3_siblings(cpu))
+    assert affinity.mask_avoiding_caller("") is None
+
+
+def test_drain_avoid_knob_modes(monkeypatch):
+    from hipsnapshot import knobs
+
+    for v, want in (("1", "core"), ("core", "core"), ("l3", "l3"), ("0", ""), ("off", "")):
+        monkeypatch.setenv("HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE", v)
+        assert knobs.drain_avoid_caller_core() == want
+    monkeypatch.delenv("HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE")
+    assert knobs.drain_avoid_caller_core() == "core"
