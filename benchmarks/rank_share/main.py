@@ -194,6 +194,7 @@ def main() -> None:
         "async_total_ms_median": round(statistics.median(total) * 1e3, 2),
         "restore_ms_median": round(statistics.median(rtimes) * 1e3, 2),
         "restore_bitwise_ok": ok,
+        "native_restore_stats": _native_restore_stats(),
         **({"host_siblings": args.host_siblings, "sibling_dma_pass": bool(args.sibling_dma_pass),
             "sibling_bytes_each": sum(sib.sizes),
             "contended_take_ms_median": round(statistics.median(contended) * 1e3, 2),
@@ -207,6 +208,12 @@ def main() -> None:
     }), flush=True)
     shutil.rmtree(root, ignore_errors=True)
     dist.destroy_process_group()
+
+
+def _native_restore_stats() -> dict:
+    from hipsnapshot.engine import native_restore
+
+    return dict(native_restore.last_stats)
 
 
 def _sibling_main(i: int, sizes, root: str, dma_pass: bool, go, done, hint: int) -> None:

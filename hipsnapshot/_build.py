@@ -53,7 +53,8 @@ def build_hsio(force: bool = False) -> str:
 
 def build_hsgpu(force: bool = False) -> str:
     srcs = [os.path.join(CSRC, "hsgpu.hip"), os.path.join(CSRC, "hsz.hip"),
-            os.path.join(CSRC, "hsdma.hip"), os.path.join(CSRC, "hsdrain.hip")]
+            os.path.join(CSRC, "hsdma.hip"), os.path.join(CSRC, "hsdrain.hip"),
+            os.path.join(CSRC, "hsrestore.hip")]
     if force or _stale(HSGPU_SO, srcs):
         hipcc = os.path.join(ROCM, "bin", "hipcc")
         if not os.path.exists(hipcc):

@@ -378,6 +378,28 @@ int hsg_sdma_h2d(int dev, void* dst, const void* src, uint64_t n) {
   return 0;
 }
 
+// Asynchronous hsg_sdma_h2d: submits the copy and returns at once with
+// *handle naming its completion signal (pass it to hsg_sdma_wait exactly
+// once; `src` and `dst` stay valid until then).  The native restore keeps
+// several uploads queued so the link never idles between them.
+int hsg_sdma_h2d_submit(int dev, void* dst, const void* src, uint64_t n, uint64_t* handle) {
+  *handle = 0;
+  DevInfo* d = dev_info(dev);
+  if (!d) return -1;
+  if (n == 0) return 0;
+  hsa_signal_t s = take_signal();
+  if (s.handle == 0) return -5;
+  g_api.signal_store(s, 1);
+  const hsa_status_t st = g_api.async_copy(dst, d->gpu, src, d->cpu, n, 0, nullptr, s);
+  if (st != HSA_STATUS_SUCCESS) {
+    give_signal(s);
+    snprintf(g_err, sizeof(g_err), "hsa_amd_memory_async_copy (h2d): status 0x%x", unsigned(st));
+    return -6;
+  }
+  *handle = s.handle;
+  return 0;
+}
+
 // Wait for a copy submitted by hsg_sdma_d2h_submit; 0 = done, < 0 = the
 // engine reported an error (the copy did not complete).  handle 0: no-op.
 int hsg_sdma_wait(uint64_t handle) {

@@ -1,0 +1,735 @@
+// hsrestore: native restore of local-FS blobs into HBM.
+//
+// The Python read pipeline (engine/scheduler.py execute_read_reqs) spends
+// ~1 ms of interpreter work per blob -- pinned destinations, the header
+// parse, upload and decode launches, region descriptors -- on consumer
+// threads that contend for the GIL; at one rank's share of an 8-GPU
+// Llama-3-8B restore that was a third of the restore and the PCIe link ran
+// at 46 GB/s of its 57 (profiles/r4/restore_native/).  Here every blob whose
+// bytes all land in HBM is restored by ONE call:
+//
+//   readers      claim the next chunk (<= slot bytes) of the plan in order,
+//                pread() it from the page cache into a free pinned slot and
+//                submit its SDMA upload into the blob's uncached device
+//                block (csrc/hsdma.hip; several uploads stay queued, so the
+//                link does not idle between chunks or blobs);
+//   completion   waits the uploads in submission order, returns slots; when
+//                a blob's last chunk has landed it validates the blob's HSZ1
+//                frame table (kept from its first chunk) and launches the
+//                device work on one of two streams: the HSZ1 decode
+//                (csrc/hsz.hip) straight into the destination or into a
+//                scratch block, then ONE hs_copy_nd launch (csrc/hsgpu.hip)
+//                writing every destination view (strided / narrowed / cast);
+//   retire       waits each blob's completion event and returns its device
+//                blocks, so the HBM the pipeline holds stays within a budget.
+//
+// The uncached upload target needs no acquire before the kernels read it
+// (see hsg_sdma_h2d); the kernels write the destinations through the L2 like
+// any other kernel, ordered after the destinations' producer streams.
+// Reference behaviour being replaced: `/root/reference/torchsnapshot/
+// scheduler.py:384-444` (read pipeline) and `io_preparers/tensor.py:294-346`
+// (buffer consumers copying into the target tensors).
+
+#include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+extern "C" {
+int hsg_sdma_h2d_submit(int dev, void* dst, const void* src, uint64_t n, uint64_t* handle);
+int hsg_sdma_wait(uint64_t handle);
+void* hsg_pinned_acquire(uint64_t nbytes);
+int hsg_pinned_release(void* p);
+int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t first,
+                   uint32_t count, uint64_t logical, int w, uint32_t frame_bytes, void* out,
+                   void* stream, void* err);
+uint64_t hsg_copy_workspace_bytes(const void* descs, int n);
+int hsg_copy_nd(int dev, const void* descs, int n, void* workspace, uint64_t ws_bytes,
+                void* pinned_stage, void* stream, int sync);
+uint64_t hsg_desc_size();
+void* hsg_copy_stream(int dev, int slot);
+}
+
+namespace {
+
+constexpr uint64_t kGranule = uint64_t(2) << 20;
+constexpr uint64_t kHszHeader = 64;
+constexpr uint64_t kHszFrameHeader = 32;
+constexpr int kCodecRaw = 0;
+constexpr int kCodecHsz = 1;
+constexpr int kRestoreSlot = 2000;  // persistent streams (dev, 2000 + s), s = 0, 1
+
+uint64_t now_ns() {
+  return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
+      std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
+uint64_t align16(uint64_t n) { return (n + 15) & ~uint64_t(15); }
+
+// ---- device block pools (uncached upload targets, plain scratch) -----------
+//
+// Cached per device by size (best fit up to 2x, 2 MiB granules) across
+// restores; hsg_restore_trim() frees the idle ones.
+struct DevPool {
+  std::mutex mu;
+  std::map<int, std::multimap<uint64_t, void*>> free_blocks;
+  std::unordered_map<void*, std::pair<int, uint64_t>> live;
+  uint64_t idle_bytes = 0;
+  unsigned flags;  // hipExtMallocWithFlags flags (0 = hipMalloc)
+
+  explicit DevPool(unsigned f) : flags(f) {}
+
+  void* acquire(int dev, uint64_t nbytes) {
+    const uint64_t want = (std::max<uint64_t>(nbytes, 1) + kGranule - 1) / kGranule * kGranule;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto& fl = free_blocks[dev];
+      auto it = fl.lower_bound(want);
+      if (it != fl.end() && it->first <= 2 * want) {
+        void* p = it->second;
+        live[p] = {dev, it->first};
+        idle_bytes -= it->first;
+        fl.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipSetDevice(dev) != hipSuccess) return nullptr;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const hipError_t e = flags ? hipExtMallocWithFlags(&p, want, flags) : hipMalloc(&p, want);
+      if (e == hipSuccess) break;
+      p = nullptr;
+      (void)hipGetLastError();
+      if (attempt == 0) trim(dev, 0);  // drop this device's idle blocks and retry
+    }
+    if (!p) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    live[p] = {dev, want};
+    return p;
+  }
+
+  void release(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = live.find(p);
+    if (it == live.end()) return;
+    free_blocks[it->second.first].emplace(it->second.second, p);
+    idle_bytes += it->second.second;
+    live.erase(it);
+  }
+
+  // free idle blocks of `dev` (-1: all devices) until at most `keep` idle
+  // bytes remain (largest first); returns the bytes freed
+  uint64_t trim(int dev, uint64_t keep) {
+    std::vector<void*> drop;
+    uint64_t freed = 0;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (auto& dv : free_blocks) {
+        if (dev >= 0 && dv.first != dev) continue;
+        auto& fl = dv.second;
+        while (!fl.empty() && idle_bytes > keep) {
+          auto it = std::prev(fl.end());
+          drop.push_back(it->second);
+          idle_bytes -= it->first;
+          freed += it->first;
+          fl.erase(it);
+        }
+      }
+    }
+    for (void* q : drop) (void)hipFree(q);
+    return freed;
+  }
+};
+
+DevPool g_upload_pool(hipDeviceMallocUncached);
+DevPool g_scratch_pool(0);
+
+// ---- the job -----------------------------------------------------------------
+
+struct Item {
+  std::string path;
+  uint64_t file_lo = 0;    // first file byte to read
+  uint64_t nbytes = 0;     // bytes to read (the whole stored blob for HSZ1)
+  int codec = kCodecRaw;
+  uint64_t logical = 0;    // HSZ1: expected logical size
+  uint64_t direct = 0;     // HSZ1: decode straight into this device address
+  uint64_t base_off = 0;   // region sources start here in the decoded / raw bytes
+  int64_t desc_off = 0;    // first descriptor in the job's table
+  int desc_n = 0;
+
+  // runtime
+  std::mutex mu;
+  int fd = -1;
+  int pieces_read = 0;     // pieces read so far (the last one closes fd)
+  int npieces = 0;
+  void* block = nullptr;   // uncached upload target
+  void* scratch = nullptr; // HSZ1 decode output when not direct
+  void* ws = nullptr;      // copy descriptor / tile workspace
+  void* stage = nullptr;   // pinned stage of the workspace tables
+  uint64_t charged = 0;    // device bytes counted against the budget
+  int nchunks = 0;
+  std::atomic<int> chunks_left{0};
+  std::vector<uint8_t> head;  // HSZ1 header + frame table (from chunk 0)
+  hipEvent_t done = nullptr;
+};
+
+struct Chunk {
+  int item;
+  int index;
+  uint64_t off;  // within the item
+  uint64_t n;
+  int slot;
+  uint64_t handle;
+};
+
+// A pinned slot being filled: one upload unit (<= slot bytes of one item),
+// read by several readers in pieces; the reader finishing the last piece
+// submits the upload.
+struct SlotFill {
+  int item = -1;
+  int chunk = -1;
+  uint64_t off = 0;  // within the item
+  uint64_t n = 0;
+  int pieces = 0;
+  int next_piece = 0;
+  std::atomic<int> left{0};
+};
+
+enum Stat {
+  kRead,         // readers in pread
+  kSlotWait,     // readers waiting for a free pinned slot
+  kBudgetWait,   // readers waiting for device budget
+  kAlloc,        // readers acquiring device blocks
+  kSubmit,       // readers submitting uploads
+  kUploadWait,   // completion thread waiting for uploads
+  kLaunch,       // completion thread validating + launching device work
+  kRetireWait,   // retire thread waiting for device work
+  kFirstUpload,  // start -> first upload submitted
+  kWall,
+  kNumStats
+};
+
+struct Job {
+  int dev = 0;
+  uint64_t slot_bytes = 0;
+  uint64_t budget = 0;
+  std::vector<Item> items;
+  std::vector<uint8_t> descs;  // packed CopyDesc table (sources relative)
+  uint64_t desc_size = 0;
+  uint32_t* err_words = nullptr;  // host-mapped, one per item
+  hipStream_t streams[2] = {nullptr, nullptr};
+
+  std::vector<void*> slots;
+  std::unique_ptr<SlotFill[]> fills;
+  uint64_t piece_bytes = 0;
+  int filling = -1;  // the slot readers currently claim pieces of
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<int> free_slots;
+  std::deque<Chunk> inflight;
+  std::deque<int> retire;
+  int cursor_item = 0;
+  int cursor_chunk = 0;
+  int readers_left = 0;
+  bool completion_done = false;
+  uint64_t used = 0;  // device bytes charged
+  int launched = 0;
+
+  std::atomic<int> err{0};
+  int err_item = -1;
+  char errmsg[320] = {0};
+  std::atomic<uint64_t> ns[kNumStats] = {};
+  std::atomic<uint64_t> bytes_read{0};
+  std::atomic<bool> first_upload{false};
+  uint64_t t_start = 0;
+  std::vector<std::thread> threads;
+
+  void add(Stat k, uint64_t t0) { ns[k].fetch_add(now_ns() - t0); }
+
+  void fail(int code, int item, const char* what) {
+    int expected = 0;
+    if (err.compare_exchange_strong(expected, code)) {
+      std::lock_guard<std::mutex> g(mu);
+      err_item = item;
+      snprintf(errmsg, sizeof(errmsg), "%s %s: %s", what,
+               item >= 0 ? items[item].path.c_str() : "",
+               code < 0 && code > -4096 ? strerror(-code) : "error");
+    }
+    cv.notify_all();
+  }
+};
+
+int chunks_of(const Job* j, const Item& it) {
+  return it.nbytes ? int((it.nbytes + j->slot_bytes - 1) / j->slot_bytes) : 0;
+}
+
+// Device blocks of item i (upload target, decode scratch); waits for budget.
+bool ensure_blocks(Job* j, int i) {
+  Item& it = j->items[i];
+  std::lock_guard<std::mutex> g(it.mu);
+  if (it.block) return true;
+  const uint64_t need = (it.nbytes + kGranule - 1) / kGranule * kGranule +
+                        (it.codec == kCodecHsz && !it.direct
+                             ? (it.logical + kGranule - 1) / kGranule * kGranule : 0);
+  uint64_t t0 = now_ns();
+  {
+    std::unique_lock<std::mutex> lk(j->mu);
+    j->cv.wait(lk, [&] { return j->used == 0 || j->used + need <= j->budget || j->err.load(); });
+    if (j->err.load()) return false;
+    j->used += need;
+  }
+  it.charged = need;
+  j->add(kBudgetWait, t0);
+  t0 = now_ns();
+  it.block = g_upload_pool.acquire(j->dev, it.nbytes);
+  if (it.block && it.codec == kCodecHsz && !it.direct)
+    it.scratch = g_scratch_pool.acquire(j->dev, it.logical);
+  j->add(kAlloc, t0);
+  if (!it.block || (it.codec == kCodecHsz && !it.direct && !it.scratch)) {
+    j->fail(-ENOMEM, i, "device block");
+    return false;
+  }
+  return true;
+}
+
+int pieces_of(const Job* j, uint64_t n) { return int((n + j->piece_bytes - 1) / j->piece_bytes); }
+
+void reader_thread(Job* j) {
+  (void)hipSetDevice(j->dev);
+  const int nitems = int(j->items.size());
+  for (;;) {
+    int s, i;
+    uint64_t poff, pn;
+    {
+      std::unique_lock<std::mutex> lk(j->mu);
+      bool finished = false;
+      for (;;) {
+        if (j->err.load()) {
+          finished = true;
+          break;
+        }
+        if (j->filling >= 0 && j->fills[j->filling].next_piece < j->fills[j->filling].pieces)
+          break;
+        while (j->cursor_item < nitems &&
+               j->cursor_chunk >= j->items[j->cursor_item].nchunks) {
+          ++j->cursor_item;
+          j->cursor_chunk = 0;
+        }
+        if (j->cursor_item >= nitems) {
+          finished = true;
+          break;
+        }
+        if (j->free_slots.empty()) {
+          const uint64_t t0 = now_ns();
+          j->cv.wait(lk);
+          j->add(kSlotWait, t0);
+          continue;
+        }
+        // start filling a free slot with the plan's next range
+        const int fs = j->free_slots.back();
+        j->free_slots.pop_back();
+        Item& ci = j->items[j->cursor_item];
+        SlotFill& f = j->fills[fs];
+        f.item = j->cursor_item;
+        f.chunk = j->cursor_chunk++;
+        f.off = uint64_t(f.chunk) * j->slot_bytes;
+        f.n = std::min(j->slot_bytes, ci.nbytes - f.off);
+        f.pieces = pieces_of(j, f.n);
+        f.next_piece = 0;
+        f.left.store(f.pieces);
+        j->filling = fs;
+      }
+      if (finished) break;
+      s = j->filling;
+      SlotFill& f = j->fills[s];
+      const int k = f.next_piece++;
+      i = f.item;
+      poff = uint64_t(k) * j->piece_bytes;
+      pn = std::min(j->piece_bytes, f.n - poff);
+    }
+    // other readers may claim the slot's remaining pieces at once
+    j->cv.notify_all();
+    SlotFill& f = j->fills[s];
+    Item& it = j->items[i];
+    if (!ensure_blocks(j, i)) break;
+    {
+      std::lock_guard<std::mutex> g(it.mu);
+      if (it.fd < 0 && it.pieces_read < it.npieces) {
+        it.fd = open(it.path.c_str(), O_RDONLY | O_CLOEXEC);
+        if (it.fd < 0) {
+          j->fail(-errno, i, "open");
+          break;
+        }
+      }
+    }
+    char* p = static_cast<char*>(j->slots[s]) + poff;
+    uint64_t t0 = now_ns();
+    uint64_t done = 0;
+    int rerr = 0;
+    while (done < pn) {
+      const ssize_t r = pread(it.fd, p + done, pn - done, off_t(it.file_lo + f.off + poff + done));
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        rerr = -errno;
+        break;
+      }
+      if (r == 0) {
+        rerr = -ENODATA;  // the file is shorter than the manifest says
+        break;
+      }
+      done += uint64_t(r);
+    }
+    j->add(kRead, t0);
+    {
+      std::lock_guard<std::mutex> g(it.mu);
+      if (++it.pieces_read == it.npieces && it.fd >= 0) {
+        close(it.fd);
+        it.fd = -1;
+      }
+    }
+    if (rerr) {
+      j->fail(rerr, i, "read");
+      break;
+    }
+    j->bytes_read.fetch_add(pn);
+    if (f.left.fetch_sub(1) != 1) continue;
+    // the slot is full: upload it
+    const char* sp = static_cast<const char*>(j->slots[s]);
+    if (f.chunk == 0 && it.codec == kCodecHsz) {
+      // header + frame table: validated once every chunk has landed
+      uint64_t nf = 0;
+      memcpy(&nf, sp + 24, 4);
+      const uint64_t hb = std::min<uint64_t>(f.n, kHszHeader + 8 * (nf + 1));
+      it.head.assign(sp, sp + hb);
+    }
+    t0 = now_ns();
+    uint64_t h = 0;
+    const int r = hsg_sdma_h2d_submit(j->dev, static_cast<char*>(it.block) + f.off, sp, f.n, &h);
+    if (!j->first_upload.exchange(true)) j->ns[kFirstUpload].store(now_ns() - j->t_start);
+    j->add(kSubmit, t0);
+    if (r != 0) {
+      j->fail(-EIO, i, "sdma upload");
+      break;
+    }
+    {
+      std::lock_guard<std::mutex> g(j->mu);
+      j->inflight.push_back(Chunk{i, f.chunk, f.off, f.n, s, h});
+    }
+    j->cv.notify_all();
+  }
+  {
+    std::lock_guard<std::mutex> g(j->mu);
+    --j->readers_left;
+  }
+  j->cv.notify_all();
+}
+
+// Validate item i's HSZ1 header + frame table (what codec.validate_offsets
+// checks in Python) before any kernel walks the frames.
+bool hsz_header_ok(const Item& it, int* w, uint32_t* fb, uint32_t* nf) {
+  const std::vector<uint8_t>& h = it.head;
+  if (h.size() < kHszHeader || memcmp(h.data(), "HSZ1", 4) != 0) return false;
+  uint32_t version, width, frame_bytes, n_frames;
+  uint64_t logical;
+  memcpy(&version, h.data() + 4, 4);
+  memcpy(&logical, h.data() + 8, 8);
+  memcpy(&width, h.data() + 16, 4);
+  memcpy(&frame_bytes, h.data() + 20, 4);
+  memcpy(&n_frames, h.data() + 24, 4);
+  if (version != 1 && version != 2) return false;
+  if (logical != it.logical) return false;
+  if (!(width == 1 || width == 2 || width == 4 || width == 8)) return false;
+  if (frame_bytes == 0 || frame_bytes % 16 || frame_bytes % width) return false;
+  const uint64_t want_nf = std::max<uint64_t>(1, (logical + frame_bytes - 1) / frame_bytes);
+  if (n_frames != want_nf) return false;
+  if (h.size() < kHszHeader + 8 * (uint64_t(n_frames) + 1)) return false;
+  const uint64_t* offs = reinterpret_cast<const uint64_t*>(h.data() + kHszHeader);
+  if (offs[0] < kHszHeader + 8 * (uint64_t(n_frames) + 1) || offs[n_frames] > it.nbytes)
+    return false;
+  for (uint32_t f = 0; f < n_frames; ++f) {
+    const uint64_t lo = uint64_t(f) * frame_bytes;
+    const uint64_t len = std::min<uint64_t>(frame_bytes, logical - std::min(lo, logical));
+    if (offs[f + 1] < offs[f] + kHszFrameHeader ||
+        offs[f + 1] - offs[f] > align16(kHszFrameHeader + len))
+      return false;
+  }
+  *w = int(width);
+  *fb = frame_bytes;
+  *nf = n_frames;
+  return true;
+}
+
+// Decode / copy launches for item i on stream s; records it.done.
+int launch_item(Job* j, int i, hipStream_t s) {
+  Item& it = j->items[i];
+  char* base = static_cast<char*>(it.block);
+  if (it.codec == kCodecHsz) {
+    int w;
+    uint32_t fb, nf;
+    if (!hsz_header_ok(it, &w, &fb, &nf)) {
+      j->fail(-EBADMSG, i, "corrupt HSZ1 header or frame table in");
+      return -1;
+    }
+    void* out = it.direct ? reinterpret_cast<void*>(it.direct) : it.scratch;
+    if (hsg_hsz_decode(j->dev, it.block, base + kHszHeader, 0, nf, it.logical, w, fb, out, s,
+                       j->err_words + i) != 0) {
+      j->fail(-EIO, i, "decode launch");
+      return -1;
+    }
+    base = static_cast<char*>(out);
+  }
+  if (it.desc_n > 0) {
+    std::vector<uint8_t> d(j->descs.begin() + it.desc_off * int64_t(j->desc_size),
+                           j->descs.begin() + (it.desc_off + it.desc_n) * int64_t(j->desc_size));
+    const uint64_t src_base = reinterpret_cast<uint64_t>(base) + it.base_off;
+    for (int k = 0; k < it.desc_n; ++k) {
+      uint64_t v;
+      memcpy(&v, d.data() + uint64_t(k) * j->desc_size, 8);
+      v += src_base;
+      memcpy(d.data() + uint64_t(k) * j->desc_size, &v, 8);
+    }
+    const uint64_t wsb = hsg_copy_workspace_bytes(d.data(), it.desc_n);
+    it.ws = g_scratch_pool.acquire(j->dev, wsb);
+    it.stage = hsg_pinned_acquire(wsb);
+    if (!it.ws || !it.stage) {
+      j->fail(-ENOMEM, i, "copy workspace");
+      return -1;
+    }
+    if (hsg_copy_nd(j->dev, d.data(), it.desc_n, it.ws, wsb, it.stage, s, 0) != 0) {
+      j->fail(-EIO, i, "copy launch");
+      return -1;
+    }
+  }
+  if (hipEventCreateWithFlags(&it.done, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(it.done, s) != hipSuccess) {
+    j->fail(-EIO, i, "completion event");
+    return -1;
+  }
+  return 0;
+}
+
+void release_item(Job* j, Item& it) {
+  g_upload_pool.release(it.block);
+  g_scratch_pool.release(it.scratch);
+  g_scratch_pool.release(it.ws);
+  if (it.stage) hsg_pinned_release(it.stage);
+  it.block = it.scratch = it.ws = it.stage = nullptr;
+  if (it.done) {
+    hipEventDestroy(it.done);
+    it.done = nullptr;
+  }
+  {
+    std::lock_guard<std::mutex> g(j->mu);
+    j->used -= it.charged;
+  }
+  it.charged = 0;
+  j->cv.notify_all();
+}
+
+void completion_thread(Job* j) {
+  (void)hipSetDevice(j->dev);
+  for (;;) {
+    Chunk c;
+    {
+      std::unique_lock<std::mutex> lk(j->mu);
+      j->cv.wait(lk, [&] { return !j->inflight.empty() || j->readers_left == 0; });
+      if (j->inflight.empty()) break;
+      c = j->inflight.front();
+      j->inflight.pop_front();
+    }
+    // every submitted upload is waited for, even after an error: the engine
+    // must be done with a slot and a block before they are reused
+    uint64_t t0 = now_ns();
+    const int r = hsg_sdma_wait(c.handle);
+    j->add(kUploadWait, t0);
+    {
+      std::lock_guard<std::mutex> g(j->mu);
+      j->free_slots.push_back(c.slot);
+    }
+    j->cv.notify_all();
+    if (r != 0) j->fail(-EIO, c.item, "sdma upload");
+    Item& it = j->items[c.item];
+    if (it.chunks_left.fetch_sub(1) != 1 || j->err.load()) continue;
+    t0 = now_ns();
+    const int rc = launch_item(j, c.item, j->streams[j->launched++ & 1]);
+    j->add(kLaunch, t0);
+    std::lock_guard<std::mutex> g(j->mu);
+    if (rc == 0) j->retire.push_back(c.item);
+    j->cv.notify_all();
+  }
+  std::lock_guard<std::mutex> g(j->mu);
+  j->completion_done = true;
+  j->cv.notify_all();
+}
+
+void retire_thread(Job* j) {
+  (void)hipSetDevice(j->dev);
+  for (;;) {
+    int i;
+    {
+      std::unique_lock<std::mutex> lk(j->mu);
+      j->cv.wait(lk, [&] { return !j->retire.empty() || j->completion_done; });
+      if (j->retire.empty()) break;
+      i = j->retire.front();
+      j->retire.pop_front();
+    }
+    const uint64_t t0 = now_ns();
+    if (hipEventSynchronize(j->items[i].done) != hipSuccess) j->fail(-EIO, i, "device work");
+    j->add(kRetireWait, t0);
+    release_item(j, j->items[i]);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Start restoring `n` items.  Item i: read file bytes [file_lo[i], file_lo[i]
+// + nbytes[i]) of paths[i]; codec[i] 0 = raw bytes, 1 = a whole HSZ1 blob of
+// logical[i] logical bytes (decoded into direct[i] when nonzero, else into a
+// scratch block); then descriptors [desc_off[i], desc_off[i] + desc_n[i]) of
+// `descs` (CopyDesc rows whose `src` is an offset into the raw / decoded
+// bytes, relative to base_off[i]) copy the bytes into their destinations.
+// Device work is ordered after every stream in `producers`.  `err_words`:
+// host-mapped uint32 per item (decoders flag corrupt frames there).
+// Returns a handle for hsg_restore_wait, or null with *err set.
+void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t* file_lo,
+                        const uint64_t* nbytes, const int* codec, const uint64_t* logical,
+                        const uint64_t* direct, const uint64_t* base_off, const int64_t* desc_off,
+                        const int* desc_n, const void* descs, int64_t n_descs,
+                        const uint64_t* producers, int n_producers, uint32_t* err_words,
+                        uint64_t slot_bytes, uint64_t piece_bytes, int nslots, int nreaders,
+                        uint64_t budget, int* err) {
+  *err = 0;
+  if (hipSetDevice(dev) != hipSuccess) {
+    *err = -1;
+    return nullptr;
+  }
+  Job* j = new Job();
+  j->dev = dev;
+  j->slot_bytes = (std::max<uint64_t>(slot_bytes, 1 << 20) + 4095) / 4096 * 4096;
+  j->piece_bytes = std::min<uint64_t>(j->slot_bytes,
+                                      (std::max<uint64_t>(piece_bytes, 256 << 10) + 4095) / 4096 * 4096);
+  j->budget = std::max<uint64_t>(budget, kGranule);
+  j->desc_size = hsg_desc_size();
+  j->err_words = err_words;
+  j->descs.assign(static_cast<const uint8_t*>(descs),
+                  static_cast<const uint8_t*>(descs) + n_descs * int64_t(j->desc_size));
+  j->items = std::vector<Item>(n);
+  for (int i = 0; i < n; ++i) {
+    Item& it = j->items[i];
+    it.path = paths[i];
+    it.file_lo = file_lo[i];
+    it.nbytes = nbytes[i];
+    it.codec = codec[i];
+    it.logical = logical[i];
+    it.direct = direct[i];
+    it.base_off = base_off[i];
+    it.desc_off = desc_off[i];
+    it.desc_n = desc_n[i];
+    it.nchunks = chunks_of(j, it);
+    it.chunks_left.store(it.nchunks);
+    for (int c = 0; c < it.nchunks; ++c)
+      it.npieces += pieces_of(j, std::min(j->slot_bytes, it.nbytes - uint64_t(c) * j->slot_bytes));
+    if (desc_off[i] < 0 || desc_off[i] + desc_n[i] > n_descs || it.nchunks == 0 ||
+        (it.codec == kCodecHsz && it.nbytes < kHszHeader)) {
+      delete j;
+      *err = -3;
+      return nullptr;
+    }
+  }
+  // persistent streams (creating one costs ~1 ms of HIP runtime time)
+  for (int s = 0; s < 2; ++s) {
+    j->streams[s] = static_cast<hipStream_t>(hsg_copy_stream(dev, kRestoreSlot + s));
+    if (!j->streams[s]) {
+      delete j;
+      *err = -4;
+      return nullptr;
+    }
+  }
+  // the destinations' producers: their queued work finishes before ours
+  for (int p = 0; p < n_producers; ++p) {
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) continue;
+    if (hipEventRecord(ev, reinterpret_cast<hipStream_t>(producers[p])) == hipSuccess)
+      for (int s = 0; s < 2; ++s) (void)hipStreamWaitEvent(j->streams[s], ev, 0);
+    hipEventDestroy(ev);
+  }
+  nslots = std::max(nslots, 2);
+  j->fills.reset(new SlotFill[nslots]);
+  for (int s = 0; s < nslots; ++s) {
+    void* p = hsg_pinned_acquire(j->slot_bytes);
+    if (!p) {
+      for (void* q : j->slots) hsg_pinned_release(q);
+      delete j;
+      *err = -2;
+      return nullptr;
+    }
+    j->slots.push_back(p);
+    j->free_slots.push_back(s);
+  }
+  std::reverse(j->free_slots.begin(), j->free_slots.end());
+  j->t_start = now_ns();
+  nreaders = std::max(nreaders, 1);
+  j->readers_left = nreaders;
+  for (int r = 0; r < nreaders; ++r) j->threads.emplace_back(reader_thread, j);
+  j->threads.emplace_back(completion_thread, j);
+  j->threads.emplace_back(retire_thread, j);
+  return j;
+}
+
+// Wait for the restore (blocking; Python calls it without the GIL).  Returns
+// 0 or the first error (negative errno); *err_item = the item it concerns
+// (-1: none); `msg` (>= 320 bytes) its text; `stats` (kNumStats doubles:
+// seconds) where the time went; *bytes_read the bytes read from files.
+// Everything launched has finished when this returns (decode error words
+// are final).  Frees the job: call exactly once per handle.
+int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
+                     uint64_t* bytes_read) {
+  Job* j = static_cast<Job*>(handle);
+  for (auto& t : j->threads) t.join();
+  for (int s = 0; s < 2; ++s) {
+    if (hipStreamSynchronize(j->streams[s]) != hipSuccess) j->fail(-EIO, -1, "device work");
+  }
+  j->add(kWall, j->t_start);
+  for (auto& it : j->items) {
+    if (it.fd >= 0) close(it.fd);
+    if (it.block || it.scratch || it.ws || it.stage || it.done) release_item(j, it);
+  }
+  for (void* p : j->slots) hsg_pinned_release(p);
+  if (stats)
+    for (int k = 0; k < kNumStats; ++k) stats[k] = 1e-9 * double(j->ns[k].load());
+  if (bytes_read) *bytes_read = j->bytes_read.load();
+  const int e = j->err.load();
+  if (err_item) *err_item = j->err_item;
+  if (msg) snprintf(msg, 320, "%s", j->errmsg);
+  delete j;
+  return e;
+}
+
+// Free idle device blocks of the restore pools until at most `keep` idle
+// bytes remain in each (per call; -1 device = all).  Returns bytes freed.
+uint64_t hsg_restore_trim(int dev, uint64_t keep) {
+  return g_upload_pool.trim(dev, keep) + g_scratch_pool.trim(dev, keep);
+}
+
+}  // extern "C"

@@ -1,0 +1,204 @@
+"""Native restore of local-FS blobs whose bytes all land in HBM.
+
+``execute_read_reqs`` (engine/scheduler.py) hands every eligible read to ONE
+``native.NativeRestore`` job per device (csrc/hsrestore.hip): reader threads
+``pread`` the blobs from the page cache into pinned slots and queue their
+SDMA uploads back to back, the completion thread launches each blob's HSZ1
+decode and ONE region-copy kernel as soon as its bytes have landed -- no
+Python (and no GIL hand-over) per blob.  Eligible: a read from the FS plugin
+whose consumer exposes ``device_regions`` for all of its bytes (plain tensors,
+DTensor / ShardedTensor pieces, batched slabs of them) into non-managed HBM
+with casts the copy kernel does, stored raw or as an HSZ1 blob read (mostly)
+whole.  Everything else keeps the Python pipeline.
+
+The plan for a job -- destinations, descriptor tables with source offsets
+relative to the uploaded / decoded bytes -- is built here on the caller's
+thread; the descriptors' fast paths depend on the alignment of those offsets
+only (upload and decode blocks are 2 MiB aligned).
+
+Reference counterpart: `/root/reference/torchsnapshot/scheduler.py:384-444`
+(read pipeline) and `/root/reference/torchsnapshot/io_preparers/tensor.py:294-346`.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import time
+from collections import defaultdict
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from .. import knobs
+from ..io_types import ReadReq, StoragePlugin
+from ..ops import native
+from ..utils.tracing import timeline
+
+logger = logging.getLogger(__name__)
+
+last_stats: Dict[str, float] = {}  # the last job's phase seconds (NativeRestore.STATS)
+
+_RAW, _HSZ = 0, 1
+
+
+def _root(storage: StoragePlugin) -> Optional[str]:
+    fn = getattr(storage, "native_read_root", None)
+    return fn() if fn is not None else None
+
+
+def _regions(consumer) -> Optional[list]:
+    """Device regions covering every byte the consumer needs, or None."""
+    from ..io.batcher import BatchedBufferConsumer
+
+    if isinstance(consumer, BatchedBufferConsumer):
+        if consumer._other or not consumer._gpu:
+            return None
+        out = []
+        for _rng, _c, regions in consumer._gpu:
+            out.extend(regions)
+        return out
+    fn = getattr(consumer, "device_regions", None)
+    if fn is None or getattr(consumer, "_direct", False):
+        return None
+    return fn(0) or None
+
+
+def _producers(consumer) -> List[int]:
+    from ..io.batcher import BatchedBufferConsumer
+
+    cs = [c for _r, c, _g in consumer._gpu] if isinstance(consumer, BatchedBufferConsumer) \
+        else [consumer]
+    out = []
+    for c in cs:
+        p = getattr(c, "producer", None)
+        if p is not None:
+            out.append(int(p))
+    return out
+
+
+def _plan_one(rr: ReadReq, root: str, slot_bytes: int):
+    """(device, item tuple, producers) for ``NativeRestore``, or None."""
+    from ..ops import codec as hsz
+    from . import staging
+    from .scheduler import _expected_read_bytes
+
+    regions = _regions(rr.buffer_consumer)
+    if not regions:
+        return None
+    devs = set()
+    for src_dtype, _shape, _off, _nar, dst in regions:
+        if not dst.is_cuda or staging._is_managed(dst) or dst.dim() > native.MAX_DIMS \
+                or not native.can_cast_on_device(src_dtype, dst.dtype):
+            return None
+        devs.add(staging.device_of(dst))
+    if len(devs) != 1:
+        return None
+    dev = devs.pop()
+    path = os.path.join(root, rr.path)
+    if rr.codec is None:
+        n = _expected_read_bytes(rr)
+        if not n:
+            return None
+        lo = rr.byte_range[0] if rr.byte_range is not None else 0
+        codec, logical, base, direct = _RAW, n, 0, 0
+        file_lo, nbytes = lo, n
+    else:
+        info = rr.codec
+        if info.get("name", hsz.CODEC_NAME) != hsz.CODEC_NAME:
+            return None
+        logical = int(info["blob_bytes"])
+        lo, hi = rr.byte_range if rr.byte_range is not None else (0, logical)
+        nf = hsz.n_frames_for(logical, int(info["frame_bytes"]))
+        # the whole blob is read and decoded: not for a small part of it
+        if logical <= 0 or 2 * (hi - lo) < logical or hsz.payload_start(nf) > slot_bytes:
+            return None
+        try:
+            nbytes = os.path.getsize(path)
+        except OSError:
+            return None
+        codec, file_lo, base, direct = _HSZ, 0, lo, 0
+        if lo == 0 and hi == logical and len(regions) == 1:
+            src_dtype, src_shape, off, narrows, dst = regions[0]
+            whole = off == 0 and all(st == 0 and ln == int(src_shape[d])
+                                     for d, st, ln in (narrows or ()))
+            if (whole and dst.dtype == src_dtype and dst.is_contiguous()
+                    and dst.numel() * dst.element_size() == logical
+                    and dst.data_ptr() % 16 == 0):
+                direct = dst.data_ptr()
+    descs = np.zeros(0, dtype=native.COPY_DESC_DTYPE)
+    if not direct:
+        batch = native.CopyBatch()
+        for src_dtype, src_shape, off, narrows, dst in regions:
+            es = staging._elem_size(src_dtype)
+            shape = [int(z) for z in src_shape]
+            strides = staging._contig_strides(shape)
+            # source offset within the uploaded (raw) / decoded (HSZ1) bytes
+            ptr = base + off
+            if narrows:
+                for d, st, ln in narrows:
+                    ptr += st * strides[d] * es
+                    shape[d] = ln
+            batch.add(ptr, src_dtype, strides, dst.data_ptr(), dst.dtype, dst.stride(), shape, es)
+        descs = batch.pack()
+    item = (path, file_lo, nbytes, codec, logical, direct, 0, descs)
+    return dev, item, _producers(rr.buffer_consumer)
+
+
+def split(read_reqs: List[ReadReq], storage: StoragePlugin
+          ) -> Tuple[Dict[int, list], List[ReadReq]]:
+    """({device: [(read req, item)], ...} for native jobs, the Python part)."""
+    if not read_reqs or not knobs.native_restore_enabled() or _root(storage) is None \
+            or not native.gpu_available():
+        return {}, list(read_reqs)
+    root = _root(storage)
+    slot_bytes = knobs.get_restore_slot_bytes()
+    jobs: Dict[int, list] = defaultdict(list)
+    py: List[ReadReq] = []
+    t0 = time.perf_counter()
+    for rr in read_reqs:
+        got = _plan_one(rr, root, slot_bytes)
+        if got is None:
+            py.append(rr)
+        else:
+            jobs[got[0]].append((rr, got[1], got[2]))
+    timeline.add("native_restore_plan", "phase", t0, time.perf_counter(), n=len(read_reqs),
+                 native=sum(len(v) for v in jobs.values()))
+    return dict(jobs), py
+
+
+def run(jobs: Dict[int, list]) -> int:
+    """Run the planned jobs (blocking; call off the event loop); returns the
+    logical bytes restored.  Raises ``CorruptBlobError`` for rejected frames,
+    ``OSError`` / ``HipError`` for other failures."""
+    total = 0
+    for dev, entries in jobs.items():
+        t0 = time.perf_counter()
+        items = [e[1] for e in entries]
+        prods = sorted({p for e in entries for p in e[2]})
+        job = native.NativeRestore(dev, items, prods, knobs.get_restore_slot_bytes(),
+                                   knobs.get_restore_piece_bytes(), knobs.get_restore_slots(),
+                                   knobs.get_restore_readers(), knobs.get_restore_device_budget())
+        rc, item, msg = job.wait()
+        bad = job.corrupt_items()
+        native.restore_trim(dev, knobs.get_restore_keep_bytes())
+        nbytes = sum(it[4] for it in items)
+        timeline.add("native_restore", "io", t0, time.perf_counter(), n=len(items),
+                     bytes=job.bytes_read, logical=nbytes, **job.stats)
+        last_stats.clear()
+        last_stats.update(job.stats, items=len(items), bytes=job.bytes_read, logical=nbytes)
+        if bad:
+            raise native.CorruptBlobError(
+                "corrupt HSZ1 blob: the GPU decoder rejected a frame of "
+                + ", ".join(entries[i][0].path for i in bad[:4]))
+        if rc != 0:
+            where = entries[item][0].path if item is not None else ""
+            import errno
+
+            if rc == -errno.EBADMSG:
+                raise native.CorruptBlobError(f"corrupt HSZ1 blob {where}: {msg}")
+            if rc < 0 and -rc in errno.errorcode:
+                raise OSError(-rc, msg)
+            raise native.HipError(f"native restore failed ({rc}): {msg}")
+        total += nbytes
+    return total

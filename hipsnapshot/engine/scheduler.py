@@ -589,6 +589,35 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                             memory_budget_bytes: int, rank: int,
                             consume_threads: Optional[int] = None,
                             io_concurrency: Optional[int] = None) -> PipelineStats:
+    from . import native_restore
+
+    # reads whose bytes all land in HBM: one native job per device, beside
+    # the Python pipeline for the rest
+    native_jobs, read_reqs = native_restore.split(read_reqs, storage)
+    native_fut = None
+    if native_jobs:
+        native_fut = asyncio.get_running_loop().run_in_executor(
+            aux_pool(), native_restore.run, native_jobs)
+    try:
+        stats = await _execute_python_reads(read_reqs, storage, memory_budget_bytes, rank,
+                                            consume_threads, io_concurrency) \
+            if read_reqs or not native_jobs else PipelineStats()
+    finally:
+        if native_fut is not None:
+            # never leave the job running: it writes into the destinations
+            native_bytes = await asyncio.gather(native_fut, return_exceptions=True)
+    if native_fut is not None:
+        if isinstance(native_bytes[0], BaseException):
+            raise native_bytes[0]
+        stats.bytes_written += native_bytes[0]
+        stats.n_reqs += sum(len(v) for v in native_jobs.values())
+    return stats
+
+
+async def _execute_python_reads(read_reqs: List[ReadReq], storage: StoragePlugin,
+                                memory_budget_bytes: int, rank: int,
+                                consume_threads: Optional[int] = None,
+                                io_concurrency: Optional[int] = None) -> PipelineStats:
     consume_threads = consume_threads or knobs.get_stage_threads()
     io_concurrency = io_concurrency or knobs.get_io_threads()
     # reads are split across all I/O workers by the native engine, so a few

@@ -426,6 +426,48 @@ def plan_cache_enabled() -> bool:
     return _get_bool("PLAN_CACHE", True)
 
 
+def native_restore_enabled() -> bool:
+    """Reads whose bytes all land in HBM go through ONE native job per device
+    (engine/native_restore.py, csrc/hsrestore.hip): pread -> pinned slots ->
+    SDMA uploads -> GPU decode / region copy, no Python per blob."""
+    return _get_bool("NATIVE_RESTORE", True)
+
+
+def get_restore_slot_bytes() -> int:
+    """Pinned slot size of the native restore = the largest SDMA upload: 8
+    MiB uploads ran the link at 38 GB/s, 32 MiB at 45 (one request's fixed
+    cost is tens of microseconds; profiles/r4/restore_native/)."""
+    return max(1 << 20, _get_int("RESTORE_SLOT_BYTES", 32 << 20))
+
+
+def get_restore_piece_bytes() -> int:
+    """Bytes one reader ``pread``s at a time: several readers fill a slot."""
+    return max(256 << 10, _get_int("RESTORE_PIECE_BYTES", 4 << 20))
+
+
+def get_restore_slots() -> int:
+    return max(2, _get_int("RESTORE_SLOTS", 8))
+
+
+def get_restore_readers() -> int:
+    """pread threads of the native restore (page-cache copies of ~8 GB/s
+    each feed a 57 GB/s link): ``HIPSNAPSHOT_RESTORE_READERS``, else the I/O
+    thread count."""
+    v = _get("RESTORE_READERS")
+    return max(1, int(v)) if v is not None else max(4, min(12, get_io_threads()))
+
+
+def get_restore_device_budget() -> int:
+    """HBM the native restore's upload / decode blocks may hold at once."""
+    return max(4 << 20, _get_int("RESTORE_DEVICE_BUDGET", 4 << 30))
+
+
+def get_restore_keep_bytes() -> int:
+    """Idle restore blocks kept per pool after a restore (the next restore
+    of the same shapes then allocates nothing)."""
+    return max(0, _get_int("RESTORE_KEEP_BYTES", 1 << 30))
+
+
 def get_stage_threads() -> int:
     return _get_int("STAGE_THREADS", 4)
 

@@ -268,6 +268,17 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_void_p, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64), c_char_p,
                   ctypes.POINTER(ctypes.c_double)])
         _declare(lib, "hsg_drain_pending", c_int, [c_void_p])
+        P = ctypes.POINTER
+        _declare(lib, "hsg_restore_start", c_void_p,
+                 [c_int, c_int, P(c_char_p), P(c_uint64), P(c_uint64), P(c_int), P(c_uint64),
+                  P(c_uint64), P(c_uint64), P(c_int64), P(c_int), c_void_p, c_int64,
+                  P(c_uint64), c_int, c_void_p, c_uint64, c_uint64, c_int, c_int, c_uint64,
+                  P(c_int)])
+        _declare(lib, "hsg_restore_wait", c_int,
+                 [c_void_p, P(c_int), c_char_p, P(ctypes.c_double), P(c_uint64)])
+        _declare(lib, "hsg_restore_trim", c_uint64, [c_int, c_uint64])
+        _declare(lib, "hsg_sdma_h2d_submit", c_int,
+                 [c_int, c_void_p, c_void_p, c_uint64, P(c_uint64)])
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
         _declare(lib, "hsg_managed_location", c_int,
                  [c_void_p, c_uint64, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
@@ -836,6 +847,85 @@ class NativeDrain:
                 raise OSError(-r, text)
             raise HipError(f"native drain failed ({r}): {text}")
         return list(sums[: self.n]), int(written.value)
+
+
+class NativeRestore:
+    """``hsg_restore_start`` / ``hsg_restore_wait`` (csrc/hsrestore.hip):
+    file byte ranges (raw, or whole HSZ1 blobs) -> HBM destinations in
+    native threads: pread into pinned slots, SDMA uploads into uncached
+    blocks, GPU decode and ONE region-copy launch per item.
+
+    ``items``: (path, file_lo, nbytes, codec (0 raw / 1 hsz1), logical,
+    direct device address or 0, base_off, descriptor rows (packed
+    COPY_DESC_DTYPE array whose ``src`` are offsets)).  ``producers``:
+    stream handles the device work is ordered after."""
+
+    STATS = ("read", "slot_wait", "budget_wait", "alloc", "submit", "upload_wait", "launch",
+             "retire_wait", "first_upload", "wall")
+
+    def __init__(self, dev: int, items: Sequence[tuple], producers: Sequence[int],
+                 slot_bytes: int, piece_bytes: int, nslots: int, nreaders: int,
+                 budget: int) -> None:
+        import torch
+
+        lib = require_gpu_lib()
+        n = len(items)
+        self.n = n
+        m = max(n, 1)
+        self._paths = (c_char_p * m)(*[os.fsencode(it[0]) for it in items])
+        self._lo = (c_uint64 * m)(*[it[1] for it in items])
+        self._nb = (c_uint64 * m)(*[it[2] for it in items])
+        self._codec = (c_int * m)(*[it[3] for it in items])
+        self._logical = (c_uint64 * m)(*[it[4] for it in items])
+        self._direct = (c_uint64 * m)(*[it[5] for it in items])
+        self._base = (c_uint64 * m)(*[it[6] for it in items])
+        offs, counts, tables = [], [], []
+        k = 0
+        for it in items:
+            offs.append(k)
+            counts.append(len(it[7]))
+            k += len(it[7])
+            if len(it[7]):
+                tables.append(it[7])
+        self._doff = (c_int64 * m)(*offs)
+        self._dn = (c_int * m)(*counts)
+        self._descs = np.concatenate(tables) if tables else np.zeros(1, dtype=COPY_DESC_DTYPE)
+        self._prod = (c_uint64 * max(len(producers), 1))(*producers)
+        # one host-mapped word per item: the decoder flags corrupt frames there
+        self.err_words = torch.zeros(m, dtype=torch.int32, pin_memory=True)
+        err = c_int(0)
+        self._h = lib.hsg_restore_start(
+            dev, n, self._paths, self._lo, self._nb, self._codec, self._logical, self._direct,
+            self._base, self._doff, self._dn, self._descs.ctypes.data, k, self._prod,
+            len(producers), self.err_words.data_ptr(), slot_bytes, piece_bytes, nslots, nreaders,
+            budget, ctypes.byref(err))
+        if not self._h:
+            raise HipError(f"hsg_restore_start failed ({err.value})")
+
+    def wait(self) -> Tuple[int, Optional[int], str]:
+        """Blocks (GIL released) until every item is in place.  Returns (0 or
+        the first error (negative errno), the item it concerns, its text);
+        ``self.stats``: seconds per phase; ``self.bytes_read``."""
+        lib = require_gpu_lib()
+        item = c_int(-1)
+        msg = ctypes.create_string_buffer(320)
+        st = (ctypes.c_double * len(self.STATS))()
+        nread = c_uint64(0)
+        h, self._h = self._h, None
+        r = lib.hsg_restore_wait(h, ctypes.byref(item), msg, st, ctypes.byref(nread))
+        self.stats = {k: round(v, 5) for k, v in zip(self.STATS, st)}
+        self.bytes_read = int(nread.value)
+        return int(r), (int(item.value) if item.value >= 0 else None), \
+            msg.value.decode(errors="replace")
+
+    def corrupt_items(self) -> List[int]:
+        """Items whose frames the GPU decoder rejected (after ``wait``)."""
+        return [i for i in range(self.n) if int(self.err_words[i]) != 0]
+
+
+def restore_trim(dev: int, keep_bytes: int) -> int:
+    """Free idle restore device blocks beyond ``keep_bytes`` per pool."""
+    return int(require_gpu_lib().hsg_restore_trim(dev, keep_bytes))
 
 
 def managed_location(ptr: int, nbytes: int) -> Tuple[int, int]:

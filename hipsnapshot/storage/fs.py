@@ -107,6 +107,10 @@ class FSStoragePlugin(StoragePlugin):
         writes O_DIRECT or ``HIPSNAPSHOT_DRAIN_DIRECT_IO`` asks for it."""
         return self.root, self.fsync, self.direct_io or knobs.drain_direct_io()
 
+    def native_read_root(self) -> str:
+        """Root of the blobs for the native restore (engine/native_restore.py)."""
+        return self.root
+
     # -- StoragePlugin -------------------------------------------------------
 
     async def write(self, write_io: WriteIO) -> None:
