@@ -124,6 +124,7 @@ def main() -> None:
     times = []
     contended = []
     per_val = {v: [] for v in ab_vals}
+    cpu0 = _cpu_s()
     for _ in range(args.steps):
         for v in ab_vals:
             if ab_name:
@@ -142,15 +143,24 @@ def main() -> None:
                                           "mean": round(statistics.mean(t) * 1e3, 2)}
                                       for v, t in per_val.items()}}), flush=True)
         os.environ[ab_name] = ab_vals[0]
+    solo_cpu_s = (_cpu_s() - cpu0) / max(1, len(times))
+    stored = sum(os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(path)
+                 for f in fs if not f.startswith("."))
     sib_ms = []
+    sib_cpu = []
+    cont_cpu = []
     if sib is not None:
         for _ in range(args.steps):
             torch.cuda.synchronize()
             sib.go()
+            c0 = _cpu_s()
             t0 = time.perf_counter()
             take()
             contended.append(time.perf_counter() - t0)
-            sib_ms.append(max(sib.wait()) * 1e3)
+            cont_cpu.append(_cpu_s() - c0)
+            got = sib.wait()
+            sib_ms.append(max(g[0] for g in got) * 1e3)
+            sib_cpu.append(statistics.mean(g[1] for g in got))
         sib.stop()
     unblock, total = [], []
     for _ in range(args.async_iters):
@@ -163,6 +173,7 @@ def main() -> None:
     refs = {k: v._local_tensor.clone() for k, v in params.items()}
     rtimes = []
     r_per_val = {v: [] for v in ab_vals}
+    r_stats = {}
     for _ in range(args.restore_iters):
         for val in ab_vals:
             if ab_name:
@@ -175,12 +186,14 @@ def main() -> None:
             torch.cuda.synchronize()
             rtimes.append(time.perf_counter() - t0)
             r_per_val[val].append(rtimes[-1])
+            r_stats[val] = _native_restore_stats()
     if ab_name and args.restore_iters > 1:
         print(json.dumps({"bench": "rank_share_restore_ab", "world": args.world,
                           "knob": ab_name, "compression": args.compression,
                           "restore_ms": {v: {"median": round(statistics.median(t) * 1e3, 2),
                                              "min": round(min(t) * 1e3, 2)}
-                                         for v, t in r_per_val.items()}}), flush=True)
+                                         for v, t in r_per_val.items()},
+                          "native_restore_stats": r_stats}), flush=True)
         os.environ[ab_name] = ab_vals[0]
     ok = all(torch.equal(refs[k], app_state["model"][k]._local_tensor) for k in refs)
     med = statistics.median(times)
@@ -195,12 +208,21 @@ def main() -> None:
         "restore_ms_median": round(statistics.median(rtimes) * 1e3, 2),
         "restore_bitwise_ok": ok,
         "native_restore_stats": _native_restore_stats(),
+        # host CPU time (user + system, every thread of the process) per take
+        # and per stored GB; the kernel's page-cache writeback threads are
+        # not charged to the process
+        "stored_bytes": stored,
+        "take_cpu_s": round(solo_cpu_s, 4),
+        "take_cpu_s_per_stored_GB": round(solo_cpu_s / (stored / 1e9), 4) if stored else None,
         **({"host_siblings": args.host_siblings, "sibling_dma_pass": bool(args.sibling_dma_pass),
             "sibling_bytes_each": sum(sib.sizes),
             "contended_take_ms_median": round(statistics.median(contended) * 1e3, 2),
             "contended_take_ms_each": [round(t * 1e3, 1) for t in contended],
             "sibling_host_ms_median": round(statistics.median(sib_ms), 2),
             "contended_vs_solo": round(statistics.median(contended) / med, 3),
+            "contended_take_cpu_s_per_stored_GB": round(
+                statistics.median(cont_cpu) / (stored / 1e9), 4) if stored else None,
+            "sibling_cpu_s_per_GB": round(statistics.median(sib_cpu) / (sum(sib.sizes) / 1e9), 4),
             "contended_aggregate_GBps": round(
                 args.world * share / max(statistics.median(contended),
                                          statistics.median(sib_ms) / 1e3) / 1e9, 1)}
@@ -208,6 +230,13 @@ def main() -> None:
     }), flush=True)
     shutil.rmtree(root, ignore_errors=True)
     dist.destroy_process_group()
+
+
+def _cpu_s() -> float:
+    import resource
+
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    return ru.ru_utime + ru.ru_stime
 
 
 def _native_restore_stats() -> dict:
@@ -254,10 +283,11 @@ def _sibling_main(i: int, sizes, root: str, dma_pass: bool, go, done, hint: int)
 
     while go.get() is not None:
         t0 = time.perf_counter()
+        c0 = _cpu_s()
         if dma_pass:
             staging.fill(2)
         loop.run_until_complete(write_all())
-        done.put(time.perf_counter() - t0)
+        done.put((time.perf_counter() - t0, _cpu_s() - c0))
     fs.sync_close(loop)
     loop.close()
 

@@ -13,9 +13,10 @@
 // Ordering: the caller has synchronised the producer (the bytes are final);
 // before reading HBM the SDMA engine must see them at system scope, so a
 // hipEventReleaseToSystem event is recorded and waited on the copy stream
-// first (writes back dirty L2 lines).  Only the device -> host direction is
-// provided: the host -> device direction would need a system-scope acquire in
-// every consumer, which HIP cannot be told about.
+// first (writes back dirty L2 lines).  Host -> device copies (restores) go
+// only into uncached device memory, which no L2 line can shadow, so the
+// kernels that read them need no system-scope acquire (see the end of this
+// file).
 //
 // By default a copy is one request on the engine ROCr assigns; optionally it
 // is split into pieces over the engines ROCr reports as free for the GPU ->
@@ -52,6 +53,7 @@ struct DevInfo {
   hsa_agent_t gpu{0};
   hsa_agent_t cpu{0};
   uint32_t engines = 0;  // free SDMA engine mask for GPU -> CPU copies
+  uint32_t h2d_engines = 0;  // ... and for CPU -> GPU copies
   bool ok = false;
 };
 
@@ -140,6 +142,9 @@ DevInfo* dev_info(int dev) {
       uint32_t mask = 0;
       if (g_api.engine_status(d.cpu, d.gpu, &mask) != HSA_STATUS_SUCCESS) mask = 0;
       d.engines = mask;
+      mask = 0;
+      if (g_api.engine_status(d.gpu, d.cpu, &mask) != HSA_STATUS_SUCCESS) mask = 0;
+      d.h2d_engines = mask;
       d.ok = true;
       return &d;
     }
@@ -382,7 +387,22 @@ int hsg_sdma_h2d(int dev, void* dst, const void* src, uint64_t n) {
 // *handle naming its completion signal (pass it to hsg_sdma_wait exactly
 // once; `src` and `dst` stay valid until then).  The native restore keeps
 // several uploads queued so the link never idles between them.
+int hsg_sdma_h2d_submit_on(int dev, void* dst, const void* src, uint64_t n, int engine,
+                           uint64_t* handle);
+
 int hsg_sdma_h2d_submit(int dev, void* dst, const void* src, uint64_t n, uint64_t* handle) {
+  return hsg_sdma_h2d_submit_on(dev, dst, src, n, -1, handle);
+}
+
+// Free SDMA engines for host -> device copies of `dev` (bit mask).
+uint32_t hsg_sdma_h2d_engine_mask(int dev) {
+  DevInfo* d = dev_info(dev);
+  return d ? d->h2d_engines : 0;
+}
+
+// hsg_sdma_h2d_submit on SDMA engine `engine` (-1: the one ROCr picks).
+int hsg_sdma_h2d_submit_on(int dev, void* dst, const void* src, uint64_t n, int engine,
+                           uint64_t* handle) {
   *handle = 0;
   DevInfo* d = dev_info(dev);
   if (!d) return -1;
@@ -390,7 +410,11 @@ int hsg_sdma_h2d_submit(int dev, void* dst, const void* src, uint64_t n, uint64_
   hsa_signal_t s = take_signal();
   if (s.handle == 0) return -5;
   g_api.signal_store(s, 1);
-  const hsa_status_t st = g_api.async_copy(dst, d->gpu, src, d->cpu, n, 0, nullptr, s);
+  const hsa_status_t st =
+      engine >= 0 ? g_api.async_copy_on_engine(dst, d->gpu, src, d->cpu, n, 0, nullptr, s,
+                                               static_cast<hsa_amd_sdma_engine_id_t>(1u << engine),
+                                               true)
+                  : g_api.async_copy(dst, d->gpu, src, d->cpu, n, 0, nullptr, s);
   if (st != HSA_STATUS_SUCCESS) {
     give_signal(s);
     snprintf(g_err, sizeof(g_err), "hsa_amd_memory_async_copy (h2d): status 0x%x", unsigned(st));

@@ -43,6 +43,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -54,7 +55,9 @@
 #include <vector>
 
 extern "C" {
-int hsg_sdma_h2d_submit(int dev, void* dst, const void* src, uint64_t n, uint64_t* handle);
+int hsg_sdma_h2d_submit_on(int dev, void* dst, const void* src, uint64_t n, int engine,
+                           uint64_t* handle);
+uint32_t hsg_sdma_h2d_engine_mask(int dev);
 int hsg_sdma_wait(uint64_t handle);
 void* hsg_pinned_acquire(uint64_t nbytes);
 int hsg_pinned_release(void* p);
@@ -224,6 +227,7 @@ enum Stat {
   kLaunch,       // completion thread validating + launching device work
   kRetireWait,   // retire thread waiting for device work
   kFirstUpload,  // start -> first upload submitted
+  kUploadBusy,   // time with at least one upload in flight
   kWall,
   kNumStats
 };
@@ -232,6 +236,7 @@ struct Job {
   int dev = 0;
   uint64_t slot_bytes = 0;
   uint64_t budget = 0;
+  int engine = -1;  // SDMA engine of the uploads (-1: ROCr's choice)
   std::vector<Item> items;
   std::vector<uint8_t> descs;  // packed CopyDesc table (sources relative)
   uint64_t desc_size = 0;
@@ -253,6 +258,9 @@ struct Job {
   bool completion_done = false;
   uint64_t used = 0;  // device bytes charged
   int launched = 0;
+  uint64_t busy_since = 0;  // outstanding went non-zero at (kUploadBusy)
+  int outstanding = 0;      // uploads submitted and not yet waited for
+  int debug = 0;  // HIPSNAPSHOT_RESTORE_DEBUG: 1 = no preads, 2 = no uploads (timing probes)
 
   std::atomic<int> err{0};
   int err_item = -1;
@@ -385,6 +393,7 @@ void reader_thread(Job* j) {
     uint64_t t0 = now_ns();
     uint64_t done = 0;
     int rerr = 0;
+    if (j->debug & 1) done = pn;
     while (done < pn) {
       const ssize_t r = pread(it.fd, p + done, pn - done, off_t(it.file_lo + f.off + poff + done));
       if (r < 0) {
@@ -423,7 +432,9 @@ void reader_thread(Job* j) {
     }
     t0 = now_ns();
     uint64_t h = 0;
-    const int r = hsg_sdma_h2d_submit(j->dev, static_cast<char*>(it.block) + f.off, sp, f.n, &h);
+    const int r = (j->debug & 2) ? 0
+                  : hsg_sdma_h2d_submit_on(j->dev, static_cast<char*>(it.block) + f.off, sp,
+                                           f.n, j->engine, &h);
     if (!j->first_upload.exchange(true)) j->ns[kFirstUpload].store(now_ns() - j->t_start);
     j->add(kSubmit, t0);
     if (r != 0) {
@@ -432,6 +443,7 @@ void reader_thread(Job* j) {
     }
     {
       std::lock_guard<std::mutex> g(j->mu);
+      if (j->outstanding++ == 0) j->busy_since = now_ns();
       j->inflight.push_back(Chunk{i, f.chunk, f.off, f.n, s, h});
     }
     j->cv.notify_all();
@@ -564,6 +576,7 @@ void completion_thread(Job* j) {
     {
       std::lock_guard<std::mutex> g(j->mu);
       j->free_slots.push_back(c.slot);
+      if (--j->outstanding == 0) j->ns[kUploadBusy].fetch_add(now_ns() - j->busy_since);
     }
     j->cv.notify_all();
     if (r != 0) j->fail(-EIO, c.item, "sdma upload");
@@ -618,7 +631,7 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
                         const int* desc_n, const void* descs, int64_t n_descs,
                         const uint64_t* producers, int n_producers, uint32_t* err_words,
                         uint64_t slot_bytes, uint64_t piece_bytes, int nslots, int nreaders,
-                        uint64_t budget, int* err) {
+                        uint64_t budget, int engine, int* err) {
   *err = 0;
   if (hipSetDevice(dev) != hipSuccess) {
     *err = -1;
@@ -630,6 +643,11 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   j->piece_bytes = std::min<uint64_t>(j->slot_bytes,
                                       (std::max<uint64_t>(piece_bytes, 256 << 10) + 4095) / 4096 * 4096);
   j->budget = std::max<uint64_t>(budget, kGranule);
+  // engine -2: the lowest free host -> device engine; >= 0 as given if free
+  const uint32_t emask = hsg_sdma_h2d_engine_mask(dev);
+  if (engine == -2) engine = emask ? __builtin_ctz(emask) : -1;
+  j->engine = (engine >= 0 && engine < 32 && (emask & (1u << engine))) ? engine : -1;
+  if (const char* dbg = getenv("HIPSNAPSHOT_RESTORE_DEBUG")) j->debug = atoi(dbg);
   j->desc_size = hsg_desc_size();
   j->err_words = err_words;
   j->descs.assign(static_cast<const uint8_t*>(descs),

@@ -178,7 +178,8 @@ def run(jobs: Dict[int, list]) -> int:
         prods = sorted({p for e in entries for p in e[2]})
         job = native.NativeRestore(dev, items, prods, knobs.get_restore_slot_bytes(),
                                    knobs.get_restore_piece_bytes(), knobs.get_restore_slots(),
-                                   knobs.get_restore_readers(), knobs.get_restore_device_budget())
+                                   knobs.get_restore_readers(), knobs.get_restore_device_budget(),
+                                   knobs.get_restore_sdma_engine())
         rc, item, msg = job.wait()
         bad = job.corrupt_items()
         native.restore_trim(dev, knobs.get_restore_keep_bytes())

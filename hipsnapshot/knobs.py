@@ -445,6 +445,13 @@ def get_restore_piece_bytes() -> int:
     return max(256 << 10, _get_int("RESTORE_PIECE_BYTES", 4 << 20))
 
 
+def get_restore_sdma_engine() -> int:
+    """SDMA engine of the native restore's uploads: -1 = the one ROCr picks
+    per request, -2 = the lowest engine ROCr reports free for host -> device
+    copies, k = engine k (when free)."""
+    return _get_int("RESTORE_SDMA_ENGINE", -1)
+
+
 def get_restore_slots() -> int:
     return max(2, _get_int("RESTORE_SLOTS", 8))
 
