@@ -588,12 +588,16 @@ def _expected_read_bytes(rr: ReadReq) -> Optional[int]:
 async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                             memory_budget_bytes: int, rank: int,
                             consume_threads: Optional[int] = None,
-                            io_concurrency: Optional[int] = None) -> PipelineStats:
+                            io_concurrency: Optional[int] = None,
+                            native_jobs: Optional[dict] = None) -> PipelineStats:
+    """Run ``read_reqs``.  Reads whose bytes all land in HBM go to one native
+    job per device (engine/native_restore.py) beside the Python pipeline for
+    the rest; ``native_jobs``: a split the caller already made
+    (``native_restore.split``), ``read_reqs`` then being the Python part."""
     from . import native_restore
 
-    # reads whose bytes all land in HBM: one native job per device, beside
-    # the Python pipeline for the rest
-    native_jobs, read_reqs = native_restore.split(read_reqs, storage)
+    if native_jobs is None:
+        native_jobs, read_reqs = native_restore.split(read_reqs, storage)
     native_fut = None
     if native_jobs:
         native_fut = asyncio.get_running_loop().run_in_executor(
@@ -817,9 +821,11 @@ def order_reads_for_pipeline(read_reqs: List[ReadReq], lead_min_bytes: int = 1 <
 
 def sync_execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                            memory_budget_bytes: int, rank: int,
-                           event_loop: asyncio.AbstractEventLoop) -> PipelineStats:
+                           event_loop: asyncio.AbstractEventLoop,
+                           native_jobs: Optional[dict] = None) -> PipelineStats:
     return run_sync(event_loop,
-        execute_read_reqs(read_reqs, storage, memory_budget_bytes, rank))
+        execute_read_reqs(read_reqs, storage, memory_budget_bytes, rank,
+                          native_jobs=native_jobs))
 
 
 def hostname() -> str:

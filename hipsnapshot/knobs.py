@@ -433,6 +433,12 @@ def native_restore_enabled() -> bool:
     return _get_bool("NATIVE_RESTORE", True)
 
 
+def restore_plan_cache_enabled() -> bool:
+    """A restore of the same snapshot into the same device tensors reuses the
+    previous restore's native plan (engine/restore_cache.py)."""
+    return _get_bool("RESTORE_PLAN_CACHE", True)
+
+
 def get_restore_slot_bytes() -> int:
     """Pinned slot size of the native restore = the largest SDMA upload: 8
     MiB uploads ran the link at 38 GB/s, 32 MiB at 45 (one request's fixed

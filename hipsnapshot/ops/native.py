@@ -892,7 +892,8 @@ class NativeRestore:
         self._descs = np.concatenate(tables) if tables else np.zeros(1, dtype=COPY_DESC_DTYPE)
         self._prod = (c_uint64 * max(len(producers), 1))(*producers)
         # one host-mapped word per item: the decoder flags corrupt frames there
-        self.err_words = torch.zeros(m, dtype=torch.int32, pin_memory=True)
+        # (pinned arrays are reused: a hipHostMalloc per restore costs ~1 ms)
+        self.err_words = _take_err_words(m)
         err = c_int(0)
         self._h = lib.hsg_restore_start(
             dev, n, self._paths, self._lo, self._nb, self._codec, self._logical, self._direct,
@@ -919,8 +920,35 @@ class NativeRestore:
             msg.value.decode(errors="replace")
 
     def corrupt_items(self) -> List[int]:
-        """Items whose frames the GPU decoder rejected (after ``wait``)."""
-        return [i for i in range(self.n) if int(self.err_words[i]) != 0]
+        """Items whose frames the GPU decoder rejected (after ``wait``); gives
+        the error words back."""
+        w = self.err_words
+        if w is None:
+            return []
+        bad = torch.nonzero(w[: self.n]).flatten().tolist() if self.n else []
+        self.err_words = None
+        _give_err_words(w)
+        return bad
+
+
+_err_words_lock = threading.Lock()
+_err_words_free: List[torch.Tensor] = []
+
+
+def _take_err_words(n: int) -> torch.Tensor:
+    with _err_words_lock:
+        for i, t in enumerate(_err_words_free):
+            if t.numel() >= n:
+                _err_words_free.pop(i)
+                t.zero_()
+                return t
+    return torch.zeros(max(n, 1024), dtype=torch.int32, pin_memory=True)
+
+
+def _give_err_words(t: torch.Tensor) -> None:
+    with _err_words_lock:
+        if len(_err_words_free) < 8:
+            _err_words_free.append(t)
 
 
 def restore_trim(dev: int, keep_bytes: int) -> int:

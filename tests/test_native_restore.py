@@ -167,3 +167,41 @@ def test_native_restore_device_budget_smaller_than_items(gpu, tmp_path):
     torch.cuda.synchronize()
     assert native_restore.last_stats.get("items", 0) == 6
     _eq(dst, src)
+
+
+def test_restore_plan_cache_hits_and_invalidates(gpu, tmp_path):
+    """A second restore of the same snapshot into the same tensors reuses the
+    native plan; a new take at the path, or a replaced tensor, plans again."""
+    from hipsnapshot.engine import restore_cache
+
+    restore_cache.clear()
+    g = torch.Generator(device=gpu).manual_seed(2)
+    sd = StateDict(a=(torch.randn(1 << 20, device=gpu, generator=g) * 0.02).to(torch.bfloat16),
+                   b=torch.randn(300, 7, device=gpu, generator=g))
+    path = str(tmp_path / "p")
+    Snapshot.take(path, {"sd": sd}, compression="hsz1")
+    want = {k: v.clone() for k, v in sd.items()}
+    h0 = dict(restore_cache.stats)
+    for _ in range(3):
+        for v in sd.values():
+            v.zero_()
+        Snapshot(path).restore({"sd": sd})
+        _eq(sd, want)
+    assert restore_cache.stats["stores"] == h0["stores"] + 1
+    assert restore_cache.stats["hits"] == h0["hits"] + 2
+    # a new take at the same path: new metadata identity -> a new plan
+    sd["a"].add_(1)
+    Snapshot.take(path, {"sd": sd}, compression="hsz1")
+    want = {k: v.clone() for k, v in sd.items()}
+    for v in sd.values():
+        v.zero_()
+    Snapshot(path).restore({"sd": sd})
+    _eq(sd, want)
+    assert restore_cache.stats["stores"] == h0["stores"] + 2
+    # a replaced leaf: no hit
+    hits = restore_cache.stats["hits"]
+    sd["b"] = torch.zeros(300, 7, device=gpu)
+    Snapshot(path).restore({"sd": sd})
+    _eq(sd, want)
+    assert restore_cache.stats["hits"] == hits
+    restore_cache.clear()
