@@ -441,6 +441,7 @@ def main() -> None:
     restore_ok = None
     restore_gbps = None
     restore_each = None
+    restore_info = {}
     gc_restore_ms = None
     if not args.no_restore_check:
         # bitwise restore check of EVERY local shard (HBM holds the copies)
@@ -448,6 +449,9 @@ def main() -> None:
         refs = [p._local_tensor.clone() for _, p in named]
         times, bad = [], []
         gc_restore_ms = 0.0
+        from hipsnapshot.engine import native_restore, restore_cache
+
+        rc0 = dict(restore_cache.stats)
         for _ in range(max(1, args.restore_iters)):
             for _, p in named:
                 p._local_tensor.zero_()
@@ -474,8 +478,14 @@ def main() -> None:
         restore_gbps = total_bytes / restore_s / 1e9
         del refs
         restore_each = [round(total_bytes / t / 1e9, 2) for t in times]
+        # the first restore plans from scratch, later ones of the same
+        # snapshot into the same tensors reuse its plan (engine/restore_cache.py)
+        restore_info = {"restore_cold_GBps": restore_each[0],
+                        "restore_plan_cache": {k: restore_cache.stats[k] - rc0.get(k, 0)
+                                               for k in ("hits", "misses", "stores")},
+                        "native_restore_stats": dict(native_restore.last_stats)}
         log(f"restore: {restore_s:.3f}s ({restore_gbps:.2f} GB/s) ok={restore_ok} "
-            f"each {restore_each} GB/s")
+            f"each {restore_each} GB/s; {restore_info}")
 
     # BASELINE config 3: the N-rank FSDP checkpoint restored into N/2 ranks
     elastic = {}
@@ -731,7 +741,7 @@ def main() -> None:
             "async_total_ms": round(statistics.median(drain), 2) if drain else None,
             "restore_bitwise_ok": restore_ok,
             "restore_GBps": round(restore_gbps, 2) if restore_gbps else None,
-            "restore_GBps_each": restore_each,
+            "restore_GBps_each": restore_each, **restore_info,
             "compression": args.compression,
             "stored_bytes": stored,
             # rank 0's Python cyclic-GC time inside the timed takes / restores

@@ -61,6 +61,21 @@ def _cgroup_cpu() -> dict:
     return out
 
 
+def _cpu_khz():
+    """Current clock (kHz) of the CPU this thread last ran on (cpufreq), or
+    None: a launch-bound step is as fast as that core's clock."""
+    from hipsnapshot.utils.affinity import current_cpu
+
+    cpu = current_cpu()
+    if cpu is None:
+        return None
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{cpu}/cpufreq/scaling_cur_freq") as f:
+            return int(f.read())
+    except (OSError, ValueError):
+        return None
+
+
 def _local(t):
     return t._local_tensor if hasattr(t, "_local_tensor") else t
 
@@ -121,12 +136,18 @@ def main() -> None:
 
     from hipsnapshot.utils.tracing import timeline
 
+    freq_log = []  # (step end time, kHz of the CPU the trainer thread ran on)
+
     def step() -> float:
         t0 = time.perf_counter()
         try:
             return _step(t0)
         finally:
-            timeline.add("train_step", "train", t0, time.perf_counter())
+            t1 = time.perf_counter()
+            timeline.add("train_step", "train", t0, t1)
+            f = _cpu_khz()
+            if f is not None:
+                freq_log.append((t1, f))
 
     def _step(t0: float) -> float:
         tok = torch.randint(0, cfg.vocab_size, (args.batch, args.seq + 1), device=dev,
@@ -221,6 +242,7 @@ def main() -> None:
         return bool(f.item())
 
     gap = []  # steps between checkpoints (no drain running)
+    ck_starts = []
     from hipsnapshot.utils.tracing import GcWatch
 
     gcw = GcWatch().start()
@@ -246,6 +268,7 @@ def main() -> None:
                 torch.cuda.current_stream(dev).synchronize() if dev.type == "cuda" else None
                 clone_s = time.perf_counter() - tc
             t_ck = time.perf_counter()
+            ck_starts.append(t_ck)
             pending = Snapshot.async_take(f"{root}/async", app, storage_options=opts,
                                           compression=args.compression)
             unblocks.append(time.perf_counter() - t_ck)
@@ -255,6 +278,11 @@ def main() -> None:
         during.append(step())
         during_k[-1].append(during[-1])
     drain = statistics.mean(drains)
+    windows = [(t, t + d) for t, d in zip(ck_starts, drains)]
+    f_in = [f for t, f in freq_log if any(a <= t <= b for a, b in windows)]
+    f_out = [f for t, f in freq_log if not any(a <= t <= b for a, b in windows)]
+    freq = {"trainer_cpu_MHz_during_drain": round(statistics.median(f_in) / 1e3) if f_in else None,
+            "trainer_cpu_MHz_otherwise": round(statistics.median(f_out) / 1e3) if f_out else None}
     unblock = statistics.median(unblocks)
     # training time lost to the checkpoints: wall time from the first
     # async_take call through a window of at least --window-steps steps (the
@@ -325,7 +353,7 @@ def main() -> None:
           "baseline_step_ms": round(base_ms, 2), "baseline_step_ms_pre": round(base_pre_ms, 2),
           "baseline_step_ms_post": round(base_post_ms, 2),
           "async_unblock_gc_ms_each": [round(g, 1) for g in unblock_gc],
-          "gc_ms_in_window": round(gc_window_ms, 1), "cgroup_cpu_in_window": cgroup, "sync_take_s": round(sync_s, 3),
+          "gc_ms_in_window": round(gc_window_ms, 1), **freq, "cgroup_cpu_in_window": cgroup, "sync_take_s": round(sync_s, 3),
           "sync_take_GBps": round(ckpt_bytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 2), "async_drain_s": round(drain, 3),
           "cold_async_unblock_ms": [round(c[0] * 1e3, 1) for c in cold],

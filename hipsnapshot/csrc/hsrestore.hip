@@ -252,8 +252,17 @@ struct Job {
   std::vector<int> free_slots;
   std::deque<Chunk> inflight;
   std::deque<int> retire;
-  int cursor_item = 0;
-  int cursor_chunk = 0;
+  // upload units in plan order: the job's first is small (the link starts
+  // early), the rest up to slot bytes (few, large SDMA requests: each costs a
+  // fixed ~0.1 ms on the engine, profiles/r4/restore_native/)
+  struct Span {
+    int item;
+    int index;
+    uint64_t off;
+    uint64_t n;
+  };
+  std::vector<Span> spans;
+  size_t cursor = 0;
   int readers_left = 0;
   bool completion_done = false;
   uint64_t used = 0;  // device bytes charged
@@ -286,9 +295,6 @@ struct Job {
   }
 };
 
-int chunks_of(const Job* j, const Item& it) {
-  return it.nbytes ? int((it.nbytes + j->slot_bytes - 1) / j->slot_bytes) : 0;
-}
 
 // Device blocks of item i (upload target, decode scratch); waits for budget.
 bool ensure_blocks(Job* j, int i) {
@@ -323,7 +329,6 @@ int pieces_of(const Job* j, uint64_t n) { return int((n + j->piece_bytes - 1) / 
 
 void reader_thread(Job* j) {
   (void)hipSetDevice(j->dev);
-  const int nitems = int(j->items.size());
   for (;;) {
     int s, i;
     uint64_t poff, pn;
@@ -337,12 +342,7 @@ void reader_thread(Job* j) {
         }
         if (j->filling >= 0 && j->fills[j->filling].next_piece < j->fills[j->filling].pieces)
           break;
-        while (j->cursor_item < nitems &&
-               j->cursor_chunk >= j->items[j->cursor_item].nchunks) {
-          ++j->cursor_item;
-          j->cursor_chunk = 0;
-        }
-        if (j->cursor_item >= nitems) {
+        if (j->cursor >= j->spans.size()) {
           finished = true;
           break;
         }
@@ -352,15 +352,15 @@ void reader_thread(Job* j) {
           j->add(kSlotWait, t0);
           continue;
         }
-        // start filling a free slot with the plan's next range
+        // start filling a free slot with the plan's next span
         const int fs = j->free_slots.back();
         j->free_slots.pop_back();
-        Item& ci = j->items[j->cursor_item];
+        const Job::Span& sp = j->spans[j->cursor++];
         SlotFill& f = j->fills[fs];
-        f.item = j->cursor_item;
-        f.chunk = j->cursor_chunk++;
-        f.off = uint64_t(f.chunk) * j->slot_bytes;
-        f.n = std::min(j->slot_bytes, ci.nbytes - f.off);
+        f.item = sp.item;
+        f.chunk = sp.index;
+        f.off = sp.off;
+        f.n = sp.n;
         f.pieces = pieces_of(j, f.n);
         f.next_piece = 0;
         f.left.store(f.pieces);
@@ -630,8 +630,8 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
                         const uint64_t* direct, const uint64_t* base_off, const int64_t* desc_off,
                         const int* desc_n, const void* descs, int64_t n_descs,
                         const uint64_t* producers, int n_producers, uint32_t* err_words,
-                        uint64_t slot_bytes, uint64_t piece_bytes, int nslots, int nreaders,
-                        uint64_t budget, int engine, int* err) {
+                        uint64_t slot_bytes, uint64_t first_bytes, uint64_t piece_bytes,
+                        int nslots, int nreaders, uint64_t budget, int engine, int* err) {
   *err = 0;
   if (hipSetDevice(dev) != hipSuccess) {
     *err = -1;
@@ -640,6 +640,7 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   Job* j = new Job();
   j->dev = dev;
   j->slot_bytes = (std::max<uint64_t>(slot_bytes, 1 << 20) + 4095) / 4096 * 4096;
+  first_bytes = std::max<uint64_t>(first_bytes, 1 << 20);
   j->piece_bytes = std::min<uint64_t>(j->slot_bytes,
                                       (std::max<uint64_t>(piece_bytes, 256 << 10) + 4095) / 4096 * 4096);
   j->budget = std::max<uint64_t>(budget, kGranule);
@@ -664,10 +665,14 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
     it.base_off = base_off[i];
     it.desc_off = desc_off[i];
     it.desc_n = desc_n[i];
-    it.nchunks = chunks_of(j, it);
+    for (uint64_t off = 0; off < it.nbytes;) {
+      const uint64_t cap = j->spans.empty() ? std::min(j->slot_bytes, first_bytes) : j->slot_bytes;
+      const uint64_t n = std::min(cap, it.nbytes - off);
+      j->spans.push_back(Job::Span{i, it.nchunks++, off, n});
+      it.npieces += pieces_of(j, n);
+      off += n;
+    }
     it.chunks_left.store(it.nchunks);
-    for (int c = 0; c < it.nchunks; ++c)
-      it.npieces += pieces_of(j, std::min(j->slot_bytes, it.nbytes - uint64_t(c) * j->slot_bytes));
     if (desc_off[i] < 0 || desc_off[i] + desc_n[i] > n_descs || it.nchunks == 0 ||
         (it.codec == kCodecHsz && it.nbytes < kHszHeader)) {
       delete j;

@@ -152,7 +152,8 @@ def split(read_reqs: List[ReadReq], storage: StoragePlugin
             or not native.gpu_available():
         return {}, list(read_reqs)
     root = _root(storage)
-    slot_bytes = knobs.get_restore_slot_bytes()
+    # an HSZ1 blob's header and frame table must fit its first upload span
+    slot_bytes = min(knobs.get_restore_slot_bytes(), knobs.get_restore_first_bytes())
     jobs: Dict[int, list] = defaultdict(list)
     py: List[ReadReq] = []
     t0 = time.perf_counter()
@@ -179,7 +180,8 @@ def run(jobs: Dict[int, list]) -> int:
         job = native.NativeRestore(dev, items, prods, knobs.get_restore_slot_bytes(),
                                    knobs.get_restore_piece_bytes(), knobs.get_restore_slots(),
                                    knobs.get_restore_readers(), knobs.get_restore_device_budget(),
-                                   knobs.get_restore_sdma_engine())
+                                   knobs.get_restore_sdma_engine(),
+                                   knobs.get_restore_first_bytes())
         rc, item, msg = job.wait()
         bad = job.corrupt_items()
         native.restore_trim(dev, knobs.get_restore_keep_bytes())

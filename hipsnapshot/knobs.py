@@ -441,9 +441,15 @@ def restore_plan_cache_enabled() -> bool:
 
 def get_restore_slot_bytes() -> int:
     """Pinned slot size of the native restore = the largest SDMA upload: 8
-    MiB uploads ran the link at 38 GB/s, 32 MiB at 45 (one request's fixed
-    cost is tens of microseconds; profiles/r4/restore_native/)."""
-    return max(1 << 20, _get_int("RESTORE_SLOT_BYTES", 32 << 20))
+    MiB uploads ran the link at 38 GB/s, 32 MiB at 45; a request costs the
+    engine a fixed ~0.1 ms (profiles/r4/restore_native/)."""
+    return max(1 << 20, _get_int("RESTORE_SLOT_BYTES", 128 << 20))
+
+
+def get_restore_first_bytes() -> int:
+    """The job's first upload is at most this large: the link starts once it
+    is read, not once a whole slot is."""
+    return max(1 << 20, _get_int("RESTORE_FIRST_BYTES", 16 << 20))
 
 
 def get_restore_piece_bytes() -> int:
@@ -459,7 +465,7 @@ def get_restore_sdma_engine() -> int:
 
 
 def get_restore_slots() -> int:
-    return max(2, _get_int("RESTORE_SLOTS", 8))
+    return max(2, _get_int("RESTORE_SLOTS", 6))
 
 
 def get_restore_readers() -> int:

@@ -272,8 +272,8 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_restore_start", c_void_p,
                  [c_int, c_int, P(c_char_p), P(c_uint64), P(c_uint64), P(c_int), P(c_uint64),
                   P(c_uint64), P(c_uint64), P(c_int64), P(c_int), c_void_p, c_int64,
-                  P(c_uint64), c_int, c_void_p, c_uint64, c_uint64, c_int, c_int, c_uint64,
-                  c_int, P(c_int)])
+                  P(c_uint64), c_int, c_void_p, c_uint64, c_uint64, c_uint64, c_int, c_int,
+                  c_uint64, c_int, P(c_int)])
         _declare(lib, "hsg_restore_wait", c_int,
                  [c_void_p, P(c_int), c_char_p, P(ctypes.c_double), P(c_uint64)])
         _declare(lib, "hsg_restore_trim", c_uint64, [c_int, c_uint64])
@@ -865,7 +865,7 @@ class NativeRestore:
 
     def __init__(self, dev: int, items: Sequence[tuple], producers: Sequence[int],
                  slot_bytes: int, piece_bytes: int, nslots: int, nreaders: int,
-                 budget: int, engine: int = -1) -> None:
+                 budget: int, engine: int = -1, first_bytes: int = 16 << 20) -> None:
         import torch
 
         lib = require_gpu_lib()
@@ -898,8 +898,8 @@ class NativeRestore:
         self._h = lib.hsg_restore_start(
             dev, n, self._paths, self._lo, self._nb, self._codec, self._logical, self._direct,
             self._base, self._doff, self._dn, self._descs.ctypes.data, k, self._prod,
-            len(producers), self.err_words.data_ptr(), slot_bytes, piece_bytes, nslots, nreaders,
-            budget, engine, ctypes.byref(err))
+            len(producers), self.err_words.data_ptr(), slot_bytes, first_bytes, piece_bytes,
+            nslots, nreaders, budget, engine, ctypes.byref(err))
         if not self._h:
             raise HipError(f"hsg_restore_start failed ({err.value})")
 
