@@ -692,7 +692,7 @@ class Snapshot:
             if own is not None and len(objs) == len(own) and \
                     all(objs.get(k) is v for k, v in own.items()) and \
                     _inplace_load_noop(stateful):
-                if not py_reads and not containers:
+                if not py_reads:
                     restore_cache.store(cache_key, stateful, native_jobs, own)
                 return
             state_dict = inflate(containers, objs, prefix=key)
