@@ -57,6 +57,9 @@ def main() -> None:
                     help="K host-only processes replaying sibling ranks' host work per take")
     ap.add_argument("--sibling-dma-pass", type=int, default=1,
                     help="siblings write their staging memory once per take (DMA stand-in)")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="leave the process unbound (a real rank binds to its GPU's NUMA "
+                         "node, as bench.py does)")
     ap.add_argument("--switch-interval", type=float, default=None,
                     help="sys.setswitchinterval for the run (GIL hand-over latency)")
     args = ap.parse_args()
@@ -76,6 +79,11 @@ def main() -> None:
     os.environ.update(RANK="0", WORLD_SIZE="1")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    numa = None
+    if not args.no_numa_bind:
+        from hipsnapshot.utils.affinity import bind_to_gpu_numa
+
+        numa = bind_to_gpu_numa(0)
     dist.init_process_group("nccl", device_id=dev)
     mesh = init_device_mesh("cuda", (1,))
     cfg = getattr(LlamaConfig, args.model)()
@@ -208,6 +216,7 @@ def main() -> None:
         "restore_ms_median": round(statistics.median(rtimes) * 1e3, 2),
         "restore_bitwise_ok": ok,
         "native_restore_stats": _native_restore_stats(),
+        "numa_bind": numa,
         # host CPU time (user + system, every thread of the process) per take
         # and per stored GB; the kernel's page-cache writeback threads are
         # not charged to the process

@@ -67,11 +67,13 @@ def split(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[List[WriteReq],
 def _run(dev: int, wrs: List[WriteReq], blobs, fsync: bool, want_sums: bool, direct: bool):
     """One device's drain in this process's native threads.  Returns (hs64
     partial sums, bytes written, stats, "in_process")."""
-    from ..utils.affinity import threads_avoiding_caller
+    from ..utils.affinity import drain_thread_mask, threads_with_mask
 
     args = (knobs.get_drain_slot_bytes(), knobs.get_drain_slots(), knobs.get_drain_writers())
     # the drain's threads inherit a mask without the training thread's core
-    with threads_avoiding_caller(knobs.drain_avoid_caller_core()):
+    # (or L3 domain), on the GPU's NUMA node when that leaves enough CPUs
+    with threads_with_mask(drain_thread_mask(dev, knobs.drain_avoid_caller_core(),
+                                             knobs.native_io_numa_local())):
         job = native.NativeDrain(dev, blobs, *args, fsync, want_sums, knobs.get_hash_grid(),
                                  knobs.get_drain_nice(), direct, knobs.drain_hash_high_priority())
     partial, written = job.wait()

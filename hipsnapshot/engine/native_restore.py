@@ -177,11 +177,17 @@ def run(jobs: Dict[int, list]) -> int:
         t0 = time.perf_counter()
         items = [e[1] for e in entries]
         prods = sorted({p for e in entries for p in e[2]})
-        job = native.NativeRestore(dev, items, prods, knobs.get_restore_slot_bytes(),
-                                   knobs.get_restore_piece_bytes(), knobs.get_restore_slots(),
-                                   knobs.get_restore_readers(), knobs.get_restore_device_budget(),
-                                   knobs.get_restore_sdma_engine(),
-                                   knobs.get_restore_first_bytes())
+        from ..utils.affinity import gpu_node_mask, threads_with_mask
+
+        # readers (and the pinned slots they fill) on the GPU's NUMA node
+        mask = gpu_node_mask(dev) if knobs.native_io_numa_local() else None
+        with threads_with_mask(mask):
+            job = native.NativeRestore(dev, items, prods, knobs.get_restore_slot_bytes(),
+                                       knobs.get_restore_piece_bytes(),
+                                       knobs.get_restore_slots(), knobs.get_restore_readers(),
+                                       knobs.get_restore_device_budget(),
+                                       knobs.get_restore_sdma_engine(),
+                                       knobs.get_restore_first_bytes())
         rc, item, msg = job.wait()
         bad = job.corrupt_items()
         native.restore_trim(dev, knobs.get_restore_keep_bytes())

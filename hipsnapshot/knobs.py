@@ -439,6 +439,13 @@ def restore_plan_cache_enabled() -> bool:
     return _get_bool("RESTORE_PLAN_CACHE", True)
 
 
+def native_io_numa_local() -> bool:
+    """The native restore's reader threads run on the CPUs of their GPU's
+    NUMA node (the process's own mask is left alone): unbound, one rank's
+    W = 8 share restored in 42 ms, bound in 29 (profiles/r4/restore_native/)."""
+    return _get_bool("NATIVE_IO_NUMA_LOCAL", True)
+
+
 def get_restore_slot_bytes() -> int:
     """Pinned slot size of the native restore = the largest SDMA upload: 8
     MiB uploads ran the link at 38 GB/s, 32 MiB at 45; a request costs the

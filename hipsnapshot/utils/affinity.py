@@ -214,3 +214,69 @@ class threads_avoiding_caller:
                 os.sched_setaffinity(0, self.prev)
             except OSError:
                 pass
+
+
+# ---- native I/O threads next to their GPU --------------------------------------
+#
+# The native restore's readers copy page-cache pages into pinned slots that
+# the GPU's SDMA engine then reads: with the threads (and the slots they
+# first touch) on the GPU's NUMA node, one rank's W = 8 share restored in
+# 29 ms instead of 42 (profiles/r4/restore_native/).  Binding the whole
+# process is the caller's choice (``bind_to_gpu_numa``); the native jobs only
+# create their own threads under the GPU node's mask.
+
+
+def gpu_node_mask(device: int, min_cpus: int = 4) -> Optional[Set[int]]:
+    """This thread's allowed CPUs on ``device``'s NUMA node, or None when
+    unknown / too few / no narrower than the current mask."""
+    node = gpu_numa_node(device)
+    if node is None:
+        return None
+    try:
+        allowed = os.sched_getaffinity(0)
+    except OSError:
+        return None
+    local = node_cpus(node) & allowed
+    if len(local) < min_cpus or local == allowed:
+        return None
+    return local
+
+
+class threads_with_mask:
+    """Context manager: threads created inside it inherit ``mask`` (None: no
+    change); the calling thread's own mask is restored on exit."""
+
+    def __init__(self, mask: Optional[Set[int]]) -> None:
+        self.mask = mask
+        self.prev: Optional[Set[int]] = None
+
+    def __enter__(self) -> "threads_with_mask":
+        if self.mask:
+            try:
+                self.prev = os.sched_getaffinity(0)
+                os.sched_setaffinity(0, self.mask)
+            except OSError:
+                self.prev = None
+        return self
+
+    def __exit__(self, *exc) -> None:
+        if self.prev is not None:
+            try:
+                os.sched_setaffinity(0, self.prev)
+            except OSError:
+                pass
+
+
+def drain_thread_mask(device: int, avoid: str, numa_local: bool) -> Optional[Set[int]]:
+    """Mask for an async drain's native threads: off the noted caller's core
+    / L3 (``avoid``, see ``mask_avoiding_caller``), and within ``device``'s
+    NUMA node when ``numa_local`` and at least 2 CPUs remain; None = leave
+    the threads' mask as the caller's."""
+    mask = mask_avoiding_caller(avoid) if avoid else None
+    if numa_local:
+        node = gpu_node_mask(device)
+        if node is not None:
+            both = (mask if mask is not None else os.sched_getaffinity(0)) & node
+            if len(both) >= 2:
+                mask = both
+    return mask
