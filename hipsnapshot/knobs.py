@@ -330,8 +330,14 @@ def get_drain_slots() -> int:
 
 
 def get_drain_writers() -> int:
+    """Writer threads of an async take's native drain: 3 (at most half the
+    rank's CPU share, at least 2).  The drain runs beside training: with 8
+    writers a launch-bound seq-512 Llama-3-8B step ran 5-9 % slower while a
+    48 GB drain was in flight, with 3 writers 2-5 % (the drain takes 2.6 s
+    instead of 1.4-2.1 s; the training time lost per checkpoint is about the
+    same, 0.22 vs 0.25 of a blocking take; profiles/r4/overlap_ab_writers/)."""
     share = available_cpus() // max(_local_ranks_hint[0], 1)
-    return max(1, _get_int("DRAIN_WRITERS", min(16, get_io_threads(), max(2, share // 2))))
+    return max(1, _get_int("DRAIN_WRITERS", min(3, get_io_threads(), max(2, share // 2))))
 
 
 def get_drain_nice() -> int:
