@@ -166,6 +166,54 @@ struct DevPool {
 DevPool g_upload_pool(hipDeviceMallocUncached);
 DevPool g_scratch_pool(0);
 
+// A job's device memory: one block per kind (uncached upload targets, decode
+// scratch) carved into per-item ranges in plan order and returned in any
+// order; a range is reusable once every range before it came back.  One
+// allocation per job instead of one per blob (the first restore of a
+// checkpoint paid a hipMalloc per blob).
+struct Ring {
+  char* base = nullptr;
+  uint64_t cap = 0;
+  uint64_t head = 0, tail = 0;  // virtual byte counters (offset = v % cap)
+  struct Range {
+    uint64_t v0, v1;
+    bool released;
+  };
+  std::deque<Range> live;
+
+  bool fits(uint64_t n) const {
+    uint64_t start = head;
+    const uint64_t phys = start % cap;
+    if (phys + n > cap) start += cap - phys;  // wrap: the tail end stays unused
+    return start + n - tail <= cap;
+  }
+  // caller checked fits(n); returns the range's virtual start (its id)
+  uint64_t alloc(uint64_t n, char** p) {
+    const uint64_t v0 = head;
+    uint64_t start = head;
+    const uint64_t phys = start % cap;
+    if (phys + n > cap) start += cap - phys;
+    live.push_back(Range{v0, start + n, false});
+    head = start + n;
+    *p = base + start % cap;
+    return v0;
+  }
+  void release(uint64_t v0) {
+    for (auto& r : live)
+      if (r.v0 == v0) {
+        r.released = true;
+        break;
+      }
+    while (!live.empty() && live.front().released) {
+      tail = live.front().v1;
+      live.pop_front();
+    }
+    if (live.empty()) tail = head;
+  }
+};
+
+uint64_t align4k(uint64_t n) { return (n + 4095) & ~uint64_t(4095); }
+
 // ---- the job -----------------------------------------------------------------
 
 struct Item {
@@ -188,7 +236,9 @@ struct Item {
   void* scratch = nullptr; // HSZ1 decode output when not direct
   void* ws = nullptr;      // copy descriptor / tile workspace
   void* stage = nullptr;   // pinned stage of the workspace tables
-  uint64_t charged = 0;    // device bytes counted against the budget
+  bool allocated = false;  // block (and scratch) assigned
+  bool pooled = false;     // from the pools (larger than a ring), not a ring
+  uint64_t up_v = 0, sc_v = 0;  // ring range ids
   int nchunks = 0;
   std::atomic<int> chunks_left{0};
   std::vector<uint8_t> head;  // HSZ1 header + frame table (from chunk 0)
@@ -220,7 +270,7 @@ struct SlotFill {
 enum Stat {
   kRead,         // readers in pread
   kSlotWait,     // readers waiting for a free pinned slot
-  kBudgetWait,   // readers waiting for device budget
+  kBudgetWait,   // readers waiting for ring space (earlier blobs to retire)
   kAlloc,        // readers acquiring device blocks
   kSubmit,       // readers submitting uploads
   kUploadWait,   // completion thread waiting for uploads
@@ -265,7 +315,10 @@ struct Job {
   size_t cursor = 0;
   int readers_left = 0;
   bool completion_done = false;
-  uint64_t used = 0;  // device bytes charged
+  Ring up_ring, sc_ring;
+  void* up_base = nullptr;  // pool blocks behind the rings
+  void* sc_base = nullptr;
+  int pooled_live = 0;      // items on pool blocks (one at a time, rings empty)
   int launched = 0;
   uint64_t busy_since = 0;  // outstanding went non-zero at (kUploadBusy)
   int outstanding = 0;      // uploads submitted and not yet waited for
@@ -296,33 +349,39 @@ struct Job {
 };
 
 
-// Device blocks of item i (upload target, decode scratch); waits for budget.
-bool ensure_blocks(Job* j, int i) {
+// Device memory of item i (upload target, decode scratch), assigned when
+// its first span starts filling, under j->mu and in plan order (the rings
+// are then released roughly in order).  Returns 0 = assigned, 1 = wait for
+// earlier items to retire, -1 = out of device memory.  An item larger than
+// a ring gets pool blocks, once nothing else holds device memory.
+int alloc_item_locked(Job* j, int i) {
   Item& it = j->items[i];
-  std::lock_guard<std::mutex> g(it.mu);
-  if (it.block) return true;
-  const uint64_t need = (it.nbytes + kGranule - 1) / kGranule * kGranule +
-                        (it.codec == kCodecHsz && !it.direct
-                             ? (it.logical + kGranule - 1) / kGranule * kGranule : 0);
-  uint64_t t0 = now_ns();
-  {
-    std::unique_lock<std::mutex> lk(j->mu);
-    j->cv.wait(lk, [&] { return j->used == 0 || j->used + need <= j->budget || j->err.load(); });
-    if (j->err.load()) return false;
-    j->used += need;
+  if (it.allocated) return 0;
+  const uint64_t nu = align4k(it.nbytes);
+  const uint64_t ns = (it.codec == kCodecHsz && !it.direct) ? align4k(it.logical) : 0;
+  const bool ring_ok = j->up_ring.base && nu <= j->up_ring.cap &&
+                       (ns == 0 || (j->sc_ring.base && ns <= j->sc_ring.cap));
+  if (ring_ok) {
+    if (j->pooled_live > 0 || !j->up_ring.fits(nu) || (ns && !j->sc_ring.fits(ns))) return 1;
+    char* p = nullptr;
+    it.up_v = j->up_ring.alloc(nu, &p);
+    it.block = p;
+    if (ns) {
+      it.sc_v = j->sc_ring.alloc(ns, &p);
+      it.scratch = p;
+    }
+    it.allocated = true;
+    return 0;
   }
-  it.charged = need;
-  j->add(kBudgetWait, t0);
-  t0 = now_ns();
+  if (j->pooled_live > 0 || !j->up_ring.live.empty() || !j->sc_ring.live.empty()) return 1;
+  const uint64_t t0 = now_ns();
   it.block = g_upload_pool.acquire(j->dev, it.nbytes);
-  if (it.block && it.codec == kCodecHsz && !it.direct)
-    it.scratch = g_scratch_pool.acquire(j->dev, it.logical);
+  if (it.block && ns) it.scratch = g_scratch_pool.acquire(j->dev, it.logical);
   j->add(kAlloc, t0);
-  if (!it.block || (it.codec == kCodecHsz && !it.direct && !it.scratch)) {
-    j->fail(-ENOMEM, i, "device block");
-    return false;
-  }
-  return true;
+  it.pooled = true;
+  it.allocated = true;
+  ++j->pooled_live;
+  return (it.block && (ns == 0 || it.scratch)) ? 0 : -1;
 }
 
 int pieces_of(const Job* j, uint64_t n) { return int((n + j->piece_bytes - 1) / j->piece_bytes); }
@@ -335,6 +394,7 @@ void reader_thread(Job* j) {
     {
       std::unique_lock<std::mutex> lk(j->mu);
       bool finished = false;
+      int nomem = -1;
       for (;;) {
         if (j->err.load()) {
           finished = true;
@@ -352,7 +412,23 @@ void reader_thread(Job* j) {
           j->add(kSlotWait, t0);
           continue;
         }
-        // start filling a free slot with the plan's next span
+        // start filling a free slot with the plan's next span; an item's
+        // first span gets its device memory first
+        const Job::Span& nx = j->spans[j->cursor];
+        if (nx.index == 0) {
+          const uint64_t t0 = now_ns();
+          const int a = alloc_item_locked(j, nx.item);
+          if (a == 1) {
+            j->cv.wait(lk);
+            j->add(kBudgetWait, t0);
+            continue;
+          }
+          if (a < 0) {
+            nomem = nx.item;
+            finished = true;
+            break;
+          }
+        }
         const int fs = j->free_slots.back();
         j->free_slots.pop_back();
         const Job::Span& sp = j->spans[j->cursor++];
@@ -366,7 +442,11 @@ void reader_thread(Job* j) {
         f.left.store(f.pieces);
         j->filling = fs;
       }
-      if (finished) break;
+      if (finished) {
+        lk.unlock();
+        if (nomem >= 0) j->fail(-ENOMEM, nomem, "device block");
+        break;
+      }
       s = j->filling;
       SlotFill& f = j->fills[s];
       const int k = f.next_piece++;
@@ -378,7 +458,6 @@ void reader_thread(Job* j) {
     j->cv.notify_all();
     SlotFill& f = j->fills[s];
     Item& it = j->items[i];
-    if (!ensure_blocks(j, i)) break;
     {
       std::lock_guard<std::mutex> g(it.mu);
       if (it.fd < 0 && it.pieces_read < it.npieces) {
@@ -540,20 +619,27 @@ int launch_item(Job* j, int i, hipStream_t s) {
 }
 
 void release_item(Job* j, Item& it) {
-  g_upload_pool.release(it.block);
-  g_scratch_pool.release(it.scratch);
   g_scratch_pool.release(it.ws);
   if (it.stage) hsg_pinned_release(it.stage);
-  it.block = it.scratch = it.ws = it.stage = nullptr;
   if (it.done) {
     hipEventDestroy(it.done);
     it.done = nullptr;
   }
   {
     std::lock_guard<std::mutex> g(j->mu);
-    j->used -= it.charged;
+    if (it.allocated) {
+      if (it.pooled) {
+        g_upload_pool.release(it.block);
+        g_scratch_pool.release(it.scratch);
+        --j->pooled_live;
+      } else {
+        j->up_ring.release(it.up_v);
+        if (it.scratch) j->sc_ring.release(it.sc_v);
+      }
+    }
+    it.allocated = it.pooled = false;
+    it.block = it.scratch = it.ws = it.stage = nullptr;
   }
-  it.charged = 0;
   j->cv.notify_all();
 }
 
@@ -697,12 +783,31 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
       for (int s = 0; s < 2; ++s) (void)hipStreamWaitEvent(j->streams[s], ev, 0);
     hipEventDestroy(ev);
   }
+  // the rings: at most `budget` bytes each, no more than the job needs
+  uint64_t need_up = 0, need_sc = 0;
+  for (const Item& it : j->items) {
+    need_up += align4k(it.nbytes);
+    if (it.codec == kCodecHsz && !it.direct) need_sc += align4k(it.logical);
+  }
+  const uint64_t cap_up = std::min(j->budget, need_up), cap_sc = std::min(j->budget, need_sc);
+  if (cap_up) j->up_base = g_upload_pool.acquire(dev, cap_up);
+  if (cap_sc) j->sc_base = g_scratch_pool.acquire(dev, cap_sc);
+  if (j->up_base) {
+    j->up_ring.base = static_cast<char*>(j->up_base);
+    j->up_ring.cap = cap_up;
+  }
+  if (j->sc_base) {
+    j->sc_ring.base = static_cast<char*>(j->sc_base);
+    j->sc_ring.cap = cap_sc;
+  }
   nslots = std::max(nslots, 2);
   j->fills.reset(new SlotFill[nslots]);
   for (int s = 0; s < nslots; ++s) {
     void* p = hsg_pinned_acquire(j->slot_bytes);
     if (!p) {
       for (void* q : j->slots) hsg_pinned_release(q);
+      g_upload_pool.release(j->up_base);
+      g_scratch_pool.release(j->sc_base);
       delete j;
       *err = -2;
       return nullptr;
@@ -736,8 +841,10 @@ int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
   j->add(kWall, j->t_start);
   for (auto& it : j->items) {
     if (it.fd >= 0) close(it.fd);
-    if (it.block || it.scratch || it.ws || it.stage || it.done) release_item(j, it);
+    if (it.allocated || it.ws || it.stage || it.done) release_item(j, it);
   }
+  g_upload_pool.release(j->up_base);
+  g_scratch_pool.release(j->sc_base);
   for (void* p : j->slots) hsg_pinned_release(p);
   if (stats)
     for (int k = 0; k < kNumStats; ++k) stats[k] = 1e-9 * double(j->ns[k].load());

@@ -490,14 +490,16 @@ def get_restore_readers() -> int:
 
 
 def get_restore_device_budget() -> int:
-    """HBM the native restore's upload / decode blocks may hold at once."""
-    return max(4 << 20, _get_int("RESTORE_DEVICE_BUDGET", 4 << 30))
+    """HBM of each of the native restore's two rings (uncached upload
+    targets, decode scratch): blobs in flight between their first read and
+    the end of their decode / copy kernels."""
+    return max(4 << 20, _get_int("RESTORE_DEVICE_BUDGET", 2 << 30))
 
 
 def get_restore_keep_bytes() -> int:
-    """Idle restore blocks kept per pool after a restore (the next restore
-    of the same shapes then allocates nothing)."""
-    return max(0, _get_int("RESTORE_KEEP_BYTES", 1 << 30))
+    """Idle restore blocks kept per pool after a restore: the rings of the
+    next restore then allocate nothing."""
+    return max(0, _get_int("RESTORE_KEEP_BYTES", (2 << 30) + (256 << 20)))
 
 
 def get_stage_threads() -> int:
