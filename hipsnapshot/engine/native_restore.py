@@ -145,15 +145,29 @@ def _plan_one(rr: ReadReq, root: str, slot_bytes: int):
     return dev, item, _producers(rr.buffer_consumer)
 
 
-def split(read_reqs: List[ReadReq], storage: StoragePlugin
+def sizing(budget: Optional[int]) -> Tuple[int, int, int]:
+    """(slot bytes, first-span bytes, slots) of a job: the knobs, shrunk so
+    the pinned slots stay within half of the host ``budget`` (a
+    ``read_object`` with a memory budget must not pin 768 MiB)."""
+    slot, first, n = (knobs.get_restore_slot_bytes(), knobs.get_restore_first_bytes(),
+                      knobs.get_restore_slots())
+    if budget:
+        cap = max(2 << 20, int(budget) // 2)
+        n = max(2, min(n, cap // slot))
+        slot = max(1 << 20, min(slot, cap // n))
+    return slot, min(first, slot), n
+
+
+def split(read_reqs: List[ReadReq], storage: StoragePlugin, budget: Optional[int] = None
           ) -> Tuple[Dict[int, list], List[ReadReq]]:
-    """({device: [(read req, item)], ...} for native jobs, the Python part)."""
+    """({device: [(read req, item)], ...} for native jobs, the Python part);
+    ``budget``: the read's host memory budget (``sizing``)."""
     if not read_reqs or not knobs.native_restore_enabled() or _root(storage) is None \
             or not native.gpu_available():
         return {}, list(read_reqs)
     root = _root(storage)
     # an HSZ1 blob's header and frame table must fit its first upload span
-    slot_bytes = min(knobs.get_restore_slot_bytes(), knobs.get_restore_first_bytes())
+    slot_bytes = sizing(budget)[1]
     jobs: Dict[int, list] = defaultdict(list)
     py: List[ReadReq] = []
     t0 = time.perf_counter()
@@ -168,11 +182,12 @@ def split(read_reqs: List[ReadReq], storage: StoragePlugin
     return dict(jobs), py
 
 
-def run(jobs: Dict[int, list]) -> int:
+def run(jobs: Dict[int, list], budget: Optional[int] = None) -> int:
     """Run the planned jobs (blocking; call off the event loop); returns the
     logical bytes restored.  Raises ``CorruptBlobError`` for rejected frames,
     ``OSError`` / ``HipError`` for other failures."""
     total = 0
+    slot, first, nslots = sizing(budget)
     for dev, entries in jobs.items():
         t0 = time.perf_counter()
         items = [e[1] for e in entries]
@@ -182,12 +197,10 @@ def run(jobs: Dict[int, list]) -> int:
         # readers (and the pinned slots they fill) on the GPU's NUMA node
         mask = gpu_node_mask(dev) if knobs.native_io_numa_local() else None
         with threads_with_mask(mask):
-            job = native.NativeRestore(dev, items, prods, knobs.get_restore_slot_bytes(),
-                                       knobs.get_restore_piece_bytes(),
-                                       knobs.get_restore_slots(), knobs.get_restore_readers(),
+            job = native.NativeRestore(dev, items, prods, slot, knobs.get_restore_piece_bytes(),
+                                       nslots, knobs.get_restore_readers(),
                                        knobs.get_restore_device_budget(),
-                                       knobs.get_restore_sdma_engine(),
-                                       knobs.get_restore_first_bytes())
+                                       knobs.get_restore_sdma_engine(), first)
         rc, item, msg = job.wait()
         bad = job.corrupt_items()
         native.restore_trim(dev, knobs.get_restore_keep_bytes())

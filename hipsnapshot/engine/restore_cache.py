@@ -131,7 +131,7 @@ def clear() -> None:
         _plans.clear()
 
 
-def run(plan: RestorePlan) -> int:
+def run(plan: RestorePlan, budget: Optional[int] = None) -> int:
     """Run a recorded plan's native jobs, ordered after the callers' current
     streams on each device; returns the logical bytes restored."""
     from . import native_restore
@@ -140,7 +140,7 @@ def run(plan: RestorePlan) -> int:
     for dev, entries in plan.jobs.items():
         prod = [int(torch.cuda.current_stream(dev).cuda_stream)]
         jobs[dev] = [(_Path(path), item, prod) for path, item in entries]
-    return native_restore.run(jobs)
+    return native_restore.run(jobs, budget)
 
 
 class _Path:

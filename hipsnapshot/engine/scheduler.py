@@ -597,11 +597,11 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
     from . import native_restore
 
     if native_jobs is None:
-        native_jobs, read_reqs = native_restore.split(read_reqs, storage)
+        native_jobs, read_reqs = native_restore.split(read_reqs, storage, memory_budget_bytes)
     native_fut = None
     if native_jobs:
         native_fut = asyncio.get_running_loop().run_in_executor(
-            aux_pool(), native_restore.run, native_jobs)
+            aux_pool(), native_restore.run, native_jobs, memory_budget_bytes)
     try:
         stats = await _execute_python_reads(read_reqs, storage, memory_budget_bytes, rank,
                                             consume_threads, io_concurrency) \

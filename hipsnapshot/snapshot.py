@@ -660,7 +660,7 @@ class Snapshot:
             plan = restore_cache.lookup(cache_key)
             if plan is not None:
                 with timeline.span("read_pipeline", cached=True):
-                    restore_cache.run(plan)
+                    restore_cache.run(plan, get_process_memory_budget_bytes(comm))
                 return
         containers: Dict[str, Entry] = {}
         reads: List[ReadReq] = []
@@ -680,7 +680,7 @@ class Snapshot:
                 reads = batch_read_requests(reads)
             reads = order_reads_for_pipeline(reads)
         budget = get_process_memory_budget_bytes(comm)
-        native_jobs, py_reads = native_restore.split(reads, storage)
+        native_jobs, py_reads = native_restore.split(reads, storage, budget)
         with timeline.span("read_pipeline", n=len(reads)):
             sync_execute_read_reqs(py_reads, storage, budget, comm.get_rank(), loop,
                                    native_jobs=native_jobs)

@@ -1,0 +1,27 @@
+"""CPU-side pieces of the native restore: job sizing under a memory budget,
+and that reads stay on the Python pipeline without a GPU."""
+
+from hipsnapshot.engine import native_restore
+from hipsnapshot.knobs import override_knob
+
+
+def test_sizing_defaults_and_budget():
+    slot, first, n = native_restore.sizing(None)
+    assert slot == 128 << 20 and first == 16 << 20 and n == 6
+    # a 100 MiB read budget: the pinned slots take at most half of it
+    slot, first, n = native_restore.sizing(100 << 20)
+    assert slot * n <= 50 << 20 and n >= 2 and first <= slot
+    # tiny budgets still get two 1 MiB slots
+    slot, first, n = native_restore.sizing(1 << 20)
+    assert (slot, n) == (1 << 20, 2) and first == 1 << 20
+    with override_knob("RESTORE_SLOTS", "3"), override_knob("RESTORE_SLOT_BYTES", str(8 << 20)):
+        assert native_restore.sizing(None) == (8 << 20, 8 << 20, 3)
+
+
+def test_split_without_gpu_keeps_every_read_on_python(tmp_path):
+    from hipsnapshot.io_types import ReadReq
+    from hipsnapshot.storage.fs import FSStoragePlugin
+
+    reqs = [ReadReq(path="a", buffer_consumer=None), ReadReq(path="b", buffer_consumer=None)]
+    jobs, py = native_restore.split(reqs, FSStoragePlugin(str(tmp_path)))
+    assert jobs == {} and py == reqs
