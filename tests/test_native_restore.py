@@ -205,3 +205,28 @@ def test_restore_plan_cache_hits_and_invalidates(gpu, tmp_path):
     _eq(sd, want)
     assert restore_cache.stats["hits"] == hits
     restore_cache.clear()
+
+
+def test_read_object_with_budget_keeps_pinned_slots_within_it(gpu, tmp_path):
+    """A budgeted read_object into an HBM tensor goes through the native job
+    with pinned slots of at most half the budget."""
+    from hipsnapshot.engine import native_restore
+    from hipsnapshot.knobs import override_is_batching_disabled
+    from hipsnapshot.ops import native
+
+    big = torch.randn(64 << 20, device=gpu)  # 256 MiB
+    path = str(tmp_path / "o")
+    with override_is_batching_disabled(True):
+        Snapshot.take(path, {"sd": StateDict(big=big)})
+    native.pinned_trim()
+    _cached0, used0 = native.pinned_stats()
+    out = torch.zeros_like(big)
+    native_restore.last_stats.clear()
+    budget = 32 << 20
+    Snapshot(path).read_object("0/sd/big", obj_out=out, memory_budget_bytes=budget)
+    torch.cuda.synchronize()
+    assert torch.equal(out, big)
+    assert native_restore.last_stats.get("items", 0) > 0
+    cached, used = native.pinned_stats()
+    assert used == used0
+    assert cached <= budget // 2 + (4 << 20), cached
