@@ -76,6 +76,7 @@ constexpr int kFlagDirect = 4;
 constexpr int kFlagHashLowPrio = 8;  // keep the hash stream at default priority  // O_DIRECT: the engines' slots go to the device, no CPU copy
 constexpr uint64_t kDirectAlign = 4096;
 constexpr int kNiceShift = 8;  // flags bits 8..15: nice increment of the drain threads
+constexpr int kParkedShift = 16;  // flags bits 16..23: parked writers (hsg_drain_boost)
 
 // Lower this thread's CPU priority by `inc` (Linux: per-thread nice).  The
 // drain's threads then yield a shared core to the trainer's launch thread
@@ -163,6 +164,7 @@ struct Job {
 
   std::vector<std::thread> threads;
   bool finished = false;
+  bool boost = false;  // parked writers may work (the caller waits for the drain)
 
   void fail(int code, const char* what, const std::string& path) {
     int expected = 0;
@@ -315,14 +317,19 @@ void wait_thread(Job* j) {
   j->cv.notify_all();
 }
 
-void writer_thread(Job* j) {
+// A parked writer (`parked`) takes no chunk before hsg_drain_boost: beside a
+// training loop the drain uses few writers (their page-cache copies slow a
+// launch-bound step), and all of them once the caller blocks on the drain.
+void writer_thread(Job* j, bool parked) {
   lower_priority((j->flags >> kNiceShift) & 0xff);
   for (;;) {
     Chunk c;
     {
       std::unique_lock<std::mutex> lk(j->mu);
-      j->cv.wait(lk, [&] { return !j->to_write.empty() || j->wait_done; });
-      if (j->to_write.empty()) break;
+      j->cv.wait(lk, [&] {
+        return ((!parked || j->boost) && !j->to_write.empty()) || j->wait_done;
+      });
+      if (j->to_write.empty() || (parked && !j->boost)) break;
       c = j->to_write.front();
       j->to_write.pop_front();
     }
@@ -375,7 +382,8 @@ extern "C" {
 // O_DIRECT files (the pinned slots go to the device with no CPU copy and no
 // page cache; buffered where the filesystem refuses it), 8 = hash stream at
 // default instead of high priority, bits 8..15 = nice
-// increment of every drain thread.
+// increment of every drain thread, bits 16..23 = parked writers that start
+// on hsg_drain_boost.
 // Returns a handle (> 0) for hsg_drain_wait, or 0 with *err set.
 void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* sizes,
                       const char* const* paths, uint64_t slot_bytes, int nslots, int nwriters,
@@ -414,8 +422,20 @@ void* hsg_drain_start(int dev, int n, const uint64_t* srcs, const uint64_t* size
   j->t_start = now_ns();
   j->threads.emplace_back(dma_thread, j);
   j->threads.emplace_back(wait_thread, j);
-  for (int w = 0; w < std::max(nwriters, 1); ++w) j->threads.emplace_back(writer_thread, j);
+  for (int w = 0; w < std::max(nwriters, 1); ++w) j->threads.emplace_back(writer_thread, j, false);
+  for (int w = 0; w < ((flags >> kParkedShift) & 0xff); ++w)
+    j->threads.emplace_back(writer_thread, j, true);
   return j;
+}
+
+// Let the parked writers work (the caller now waits for the drain).
+void hsg_drain_boost(void* handle) {
+  Job* j = static_cast<Job*>(handle);
+  {
+    std::lock_guard<std::mutex> g(j->mu);
+    j->boost = true;
+  }
+  j->cv.notify_all();
 }
 
 // Wait for the drain (blocking; Python calls it without the GIL).  Returns 0

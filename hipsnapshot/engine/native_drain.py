@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import logging
 import os
+import threading
 import time
 from typing import Dict, List, Tuple
 
@@ -30,6 +31,34 @@ logger = logging.getLogger(__name__)
 
 
 last_stats: Dict[str, float] = {}  # the last drain's phase seconds (NativeDrain.STATS)
+
+class Booster:
+    """Shared by one async take's drain and its ``PendingSnapshot``: once the
+    caller blocks in ``wait()`` nothing trains beside the drain any more, so
+    its parked writers start (``NativeDrain.boost``)."""
+
+    def __init__(self) -> None:
+        self._lock = threading.Lock()
+        self._jobs: List = []
+        self.boosted = False
+
+    def boost(self) -> None:
+        with self._lock:
+            self.boosted = True
+            jobs = list(self._jobs)
+        for job in jobs:
+            job.boost()
+
+    def attach(self, job) -> None:
+        with self._lock:
+            self._jobs.append(job)
+            now = self.boosted
+        if now:
+            job.boost()
+
+    def detach(self, job) -> None:
+        with self._lock:
+            self._jobs.remove(job)
 
 
 def _root(storage: StoragePlugin):
@@ -64,23 +93,33 @@ def split(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[List[WriteReq],
     return nat, py
 
 
-def _run(dev: int, wrs: List[WriteReq], blobs, fsync: bool, want_sums: bool, direct: bool):
+def _run(dev: int, wrs: List[WriteReq], blobs, fsync: bool, want_sums: bool, direct: bool,
+         booster: "Booster" = None):
     """One device's drain in this process's native threads.  Returns (hs64
     partial sums, bytes written, stats, "in_process")."""
     from ..utils.affinity import drain_thread_mask, threads_with_mask
 
     args = (knobs.get_drain_slot_bytes(), knobs.get_drain_slots(), knobs.get_drain_writers())
+    parked = max(0, knobs.get_drain_boost_writers() - args[2])
     # the drain's threads inherit a mask without the training thread's core
     # (or L3 domain), on the GPU's NUMA node when that leaves enough CPUs
     with threads_with_mask(drain_thread_mask(dev, knobs.drain_avoid_caller_core(),
                                              knobs.native_io_numa_local())):
         job = native.NativeDrain(dev, blobs, *args, fsync, want_sums, knobs.get_hash_grid(),
-                                 knobs.get_drain_nice(), direct, knobs.drain_hash_high_priority())
-    partial, written = job.wait()
+                                 knobs.get_drain_nice(), direct, knobs.drain_hash_high_priority(),
+                                 parked_writers=parked)
+    if booster is not None:
+        booster.attach(job)
+    try:
+        partial, written = job.wait()
+    finally:
+        if booster is not None:
+            booster.detach(job)
     return partial, written, job.stats, "in_process"
 
 
-def drain(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[Dict[str, int], int]:
+def drain(reqs: List[WriteReq], storage: StoragePlugin, booster: "Booster" = None
+          ) -> Tuple[Dict[str, int], int]:
     """Write every request's frozen region to its file; returns ({blob path:
     hs64}, bytes written).  Blocks (call it off the event loop)."""
     root, fsync, direct = _root(storage)
@@ -101,7 +140,7 @@ def drain(reqs: List[WriteReq], storage: StoragePlugin) -> Tuple[Dict[str, int],
         for wr in wrs:
             arena, off, nbytes = wr.buffer_stager.frozen_region
             blobs.append((arena.data_ptr() + off, nbytes, os.path.join(root, wr.path)))
-        partial, written, stats, where = _run(dev, wrs, blobs, fsync, want_sums, direct)
+        partial, written, stats, where = _run(dev, wrs, blobs, fsync, want_sums, direct, booster)
         total += written
         if want_sums:
             for wr, (_p, n, _path), s in zip(wrs, blobs, partial):

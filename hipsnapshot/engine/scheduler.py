@@ -503,6 +503,12 @@ class DeferredIOWork:
         self.rank = rank
         self.stats = first.stats
         self._second: Optional[PendingIOWork] = None
+        from .native_drain import Booster
+
+        self.booster = Booster()  # PendingSnapshot.wait() -> all drain writers
+
+    def boost(self) -> None:
+        self.booster.boost()
 
     async def complete(self) -> None:
         from . import native_drain
@@ -523,7 +529,8 @@ class DeferredIOWork:
             # one native call for every raw frozen blob: no Python (and no
             # GIL) between the arena and the files while the trainer runs
             if native_reqs:
-                cf = aux_pool().submit(native_drain.drain, native_reqs, self.storage)
+                cf = aux_pool().submit(native_drain.drain, native_reqs, self.storage,
+                                       self.booster)
                 native_fut.append(cf)
                 native_out["sums"], native_out["bytes"] = await asyncio.wrap_future(cf)
 

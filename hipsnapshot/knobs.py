@@ -340,6 +340,14 @@ def get_drain_writers() -> int:
     return max(1, _get_int("DRAIN_WRITERS", min(3, get_io_threads(), max(2, share // 2))))
 
 
+def get_drain_boost_writers() -> int:
+    """Writer threads of a native drain once its caller blocks on it
+    (``PendingSnapshot.wait``): the extra ones are parked until then.  With
+    an idle trainer 16 writers drain 16 GB in ~310 ms, 3 in ~490 ms."""
+    share = available_cpus() // max(_local_ranks_hint[0], 1)
+    return max(1, _get_int("DRAIN_BOOST_WRITERS", min(16, get_io_threads(), max(2, share // 2))))
+
+
 def get_drain_nice() -> int:
     """Nice increment of the native drain's threads (0-19, default 10): they
     yield a shared core to the training loop's launch thread."""

@@ -268,6 +268,7 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_void_p, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64), c_char_p,
                   ctypes.POINTER(ctypes.c_double)])
         _declare(lib, "hsg_drain_pending", c_int, [c_void_p])
+        _declare(lib, "hsg_drain_boost", None, [c_void_p])
         P = ctypes.POINTER
         _declare(lib, "hsg_restore_start", c_void_p,
                  [c_int, c_int, P(c_char_p), P(c_uint64), P(c_uint64), P(c_int), P(c_uint64),
@@ -803,7 +804,7 @@ class NativeDrain:
     def __init__(self, dev: int, blobs: Sequence[Tuple[int, int, str]], slot_bytes: int,
                  nslots: int, nwriters: int, fsync: bool, hash_blobs: bool,
                  max_hash_grid: int, nice: int = 0, direct: bool = False,
-                 hash_high_priority: bool = True) -> None:
+                 hash_high_priority: bool = True, parked_writers: int = 0) -> None:
         lib = require_gpu_lib()
         n = len(blobs)
         self.n = n
@@ -811,7 +812,8 @@ class NativeDrain:
         self._sizes = (c_uint64 * max(n, 1))(*[b[1] for b in blobs])
         self._paths = (c_char_p * max(n, 1))(*[os.fsencode(b[2]) for b in blobs])
         err = c_int(0)
-        flags = self.flags(fsync, hash_blobs, direct, hash_high_priority, nice)
+        flags = self.flags(fsync, hash_blobs, direct, hash_high_priority, nice) | \
+            (max(0, min(parked_writers, 255)) << 16)
         self._h = lib.hsg_drain_start(dev, n, self._srcs, self._sizes, self._paths,
                                       slot_bytes, nslots, nwriters, flags, max_hash_grid,
                                       ctypes.byref(err))
@@ -826,6 +828,12 @@ class NativeDrain:
 
     def pending(self) -> int:
         return require_gpu_lib().hsg_drain_pending(self._h) if self._h else 0
+
+    def boost(self) -> None:
+        """Start the parked writers (call while the job runs)."""
+        h = self._h
+        if h:
+            require_gpu_lib().hsg_drain_boost(h)
 
     STATS = ("slot_wait", "hash_collect", "hash_launch", "sdma_submit", "sdma_wait", "pwrite",
              "close", "open", "wall")

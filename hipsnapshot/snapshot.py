@@ -1131,6 +1131,7 @@ class PendingSnapshot:
         self._go = threading.Event()  # set by async_take once it is returning
         self._gc_after = False  # run the new plan's full GC pass after the commit
         store = get_or_create_store(comm) if comm.get_world_size() > 1 else None
+        self._pending_io_work = pending_io_work
         self.thread = threading.Thread(
             target=self._complete_snapshot, name="hipsnapshot-commit",
             kwargs=dict(path=path, rank=comm.get_rank(), world_size=comm.get_world_size(),
@@ -1200,6 +1201,7 @@ class PendingSnapshot:
             self.exc_info = sys.exc_info()
             logger.warning(f"Encountered exception while taking snapshot asynchronously:\n{e}")
         finally:
+            self._pending_io_work = None
             _release_plan({"plan": plan})  # its stagers are idle again
             try:
                 storage.sync_close(event_loop)
@@ -1213,6 +1215,11 @@ class PendingSnapshot:
         self._done = True
 
     def wait(self) -> Snapshot:
+        # nothing trains beside the drain while its caller blocks here: let
+        # the native drain use all of its writers (engine/native_drain.py)
+        boost = getattr(self._pending_io_work, "boost", None)
+        if boost is not None and not self._done:
+            boost()
         self.thread.join()
         if self.exc_info is not None:
             formatted = "".join(traceback.format_exception(*self.exc_info))

@@ -25,3 +25,32 @@ def test_split_without_gpu_keeps_every_read_on_python(tmp_path):
     reqs = [ReadReq(path="a", buffer_consumer=None), ReadReq(path="b", buffer_consumer=None)]
     jobs, py = native_restore.split(reqs, FSStoragePlugin(str(tmp_path)))
     assert jobs == {} and py == reqs
+
+
+def test_drain_booster_reaches_running_and_later_jobs():
+    """PendingSnapshot.wait() boosts the drain jobs of its own take: those
+    running, and one attached after the boost."""
+    from hipsnapshot.engine.native_drain import Booster
+
+    class Job:
+        def __init__(self):
+            self.boosted = 0
+
+        def boost(self):
+            self.boosted += 1
+
+    b = Booster()
+    a = Job()
+    b.attach(a)
+    assert a.boosted == 0
+    b.boost()
+    assert a.boosted == 1
+    late = Job()
+    b.attach(late)
+    assert late.boosted == 1
+    b.detach(a)
+    b.detach(late)
+    other = Booster()
+    c = Job()
+    other.attach(c)
+    assert c.boosted == 0  # another take's drain keeps its parked writers
