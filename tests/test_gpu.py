@@ -1100,7 +1100,7 @@ def test_gpu_take_checksums_hashed_on_device_and_verify(gpu, tmp_path, compressi
     drained = []
     real_drain = native_drain.drain
     monkeypatch.setattr(native_drain, "drain",
-                        lambda reqs, st: drained.append(len(reqs)) or real_drain(reqs, st))
+                        lambda reqs, st, *a: drained.append(len(reqs)) or real_drain(reqs, st, *a))
     a = Snapshot.async_take(str(tmp_path / "a"), {"sd": sd}, compression=compression).wait()
     # raw frozen blobs are hashed on the GPU by the native drain (hsg_hash64
     # from C++), the rest through the Python staging path
@@ -1214,7 +1214,7 @@ def _native_vs_python_drain(gpu, tmp_path, fsync, monkeypatch, native_drain, ver
     calls = []
     orig = native_drain.drain
     monkeypatch.setattr(native_drain, "drain",
-                        lambda reqs, st: calls.append(len(reqs)) or orig(reqs, st))
+                        lambda reqs, st, *a: calls.append(len(reqs)) or orig(reqs, st, *a))
     sd = _drain_state(gpu)
     ref = {k: (v.clone() if torch.is_tensor(v) else [t.clone() for t in v]
                if isinstance(v, list) else v) for k, v in sd.items()}
