@@ -131,6 +131,10 @@ def _plan_one(rr: ReadReq, root: str, slot_bytes: int):
         batch = native.CopyBatch()
         for src_dtype, src_shape, off, narrows, dst in regions:
             es = staging._elem_size(src_dtype)
+            if not narrows and dst.dtype == src_dtype and dst.is_contiguous():
+                # the common slab member: one contiguous byte range
+                batch.add_bytes(base + off, dst.data_ptr(), dst.numel() * es)
+                continue
             shape = [int(z) for z in src_shape]
             strides = staging._contig_strides(shape)
             # source offset within the uploaded (raw) / decoded (HSZ1) bytes
