@@ -230,3 +230,53 @@ def test_read_object_with_budget_keeps_pinned_slots_within_it(gpu, tmp_path):
     cached, used = native.pinned_stats()
     assert used == used0
     assert cached <= budget // 2 + (4 << 20), cached
+
+
+def test_native_restore_error_mid_job_then_clean_restore(gpu, tmp_path):
+    """A corrupt blob among several fails the restore without hanging; the
+    next restore of an intact snapshot (same process, same pools) is exact."""
+    from hipsnapshot.knobs import override_is_batching_disabled
+    from hipsnapshot.ops import codec, native
+
+    g = torch.Generator(device=gpu).manual_seed(4)
+    sd = StateDict(**{f"t{i}": (torch.randn(1 << 21, device=gpu, generator=g) * 0.02)
+                      .to(torch.bfloat16) for i in range(8)})
+    bad_path, good_path = str(tmp_path / "bad"), str(tmp_path / "good")
+    with override_is_batching_disabled(True):
+        Snapshot.take(bad_path, {"sd": sd}, compression="hsz1")
+        Snapshot.take(good_path, {"sd": sd}, compression="hsz1")
+    f = os.path.join(bad_path, "0", "sd", "t3")
+    h = codec.parse_header(open(f, "rb").read())
+    with open(f, "r+b") as fh:  # frame 1's mode byte
+        fh.seek(h.offsets[1])
+        fh.write(b"\x09")
+    out = _zeros_like_state(sd)
+    with override_is_batching_disabled(True), override_knob("RESTORE_SLOT_BYTES", str(1 << 20)), \
+            pytest.raises(native.CorruptBlobError, match="t3"):
+        Snapshot(bad_path).restore({"sd": out})
+    torch.cuda.synchronize()
+    out = _zeros_like_state(sd)
+    with override_is_batching_disabled(True):
+        Snapshot(good_path).restore({"sd": out})
+    torch.cuda.synchronize()
+    _eq(out, sd)
+
+
+def test_native_and_python_reads_in_one_restore(gpu, tmp_path):
+    """HBM tensors go through the native job while a host tensor and an
+    object take the Python pipeline, in the same restore."""
+    from hipsnapshot.engine import native_restore
+
+    g = torch.Generator(device=gpu).manual_seed(6)
+    src = {"gpu": (torch.randn(3 << 20, device=gpu, generator=g) * 0.02).to(torch.bfloat16),
+           "cpu": torch.randn(1 << 20),
+           "obj": {"step": 7, "name": "x"}}
+    path = str(tmp_path / "m")
+    Snapshot.take(path, {"sd": StateDict(**src)}, compression="hsz1")
+    dst = StateDict(gpu=torch.zeros_like(src["gpu"]), cpu=torch.zeros(1 << 20), obj=None)
+    native_restore.last_stats.clear()
+    Snapshot(path).restore({"sd": dst})
+    torch.cuda.synchronize()
+    assert native_restore.last_stats.get("items", 0) >= 1
+    assert torch.equal(dst["gpu"], src["gpu"]) and torch.equal(dst["cpu"], src["cpu"])
+    assert dst["obj"] == src["obj"]
