@@ -802,21 +802,41 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   }
   nslots = std::max(nslots, 2);
   j->fills.reset(new SlotFill[nslots]);
-  for (int s = 0; s < nslots; ++s) {
+  j->slots.assign(nslots, nullptr);
+  // two slots now, the rest from a helper thread while the readers start:
+  // a first use of pinned memory in the process registers it (~10 ms/GiB)
+  for (int s = 0; s < 2; ++s) {
     void* p = hsg_pinned_acquire(j->slot_bytes);
     if (!p) {
-      for (void* q : j->slots) hsg_pinned_release(q);
+      for (void* q : j->slots)
+        if (q) hsg_pinned_release(q);
       g_upload_pool.release(j->up_base);
       g_scratch_pool.release(j->sc_base);
       delete j;
       *err = -2;
       return nullptr;
     }
-    j->slots.push_back(p);
-    j->free_slots.push_back(s);
+    j->slots[s] = p;
+    j->free_slots.push_back(1 - s);
   }
-  std::reverse(j->free_slots.begin(), j->free_slots.end());
   j->t_start = now_ns();
+  if (nslots > 2)
+    j->threads.emplace_back([j, nslots] {
+      for (int s = 2; s < nslots && !j->err.load(); ++s) {
+        {
+          std::lock_guard<std::mutex> g(j->mu);
+          if (j->cursor >= j->spans.size()) break;  // every span already has a slot
+        }
+        void* p = hsg_pinned_acquire(j->slot_bytes);
+        if (!p) break;  // fewer slots, not an error
+        {
+          std::lock_guard<std::mutex> g(j->mu);
+          j->slots[s] = p;
+          j->free_slots.insert(j->free_slots.begin(), s);
+        }
+        j->cv.notify_all();
+      }
+    });
   nreaders = std::max(nreaders, 1);
   j->readers_left = nreaders;
   for (int r = 0; r < nreaders; ++r) j->threads.emplace_back(reader_thread, j);
@@ -845,7 +865,8 @@ int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
   }
   g_upload_pool.release(j->up_base);
   g_scratch_pool.release(j->sc_base);
-  for (void* p : j->slots) hsg_pinned_release(p);
+  for (void* p : j->slots)
+    if (p) hsg_pinned_release(p);
   if (stats)
     for (int k = 0; k < kNumStats; ++k) stats[k] = 1e-9 * double(j->ns[k].load());
   if (bytes_read) *bytes_read = j->bytes_read.load();
