@@ -1517,6 +1517,17 @@ int hsg_device_count() {
   return n;
 }
 
+// PCI domain / bus / device of HIP device `dev` (three attribute queries:
+// hipGetDeviceProperties, behind torch.cuda.get_device_properties, took
+// ~130 ms the first time in a process).  0 on success.
+int hsg_pci_location(int dev, int* domain, int* bus, int* device) {
+  if (hipDeviceGetAttribute(domain, hipDeviceAttributePciDomainId, dev) != hipSuccess ||
+      hipDeviceGetAttribute(bus, hipDeviceAttributePciBusId, dev) != hipSuccess ||
+      hipDeviceGetAttribute(device, hipDeviceAttributePciDeviceId, dev) != hipSuccess)
+    return -1;
+  return 0;
+}
+
 // ---- pinned pool ----------------------------------------------------------
 //
 // Pool blocks are anonymous memory backed by transparent huge pages and

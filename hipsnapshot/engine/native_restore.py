@@ -200,14 +200,21 @@ def run(jobs: Dict[int, list], budget: Optional[int] = None) -> int:
 
         # readers (and the pinned slots they fill) on the GPU's NUMA node
         mask = gpu_node_mask(dev) if knobs.native_io_numa_local() else None
+        t1 = time.perf_counter()
         with threads_with_mask(mask):
             job = native.NativeRestore(dev, items, prods, slot, knobs.get_restore_piece_bytes(),
                                        nslots, knobs.get_restore_readers(),
                                        knobs.get_restore_device_budget(),
                                        knobs.get_restore_sdma_engine(), first)
+        t2 = time.perf_counter()
         rc, item, msg = job.wait()
+        t3 = time.perf_counter()
         bad = job.corrupt_items()
         native.restore_trim(dev, knobs.get_restore_keep_bytes())
+        t4 = time.perf_counter()
+        # caller-side seconds: mask / start / wait / error words + trim
+        job.stats.update(py_mask=round(t1 - t0, 5), py_start=round(t2 - t1, 5),
+                         py_wait=round(t3 - t2, 5), py_after=round(t4 - t3, 5))
         nbytes = sum(it[4] for it in items)
         timeline.add("native_restore", "io", t0, time.perf_counter(), n=len(items),
                      bytes=job.bytes_read, logical=nbytes, **job.stats)

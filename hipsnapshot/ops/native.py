@@ -231,6 +231,8 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
             return None
         _declare(lib, "hsg_last_error", c_char_p, [])
         _declare(lib, "hsg_device_count", c_int, [])
+        _declare(lib, "hsg_pci_location", c_int,
+                 [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
         _declare(lib, "hsg_pinned_acquire", c_void_p, [c_uint64])
         _declare(lib, "hsg_pinned_release", c_int, [c_void_p])
         _declare(lib, "hsg_pinned_stats", None, [ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)])
@@ -386,6 +388,15 @@ class PinnedBuffer:
             self.release()
         except Exception:
             pass
+
+
+def pci_location(dev: int) -> Optional[Tuple[int, int, int]]:
+    """(domain, bus, device) of HIP device ``dev``, or None."""
+    lib = require_gpu_lib()
+    d, b, v = c_int(0), c_int(0), c_int(0)
+    if lib.hsg_pci_location(dev, ctypes.byref(d), ctypes.byref(b), ctypes.byref(v)) != 0:
+        return None
+    return int(d.value), int(b.value), int(v.value)
 
 
 def pinned_stats() -> tuple:

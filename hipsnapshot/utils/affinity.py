@@ -33,6 +33,19 @@ def _parse_cpulist(text: str) -> Set[int]:
 
 
 def gpu_pci_bus_id(device: int) -> Optional[str]:
+    """PCI address of HIP device ``device``: three attribute queries through
+    the native library (``hipGetDeviceProperties``, which
+    ``torch.cuda.get_device_properties`` runs, took ~130 ms the first time
+    in a process), torch as the fallback."""
+    try:
+        from ..ops import native
+
+        if native.hsgpu_loaded() or native.gpu_available():
+            loc = native.pci_location(device)
+            if loc is not None:
+                return f"{loc[0]:04x}:{loc[1]:02x}:{loc[2]:02x}.0"
+    except Exception:  # noqa: BLE001
+        pass
     try:
         import torch
 
@@ -43,16 +56,25 @@ def gpu_pci_bus_id(device: int) -> Optional[str]:
         return None
 
 
+_numa_nodes: dict = {}
+
+
 def gpu_numa_node(device: int) -> Optional[int]:
+    """NUMA node of HIP device ``device`` (cached per process)."""
+    if device in _numa_nodes:
+        return _numa_nodes[device]
+    node = None
     bus = gpu_pci_bus_id(device)
-    if bus is None:
-        return None
-    try:
-        with open(os.path.join(_SYS_PCI, bus, "numa_node")) as f:
-            node = int(f.read().strip())
-    except (OSError, ValueError):
-        return None
-    return node if node >= 0 else None
+    if bus is not None:
+        try:
+            with open(os.path.join(_SYS_PCI, bus, "numa_node")) as f:
+                node = int(f.read().strip())
+        except (OSError, ValueError):
+            node = None
+    node = node if node is not None and node >= 0 else None
+    if bus is not None:
+        _numa_nodes[device] = node
+    return node
 
 
 def node_cpus(node: int) -> Set[int]:
