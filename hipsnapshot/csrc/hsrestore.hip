@@ -239,6 +239,8 @@ struct Item {
   bool allocated = false;  // block (and scratch) assigned
   bool pooled = false;     // from the pools (larger than a ring), not a ring
   uint64_t up_v = 0, sc_v = 0;  // ring range ids
+  bool ws_ring = false;    // ws / stage carved from the job's small rings
+  uint64_t ws_v = 0, st_v = 0;
   int nchunks = 0;
   std::atomic<int> chunks_left{0};
   std::vector<uint8_t> head;  // HSZ1 header + frame table (from chunk 0)
@@ -318,6 +320,12 @@ struct Job {
   Ring up_ring, sc_ring;
   void* up_base = nullptr;  // pool blocks behind the rings
   void* sc_base = nullptr;
+  // copy-launch tables: descriptors + tiles in HBM, staged through pinned
+  // memory; carved per blob from one block each (a first restore in a
+  // process paid a hipMalloc and a pinned registration per slab blob)
+  Ring ws_ring, st_ring;
+  void* ws_base = nullptr;
+  void* st_base = nullptr;
   int pooled_live = 0;      // items on pool blocks (one at a time, rings empty)
   int launched = 0;
   uint64_t busy_since = 0;  // outstanding went non-zero at (kUploadBusy)
@@ -599,8 +607,23 @@ int launch_item(Job* j, int i, hipStream_t s) {
       memcpy(d.data() + uint64_t(k) * j->desc_size, &v, 8);
     }
     const uint64_t wsb = hsg_copy_workspace_bytes(d.data(), it.desc_n);
-    it.ws = g_scratch_pool.acquire(j->dev, wsb);
-    it.stage = hsg_pinned_acquire(wsb);
+    {
+      std::lock_guard<std::mutex> g(j->mu);
+      const uint64_t n = align4k(wsb);
+      if (j->ws_ring.base && j->st_ring.base && n <= j->ws_ring.cap && n <= j->st_ring.cap &&
+          j->ws_ring.fits(n) && j->st_ring.fits(n)) {
+        char* p = nullptr;
+        it.ws_v = j->ws_ring.alloc(n, &p);
+        it.ws = p;
+        it.st_v = j->st_ring.alloc(n, &p);
+        it.stage = p;
+        it.ws_ring = true;
+      }
+    }
+    if (!it.ws_ring) {  // full or too large: pool blocks
+      it.ws = g_scratch_pool.acquire(j->dev, wsb);
+      it.stage = hsg_pinned_acquire(wsb);
+    }
     if (!it.ws || !it.stage) {
       j->fail(-ENOMEM, i, "copy workspace");
       return -1;
@@ -619,8 +642,10 @@ int launch_item(Job* j, int i, hipStream_t s) {
 }
 
 void release_item(Job* j, Item& it) {
-  g_scratch_pool.release(it.ws);
-  if (it.stage) hsg_pinned_release(it.stage);
+  if (!it.ws_ring) {
+    g_scratch_pool.release(it.ws);
+    if (it.stage) hsg_pinned_release(it.stage);
+  }
   if (it.done) {
     hipEventDestroy(it.done);
     it.done = nullptr;
@@ -637,7 +662,11 @@ void release_item(Job* j, Item& it) {
         if (it.scratch) j->sc_ring.release(it.sc_v);
       }
     }
-    it.allocated = it.pooled = false;
+    if (it.ws_ring) {
+      j->ws_ring.release(it.ws_v);
+      j->st_ring.release(it.st_v);
+    }
+    it.allocated = it.pooled = it.ws_ring = false;
     it.block = it.scratch = it.ws = it.stage = nullptr;
   }
   j->cv.notify_all();
@@ -800,6 +829,19 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
     j->sc_ring.base = static_cast<char*>(j->sc_base);
     j->sc_ring.cap = cap_sc;
   }
+  bool any_desc = false;
+  for (const Item& it : j->items) any_desc |= it.desc_n > 0;
+  if (any_desc) {
+    constexpr uint64_t kTables = uint64_t(32) << 20;
+    j->ws_base = g_scratch_pool.acquire(dev, kTables);
+    j->st_base = hsg_pinned_acquire(kTables);
+    if (j->ws_base && j->st_base) {
+      j->ws_ring.base = static_cast<char*>(j->ws_base);
+      j->ws_ring.cap = kTables;
+      j->st_ring.base = static_cast<char*>(j->st_base);
+      j->st_ring.cap = kTables;
+    }
+  }
   nslots = std::max(nslots, 2);
   j->fills.reset(new SlotFill[nslots]);
   j->slots.assign(nslots, nullptr);
@@ -812,6 +854,8 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
         if (q) hsg_pinned_release(q);
       g_upload_pool.release(j->up_base);
       g_scratch_pool.release(j->sc_base);
+      g_scratch_pool.release(j->ws_base);
+      if (j->st_base) hsg_pinned_release(j->st_base);
       delete j;
       *err = -2;
       return nullptr;
@@ -865,6 +909,8 @@ int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
   }
   g_upload_pool.release(j->up_base);
   g_scratch_pool.release(j->sc_base);
+  g_scratch_pool.release(j->ws_base);
+  if (j->st_base) hsg_pinned_release(j->st_base);
   for (void* p : j->slots)
     if (p) hsg_pinned_release(p);
   if (stats)

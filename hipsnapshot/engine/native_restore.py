@@ -131,7 +131,8 @@ def _plan_one(rr: ReadReq, root: str, slot_bytes: int):
         batch = native.CopyBatch()
         for src_dtype, src_shape, off, narrows, dst in regions:
             es = staging._elem_size(src_dtype)
-            if not narrows and dst.dtype == src_dtype and dst.is_contiguous():
+            if dst.dtype == src_dtype and dst.is_contiguous() and \
+                    all(st == 0 and ln == int(src_shape[d]) for d, st, ln in (narrows or ())):
                 # the common slab member: one contiguous byte range
                 batch.add_bytes(base + off, dst.data_ptr(), dst.numel() * es)
                 continue
