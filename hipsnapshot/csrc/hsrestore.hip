@@ -832,7 +832,9 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   bool any_desc = false;
   for (const Item& it : j->items) any_desc |= it.desc_n > 0;
   if (any_desc) {
-    constexpr uint64_t kTables = uint64_t(32) << 20;
+    // a quarter of a slot (the pinned stage counts against the read's budget)
+    const uint64_t kTables = std::min<uint64_t>(uint64_t(32) << 20,
+                                                std::max<uint64_t>(1 << 20, j->slot_bytes / 4));
     j->ws_base = g_scratch_pool.acquire(dev, kTables);
     j->st_base = hsg_pinned_acquire(kTables);
     if (j->ws_base && j->st_base) {
