@@ -27,11 +27,13 @@
 // Decode (after H2D) = 2 launches, one workgroup per frame each:
 //   hsz_decode<W>   modes 0/1 (escape positions are collected from the nibble
 //                   plane first, then every element is rebuilt)
-//   hsz_decode2<W>  mode 2: the frame's streams are staged in LDS, lane t
-//                   decodes its stream through a 2048-entry LDS lookup table
-//                   and stores its groups as 16-B vectors (adjacent lanes ->
-//                   adjacent groups, so the stores coalesce); escapes are
-//                   patched in element order after a barrier
+//   hsz_decode2g<W, P>  mode 2 (default): the frame's streams are staged in
+//                   LDS, lane t decodes its stream through a 2048-entry LDS
+//                   lookup table and stores its groups as 16-B vectors
+//                   (adjacent lanes -> adjacent groups, so the stores
+//                   coalesce); escapes are patched in element order after a
+//                   barrier.  hsz_decode2<W> is the round-3 version of it
+//                   (HIPSNAPSHOT_HSZ_DECODE2=lds; profiles/r4/decode_pmc/)
 //
 // A frame is one workgroup (4 waves): a 512 MiB blob has 2048 frames, 8x the
 // CU count, so the grid fills the chip; all traffic is streaming HBM
@@ -40,6 +42,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 #include <cstdlib>
 #include <cstdio>
 
@@ -1376,6 +1379,255 @@ hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ off
   if (threadIdx.x < tail_len) o[W * n + threadIdx.x] = escv[n_esc + threadIdx.x];
 }
 
+// LUT entry of the lean decoder: code length (bits 0-3; bit 4 is 0, so the
+// entry itself is a valid v_alignbit / v_lshrrev shift amount), escape (5),
+// invalid code (6; length kMaxLen so a corrupt lane still advances by a
+// bounded amount), decoded high byte (8-15).
+constexpr uint32_t kEntEsc = 0x20u, kEntBad = 0x40u;
+
+// Lean mode-2 decoder (default; HIPSNAPSHOT_HSZ_DECODE2=lds selects the
+// original hsz_decode2).  Measured (profiles/r4/decode_pmc/): a frame's
+// decode is latency-bound -- one frame alone on a CU takes as long as 2 per
+// CU, so neither LDS bank conflicts nor issue rate set the pace, but the
+// serial chain of each lane stream (512 symbols per lane for bf16) and the
+// HBM round trips inside it.  So:
+//   * the LUT entry carries the decoded high byte itself and its length in
+//     the bits a shift reads: one LDS read per symbol, no dictionary read,
+//     escapes and invalid codes are OR-ed into a per-group flag word and
+//     handled off the chain;
+//   * the bit window is kept pre-shifted by one bit as two 32-bit halves:
+//     the chain per symbol is LUT read -> v_alignbit (by the entry) -> v_and
+//     -> next LUT read (the 64-bit shift, the length extraction and the
+//     index scaling are off it);
+//   * the window is refilled from the LDS-staged streams twice per 8 symbols
+//     (>= 56 bits cover 5 codes), and the staging copy has all of a thread's
+//     16-B loads in flight at once;
+//   * P > 0: the low-byte plane is loaded P groups ahead;
+//   * bf16 pairs are assembled with v_perm.
+// Validation and error reporting are hsz_decode2's.
+template <int W, int P>
+__global__ void __launch_bounds__(kThreads)
+hsz_decode2g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+             uint32_t first_frame, uint64_t logical, uint32_t frame_bytes,
+             uint8_t* __restrict__ out, uint32_t* err) {
+  // the LUT at the start of the big LDS array: its reads need no base add
+  // (a base past 64 KB does not fit the ds_read offset field)
+  __shared__ uint64_t smem[kLut / 4 + (kMaxCoded + 1 + 16 + 7) / 8];
+  uint16_t* lut = reinterpret_cast<uint16_t*>(smem);
+  uint64_t* coded64 = smem + kLut / 4;
+  __shared__ uint16_t hcode[16];
+  __shared__ uint8_t hlen[16];
+  __shared__ uint8_t dict[16];
+  __shared__ uint32_t eidx[kMaxEsc];
+  __shared__ uint32_t sorted[kMaxEsc];
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t ctotal;
+  __shared__ int ecount;
+  __shared__ int valid;
+  const uint64_t fl = blockIdx.x;
+  const uint64_t f = first_frame + fl;
+  const uint64_t base = f * frame_bytes;
+  const uint64_t len = min(uint64_t(frame_bytes), logical - base);
+  const uint64_t n = len / W;
+  const uint64_t nlo = uint64_t(W - 1) * n;
+  const uint8_t* fr = frames + offsets[fl];
+  const uint64_t extent = offsets[fl + 1] - offsets[fl];
+  if (offsets[fl + 1] < offsets[fl] + kFrameHeader || fr[0] != 2) return;
+  uint8_t* o = out + fl * uint64_t(frame_bytes);
+  const uint32_t n_esc = *reinterpret_cast<const uint32_t*>(fr + 4);
+  if (threadIdx.x < 16) {
+    dict[threadIdx.x] = fr[8 + threadIdx.x];
+    hlen[threadIdx.x] = (fr[24 + threadIdx.x / 2] >> (4 * (threadIdx.x & 1))) & 15;
+  }
+  if (threadIdx.x == 0) ecount = 0;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const uint32_t l = threadIdx.x < 16 ? hlen[threadIdx.x] : 0u;
+    const bool long_code = __ballot(l > uint32_t(kMaxLen)) != 0;
+    const uint32_t code = wave_canonical_code(l < uint32_t(kMaxLen) ? l : uint32_t(kMaxLen));
+    if (threadIdx.x < 16) hcode[threadIdx.x] = uint16_t(code);
+    if (threadIdx.x == 0)
+      valid = !long_code && n % 8 == 0 && n_esc <= uint32_t(kMaxEsc) &&
+              kFrameHeader + nlo + kLaneTable <= extent;
+  }
+  __syncthreads();
+  if (!valid) {
+    if (threadIdx.x == 0) flag_corrupt(err);
+    return;
+  }
+  for (int x = threadIdx.x; x < kLut; x += kThreads) {
+    uint32_t ent = kEntBad | uint32_t(kMaxLen);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const uint32_t l = hlen[c];
+      if (l && (uint32_t(x) & ((1u << l) - 1)) == hcode[c])
+        ent = (c == kEsc ? kEntEsc : uint32_t(dict[c]) << 8) | l;
+    }
+    lut[x] = uint16_t(ent);
+  }
+  const uint8_t* body = fr + kFrameHeader;
+  const uint8_t* lo = body;
+  const uint32_t lb = reinterpret_cast<const uint16_t*>(body + nlo)[threadIdx.x];
+  const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);  // (its barriers order the LUT)
+  const uint32_t c_bytes = ctotal;
+  const uint64_t tail_len = len - W * n;
+  if (c_bytes > kMaxCoded ||
+      kFrameHeader + nlo + kLaneTable + c_bytes + n_esc + tail_len > extent) {
+    if (threadIdx.x == 0) flag_corrupt(err);
+    return;  // uniform across the workgroup (ctotal is shared)
+  }
+  const uint8_t* streams = body + nlo + kLaneTable;
+  const uint64_t groups = n / 8;
+  const bool vec = ((reinterpret_cast<uintptr_t>(o) & 15) | (reinterpret_cast<uintptr_t>(lo) & 7)) == 0;
+  {
+    uint8_t* coded = reinterpret_cast<uint8_t*>(coded64);
+    if ((reinterpret_cast<uintptr_t>(streams) & 15) == 0) {
+      // every 16-B load of a thread in flight at once (<= 16): one HBM round trip
+      const uint32_t n16 = c_bytes / 16;
+      const uint4* s16 = reinterpret_cast<const uint4*>(streams);
+      uint4* d16 = reinterpret_cast<uint4*>(coded);
+      uint4 t[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t i = threadIdx.x + q * kThreads;
+        t[q] = i < n16 ? s16[i] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t i = threadIdx.x + q * kThreads;
+        if (i < n16) d16[i] = t[q];
+      }
+      for (uint32_t j = n16 * 16 + threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
+    } else {
+      for (uint32_t j = threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
+    }
+    if (threadIdx.x < 16) coded[c_bytes + threadIdx.x] = 0;
+    __syncthreads();
+  }
+  // window = stream bits << 1 (bit 0 is always 0, so `lo & 0xffe` is the
+  // LUT's byte offset); nb = valid stream bits in it
+  uint32_t wlo = 0, whi = 0;
+  int nb = 0;
+  uint32_t pos = loff;
+  uint32_t allfl = 0;
+  const uint8_t* lut8 = reinterpret_cast<const uint8_t*>(lut);
+  auto group = [&](uint64_t g, const uint64_t* lw, auto vec_tag) {
+    constexpr bool kVec = decltype(vec_tag)::value;
+    uint32_t ent[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (e == 0 || e == 5) {  // every lane at the same points: top up to >= 56 bits
+        const uint32_t q = pos >> 3, sh = (pos & 7) * 8;
+        const uint64_t a = coded64[q], b = coded64[q + 1];
+        const uint64_t bits = sh ? (a >> sh) | (b << (64 - sh)) : a;
+        // nb <= 60 here (>= 3 bits went since the last refill), so nb + 1 < 64
+        const uint64_t w = ((uint64_t(whi) << 32) | wlo) | (bits << (nb + 1));
+        wlo = uint32_t(w);
+        whi = uint32_t(w >> 32);
+        const int k = (63 - nb) >> 3;
+        pos += k;
+        nb += 8 * k;
+      }
+      ent[e] = *reinterpret_cast<const uint16_t*>(lut8 + (wlo & (2 * kLut - 2)));
+      wlo = __builtin_amdgcn_alignbit(whi, wlo, ent[e]);  // (uses bits 0-4)
+      whi >>= ent[e] & 31;
+      nb -= int(ent[e] & 15);
+    }
+    const uint32_t fl8 = ent[0] | ent[1] | ent[2] | ent[3] | ent[4] | ent[5] | ent[6] | ent[7];
+    allfl |= fl8;
+    if (fl8 & kEntEsc) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (ent[e] & kEntEsc) {
+          const int k = atomicAdd(&ecount, 1);
+          if (k < kMaxEsc) eidx[k] = uint32_t(g * 8 + e);
+        }
+    }
+    uint32_t wd[2 * W];
+    if constexpr (W == 2) {
+      // dword q = [lo 2q, hi 2q, lo 2q+1, hi 2q+1]
+      const uint32_t lw0 = uint32_t(lw[0]), lw1 = uint32_t(lw[0] >> 32);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t hh = __builtin_amdgcn_perm(ent[2 * q + 1], ent[2 * q], 0x0c0c0501u);
+        wd[q] = __builtin_amdgcn_perm(hh, q < 2 ? lw0 : lw1, (q & 1) ? 0x05030402u : 0x05010400u);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wd[e] = get_lo<W>(lw, e) | (((ent[e] >> 8) & 255u) << (8 * (W - 1)));
+    }
+    if constexpr (kVec) {
+#pragma unroll
+      for (int k = 0; k < W / 2; ++k)
+        reinterpret_cast<uint4*>(o)[g * (W / 2) + k] =
+            make_uint4(wd[4 * k], wd[4 * k + 1], wd[4 * k + 2], wd[4 * k + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2 * W; ++q)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) o[8 * W * g + 4 * q + b] = uint8_t(wd[q] >> (8 * b));
+    }
+  };
+  auto run = [&](auto vec_tag) {
+    constexpr bool kVec = decltype(vec_tag)::value;
+    // P > 0: the low bytes of group g + P * kThreads load while group g
+    // decodes (a group's 8 symbols are ~1/4 of an HBM round trip).  Taken when
+    // every lane has a multiple of P groups (all full frames): the loop then
+    // has no branch around its loads, so each wait covers exactly its load.
+    if constexpr (P > 0) {
+      if (groups % (uint64_t(P) * kThreads) == 0) {
+        uint64_t buf[P][W - 1];
+#pragma unroll
+        for (int b = 0; b < P; ++b) load_lo<W>(lo, threadIdx.x + uint64_t(b) * kThreads, kVec, buf[b]);
+        for (uint64_t g0 = threadIdx.x; g0 < groups; g0 += uint64_t(P) * kThreads) {
+#pragma unroll
+          for (int b = 0; b < P; ++b) {
+            const uint64_t g = g0 + uint64_t(b) * kThreads;
+            uint64_t lw[W - 1];
+#pragma unroll
+            for (int k = 0; k < W - 1; ++k) lw[k] = buf[b][k];
+            load_lo<W>(lo, min(g + uint64_t(P) * kThreads, groups - 1), kVec, buf[b]);
+            group(g, lw, vec_tag);
+          }
+        }
+        return;
+      }
+    }
+    for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
+      uint64_t lw[W - 1];
+      load_lo<W>(lo, g, kVec, lw);
+      group(g, lw, vec_tag);
+    }
+  };
+  if (vec) run(std::true_type{});
+  else run(std::false_type{});
+  // a lane may not read past its own stream (host decoder: same check)
+  if ((allfl & kEntBad) || uint64_t(pos - loff) * 8 - uint64_t(nb) > uint64_t(lb) * 8)
+    flag_corrupt(err);
+  __syncthreads();
+  const uint8_t* escv = streams + c_bytes;
+  const int ne = min(min(ecount, kMaxEsc), int(n_esc));
+  for (int i = threadIdx.x; i < ne; i += kThreads) {
+    const uint32_t me = eidx[i];
+    int rank = 0;
+    for (int j = 0; j < ne; ++j) rank += eidx[j] < me;
+    sorted[rank] = me;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ne; i += kThreads) o[W * uint64_t(sorted[i]) + W - 1] = escv[i];
+  if (threadIdx.x < tail_len) o[W * n + threadIdx.x] = escv[n_esc + threadIdx.x];
+}
+
+// HIPSNAPSHOT_HSZ_DECODE2 (A/B switch, read per launch): "lds" = hsz_decode2
+// (-1), "staged" = hsz_decode2g<W, 0> (0), default "staged-pf" =
+// hsz_decode2g<W, 8> (1).
+int hsz_decode2_variant() {
+  const char* v = getenv("HIPSNAPSHOT_HSZ_DECODE2");
+  if (v == nullptr || v[0] == '\0') return 1;
+  if (v[0] == 'l') return -1;
+  return strstr(v, "-pf") != nullptr ? 1 : 0;
+}
+
 thread_local char g_hsz_err[256];
 
 int fail(const char* what, hipError_t e) {
@@ -1479,12 +1731,18 @@ int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t fi
     case 8: hipLaunchKernelGGL(hsz_decode<8>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o, ew); break;
     default: return -1001;
   }
-  if (w == 2)
-    hipLaunchKernelGGL(hsz_decode2<2>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical,
-                       frame_bytes, o, ew);
-  else if (w == 4)
-    hipLaunchKernelGGL(hsz_decode2<4>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical,
-                       frame_bytes, o, ew);
+  const int v2 = hsz_decode2_variant();
+#define HSZ_D2(K) hipLaunchKernelGGL(K, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o, ew)
+  if (w == 2) {
+    if (v2 < 0) HSZ_D2(hsz_decode2<2>);
+    else if (v2 == 0) HSZ_D2((hsz_decode2g<2, 0>));
+    else HSZ_D2((hsz_decode2g<2, 8>));
+  } else if (w == 4) {
+    if (v2 < 0) HSZ_D2(hsz_decode2<4>);
+    else if (v2 == 0) HSZ_D2((hsz_decode2g<4, 0>));
+    else HSZ_D2((hsz_decode2g<4, 8>));
+  }
+#undef HSZ_D2
   e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("hsz decode launch", e);
 }

@@ -704,11 +704,15 @@ def _corruptions(blob: bytes, w: int):
     return out
 
 
+@pytest.mark.parametrize("variant", ["staged", "staged-pf", "lds"])
 @pytest.mark.parametrize("w", [2, 4])
-def test_hsz_gpu_decode_rejects_corrupt_frames(gpu, w):
+def test_hsz_gpu_decode_rejects_corrupt_frames(gpu, w, variant, monkeypatch):
     """Every frame the host decoder rejects (-74) makes the GPU decode raise
-    too, instead of leaving the output unwritten."""
+    too, instead of leaving the output unwritten; for each mode-2
+    decoder (HIPSNAPSHOT_HSZ_DECODE2)."""
     from hipsnapshot.ops import codec
+
+    monkeypatch.setenv("HIPSNAPSHOT_HSZ_DECODE2", variant)
 
     g = torch.Generator().manual_seed(3)
     x = (torch.randn(3 * 65536 // w, generator=g) * 0.02)
@@ -729,6 +733,34 @@ def test_hsz_gpu_decode_rejects_corrupt_frames(gpu, w):
     out = torch.empty(len(raw), dtype=torch.uint8, device=gpu)
     codec.decode_device_into(d, codec.parse_header(blob), out, int(s.cuda_stream))
     assert out.cpu().numpy().tobytes() == raw
+
+
+@pytest.mark.parametrize("variant", ["staged", "staged-pf", "lds"])
+@pytest.mark.parametrize("w", [2, 4])
+def test_hsz_gpu_decode_variants_bit_exact(gpu, w, variant, monkeypatch):
+    """Each mode-2 decoder reproduces the input bit for bit: escapes (values
+    outside the 15-entry dictionary), a short last frame with tail bytes, and
+    an output that is not 16-B aligned (byte-store path)."""
+    from hipsnapshot.ops import codec
+
+    monkeypatch.setenv("HIPSNAPSHOT_HSZ_DECODE2", variant)
+    g = torch.Generator().manual_seed(11)
+    n = (5 * 65536 + 4 * 1000 + 8) // w
+    x = torch.randn(n, generator=g) * 0.02
+    x[::97] *= 1e-6   # tiny exponents: escapes
+    x[::1013] *= 1e4  # large exponents: escapes
+    x = x.to(torch.bfloat16) if w == 2 else x
+    raw = x.view(torch.uint8).numpy().tobytes() + b"\x01\x02\x03"[: (w - 1)]
+    blob = codec.encode_reference(raw, w, 64 * 1024)
+    assert 2 in codec.frame_modes(blob)
+    hdr = codec.parse_header(blob)
+    s = torch.cuda.current_stream()
+    d = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(gpu)
+    for shift in (0, 1):
+        buf = torch.full((len(raw) + shift,), 0xAB, dtype=torch.uint8, device=gpu)
+        out = buf[shift:]
+        codec.decode_device_into(d, hdr, out, int(s.cuda_stream))
+        assert out.cpu().numpy().tobytes() == raw, (variant, shift)
 
 
 @pytest.mark.parametrize("direct", [True, False])
