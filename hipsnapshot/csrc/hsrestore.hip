@@ -208,7 +208,11 @@ struct Ring {
       tail = live.front().v1;
       live.pop_front();
     }
-    if (live.empty()) tail = head;
+    // empty: restart at a physical offset of 0.  Otherwise a range longer
+    // than both the space after the old head and the space before it would
+    // never fit an empty ring, and its reader would wait for a release that
+    // cannot come.
+    if (live.empty()) head = tail = (head + cap - 1) / cap * cap;
   }
 };
 

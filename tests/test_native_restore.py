@@ -169,6 +169,31 @@ def test_native_restore_device_budget_smaller_than_items(gpu, tmp_path):
     _eq(dst, src)
 
 
+def test_native_restore_ring_wraps_when_empty(gpu, tmp_path):
+    """A blob that fits the device ring only from its start, after an earlier
+    blob left the (empty) ring's head past the middle: 5 MiB then 6 MiB
+    under an 8 MiB ring (the second used to wait forever)."""
+    from hipsnapshot.engine import native_restore
+    from hipsnapshot.knobs import override_is_batching_disabled
+
+    g = torch.Generator(device=gpu).manual_seed(5)
+    src = StateDict(a=torch.randn(5 << 18, device=gpu, generator=g),
+                    b=torch.randn(6 << 18, device=gpu, generator=g))
+    path = str(tmp_path / "w")
+    with override_is_batching_disabled(True):
+        Snapshot.take(path, {"sd": src})
+    for _ in range(2):  # ring reuse across jobs too
+        dst = _zeros_like_state(src)
+        with override_is_batching_disabled(True), \
+                override_knob("RESTORE_DEVICE_BUDGET", str(8 << 20)), \
+                override_knob("RESTORE_SLOT_BYTES", str(1 << 20)), \
+                override_knob("RESTORE_SLOTS", "2"):
+            Snapshot(path).restore({"sd": dst})
+        torch.cuda.synchronize()
+        assert native_restore.last_stats.get("items", 0) == 2
+        _eq(dst, src)
+
+
 def test_restore_plan_cache_hits_and_invalidates(gpu, tmp_path):
     """A second restore of the same snapshot into the same tensors reuses the
     native plan; a new take at the path, or a replaced tensor, plans again."""
