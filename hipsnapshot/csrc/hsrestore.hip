@@ -808,13 +808,22 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
       return nullptr;
     }
   }
-  // the destinations' producers: their queued work finishes before ours
+  // the destinations' producers: their queued work finishes before ours (a
+  // failure here would let the copies race it: the job does not start)
   for (int p = 0; p < n_producers; ++p) {
     hipEvent_t ev;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) continue;
-    if (hipEventRecord(ev, reinterpret_cast<hipStream_t>(producers[p])) == hipSuccess)
-      for (int s = 0; s < 2; ++s) (void)hipStreamWaitEvent(j->streams[s], ev, 0);
-    hipEventDestroy(ev);
+    bool ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+    if (ok) {
+      ok = hipEventRecord(ev, reinterpret_cast<hipStream_t>(producers[p])) == hipSuccess;
+      for (int s = 0; ok && s < 2; ++s) ok = hipStreamWaitEvent(j->streams[s], ev, 0) == hipSuccess;
+      hipEventDestroy(ev);
+    }
+    if (!ok) {
+      (void)hipGetLastError();
+      delete j;
+      *err = -5;
+      return nullptr;
+    }
   }
   // the rings: at most `budget` bytes each, no more than the job needs
   uint64_t need_up = 0, need_sc = 0;
