@@ -938,6 +938,46 @@ int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
   return e;
 }
 
+// Warm the pools a restore job is about to draw from, beside the caller's
+// planning (a process's first restore paid ~5 ms of uncached / pinned
+// allocation in hsg_restore_start and ~7 ms before its first upload):
+// `up_bytes` / `sc_bytes` device ring blocks (0: skip), `nslots` pinned slots
+// of `slot_bytes`, the copy-table blocks of `table_bytes`, and one small SDMA
+// upload (the engine path's first use).  Everything goes back to the pools.
+// Returns 0, or -1 if an allocation failed (the job then allocates itself).
+int hsg_restore_prewarm(int dev, uint64_t up_bytes, uint64_t sc_bytes, uint64_t slot_bytes,
+                        int nslots, uint64_t table_bytes) {
+  if (hipSetDevice(dev) != hipSuccess) return -1;
+  int rc = 0;
+  void* up = up_bytes ? g_upload_pool.acquire(dev, up_bytes) : nullptr;
+  void* sc = sc_bytes ? g_scratch_pool.acquire(dev, sc_bytes) : nullptr;
+  if ((up_bytes && !up) || (sc_bytes && !sc)) rc = -1;
+  void* ws = table_bytes ? g_scratch_pool.acquire(dev, table_bytes) : nullptr;
+  void* st = table_bytes ? hsg_pinned_acquire(table_bytes) : nullptr;
+  std::vector<void*> slots;
+  const uint64_t sb = (std::max<uint64_t>(slot_bytes, 1 << 20) + 4095) / 4096 * 4096;
+  for (int s = 0; s < nslots; ++s) {
+    void* p = hsg_pinned_acquire(sb);
+    if (!p) {
+      rc = -1;
+      break;
+    }
+    slots.push_back(p);
+  }
+  void* probe = up ? up : g_upload_pool.acquire(dev, kGranule);
+  if (probe && !slots.empty()) {
+    uint64_t h = 0;
+    if (hsg_sdma_h2d_submit_on(dev, probe, slots[0], 64 << 10, -1, &h) == 0) (void)hsg_sdma_wait(h);
+  }
+  if (probe != up) g_upload_pool.release(probe);
+  for (void* p : slots) hsg_pinned_release(p);
+  if (st) hsg_pinned_release(st);
+  g_scratch_pool.release(ws);
+  g_scratch_pool.release(sc);
+  g_upload_pool.release(up);
+  return rc;
+}
+
 // Free idle device blocks of the restore pools until at most `keep` idle
 // bytes remain in each (per call; -1 device = all).  Returns bytes freed.
 uint64_t hsg_restore_trim(int dev, uint64_t keep) {

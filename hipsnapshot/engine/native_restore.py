@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import logging
 import os
+import threading
 import time
 from collections import defaultdict
 from typing import Dict, List, Optional, Tuple
@@ -187,10 +188,103 @@ def split(read_reqs: List[ReadReq], storage: StoragePlugin, budget: Optional[int
     return dict(jobs), py
 
 
+_prewarm: Optional[threading.Thread] = None
+_prewarm_lock = threading.Lock()
+
+
+def table_bytes(slot: int) -> int:
+    """The job's copy-table ring size (csrc/hsrestore.hip kTables)."""
+    return min(32 << 20, max(1 << 20, slot // 4))
+
+
+def prewarm_async(dev: int, dest_bytes: int, compressed: bool,
+                  budget: Optional[int] = None) -> None:
+    """Start filling the restore pools for a job of ~``dest_bytes`` bytes
+    into device ``dev`` on a thread, beside the caller's read planning (a
+    process's first restore paid ~12 ms of pinned / uncached allocation and
+    first-SDMA setup inside the job).  The device rings are warmed only when
+    the job will use a whole budget's worth (smaller rings are cheap and a
+    budget-sized block would not be reused for them); ``run`` joins it."""
+    global _prewarm
+    if dest_bytes <= 0 or not knobs.native_restore_enabled() or \
+            not knobs.restore_prewarm_enabled() or not native.gpu_available():
+        return
+    slot, _first, nslots = sizing(budget)
+    dev_budget = knobs.get_restore_device_budget()
+    ring = dev_budget if dest_bytes >= 2 * dev_budget else 0
+    # the job takes 2 slots at its start and allocates the rest on a helper
+    # thread while its readers run: only those 2 are on its critical path
+    n = 2
+    with _prewarm_lock:
+        if _prewarm is not None:
+            return
+
+        def work():
+            t0 = time.perf_counter()
+            rc = native.restore_prewarm(dev, ring, ring if compressed else 0, slot, n,
+                                        table_bytes(slot))
+            timeline.add("native_restore_prewarm", "phase", t0, time.perf_counter(), rc=rc,
+                         ring=ring, slots=n)
+
+        _prewarm = threading.Thread(target=work, name="hs-restore-prewarm", daemon=True)
+        _prewarm.start()
+
+
+def _has_codec(entry, depth: int = 0) -> bool:
+    if getattr(entry, "codec", None):
+        return True
+    if depth < 3:
+        for attr in ("shards", "chunks"):
+            for sub in getattr(entry, attr, None) or ():
+                if _has_codec(getattr(sub, "tensor", sub), depth + 1):
+                    return True
+    return False
+
+
+def prewarm_for(leaves, entries, budget: Optional[int] = None) -> None:
+    """``prewarm_async`` for a restore into ``leaves`` (the stateful's
+    tensors / DTensors) of manifest ``entries``: the device and bytes are
+    those of the HBM destinations."""
+    try:
+        from torch.distributed.tensor import DTensor
+    except Exception:  # pragma: no cover
+        DTensor = ()  # type: ignore[assignment]
+    per_dev: Dict[int, int] = defaultdict(int)
+    import torch
+
+    for v in leaves:
+        if DTensor and isinstance(v, DTensor):
+            t = v._local_tensor
+        elif type(v) is torch.Tensor or type(v) is torch.nn.Parameter:
+            t = v
+        else:  # ShardedTensor & co: not counted (an estimate only)
+            continue
+        if t.is_cuda:
+            per_dev[t.device.index or 0] += t.numel() * t.element_size()
+    if not per_dev:
+        return
+    dev, nbytes = max(per_dev.items(), key=lambda kv: kv[1])
+    prewarm_async(dev, nbytes, any(_has_codec(e) for e in entries), budget)
+
+
+def join_prewarm() -> None:
+    """Wait for a pending prewarm (a restore that ran no native job)."""
+    _join_prewarm()
+
+
+def _join_prewarm() -> None:
+    global _prewarm
+    with _prewarm_lock:
+        t, _prewarm = _prewarm, None
+    if t is not None:
+        t.join()
+
+
 def run(jobs: Dict[int, list], budget: Optional[int] = None) -> int:
     """Run the planned jobs (blocking; call off the event loop); returns the
     logical bytes restored.  Raises ``CorruptBlobError`` for rejected frames,
     ``OSError`` / ``HipError`` for other failures."""
+    _join_prewarm()
     total = 0
     slot, first, nslots = sizing(budget)
     for dev, entries in jobs.items():

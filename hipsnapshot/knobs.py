@@ -29,6 +29,14 @@ MI355X-specific knobs:
   ``_DRAIN_SLOTS`` (16), ``_DRAIN_WRITERS`` (min(16, io threads, half the rank's CPU share)),
   ``_DRAIN_NICE`` (10: nice increment of its threads), ``_DRAIN_DIRECT_IO`` (0:
   O_DIRECT files, no page-cache copy).
+* ``HIPSNAPSHOT_NATIVE_RESTORE`` (1) -- reads landing in HBM go through one
+  native job per device (``csrc/hsrestore.hip``): ``_RESTORE_SLOT_BYTES``
+  (128 MiB), ``_RESTORE_FIRST_BYTES`` (16 MiB), ``_RESTORE_PIECE_BYTES``
+  (4 MiB), ``_RESTORE_SLOTS`` (6), ``_RESTORE_READERS``,
+  ``_RESTORE_DEVICE_BUDGET`` (2 GiB), ``_RESTORE_KEEP_BYTES`` (2.25 GiB),
+  ``_RESTORE_PREWARM`` (1: fill its pools while the reads are planned),
+  ``_RESTORE_PLAN_CACHE`` (1), ``_HSZ_DECODE2`` (``staged-pf``; ``lds`` = the
+  round-3 HSZ1 decoder).
 * ``HIPSNAPSHOT_ASYNC_DEVICE_CODEC`` (raw) -- ``same``: an async take encodes
   its frozen device state like a blocking take.
 * ``HIPSNAPSHOT_GC_AFTER_PLAN`` (1) -- one full Python GC pass at the end of a
@@ -445,6 +453,13 @@ def native_restore_enabled() -> bool:
     (engine/native_restore.py, csrc/hsrestore.hip): pread -> pinned slots ->
     SDMA uploads -> GPU decode / region copy, no Python per blob."""
     return _get_bool("NATIVE_RESTORE", True)
+
+
+def restore_prewarm_enabled() -> bool:
+    """A restore into HBM fills the native job's pinned slots and device
+    rings on a thread while it plans its reads (engine/native_restore.py
+    prewarm_for)."""
+    return _get_bool("RESTORE_PREWARM", True)
 
 
 def restore_plan_cache_enabled() -> bool:

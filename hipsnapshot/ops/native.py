@@ -210,8 +210,16 @@ def address_of(buf) -> int:
 # _hsgpu.so
 # ---------------------------------------------------------------------------
 
+_gpu_seen = False
+
+
 def gpu_available() -> bool:
-    return torch.cuda.is_available()
+    """torch.cuda.is_available(), remembered once true (it is asked per
+    destination while a restore is planned)."""
+    global _gpu_seen
+    if not _gpu_seen:
+        _gpu_seen = torch.cuda.is_available()
+    return _gpu_seen
 
 
 def _load_hsgpu() -> Optional[ctypes.CDLL]:
@@ -280,6 +288,8 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_restore_wait", c_int,
                  [c_void_p, P(c_int), c_char_p, P(ctypes.c_double), P(c_uint64)])
         _declare(lib, "hsg_restore_trim", c_uint64, [c_int, c_uint64])
+        _declare(lib, "hsg_restore_prewarm", c_int,
+                 [c_int, c_uint64, c_uint64, c_uint64, c_int, c_uint64])
         _declare(lib, "hsg_sdma_h2d_submit", c_int,
                  [c_int, c_void_p, c_void_p, c_uint64, P(c_uint64)])
         _declare(lib, "hsg_is_managed", c_int, [c_void_p])
@@ -976,6 +986,14 @@ def _give_err_words(t: torch.Tensor) -> None:
 def restore_trim(dev: int, keep_bytes: int) -> int:
     """Free idle restore device blocks beyond ``keep_bytes`` per pool."""
     return int(require_gpu_lib().hsg_restore_trim(dev, keep_bytes))
+
+
+def restore_prewarm(dev: int, up_bytes: int, sc_bytes: int, slot_bytes: int, nslots: int,
+                    table_bytes: int) -> int:
+    """Fill the restore pools with what a job is about to take (blocking;
+    ctypes drops the GIL): 0, or -1 when an allocation failed."""
+    return int(require_gpu_lib().hsg_restore_prewarm(dev, up_bytes, sc_bytes, slot_bytes,
+                                                     nslots, table_bytes))
 
 
 def managed_location(ptr: int, nbytes: int) -> Tuple[int, int]:

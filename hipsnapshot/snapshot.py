@@ -662,6 +662,9 @@ class Snapshot:
                 with timeline.span("read_pipeline", cached=True):
                     restore_cache.run(plan, get_process_memory_budget_bytes(comm))
                 return
+        budget = get_process_memory_budget_bytes(comm)
+        # the native job's pinned slots / device rings fill beside the planning
+        native_restore.prewarm_for(flat.values(), manifest.values(), budget)
         containers: Dict[str, Entry] = {}
         reads: List[ReadReq] = []
         futs = {}
@@ -679,11 +682,11 @@ class Snapshot:
             if not knobs.is_batching_disabled():
                 reads = batch_read_requests(reads)
             reads = order_reads_for_pipeline(reads)
-        budget = get_process_memory_budget_bytes(comm)
         native_jobs, py_reads = native_restore.split(reads, storage, budget)
         with timeline.span("read_pipeline", n=len(reads)):
             sync_execute_read_reqs(py_reads, storage, budget, comm.get_rank(), loop,
                                    native_jobs=native_jobs)
+        native_restore.join_prewarm()
         with timeline.span("load_state_dict", n=len(futs)):
             objs = {k: f.obj for k, f in futs.items()}
             # every leaf was read into the module's own tensor: load_state_dict

@@ -54,3 +54,22 @@ def test_drain_booster_reaches_running_and_later_jobs():
     c = Job()
     other.attach(c)
     assert c.boosted == 0  # another take's drain keeps its parked writers
+
+
+def test_prewarm_skips_without_gpu_and_codec_detection():
+    """prewarm_for is a no-op without HBM destinations / GPU; _has_codec sees
+    codecs of nested shard entries."""
+    import torch
+
+    from hipsnapshot.engine import native_restore
+    from hipsnapshot.format.manifest import Shard, ShardedTensorEntry, TensorEntry
+
+    native_restore.prewarm_for([torch.zeros(4)], [], None)  # CPU leaves: nothing starts
+    assert native_restore._prewarm is None
+    plain = TensorEntry("a", "torch_save", "torch.float32", [4], False)
+    coded = TensorEntry("b", "buffer_protocol", "torch.bfloat16", [4], False,
+                        codec={"name": "hsz1"})
+    assert not native_restore._has_codec(plain)
+    assert native_restore._has_codec(coded)
+    assert native_restore._has_codec(ShardedTensorEntry([Shard([0], [4], coded)]))
+    assert not native_restore._has_codec(ShardedTensorEntry([Shard([0], [4], plain)]))
