@@ -1440,6 +1440,13 @@ hsz_decode2g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ of
     hlen[threadIdx.x] = (fr[24 + threadIdx.x / 2] >> (4 * (threadIdx.x & 1))) & 15;
   }
   if (threadIdx.x == 0) ecount = 0;
+  // the lane table's load overlaps the header's (bounds checked here; the
+  // frame is rejected below when it is short)
+  const uint8_t* body = fr + kFrameHeader;
+  const uint8_t* lo = body;
+  uint32_t lb = 0;
+  if (kFrameHeader + nlo + kLaneTable <= extent)
+    lb = reinterpret_cast<const uint16_t*>(body + nlo)[threadIdx.x];
   __syncthreads();
   if (threadIdx.x < 64) {
     const uint32_t l = threadIdx.x < 16 ? hlen[threadIdx.x] : 0u;
@@ -1455,20 +1462,7 @@ hsz_decode2g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ of
     if (threadIdx.x == 0) flag_corrupt(err);
     return;
   }
-  for (int x = threadIdx.x; x < kLut; x += kThreads) {
-    uint32_t ent = kEntBad | uint32_t(kMaxLen);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const uint32_t l = hlen[c];
-      if (l && (uint32_t(x) & ((1u << l) - 1)) == hcode[c])
-        ent = (c == kEsc ? kEntEsc : uint32_t(dict[c]) << 8) | l;
-    }
-    lut[x] = uint16_t(ent);
-  }
-  const uint8_t* body = fr + kFrameHeader;
-  const uint8_t* lo = body;
-  const uint32_t lb = reinterpret_cast<const uint16_t*>(body + nlo)[threadIdx.x];
-  const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);  // (its barriers order the LUT)
+  const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);
   const uint32_t c_bytes = ctotal;
   const uint64_t tail_len = len - W * n;
   if (c_bytes > kMaxCoded ||
@@ -1479,30 +1473,39 @@ hsz_decode2g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ of
   const uint8_t* streams = body + nlo + kLaneTable;
   const uint64_t groups = n / 8;
   const bool vec = ((reinterpret_cast<uintptr_t>(o) & 15) | (reinterpret_cast<uintptr_t>(lo) & 7)) == 0;
-  {
-    uint8_t* coded = reinterpret_cast<uint8_t*>(coded64);
-    if ((reinterpret_cast<uintptr_t>(streams) & 15) == 0) {
-      // every 16-B load of a thread in flight at once (<= 16): one HBM round trip
-      const uint32_t n16 = c_bytes / 16;
-      const uint4* s16 = reinterpret_cast<const uint4*>(streams);
-      uint4* d16 = reinterpret_cast<uint4*>(coded);
-      uint4 t[16];
+  // the streams' 16-B loads (all of a thread's in flight at once) are issued
+  // before the LUT is built and land in LDS after it: the HBM round trip
+  // hides behind the LUT's VALU work
+  uint8_t* coded = reinterpret_cast<uint8_t*>(coded64);
+  const bool s16_ok = (reinterpret_cast<uintptr_t>(streams) & 15) == 0;
+  const uint32_t n16 = s16_ok ? c_bytes / 16 : 0;
+  const uint4* s16 = reinterpret_cast<const uint4*>(streams);
+  uint4 t[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const uint32_t i = threadIdx.x + q * kThreads;
-        t[q] = i < n16 ? s16[i] : make_uint4(0u, 0u, 0u, 0u);
-      }
+  for (int q = 0; q < 16; ++q) {
+    const uint32_t i = threadIdx.x + q * kThreads;
+    t[q] = i < n16 ? s16[i] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  for (int x = threadIdx.x; x < kLut; x += kThreads) {
+    uint32_t ent = kEntBad | uint32_t(kMaxLen);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const uint32_t i = threadIdx.x + q * kThreads;
-        if (i < n16) d16[i] = t[q];
-      }
-      for (uint32_t j = n16 * 16 + threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
-    } else {
-      for (uint32_t j = threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
+    for (int c = 0; c < 16; ++c) {
+      const uint32_t l = hlen[c];
+      if (l && (uint32_t(x) & ((1u << l) - 1)) == hcode[c])
+        ent = (c == kEsc ? kEntEsc : uint32_t(dict[c]) << 8) | l;
     }
+    lut[x] = uint16_t(ent);
+  }
+  {
+    uint4* d16 = reinterpret_cast<uint4*>(coded);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t i = threadIdx.x + q * kThreads;
+      if (i < n16) d16[i] = t[q];
+    }
+    for (uint32_t j = n16 * 16 + threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
     if (threadIdx.x < 16) coded[c_bytes + threadIdx.x] = 0;
-    __syncthreads();
+    __syncthreads();  // orders the LUT and the staged streams before any read
   }
   // window = stream bits << 1 (bit 0 is always 0, so `lo & 0xffe` is the
   // LUT's byte offset); nb = valid stream bits in it
