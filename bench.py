@@ -82,7 +82,7 @@ def _free_port() -> int:
 
 
 def _default_dir() -> str:
-    for cand in (os.environ.get("HIPSNAPSHOT_BENCH_DIR"), "/var/tmp", "/tmp"):
+    for cand in (os.environ.get("HSBENCH_DIR"), "/var/tmp", "/tmp"):
         if cand and os.path.isdir(cand) and os.access(cand, os.W_OK):
             return os.path.join(cand, "hipsnapshot_bench")
     return "hipsnapshot_bench"
@@ -150,11 +150,11 @@ def _check_resharded(model, old: list, dev: int) -> list:
 
 
 def _selftest_hook(rank: int) -> None:
-    """``HIPSNAPSHOT_BENCH_SELFTEST`` (launcher tests on CPU, before any
+    """``HSBENCH_SELFTEST`` (launcher tests on CPU, before any
     torch import): ``ok`` -- rank 0 prints a JSON line, every rank exits 0;
     ``fail:<r>`` -- rank r exits 3 at once, the others block as a rank stuck
     in the rendezvous would."""
-    mode = os.environ.get("HIPSNAPSHOT_BENCH_SELFTEST")
+    mode = os.environ.get("HSBENCH_SELFTEST")
     if not mode:
         return
     if mode == "ok":

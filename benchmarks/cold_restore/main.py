@@ -89,7 +89,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--role", default=None, choices=["save", "restore"])
     ap.add_argument("--path", default=None)
-    ap.add_argument("--dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
     ap.add_argument("--restores", type=int, default=2)
     ap.add_argument("--port", type=int, default=29571)

@@ -27,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-params", type=int, default=200)
     ap.add_argument("--param-mb", type=int, default=100)
-    ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--work-dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     ap.add_argument("--torch-save", action="store_true")
     ap.add_argument("--repeats", type=int, default=2)
     ap.add_argument("--compression", default="none", choices=["none", "hsz1"],

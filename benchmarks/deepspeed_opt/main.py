@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--heads", type=int, default=56)
     ap.add_argument("--max-total-gb", type=float, default=40.0,
                     help="shrink the layer count so the whole snapshot fits this size")
-    ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--work-dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     ap.add_argument("--torch-save", action="store_true")
     ap.add_argument("--no-load", action="store_true")
     args = ap.parse_args()

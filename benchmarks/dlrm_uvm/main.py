@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--sharding", default="row", choices=["row", "column", "table"])
     ap.add_argument("--uvm-place", default=None, choices=["host", "device"],
                     help="advise + prefetch the UVM tables to host DRAM or HBM first")
-    ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--work-dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     ap.add_argument("--single-path", action="store_true",
                     help="every take rewrites ONE snapshot path (100 GB runs: one copy on storage)")
     args = ap.parse_args()

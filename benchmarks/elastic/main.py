@@ -49,7 +49,7 @@ def checksums(model):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--phase", choices=["save", "restore"], required=True)
-    ap.add_argument("--path", default=os.path.join(os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"),
+    ap.add_argument("--path", default=os.path.join(os.environ.get("HSBENCH_DIR", "/tmp"),
                                                    "hs_elastic"))
     ap.add_argument("--model", default="llama3_8b")
     ap.add_argument("--layers", type=int, default=None)

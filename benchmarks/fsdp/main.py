@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--dec-layers", type=int, default=20)
     ap.add_argument("--nhead", type=int, default=12)
     ap.add_argument("--ffn", type=int, default=50257)
-    ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--work-dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     ap.add_argument("--torch-save", action="store_true")
     ap.add_argument("--repeats", type=int, default=2)
     args = ap.parse_args()

@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=50000)
     ap.add_argument("--budget-mb", type=int, default=100)
-    ap.add_argument("--work-dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--work-dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     args = ap.parse_args()
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     t = torch.randn(args.n, args.n, device=dev)

@@ -218,9 +218,9 @@ def main():
             info = quant.fp8_entry_quant_info(w, rotation="none")
             assert quant.is_mx(info)
         else:
-            os.environ["HIPSNAPSHOT_FP8_SCALE"] = "fp32"
+            os.environ["HIPSNAPSHOT_FP8_FORMAT"] = "block"
             info = quant.fp8_entry_quant_info(w, rotation=mode)
-            del os.environ["HIPSNAPSHOT_FP8_SCALE"]
+            del os.environ["HIPSNAPSHOT_FP8_FORMAT"]
         blob = torch.zeros(info["total_bytes"], dtype=torch.uint8, device="cuda:0")
         payload = info["payload_bytes"]
         scales = blob[payload:] if mode == "mx_e8m0" else blob[payload:].view(torch.float32)

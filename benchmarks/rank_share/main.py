@@ -49,7 +49,7 @@ def main() -> None:
     ap.add_argument("--async-iters", type=int, default=5)
     ap.add_argument("--restore-iters", type=int, default=3)
     ap.add_argument("--compression", default="hsz1", choices=["none", "hsz1"])
-    ap.add_argument("--dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     ap.add_argument("--ab", default=None,
                     help="NAME=v1,v2[,...]: alternate env var NAME over the values take by "
                          "take (same process, interleaved) and report each value's takes")

@@ -31,7 +31,7 @@ def main():
         opt.zero_grad()
         loss.backward()
         opt.step()
-    root = os.path.join(os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"), "hs_resnet")
+    root = os.path.join(os.environ.get("HSBENCH_DIR", "/tmp"), "hs_resnet")
     if rank == 0:
         shutil.rmtree(root, ignore_errors=True)
     sync(dev)

@@ -191,7 +191,7 @@ def main() -> None:
                 "endpoint_url": url[0], "multipart_threshold": 64 << 20, "part_size": 64 << 20}
         root = "s3://ckpt/train_overlap"
     else:
-        root = args.path or os.path.join(os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"),
+        root = args.path or os.path.join(os.environ.get("HSBENCH_DIR", "/tmp"),
                                          "train_overlap")
         if rank == 0:
             shutil.rmtree(root, ignore_errors=True)

@@ -19,7 +19,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 HSIO_SO = os.path.join(PKG_DIR, "_hsio.so")
 HSGPU_SO = os.path.join(PKG_DIR, "_hsgpu.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
-GPU_ARCH = os.environ.get("HIPSNAPSHOT_GPU_ARCH", "gfx950")
+GPU_ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
 
 def _stale(out: str, srcs) -> bool:
@@ -52,9 +52,11 @@ def build_hsio(force: bool = False) -> str:
 
 
 def build_hsgpu(force: bool = False) -> str:
+    # hsdrain.cpp / hsrestore.cpp are host-only engines (their HIP calls sit
+    # in hshost.hip); hipcc builds them as plain C++ into the same library
     srcs = [os.path.join(CSRC, "hsgpu.hip"), os.path.join(CSRC, "hsz.hip"),
-            os.path.join(CSRC, "hsdma.hip"), os.path.join(CSRC, "hsdrain.hip"),
-            os.path.join(CSRC, "hsrestore.hip")]
+            os.path.join(CSRC, "hsdma.hip"), os.path.join(CSRC, "hshost.hip"),
+            os.path.join(CSRC, "hsdrain.cpp"), os.path.join(CSRC, "hsrestore.cpp")]
     if force or _stale(HSGPU_SO, srcs):
         hipcc = os.path.join(ROCM, "bin", "hipcc")
         if not os.path.exists(hipcc):

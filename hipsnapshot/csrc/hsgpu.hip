@@ -1538,7 +1538,7 @@ int hsg_pci_location(int dev, int* domain, int* bus, int* device) {
 // (pread into hipHostMalloc memory 88 GB/s, into THP-backed memory 131 GB/s,
 // 16 threads; scripts/probes/pinned_thp_probe.py, profiles/pinned/).  Registering
 // pre-faulted huge pages costs ~2 ms per GiB, once per pool block.  Any
-// failure falls back to hipHostMalloc.  HIPSNAPSHOT_PINNED_THP=0 turns it off.
+// failure falls back to hipHostMalloc.
 
 struct MappedBlock {
   void* base;
@@ -1548,8 +1548,6 @@ std::mutex g_mapped_mu;
 std::unordered_map<void*, MappedBlock> g_mapped;  // registered block -> its mapping
 
 void* alloc_thp_registered(size_t want) {
-  const char* v = getenv("HIPSNAPSHOT_PINNED_THP");
-  if (v != nullptr && v[0] == '0') return nullptr;
   constexpr size_t kHuge = size_t(2) << 20;
   const size_t len = want + kHuge;
   void* base = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
@@ -1559,12 +1557,10 @@ void* alloc_thp_registered(size_t want) {
   // fault every page in now (a huge page per 2 MiB where the kernel grants
   // one): registration then maps resident pages, and no copy pays a fault.
   // The kernel zeroes each page on its first touch; a large block is split
-  // over a few threads (HIPSNAPSHOT_PINNED_FAULT_THREADS, default 4) so a
-  // cold process's first blocks -- a restore's first reads -- wait less.
+  // over 4 threads so a cold process's first blocks -- a restore's first
+  // reads -- wait less.
   const size_t kSplit = size_t(32) << 20;
-  int nt = 4;
-  if (const char* fv = getenv("HIPSNAPSHOT_PINNED_FAULT_THREADS")) nt = std::max(1, atoi(fv));
-  nt = static_cast<int>(std::min<size_t>(size_t(nt), std::max<size_t>(1, want / kSplit)));
+  const int nt = static_cast<int>(std::min<size_t>(4, std::max<size_t>(1, want / kSplit)));
   auto touch = [p](size_t lo, size_t hi) {
     for (size_t off = lo; off < hi; off += 4096) p[off] = 0;
   };

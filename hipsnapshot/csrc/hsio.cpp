@@ -119,14 +119,8 @@ class Engine {
   explicit Engine(int nthreads) {
     efd_ = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     if (nthreads < 1) nthreads = 1;
-    // HIPSNAPSHOT_IO_NICE: workers run at this nice value (page-cache copies
-    // are CPU work: a background drain's writers then yield to the training
-    // thread that launches the GPU work; alone, they still get every CPU)
-    const char* nv = getenv("HIPSNAPSHOT_IO_NICE");
-    const int nice = nv != nullptr ? atoi(nv) : 0;
     for (int i = 0; i < nthreads; ++i)
-      workers_.emplace_back([this, nice] {
-        if (nice != 0) ::setpriority(PRIO_PROCESS, static_cast<id_t>(::syscall(SYS_gettid)), nice);
+      workers_.emplace_back([this] {
         Run();
       });
   }

@@ -29,8 +29,13 @@
 // Reference behaviour being replaced: `/root/reference/torchsnapshot/
 // scheduler.py:384-444` (read pipeline) and `io_preparers/tensor.py:294-346`
 // (buffer consumers copying into the target tensors).
-
-#include <hip/hip_runtime.h>
+//
+// Host code only: every device operation goes through a C hook -- SDMA,
+// decode and copy launches in hsdma.hip / hsz.hip / hsgpu.hip, the HIP
+// runtime calls (device, memory, events, streams) in hshost.hip -- so this
+// engine also builds without HIP, against the stubs of
+// tests/native/engine_stubs.cpp, under ThreadSanitizer and AddressSanitizer
+// (tests/test_native_sanitizers.py).
 
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -69,6 +74,14 @@ int hsg_copy_nd(int dev, const void* descs, int n, void* workspace, uint64_t ws_
                 void* pinned_stage, void* stream, int sync);
 uint64_t hsg_desc_size();
 void* hsg_copy_stream(int dev, int slot);
+int hsg_rt_set_device(int dev);
+void* hsg_rt_dev_alloc(int dev, uint64_t nbytes, int uncached);
+void hsg_rt_dev_free(void* p);
+void* hsg_rt_event_record(void* stream);
+int hsg_rt_event_sync(void* ev);
+void hsg_rt_event_free(void* ev);
+int hsg_rt_stream_after(void* waiter, void* producer);
+int hsg_rt_stream_sync(void* stream);
 }
 
 namespace {
@@ -96,9 +109,9 @@ struct DevPool {
   std::map<int, std::multimap<uint64_t, void*>> free_blocks;
   std::unordered_map<void*, std::pair<int, uint64_t>> live;
   uint64_t idle_bytes = 0;
-  unsigned flags;  // hipExtMallocWithFlags flags (0 = hipMalloc)
+  int uncached;  // device-uncached blocks (SDMA upload targets)
 
-  explicit DevPool(unsigned f) : flags(f) {}
+  explicit DevPool(int u) : uncached(u) {}
 
   void* acquire(int dev, uint64_t nbytes) {
     const uint64_t want = (std::max<uint64_t>(nbytes, 1) + kGranule - 1) / kGranule * kGranule;
@@ -115,12 +128,9 @@ struct DevPool {
       }
     }
     void* p = nullptr;
-    if (hipSetDevice(dev) != hipSuccess) return nullptr;
     for (int attempt = 0; attempt < 2; ++attempt) {
-      const hipError_t e = flags ? hipExtMallocWithFlags(&p, want, flags) : hipMalloc(&p, want);
-      if (e == hipSuccess) break;
-      p = nullptr;
-      (void)hipGetLastError();
+      p = hsg_rt_dev_alloc(dev, want, uncached);
+      if (p) break;
       if (attempt == 0) trim(dev, 0);  // drop this device's idle blocks and retry
     }
     if (!p) return nullptr;
@@ -158,12 +168,12 @@ struct DevPool {
         }
       }
     }
-    for (void* q : drop) (void)hipFree(q);
+    for (void* q : drop) hsg_rt_dev_free(q);
     return freed;
   }
 };
 
-DevPool g_upload_pool(hipDeviceMallocUncached);
+DevPool g_upload_pool(1);
 DevPool g_scratch_pool(0);
 
 // A job's device memory: one block per kind (uncached upload targets, decode
@@ -248,7 +258,7 @@ struct Item {
   int nchunks = 0;
   std::atomic<int> chunks_left{0};
   std::vector<uint8_t> head;  // HSZ1 header + frame table (from chunk 0)
-  hipEvent_t done = nullptr;
+  void* done = nullptr;  // completion event of the item's device work
 };
 
 struct Chunk {
@@ -297,7 +307,7 @@ struct Job {
   std::vector<uint8_t> descs;  // packed CopyDesc table (sources relative)
   uint64_t desc_size = 0;
   uint32_t* err_words = nullptr;  // host-mapped, one per item
-  hipStream_t streams[2] = {nullptr, nullptr};
+  void* streams[2] = {nullptr, nullptr};
 
   std::vector<void*> slots;
   std::unique_ptr<SlotFill[]> fills;
@@ -334,7 +344,6 @@ struct Job {
   int launched = 0;
   uint64_t busy_since = 0;  // outstanding went non-zero at (kUploadBusy)
   int outstanding = 0;      // uploads submitted and not yet waited for
-  int debug = 0;  // HIPSNAPSHOT_RESTORE_DEBUG: 1 = no preads, 2 = no uploads (timing probes)
 
   std::atomic<int> err{0};
   int err_item = -1;
@@ -399,7 +408,7 @@ int alloc_item_locked(Job* j, int i) {
 int pieces_of(const Job* j, uint64_t n) { return int((n + j->piece_bytes - 1) / j->piece_bytes); }
 
 void reader_thread(Job* j) {
-  (void)hipSetDevice(j->dev);
+  (void)hsg_rt_set_device(j->dev);
   for (;;) {
     int s, i;
     uint64_t poff, pn;
@@ -484,7 +493,6 @@ void reader_thread(Job* j) {
     uint64_t t0 = now_ns();
     uint64_t done = 0;
     int rerr = 0;
-    if (j->debug & 1) done = pn;
     while (done < pn) {
       const ssize_t r = pread(it.fd, p + done, pn - done, off_t(it.file_lo + f.off + poff + done));
       if (r < 0) {
@@ -523,9 +531,8 @@ void reader_thread(Job* j) {
     }
     t0 = now_ns();
     uint64_t h = 0;
-    const int r = (j->debug & 2) ? 0
-                  : hsg_sdma_h2d_submit_on(j->dev, static_cast<char*>(it.block) + f.off, sp,
-                                           f.n, j->engine, &h);
+    const int r = hsg_sdma_h2d_submit_on(j->dev, static_cast<char*>(it.block) + f.off, sp, f.n,
+                                         j->engine, &h);
     if (!j->first_upload.exchange(true)) j->ns[kFirstUpload].store(now_ns() - j->t_start);
     j->add(kSubmit, t0);
     if (r != 0) {
@@ -582,7 +589,7 @@ bool hsz_header_ok(const Item& it, int* w, uint32_t* fb, uint32_t* nf) {
 }
 
 // Decode / copy launches for item i on stream s; records it.done.
-int launch_item(Job* j, int i, hipStream_t s) {
+int launch_item(Job* j, int i, void* s) {
   Item& it = j->items[i];
   char* base = static_cast<char*>(it.block);
   if (it.codec == kCodecHsz) {
@@ -637,8 +644,8 @@ int launch_item(Job* j, int i, hipStream_t s) {
       return -1;
     }
   }
-  if (hipEventCreateWithFlags(&it.done, hipEventDisableTiming) != hipSuccess ||
-      hipEventRecord(it.done, s) != hipSuccess) {
+  it.done = hsg_rt_event_record(s);
+  if (!it.done) {
     j->fail(-EIO, i, "completion event");
     return -1;
   }
@@ -651,7 +658,7 @@ void release_item(Job* j, Item& it) {
     if (it.stage) hsg_pinned_release(it.stage);
   }
   if (it.done) {
-    hipEventDestroy(it.done);
+    hsg_rt_event_free(it.done);
     it.done = nullptr;
   }
   {
@@ -677,7 +684,7 @@ void release_item(Job* j, Item& it) {
 }
 
 void completion_thread(Job* j) {
-  (void)hipSetDevice(j->dev);
+  (void)hsg_rt_set_device(j->dev);
   for (;;) {
     Chunk c;
     {
@@ -714,7 +721,7 @@ void completion_thread(Job* j) {
 }
 
 void retire_thread(Job* j) {
-  (void)hipSetDevice(j->dev);
+  (void)hsg_rt_set_device(j->dev);
   for (;;) {
     int i;
     {
@@ -725,7 +732,7 @@ void retire_thread(Job* j) {
       j->retire.pop_front();
     }
     const uint64_t t0 = now_ns();
-    if (hipEventSynchronize(j->items[i].done) != hipSuccess) j->fail(-EIO, i, "device work");
+    if (hsg_rt_event_sync(j->items[i].done) != 0) j->fail(-EIO, i, "device work");
     j->add(kRetireWait, t0);
     release_item(j, j->items[i]);
   }
@@ -752,7 +759,7 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
                         uint64_t slot_bytes, uint64_t first_bytes, uint64_t piece_bytes,
                         int nslots, int nreaders, uint64_t budget, int engine, int* err) {
   *err = 0;
-  if (hipSetDevice(dev) != hipSuccess) {
+  if (hsg_rt_set_device(dev) != 0) {
     *err = -1;
     return nullptr;
   }
@@ -767,7 +774,6 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   const uint32_t emask = hsg_sdma_h2d_engine_mask(dev);
   if (engine == -2) engine = emask ? __builtin_ctz(emask) : -1;
   j->engine = (engine >= 0 && engine < 32 && (emask & (1u << engine))) ? engine : -1;
-  if (const char* dbg = getenv("HIPSNAPSHOT_RESTORE_DEBUG")) j->debug = atoi(dbg);
   j->desc_size = hsg_desc_size();
   j->err_words = err_words;
   j->descs.assign(static_cast<const uint8_t*>(descs),
@@ -801,7 +807,7 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   }
   // persistent streams (creating one costs ~1 ms of HIP runtime time)
   for (int s = 0; s < 2; ++s) {
-    j->streams[s] = static_cast<hipStream_t>(hsg_copy_stream(dev, kRestoreSlot + s));
+    j->streams[s] = hsg_copy_stream(dev, kRestoreSlot + s);
     if (!j->streams[s]) {
       delete j;
       *err = -4;
@@ -811,15 +817,10 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   // the destinations' producers: their queued work finishes before ours (a
   // failure here would let the copies race it: the job does not start)
   for (int p = 0; p < n_producers; ++p) {
-    hipEvent_t ev;
-    bool ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
-    if (ok) {
-      ok = hipEventRecord(ev, reinterpret_cast<hipStream_t>(producers[p])) == hipSuccess;
-      for (int s = 0; ok && s < 2; ++s) ok = hipStreamWaitEvent(j->streams[s], ev, 0) == hipSuccess;
-      hipEventDestroy(ev);
-    }
+    bool ok = true;
+    for (int s = 0; ok && s < 2; ++s)
+      ok = hsg_rt_stream_after(j->streams[s], reinterpret_cast<void*>(producers[p])) == 0;
     if (!ok) {
-      (void)hipGetLastError();
       delete j;
       *err = -5;
       return nullptr;
@@ -915,7 +916,7 @@ int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
   Job* j = static_cast<Job*>(handle);
   for (auto& t : j->threads) t.join();
   for (int s = 0; s < 2; ++s) {
-    if (hipStreamSynchronize(j->streams[s]) != hipSuccess) j->fail(-EIO, -1, "device work");
+    if (hsg_rt_stream_sync(j->streams[s]) != 0) j->fail(-EIO, -1, "device work");
   }
   j->add(kWall, j->t_start);
   for (auto& it : j->items) {
@@ -947,7 +948,7 @@ int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
 // Returns 0, or -1 if an allocation failed (the job then allocates itself).
 int hsg_restore_prewarm(int dev, uint64_t up_bytes, uint64_t sc_bytes, uint64_t slot_bytes,
                         int nslots, uint64_t table_bytes) {
-  if (hipSetDevice(dev) != hipSuccess) return -1;
+  if (hsg_rt_set_device(dev) != 0) return -1;
   int rc = 0;
   void* up = up_bytes ? g_upload_pool.acquire(dev, up_bytes) : nullptr;
   void* sc = sc_bytes ? g_scratch_pool.acquire(dev, sc_bytes) : nullptr;

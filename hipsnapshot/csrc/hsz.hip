@@ -32,8 +32,8 @@
 //                   lookup table and stores its groups as 16-B vectors
 //                   (adjacent lanes -> adjacent groups, so the stores
 //                   coalesce); escapes are patched in element order after a
-//                   barrier.  hsz_decode2<W> is the round-3 version of it
-//                   (HIPSNAPSHOT_HSZ_DECODE2=lds; profiles/r4/decode_pmc/)
+//                   barrier (round 4 rewrite of the round-3 LDS decoder,
+//                   which it replaced: profiles/r4/decode_pmc/)
 //
 // A frame is one workgroup (4 waves): a 512 MiB blob has 2048 frames, 8x the
 // CU count, so the grid fills the chip; all traffic is streaming HBM
@@ -1226,167 +1226,13 @@ __device__ __forceinline__ void refill(const uint64_t* coded64, uint32_t& pos, u
   nb += 8 * k;
 }
 
-// Mode-2 decoder (W = 2 or 4).  A frame whose fields do not fit its stored
-// extent, or whose lane streams decode invalid codes or overrun, is flagged
-// through `err` (the host validated the frame table itself).
-template <int W>
-__global__ void __launch_bounds__(kThreads)
-hsz_decode2(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
-            uint32_t first_frame, uint64_t logical, uint32_t frame_bytes,
-            uint8_t* __restrict__ out, uint32_t* err) {
-  // streams + 16 B of slack for the 8-B refill reads past the last stream
-  __shared__ uint64_t coded64[(kMaxCoded + 1 + 16 + 7) / 8];
-  __shared__ uint16_t lut[kLut];
-  __shared__ uint16_t hcode[16];
-  __shared__ uint8_t hlen[16];
-  __shared__ uint8_t dict[16];
-  __shared__ uint32_t eidx[kMaxEsc];
-  __shared__ uint32_t sorted[kMaxEsc];
-  __shared__ uint32_t wsum[4];
-  __shared__ uint32_t ctotal;
-  __shared__ int ecount;
-  __shared__ int valid;
-  const uint64_t fl = blockIdx.x;
-  const uint64_t f = first_frame + fl;
-  const uint64_t base = f * frame_bytes;
-  const uint64_t len = min(uint64_t(frame_bytes), logical - base);
-  const uint64_t n = len / W;
-  const uint64_t nlo = uint64_t(W - 1) * n;
-  const uint8_t* fr = frames + offsets[fl];
-  const uint64_t extent = offsets[fl + 1] - offsets[fl];
-  // too-short frames are reported by hsz_decode
-  if (offsets[fl + 1] < offsets[fl] + kFrameHeader || fr[0] != 2) return;
-  uint8_t* o = out + fl * uint64_t(frame_bytes);
-  const uint32_t n_esc = *reinterpret_cast<const uint32_t*>(fr + 4);
-  if (threadIdx.x < 16) {
-    dict[threadIdx.x] = fr[8 + threadIdx.x];
-    hlen[threadIdx.x] = (fr[24 + threadIdx.x / 2] >> (4 * (threadIdx.x & 1))) & 15;
-  }
-  if (threadIdx.x == 0) ecount = 0;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const uint32_t l = threadIdx.x < 16 ? hlen[threadIdx.x] : 0u;
-    const bool long_code = __ballot(l > uint32_t(kMaxLen)) != 0;
-    const uint32_t code = wave_canonical_code(l < uint32_t(kMaxLen) ? l : uint32_t(kMaxLen));
-    if (threadIdx.x < 16) hcode[threadIdx.x] = uint16_t(code);
-    if (threadIdx.x == 0)
-      valid = !long_code && n % 8 == 0 && n_esc <= uint32_t(kMaxEsc) &&
-              kFrameHeader + nlo + kLaneTable <= extent;
-  }
-  __syncthreads();
-  if (!valid) {
-    if (threadIdx.x == 0) flag_corrupt(err);
-    return;
-  }
-  for (int x = threadIdx.x; x < kLut; x += kThreads) {
-    uint16_t ent = 0;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const int l = hlen[c];
-      if (l && (uint32_t(x) & ((1u << l) - 1)) == hcode[c]) ent = uint16_t(c | (l << 8));
-    }
-    lut[x] = ent;
-  }
-  const uint8_t* body = fr + kFrameHeader;
-  const uint8_t* lo = body;
-  const uint32_t lb = reinterpret_cast<const uint16_t*>(body + nlo)[threadIdx.x];
-  const uint32_t loff = block_excl_scan(lb, wsum, &ctotal);
-  const uint32_t c_bytes = ctotal;
-  const uint64_t tail_len = len - W * n;
-  if (c_bytes > kMaxCoded ||
-      kFrameHeader + nlo + kLaneTable + c_bytes + n_esc + tail_len > extent) {
-    if (threadIdx.x == 0) flag_corrupt(err);
-    return;  // uniform across the workgroup (ctotal is shared)
-  }
-  const uint8_t* streams = body + nlo + kLaneTable;
-  uint8_t* coded = reinterpret_cast<uint8_t*>(coded64);
-  if ((reinterpret_cast<uintptr_t>(streams) & 3) == 0) {
-    const uint32_t nw = c_bytes / 4;
-    const uint32_t* sw = reinterpret_cast<const uint32_t*>(streams);
-    uint32_t* cw = reinterpret_cast<uint32_t*>(coded);
-    for (uint32_t i = threadIdx.x; i < nw; i += kThreads) cw[i] = sw[i];
-    for (uint32_t j = nw * 4 + threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
-  } else {
-    for (uint32_t j = threadIdx.x; j < c_bytes; j += kThreads) coded[j] = streams[j];
-  }
-  if (threadIdx.x < 16) coded[c_bytes + threadIdx.x] = 0;
-  __syncthreads();
-  const uint64_t groups = n / 8;
-  const bool vec = ((reinterpret_cast<uintptr_t>(o) & 15) | (reinterpret_cast<uintptr_t>(lo) & 7)) == 0;
-  uint32_t pos = loff;
-  uint64_t acc = 0;
-  int nb = 0;
-  bool bad = false;
-  for (uint64_t g = threadIdx.x; g < groups; g += kThreads) {
-    // (loading the next group's low bytes one iteration ahead measured slower
-    // here: this loop is bound by its LDS stream and LUT reads)
-    uint64_t lw[W - 1];
-    load_lo<W>(lo, g, vec, lw);
-    uint32_t wd[2 * W];
-#pragma unroll
-    for (int q = 0; q < 2 * W; ++q) wd[q] = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      // every lane refills at the same points (no divergence): >= 56 bits
-      // cover the next 4 codes of <= kMaxLen bits
-      if ((e & 3) == 0) refill(coded64, pos, acc, nb);
-      const uint32_t ent = lut[acc & (kLut - 1)];
-      uint32_t l = ent >> 8;
-      uint32_t c = ent & 15;
-      if (l == 0) {  // corrupt stream: flag it, keep going (bounded)
-        l = kMaxLen;
-        c = 0;
-        bad = true;
-      }
-      acc >>= l;
-      nb -= int(l);
-      uint32_t hi = dict[c];
-      if (c == kEsc) {
-        const int k = atomicAdd(&ecount, 1);
-        if (k < kMaxEsc) eidx[k] = uint32_t(g * 8 + e);
-        hi = 0;
-      }
-      const uint32_t v = get_lo<W>(lw, e) | (hi << (8 * (W - 1)));
-      if constexpr (W == 2) wd[e >> 1] |= v << (16 * (e & 1));
-      else wd[e] = v;
-    }
-    if (vec) {
-#pragma unroll
-      for (int k = 0; k < W / 2; ++k)
-        reinterpret_cast<uint4*>(o)[g * (W / 2) + k] =
-            make_uint4(wd[4 * k], wd[4 * k + 1], wd[4 * k + 2], wd[4 * k + 3]);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 2 * W; ++q)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) o[8 * W * g + 4 * q + b] = uint8_t(wd[q] >> (8 * b));
-    }
-  }
-  // a lane may not read past its own stream (host decoder: same check)
-  if (bad || uint64_t(pos - loff) * 8 - uint64_t(nb) > uint64_t(lb) * 8) flag_corrupt(err);
-  // the barrier orders every wave's element stores before the escape patches
-  __syncthreads();
-  const uint8_t* escv = streams + c_bytes;
-  const int ne = min(min(ecount, kMaxEsc), int(n_esc));
-  for (int i = threadIdx.x; i < ne; i += kThreads) {
-    const uint32_t me = eidx[i];
-    int rank = 0;
-    for (int j = 0; j < ne; ++j) rank += eidx[j] < me;
-    sorted[rank] = me;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < ne; i += kThreads) o[W * uint64_t(sorted[i]) + W - 1] = escv[i];
-  if (threadIdx.x < tail_len) o[W * n + threadIdx.x] = escv[n_esc + threadIdx.x];
-}
-
 // LUT entry of the lean decoder: code length (bits 0-3; bit 4 is 0, so the
 // entry itself is a valid v_alignbit / v_lshrrev shift amount), escape (5),
 // invalid code (6; length kMaxLen so a corrupt lane still advances by a
 // bounded amount), decoded high byte (8-15).
 constexpr uint32_t kEntEsc = 0x20u, kEntBad = 0x40u;
 
-// Lean mode-2 decoder (default; HIPSNAPSHOT_HSZ_DECODE2=lds selects the
-// original hsz_decode2).  Measured (profiles/r4/decode_pmc/): a frame's
+// Lean mode-2 decoder (it replaced the round-3 LDS decoder).  Measured (profiles/r4/decode_pmc/): a frame's
 // decode is latency-bound -- one frame alone on a CU takes as long as 2 per
 // CU, so neither LDS bank conflicts nor issue rate set the pace, but the
 // serial chain of each lane stream (512 symbols per lane for bf16) and the
@@ -1404,7 +1250,9 @@ constexpr uint32_t kEntEsc = 0x20u, kEntBad = 0x40u;
 //     16-B loads in flight at once;
 //   * P > 0: the low-byte plane is loaded P groups ahead;
 //   * bf16 pairs are assembled with v_perm.
-// Validation and error reporting are hsz_decode2's.
+// A frame whose fields do not fit its stored extent, or whose lane streams
+// decode invalid codes or overrun, is flagged through `err` (the host
+// validated the frame table itself).
 template <int W, int P>
 __global__ void __launch_bounds__(kThreads)
 hsz_decode2g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
@@ -1621,29 +1469,11 @@ hsz_decode2g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ of
   if (threadIdx.x < tail_len) o[W * n + threadIdx.x] = escv[n_esc + threadIdx.x];
 }
 
-// HIPSNAPSHOT_HSZ_DECODE2 (A/B switch, read per launch): "lds" = hsz_decode2
-// (-1), "staged" = hsz_decode2g<W, 0> (0), default "staged-pf" =
-// hsz_decode2g<W, 8> (1).
-int hsz_decode2_variant() {
-  const char* v = getenv("HIPSNAPSHOT_HSZ_DECODE2");
-  if (v == nullptr || v[0] == '\0') return 1;
-  if (v[0] == 'l') return -1;
-  return strstr(v, "-pf") != nullptr ? 1 : 0;
-}
-
 thread_local char g_hsz_err[256];
 
 int fail(const char* what, hipError_t e) {
   snprintf(g_hsz_err, sizeof(g_hsz_err), "%s: %s", what, hipGetErrorString(e));
   return -static_cast<int>(e) - 1;
-}
-
-// HIPSNAPSHOT_SPLIT_ENCODE: 0 = one-thread-per-stream mode-2 encoder for every
-// width, 1 (default) = split encoder for 2-byte elements, 2 = for 4-byte too
-// (A/B switch; read per launch so a process can alternate).
-int hsz_split_encode() {
-  const char* v = getenv("HIPSNAPSHOT_SPLIT_ENCODE");
-  return v == nullptr || v[0] == '\0' ? 1 : atoi(v);
 }
 
 }  // namespace
@@ -1693,13 +1523,8 @@ int hsg_hsz_encode(int dev, const void* src, uint64_t logical, int w, uint32_t f
   // bf16/fp16: split-stream encoder (802 -> 420 us per GiB); fp32 stays on
   // hsz_encode2 (449 us vs 525 us: twice the bytes per group under the split
   // kernel's 64-VGPR budget) -- profiles/codec_r2/split_encode.md
-  const int split_mode = hsz_split_encode();
-  const bool split = encode2x_fits(w, frame_bytes) && (w == 2 ? split_mode > 0 : split_mode > 1);
-  if (split && w == 2)
+  if (w == 2 && encode2x_fits(w, frame_bytes))
     hipLaunchKernelGGL(hsz_encode2x<2>, dim3(g), dim3(kThreadsX), 0, s, src8, logical,
-                       frame_bytes, m, lanes, pbits, o, nf);
-  else if (split && w == 4)
-    hipLaunchKernelGGL(hsz_encode2x<4>, dim3(g), dim3(kThreadsX), 0, s, src8, logical,
                        frame_bytes, m, lanes, pbits, o, nf);
   else if (w == 2)
     hipLaunchKernelGGL(hsz_encode2<2>, dim3(g), dim3(kThreads), 0, s, src8, logical, frame_bytes,
@@ -1734,18 +1559,12 @@ int hsg_hsz_decode(int dev, const void* frames, const void* offsets, uint32_t fi
     case 8: hipLaunchKernelGGL(hsz_decode<8>, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o, ew); break;
     default: return -1001;
   }
-  const int v2 = hsz_decode2_variant();
-#define HSZ_D2(K) hipLaunchKernelGGL(K, dim3(count), dim3(kThreads), 0, s, fr, off, first, logical, frame_bytes, o, ew)
-  if (w == 2) {
-    if (v2 < 0) HSZ_D2(hsz_decode2<2>);
-    else if (v2 == 0) HSZ_D2((hsz_decode2g<2, 0>));
-    else HSZ_D2((hsz_decode2g<2, 8>));
-  } else if (w == 4) {
-    if (v2 < 0) HSZ_D2(hsz_decode2<4>);
-    else if (v2 == 0) HSZ_D2((hsz_decode2g<4, 0>));
-    else HSZ_D2((hsz_decode2g<4, 8>));
-  }
-#undef HSZ_D2
+  if (w == 2)
+    hipLaunchKernelGGL((hsz_decode2g<2, 8>), dim3(count), dim3(kThreads), 0, s, fr, off, first,
+                       logical, frame_bytes, o, ew);
+  else if (w == 4)
+    hipLaunchKernelGGL((hsz_decode2g<4, 8>), dim3(count), dim3(kThreads), 0, s, fr, off, first,
+                       logical, frame_bytes, o, ew);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("hsz decode launch", e);
 }

@@ -191,7 +191,7 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
     return frozen
 
 
-# Arena kept between async takes (HIPSNAPSHOT_HBM_ARENA_KEEP): device ->
+# Arena kept between async takes (knobs.TUNING.hbm_arena_keep): device ->
 # [tensor, busy].  A training loop frees and re-allocates activations between
 # checkpoints; a 48 GB arena handed back to torch's caching allocator gets
 # split up by them, and the next take's torch.empty then goes through

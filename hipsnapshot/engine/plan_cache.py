@@ -23,8 +23,8 @@ Soundness:
   (data_ptr, shape, strides, dtype, device; DTensor placements + mesh +
   global shape; ShardedTensor shard boxes) in the same logical order, and
   the settings key (rank, world size, sync/async, quantize globs,
-  compression, every ``HIPSNAPSHOT_*``/``TORCHSNAPSHOT_*`` variable, the
-  app-state keys) matches;
+  compression, the knob values a plan depends on (``knobs.plan_settings``),
+  the app-state keys) matches;
 * the plan holds the leaves it was built from, so no address it matched can
   be recycled by the caching allocator while the plan exists -- equal
   data_ptr means the same memory.  The plan is dropped when an app-state
@@ -132,10 +132,10 @@ def settings_key(app_state: Dict[str, Any], rank: int, world_size: int, is_async
     are part of it, not the objects: ``{"model": m, "progress": StateDict(
     step=i)}`` rebuilt for every take must still reuse the model's plan (the
     leaf signatures establish that the model's tensors are the same)."""
-    env = tuple(sorted((k, v) for k, v in os.environ.items()
-                       if k.startswith(("HIPSNAPSHOT_", "TORCHSNAPSHOT_"))))
+    from .. import knobs
+
     return (tuple(sorted(app_state)), rank, world_size, bool(is_async),
-            tuple(quantize or ()), compression, env)
+            tuple(quantize or ()), compression, knobs.plan_settings())
 
 
 def _tensor_stagers(write_reqs: List[WriteReq]) -> Iterator[Any]:

@@ -18,8 +18,9 @@ Soundness (mirrors engine/plan_cache.py):
   size, mtime: a take rewrites the metadata last, by rename, so any new take
   at that path is a different key -- the blob sizes the plan read with
   ``stat`` belong to that snapshot), the stateful's key, rank, world size,
-  every ``HIPSNAPSHOT_*`` / ``TORCHSNAPSHOT_*`` variable, and the identity
-  signature of every leaf in order;
+  the knob values a plan depends on (``knobs.plan_settings``: not tracing,
+  thread counts or other variables that leave the plan as it is), and the
+  identity signature of every leaf in order;
 * the plan holds the leaves, so no address it matched can be recycled while
   it exists; it is dropped when the stateful object is garbage collected,
   on ``clear()``, or when more than ``_MAX`` plans are cached;
@@ -85,9 +86,10 @@ def key_for(metadata_key: Optional[tuple], stateful_key: str, rank: int, world_s
     sigs = fast_signatures(flat)
     if sigs is None:
         sigs = tuple((k, leaf_sig(v)) for k, v in flat.items())
-    env = tuple(sorted((k, v) for k, v in os.environ.items()
-                       if k.startswith(("HIPSNAPSHOT_", "TORCHSNAPSHOT_"))))
-    return (metadata_key, stateful_key, rank, world_size, env, tuple(flat), sigs)
+    from .. import knobs
+
+    return (metadata_key, stateful_key, rank, world_size, knobs.plan_settings(), tuple(flat),
+            sigs)
 
 
 def lookup(key: Optional[tuple]) -> Optional[RestorePlan]:

@@ -55,13 +55,7 @@ def _acquire_pool(kind: str, n: int, rank: int) -> ThreadPoolExecutor:
         lst = _idle_pools.get(key)
         if lst:
             return lst.pop()
-    init = None
-    if kind == "stage_bg":  # async-take drain: kernels on a slice of the GPU
-        from .staging import mark_background_thread
-
-        init = mark_background_thread
-    ex = ThreadPoolExecutor(max_workers=n, thread_name_prefix=f"hipsnapshot-{kind}-{rank}",
-                            initializer=init)
+    ex = ThreadPoolExecutor(max_workers=n, thread_name_prefix=f"hipsnapshot-{kind}-{rank}")
     ex._hs_key = key  # type: ignore[attr-defined]
     return ex
 
@@ -81,7 +75,8 @@ def _release_pool(ex: ThreadPoolExecutor, reusable: bool) -> None:
 
 
 def get_local_world_size(pg) -> int:
-    if pg is None or pg.get_world_size() == 1:
+    solo = getattr(pg, "solo", None)
+    if pg is None or (solo() if solo is not None else pg.get_world_size() == 1):
         return 1
     names = [None] * pg.get_world_size()
     pg.all_gather_object(names, socket.gethostname())
@@ -809,21 +804,6 @@ async def _execute_python_reads(read_reqs: List[ReadReq], storage: StoragePlugin
     logger.debug(f"Rank {rank} read {stats.bytes_written / 1e9:.3f} GB in "
                  f"{stats.t_done - stats.t_start:.3f}s")
     return stats
-
-
-def order_reads_for_pipeline(read_reqs: List[ReadReq], lead_min_bytes: int = 1 << 20
-                             ) -> List[ReadReq]:
-    """With ``HIPSNAPSHOT_READ_ORDER=pipeline``: largest reads first, led by
-    the smallest read of at least ``lead_min_bytes`` (the first H2D starts
-    5 ms earlier).  Off by default: the whole restore measured 4-8 % slower
-    than manifest order (knobs.get_read_order)."""
-    if len(read_reqs) < 3 or knobs.get_read_order() == "plan":
-        return list(read_reqs)
-    sized = [(rr.buffer_consumer.get_consuming_cost_bytes(), i, rr)
-             for i, rr in enumerate(read_reqs)]
-    lead = min((t for t in sized if t[0] >= lead_min_bytes), default=None)
-    rest = sorted((t for t in sized if t is not lead), key=lambda t: (-t[0], t[1]))
-    return ([lead[2]] if lead is not None else []) + [t[2] for t in rest]
 
 
 def sync_execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,

@@ -42,16 +42,6 @@ NUM_COPY_SLOTS = 4
 _HASH_SLOT_BASE = 64  # hash streams: slots 64.. (copy slots stay below)
 
 
-def mark_background_thread() -> None:
-    """Executor-thread initializer of an async-take drain: this thread's
-    kernels (encode, slab gathers) are capped at ``HIPSNAPSHOT_DRAIN_CUS``
-    workgroups so a concurrent training step keeps the rest of the GPU."""
-    from .. import knobs
-
-    if native.hsgpu_loaded() and native.gpu_available():
-        native.set_thread_grid_cap(knobs.get_drain_cus())
-
-
 def copy_slot() -> int:
     """A copy-stream slot per OS thread (concurrent DMAs from executor threads):
     at least as many slots as staging threads, so two threads never share a
@@ -257,7 +247,7 @@ def bulk_d2h(dev: int, slot: int, dst: int, src: int, nbytes: int,
              producer: Optional[int] = None) -> None:
     """Blocking device -> pinned-host copy of ``nbytes``, ordered after the
     copy stream (dev, slot) and, if given, after ``producer``.  Runs on the
-    SDMA engines when ``HIPSNAPSHOT_D2H_ENGINE=sdma`` (no CU time taken from
+    SDMA engines when ``knobs.TUNING.d2h_engine`` is ``sdma`` (no CU time taken from
     a concurrent training step), else as hipMemcpyAsync."""
     t_s = time.perf_counter()
     if nbytes and _use_sdma(dev):
@@ -303,13 +293,13 @@ def d2h_staged(dev: int, slot: int, staged: StagedBuffer, src: int, nbytes: int,
     """Device -> pinned copy of ``nbytes`` at ``src`` into ``staged`` (and the
     hash started as ``hash_handle`` on ``hash_slot(slot)``, if any).
 
-    On the SDMA engines (``HIPSNAPSHOT_ASYNC_DMA``, default on) the copy is
+    On the SDMA engines (``knobs.TUNING.async_dma``, default on) the copy is
     only SUBMITTED here: ``staged.ready`` then waits for it (the writer calls
     it before writing) and the staging worker goes on to prepare its next
     blob while the engine works through its queue -- the engine no longer
     idles while every worker encodes.  ``keep`` holds the device buffers the
     copy reads; they are dropped once it is done.  At most
-    ``HIPSNAPSHOT_DMA_INFLIGHT`` copies per device are in flight (device
+    ``knobs.TUNING.dma_inflight`` copies per device are in flight (device
     buffers of queued blobs stay allocated until then)."""
     from .. import knobs
 
@@ -477,7 +467,7 @@ _encode_locks_mu = threading.Lock()
 
 @contextmanager
 def _encode_turn(dev: int, nbytes: int) -> Iterator[None]:
-    """Large HSZ1 encodes take turns per device (``HIPSNAPSHOT_SERIAL_ENCODE``).
+    """Large HSZ1 encodes take turns per device (``knobs.TUNING.serial_encode``).
 
     Encodes launched by several staging threads at once share the CUs, so
     each finishes only when all do: at the start of a take four 512 MiB
@@ -966,7 +956,7 @@ _sdma_ok: Dict[int, bool] = {}
 
 
 def _sdma_uploads(dev: int) -> bool:
-    """Encoded frames go up on the SDMA engines (``HIPSNAPSHOT_H2D_ENGINE``,
+    """Encoded frames go up on the SDMA engines (``knobs.TUNING.h2d_engine``,
     default sdma, when ROCr reports an engine)."""
     from .. import knobs
 

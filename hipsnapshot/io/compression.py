@@ -33,10 +33,19 @@ _ELEM_WIDTH = {torch.bfloat16: 2, torch.float16: 2, torch.float32: 4, torch.floa
 def resolve(compression: Optional[str]) -> str:
     from .. import knobs
 
-    c = (compression or knobs.get_compression()).lower()
-    if c not in CODECS:
-        raise ValueError(f"unknown compression {c!r}; expected one of {CODECS}")
-    return c
+    c = (compression or knobs.get_compression()).strip().lower()
+    base, _, extra = c.partition("+")
+    if base not in CODECS or extra not in ("", "host") or (extra and base == "none"):
+        raise ValueError(f"unknown compression {c!r}; expected one of {CODECS} "
+                         "(a codec may carry '+host': host tensors too)")
+    return base
+
+
+def host_requested(compression: Optional[str]) -> bool:
+    """``"hsz1+host"``: host (CPU) tensors are encoded too (C++ codec)."""
+    from .. import knobs
+
+    return (compression or knobs.get_compression()).strip().lower().endswith("+host")
 
 
 def _info(w: int, blob_bytes: int, frame_bytes: int) -> dict:
@@ -62,7 +71,7 @@ def plan_compression(write_reqs: List[WriteReq],
                      include_host: Optional[bool] = None) -> int:
     """Mark eligible write requests; returns the number of compressed blobs.
 
-    ``include_host`` (default: ``HIPSNAPSHOT_COMPRESSION_HOST``) also encodes
+    ``include_host`` (default: ``HIPSNAPSHOT_COMPRESSION=hsz1+host``) also encodes
     host tensors with the C++ codec -- worth it when storage, not host memory
     bandwidth, is the bottleneck (network filesystems, object stores).
     """

@@ -6,50 +6,24 @@ threshold, batching on, per-rank memory budget min(0.6*avail/local_ws, 32 GiB).
 Every variable is read as ``HIPSNAPSHOT_<NAME>`` first and the reference's
 ``TORCHSNAPSHOT_<NAME>`` second, so existing job scripts keep working.
 
-MI355X-specific knobs:
+The environment surface is ``ENV_KNOBS`` (25 names, documented in
+docs/getting_started.md): the reference's five, then
 
-* ``HIPSNAPSHOT_IO_THREADS`` (16) -- native I/O engine workers per storage plugin.
-* ``HIPSNAPSHOT_COMPRESSION`` (none) -- ``hsz1`` = lossless GPU compression of
-  floating-point blobs (see ``ops/codec.py``); per call via ``compression=``.
-* ``HIPSNAPSHOT_READ_INFLIGHT`` (8) -- whole-blob reads in flight during restore.
-* ``HIPSNAPSHOT_IO_READ_SPLIT_BYTES`` (8 MiB) -- reads larger than 1.5x this are
-  split across I/O workers (parallel page-cache reads of one file; 0 = off).
-* ``HIPSNAPSHOT_STAGE_THREADS`` (4) -- concurrent staging jobs (DMA/pack/serialize).
-* ``HIPSNAPSHOT_FS_DIRECT_IO`` (0) -- O_DIRECT for the aligned body of blobs.
-* ``HIPSNAPSHOT_FS_FSYNC`` (0) -- fdatasync every blob (durable checkpoints).
-* ``HIPSNAPSHOT_ASYNC_HBM_STAGING`` (1) -- async_take snapshots device state into
-  spare HBM with one gather-kernel launch and drains it in the background.
-* ``HIPSNAPSHOT_HBM_STAGING_RESERVE_BYTES`` (8 GiB) -- HBM left free for training.
-* ``HIPSNAPSHOT_HBM_STAGING_MAX_BYTES`` (unlimited) -- cap on the async-take HBM
-  arena; requests beyond it are host-staged before ``async_take`` returns.
-* ``HIPSNAPSHOT_HBM_ARENA_KEEP`` (1) -- keep the async-take HBM arena between
-  takes (``hipsnapshot.release_hbm_arena()`` frees it).
-* ``HIPSNAPSHOT_NATIVE_DRAIN`` (1) -- drain raw frozen blobs to local files in
-  C++ threads (``csrc/hsdrain.hip``); ``HIPSNAPSHOT_DRAIN_SLOT_BYTES`` (64 MiB),
-  ``_DRAIN_SLOTS`` (16), ``_DRAIN_WRITERS`` (min(16, io threads, half the rank's CPU share)),
-  ``_DRAIN_NICE`` (10: nice increment of its threads), ``_DRAIN_DIRECT_IO`` (0:
-  O_DIRECT files, no page-cache copy).
-* ``HIPSNAPSHOT_NATIVE_RESTORE`` (1) -- reads landing in HBM go through one
-  native job per device (``csrc/hsrestore.hip``): ``_RESTORE_SLOT_BYTES``
-  (128 MiB), ``_RESTORE_FIRST_BYTES`` (16 MiB), ``_RESTORE_PIECE_BYTES``
-  (4 MiB), ``_RESTORE_SLOTS`` (6), ``_RESTORE_READERS``,
-  ``_RESTORE_DEVICE_BUDGET`` (2 GiB), ``_RESTORE_KEEP_BYTES`` (2.25 GiB),
-  ``_RESTORE_PREWARM`` (1: fill its pools while the reads are planned),
-  ``_RESTORE_PLAN_CACHE`` (1), ``_HSZ_DECODE2`` (``staged-pf``; ``lds`` = the
-  round-3 HSZ1 decoder).
-* ``HIPSNAPSHOT_ASYNC_DEVICE_CODEC`` (raw) -- ``same``: an async take encodes
-  its frozen device state like a blocking take.
-* ``HIPSNAPSHOT_GC_AFTER_PLAN`` (1) -- one full Python GC pass at the end of a
-  take that built a new take plan, not in a later take or training step.
-* ``HIPSNAPSHOT_REBALANCE`` (0) -- move whole blobs from loaded ranks to idle
-  ones over xGMI before a sync take writes (``parallel/rebalance.py``).
-* ``HIPSNAPSHOT_UVM_ASSUME_HOST`` (1 unless the device runs with XNACK on) -- managed tensors
-  never placed with ``ops.uvm.place`` are host-resident: blocking takes write
-  host-resident UVM pages in place and restores read into them, instead of
-  copying them over PCIe and back.
-* ``HIPSNAPSHOT_SLAB_ALIGN`` (256) -- byte alignment of slab members.
-* ``HIPSNAPSHOT_TRUST_OBJECTS`` (0) -- allow full unpickling of ``object``
-  entries written by OTHER tools (our own writes are trusted by the reader).
+* storage: ``IO_THREADS``, ``COMPRESSION`` (``none`` | ``hsz1`` |
+  ``hsz1+host``), ``CHECKSUM``, ``FS_DIRECT_IO``, ``FS_FSYNC``;
+* async takes: ``ASYNC_HBM_STAGING``, ``HBM_STAGING_RESERVE_BYTES``,
+  ``HBM_STAGING_MAX_BYTES``, ``NATIVE_DRAIN``, ``DRAIN_WRITERS``;
+* restore: ``NATIVE_RESTORE``, ``TRUST_OBJECTS``;
+* distributed: ``REBALANCE``, ``STATE_DICT_BARRIERS``, ``FORCE_COLLECTIVES``;
+* host: ``NUMA_BIND``, ``PINNED_POOL_MAX_BYTES``;
+* format: ``FP8_FORMAT`` (``mx`` | ``block`` | ``hadamard32``);
+* tracing: ``TIMELINE``, ``ROCTX``.
+
+Everything else that used to be an environment switch -- engine sizing,
+copy-engine choice, A/B variants whose measurement concluded -- is a
+constant of ``TUNING`` below, each with the record that chose it.  Tests and
+probes change them in-process with ``override_knob`` / ``override_tuning``;
+they are not read from the environment.
 """
 
 from __future__ import annotations
@@ -172,113 +146,153 @@ def get_io_threads() -> int:
     return max(4, min(16, 2 * available_cpus() // _local_ranks_hint[0]))
 
 
-def compress_host_tensors() -> bool:
-    return _get_bool("COMPRESSION_HOST", False)
+ENV_KNOBS = (
+    MAX_CHUNK_SIZE, MAX_SHARD_SIZE, SLAB_SIZE_THRESHOLD, DISABLE_BATCHING, MEMORY_BUDGET,
+    "IO_THREADS", "COMPRESSION", "CHECKSUM", "FS_DIRECT_IO", "FS_FSYNC",
+    "ASYNC_HBM_STAGING", "HBM_STAGING_RESERVE_BYTES", "HBM_STAGING_MAX_BYTES", "NATIVE_DRAIN",
+    "DRAIN_WRITERS", "NATIVE_RESTORE", "TRUST_OBJECTS", "REBALANCE", "STATE_DICT_BARRIERS",
+    "FORCE_COLLECTIVES", "NUMA_BIND", "PINNED_POOL_MAX_BYTES", "FP8_FORMAT", "TIMELINE", "ROCTX",
+)
 
 
-def get_read_inflight() -> int:
-    return max(1, _get_int("READ_INFLIGHT", 8))
+class _Tuning:
+    """Engine constants (not read from the environment).  Attribute =
+    value; ``override_knob("RESTORE_SLOTS", 3)`` (upper-case name) or
+    ``override_tuning(restore_slots=3)`` change one for a test."""
+
+    # -- take / staging --------------------------------------------------------
+    read_inflight = 8          # whole-blob reads in flight (Python read pipeline)
+    io_read_split_bytes = 8 << 20   # reads > 1.5x this are split across I/O workers
+    stage_threads = 4          # concurrent staging jobs
+    # device -> pinned copies on the SDMA engines (falls back to blit when ROCr
+    # reports none): same PCIe-bound rate, no CU time, +4 % on the Llama-3-8B
+    # save (profiles/dma/)
+    d2h_engine = "sdma"
+    # a restore's HSZ1 uploads through SDMA into uncached blocks: hipMemcpyAsync
+    # calls block for milliseconds when several threads upload
+    # (profiles/r4/restore_trace/)
+    h2d_engine = "sdma"
+    async_dma = True           # staging workers submit the copy and move on
+    dma_inflight = 8           # SDMA device -> host copies in flight per device
+    serial_encode = True       # staging threads take turns on a device's HSZ1 encodes
+    thread_staging = True      # long-running staging threads pull requests
+    # checksum launch width: a full-chip hash slows the concurrent SDMA copies
+    # (scripts/probes/hash_probe.py); blobs only need hashing at PCIe rate
+    hash_grid = 64
+    gpu_slab_gather = True
+    slab_align = 256
+    gc_after_plan = True       # one full GC pass after a take that built a plan
+    plan_cache = True          # reuse a take's plan (engine/plan_cache.py)
+    # async takes drain the frozen device state raw: the encoder on the CUs
+    # beside a training step cost +30 % step time (profiles/overlap_iso/)
+    async_device_codec = "raw"
+    hbm_arena_keep = True      # release_hbm_arena() frees the async-take arena
+    # -- native drain (csrc/hsdrain.cpp) -----------------------------------------
+    # 16 slots of 64 MiB drain the 16 GB Llama-3-8B arena at the PCIe rate
+    # (profiles/r3/s2/drain_sizing/)
+    drain_slot_bytes = 64 << 20
+    drain_slots = 16
+    drain_nice = 10            # the drain's threads yield a shared core to the trainer
+    drain_avoid_caller_core = "core"   # "core" | "l3" | "" (utils/affinity.py)
+    drain_hash_high_priority = True    # profiles/r3/drain_probe/
+    # -- restore (csrc/hsrestore.cpp) -------------------------------------------------
+    # HSZ1 blobs > 2x this are read as head + rest.  (Reads go in plan order:
+    # "a small lead read, then largest first" measured 65.1 / 68.2 GB/s vs
+    # 70.7 / 72.8, profiles/timeline_r2/read_order.txt)
+    read_head_bytes = 16 << 20
+    restore_prewarm = True
+    restore_plan_cache = True
+    native_io_numa_local = True   # readers on their GPU's NUMA node: 42 -> 29 ms
+    # 8 MiB uploads ran the link at 38 GB/s, 32 MiB at 45; a request costs the
+    # engine ~0.1 ms (profiles/r4/restore_native/)
+    restore_slot_bytes = 128 << 20
+    restore_first_bytes = 16 << 20
+    restore_piece_bytes = 4 << 20
+    restore_sdma_engine = -1
+    restore_slots = 6
+    restore_readers = 0        # 0: max(4, min(12, I/O threads))
+    restore_device_budget = 2 << 30
+    # idle restore blocks kept per pool after a restore (HBM outside torch's
+    # allocator): none, so training after a restore has all of it
+    restore_keep_bytes = 0
+    # -- distributed -------------------------------------------------------------------
+    rebalance_host = False     # let the rebalancer move host blobs too (gloo tests)
+    rebalance_min_gain = 0.1
+    # -- UVM ------------------------------------------------------------------------------
+    uvm_assume_host = None     # None: unless the device runs with XNACK on
+
+
+TUNING = _Tuning()
+
+
+def _tuned(name: str):
+    return getattr(TUNING, name)
 
 
 def get_compression() -> str:
-    return str(_get("COMPRESSION") or "none")
+    """``none`` | ``hsz1`` (GPU-resident floating blobs) | ``hsz1+host``
+    (host tensors too, with the C++ codec: worth it when storage, not host
+    memory bandwidth, is the bottleneck)."""
+    return str(_get("COMPRESSION") or "none").strip().lower()
+
+
+def compress_host_tensors() -> bool:
+    return get_compression().endswith("+host")
+
+
+def get_read_inflight() -> int:
+    return max(1, int(_tuned("read_inflight")))
 
 
 def get_io_read_split_bytes() -> int:
-    return _get_int("IO_READ_SPLIT_BYTES", 8 * 1024 * 1024)
+    return int(_tuned("io_read_split_bytes"))
 
 
 def get_d2h_engine() -> str:
-    """Engine for bulk device -> pinned-host copies: ``blit`` = hipMemcpyAsync
-    (the HIP runtime's copy kernel on the CUs), ``sdma`` = the GPU's DMA
-    engines through ROCr (``csrc/hsdma.hip``; falls back to blit when ROCr
-    reports no engine).  Default sdma: same PCIe-bound bandwidth, no CU time,
-    +4 % on the Llama-3-8B save (profiles/dma/)."""
-    v = str(_get("D2H_ENGINE") or "sdma").strip().lower()
+    """Engine for bulk device -> pinned-host copies (``TUNING.d2h_engine``):
+    ``blit`` = hipMemcpyAsync, ``sdma`` = the DMA engines (csrc/hsdma.hip)."""
+    v = str(_tuned("d2h_engine")).lower()
     if v not in ("blit", "sdma"):
-        raise ValueError(f"HIPSNAPSHOT_D2H_ENGINE must be blit or sdma, not {v!r}")
+        raise ValueError(f"d2h engine must be blit or sdma, not {v!r}")
     return v
 
 
 def get_h2d_engine() -> str:
-    """Engine for a restore's uploads of encoded (HSZ1) frames: ``sdma`` (the
-    DMA engines through ROCr into uncached device memory, ``csrc/hsdma.hip``)
-    or ``hip`` (hipMemcpyAsync, whose calls block for milliseconds when
-    several threads upload; profiles/r4/restore_trace/).  Default sdma when
-    ROCr reports an engine."""
-    v = str(_get("H2D_ENGINE") or "sdma").strip().lower()
+    v = str(_tuned("h2d_engine")).lower()
     if v not in ("hip", "sdma"):
-        raise ValueError(f"HIPSNAPSHOT_H2D_ENGINE must be hip or sdma, not {v!r}")
+        raise ValueError(f"h2d engine must be hip or sdma, not {v!r}")
     return v
 
 
 def async_dma() -> bool:
-    """Staging workers submit their SDMA copy and move on; the writer waits
-    for it (engine/staging.py ``d2h_staged``)."""
-    return _get_bool("ASYNC_DMA", True)
+    return bool(_tuned("async_dma"))
 
 
 def get_dma_inflight() -> int:
-    """Device -> host SDMA copies in flight per device (async staging)."""
-    return max(1, _get_int("DMA_INFLIGHT", 8))
+    return max(1, int(_tuned("dma_inflight")))
 
 
 def serial_encode() -> bool:
-    """Staging threads take turns launching (and waiting for) HSZ1 encodes on
-    a device instead of sharing the CUs (engine/staging.py ``_encode_turn``)."""
-    return _get_bool("SERIAL_ENCODE", True)
-
-
-def get_gil_switch_us() -> int:
-    """GIL switch interval (microseconds) while a take / restore runs on the
-    calling thread; 0 = leave Python's (5000)."""
-    return _get_int("GIL_SWITCH_US", 0)
+    return bool(_tuned("serial_encode"))
 
 
 def thread_staging_enabled() -> bool:
-    """Stage writes on long-running worker threads that pull the next request
-    themselves (engine/scheduler.py ``_stage_on_threads``); 0 = one event-loop
-    round trip per request (custom stagers always take that path)."""
-    return _get_bool("THREAD_STAGING", True)
+    return bool(_tuned("thread_staging"))
 
 
 def checksum_enabled() -> bool:
     """Record an hs64 checksum of every blob a take writes
     (``.snapshot_checksums/<rank>``, ops/checksum.py); ``Snapshot.verify``
-    checks them."""
+    and ``restore(verify=True)`` check them."""
     return _get_bool("CHECKSUM", True)
 
 
 def get_hash_grid() -> int:
-    """Workgroups of one blob-checksum launch (0 = whole chip).  Narrow by
-    default: a full-width hash saturates HBM reads and slows the concurrent
-    SDMA copies (scripts/probes/hash_probe.py); blobs only need hashing at PCIe rate."""
-    return _get_int("HASH_GRID", 64)
-
-
-def get_drain_cus() -> int:
-    """Grid cap (workgroups, ~CUs) for the kernels of an async-take drain
-    while training continues; 0 (default) = uncapped.  Measured on Llama-3-8B
-    + AdamW (profiles/overlap_iso/README.md): caps of 16-128 stretch the drain
-    (the encoder runs at 1.8 GB/s per workgroup) without lowering the total
-    training time a checkpoint costs (250-400 ms either way), so no cap."""
-    return max(0, _get_int("DRAIN_CUS", 0))
+    return int(_tuned("hash_grid"))
 
 
 def get_read_head_bytes() -> int:
-    """Whole HSZ1 blobs larger than twice this are read as a head of this
-    many bytes and the rest, as two requests: the head's frames go to the GPU
-    while the rest is still being read (the restore's first H2D starts after
-    the head, not after the whole first blob).  0 = one read per blob."""
-    return max(0, _get_int("READ_HEAD_BYTES", 16 * 1024 * 1024))
-
-
-def get_read_order() -> str:
-    """Restore read order: ``plan`` (manifest order, default) or ``pipeline``
-    (a small lead read, then largest first).  Measured A/B on one MI355X,
-    Llama-3-8B restore, median of 5: plan 70.7 / 72.8 GB/s, pipeline 65.1 /
-    68.2 GB/s (profiles/timeline_r2/read_order.txt)."""
-    return str(_get("READ_ORDER") or "plan")
+    return max(0, int(_tuned("read_head_bytes")))
 
 
 def get_state_dict_barriers() -> str:
@@ -293,6 +307,13 @@ def get_state_dict_barriers() -> str:
     return {"1": "always", "true": "always", "0": "never", "false": "never"}.get(v, v)
 
 
+def force_collectives() -> bool:
+    """Issue every metadata collective (and the async commit's store barrier)
+    even in a one-rank process group, as the reference does
+    (`pg_wrapper.py:42-56`); by default a one-rank group skips them."""
+    return _get_bool("FORCE_COLLECTIVES", False)
+
+
 def rebalance_enabled() -> bool:
     """Move whole blobs from heavily to lightly loaded ranks over xGMI before
     a blocking take stages (parallel/rebalance.py).  Off by default."""
@@ -300,66 +321,54 @@ def rebalance_enabled() -> bool:
 
 
 def rebalance_host() -> bool:
-    """Let the rebalancer move host (CPU) blobs too (gloo tests)."""
-    return _get_bool("REBALANCE_HOST", False)
+    return bool(_tuned("rebalance_host"))
 
 
 def rebalance_min_gain() -> float:
-    """Stop once the load spread is below this fraction of the mean."""
-    return float(_get("REBALANCE_MIN_GAIN") or 0.1)
+    return float(_tuned("rebalance_min_gain"))
 
 
 def hbm_arena_keep() -> bool:
-    """Keep the async-take HBM arena allocated between takes and reuse it
-    (``hipsnapshot.release_hbm_arena()`` frees it).  Default on."""
-    return _get_bool("HBM_ARENA_KEEP", True)
+    return bool(_tuned("hbm_arena_keep"))
 
 
 def native_drain_enabled() -> bool:
     """Drain an async take's raw frozen blobs to the local FS in native
-    threads (engine/native_drain.py, csrc/hsdrain.hip)."""
+    threads (engine/native_drain.py, csrc/hsdrain.cpp)."""
     return _get_bool("NATIVE_DRAIN", True)
 
 
-# native drain sizing: 16 writers x 16 slots of 64 MiB drain the 16 GB
-# Llama-3-8B arena at the PCIe rate with an idle trainer (307 ms, was 380-475
-# ms with 8 x 12 x 32 MiB; profiles/r3/s2/drain_sizing/).  The writers stay
-# within half of this rank's CPU share: a drain runs next to a training
-# loop, and writer threads that use up a cgroup CPU quota stall the
-# trainer's thread with them (8 writers on the 16-CPU box).
 def get_drain_slot_bytes() -> int:
-    return max(1 << 20, _get_int("DRAIN_SLOT_BYTES", 64 << 20))
+    return max(1 << 20, int(_tuned("drain_slot_bytes")))
 
 
 def get_drain_slots() -> int:
     """Pinned slots the native drain cycles through (slots x slot bytes of
     pinned host memory while a drain runs, outside the memory budget)."""
-    return max(2, _get_int("DRAIN_SLOTS", 16))
+    return max(2, int(_tuned("drain_slots")))
 
 
 def get_drain_writers() -> int:
-    """Writer threads of an async take's native drain: 3 (at most half the
-    rank's CPU share, at least 2).  The drain runs beside training: with 8
-    writers a launch-bound seq-512 Llama-3-8B step ran 5-9 % slower while a
-    48 GB drain was in flight, with 3 writers 2-5 % (the drain takes 2.6 s
-    instead of 1.4-2.1 s; the training time lost per checkpoint is about the
-    same, 0.22 vs 0.25 of a blocking take; profiles/r4/overlap_ab_writers/)."""
+    """Writer threads of an async take's native drain while training goes
+    on: 3 (at most half the rank's CPU share, at least 2).  With 8 writers a
+    launch-bound seq-512 Llama-3-8B step ran 5-9 % slower while a 48 GB drain
+    was in flight, with 3 writers 2-5 % (profiles/r4/overlap_ab_writers/)."""
     share = available_cpus() // max(_local_ranks_hint[0], 1)
     return max(1, _get_int("DRAIN_WRITERS", min(3, get_io_threads(), max(2, share // 2))))
 
 
 def get_drain_boost_writers() -> int:
     """Writer threads of a native drain once its caller blocks on it
-    (``PendingSnapshot.wait``): the extra ones are parked until then.  With
-    an idle trainer 16 writers drain 16 GB in ~310 ms, 3 in ~490 ms."""
+    (``PendingSnapshot.wait``): the extra ones are parked until then.  Nothing
+    trains while the caller waits, so they may use the rank's whole CPU share
+    (not half of it): the ZeRO-3 OPT-shape save (40 GB) ran at 24 GB/s with
+    8 writers and 34-49 GB/s with 16 (profiles/r5/zero3_ab/)."""
     share = available_cpus() // max(_local_ranks_hint[0], 1)
-    return max(1, _get_int("DRAIN_BOOST_WRITERS", min(16, get_io_threads(), max(2, share // 2))))
+    return max(get_drain_writers(), min(16, get_io_threads(), max(2, share)))
 
 
 def get_drain_nice() -> int:
-    """Nice increment of the native drain's threads (0-19, default 10): they
-    yield a shared core to the training loop's launch thread."""
-    return max(0, min(19, _get_int("DRAIN_NICE", 10)))
+    return max(0, min(19, int(_tuned("drain_nice"))))
 
 
 def _arch_features(arch_name: str) -> dict:
@@ -389,147 +398,101 @@ def device_xnack_enabled(index: int = 0) -> bool:
 
 def uvm_assume_host() -> bool:
     """Managed (UVM) tensors that were never advised / prefetched are in host
-    DRAM (blocking takes write them in place).  Default: unless the device runs
-    with XNACK on (``device_xnack_enabled``), where pages migrate to the GPU that
-    touches them.  Measured: a never-placed table reads at 57 GB/s from a kernel
-    (PCIe), 3.9 TB/s once prefetched to the GPU (profiles/r3/uvm/)."""
-    if _get("UVM_ASSUME_HOST") is not None:
-        return _get_bool("UVM_ASSUME_HOST", True)
+    DRAM (blocking takes write them in place) -- unless the device runs with
+    XNACK on (``device_xnack_enabled``), where pages migrate to the GPU that
+    touches them.  Measured: a never-placed table reads at 57 GB/s from a
+    kernel (PCIe), 3.9 TB/s once prefetched to the GPU (profiles/r3/uvm/)."""
+    v = _tuned("uvm_assume_host")
+    if v is not None:
+        return bool(v)
     return not device_xnack_enabled()
 
 
 def drain_avoid_caller_core() -> str:
-    """Where the native drain's threads may NOT run, relative to the thread
-    that called ``async_take`` (utils/affinity.py): ``"core"`` (default) its
-    physical core -- a launch-bound training step loses issue slots to an SMT
-    sibling busy with page-cache copies; ``"l3"`` every CPU sharing its L3
-    (the writers' streaming copies then evict none of the trainer's cached
-    interpreter and allocator state); ``""`` anywhere is fine.  Env
-    ``DRAIN_AVOID_CALLER_CORE``: 0/1 or core/l3."""
-    v = (_get("DRAIN_AVOID_CALLER_CORE") or "core").strip().lower()
-    if v in ("0", "false", "no", "off", ""):
-        return ""
-    return "l3" if v == "l3" else "core"
+    v = str(_tuned("drain_avoid_caller_core") or "").strip().lower()
+    return "" if v in ("0", "false", "no", "off", "") else ("l3" if v == "l3" else "core")
 
 
 def drain_hash_high_priority() -> bool:
-    """The native drain's hs64 launches run on a high-priority stream
-    (default): at normal priority a training step's GEMMs starved them
-    (profiles/r3/drain_probe/)."""
-    return _get_bool("DRAIN_HASH_HIGH_PRIORITY", True)
+    return bool(_tuned("drain_hash_high_priority"))
 
 
 def gc_after_plan() -> bool:
-    """One full Python GC pass at the end of a take that built a new take
-    plan (utils/tracing.paused_gc)."""
-    return _get_bool("GC_AFTER_PLAN", True)
-
-
-def drain_direct_io() -> bool:
-    """O_DIRECT files for the native drain of an async take: no CPU copy into
-    the page cache (and none of its cache / memory-bandwidth pressure on the
-    training process), at the storage device's write rate."""
-    return _get_bool("DRAIN_DIRECT_IO", False)
+    return bool(_tuned("gc_after_plan"))
 
 
 def async_device_codec() -> str:
-    """What an ``async_take`` with ``compression="hsz1"`` does with the device
-    state it froze in HBM: ``raw`` (default) drains it uncompressed -- the
-    encoder kernels would compete with the training step for the compute
-    units (+30 % step time while they run, profiles/overlap_iso/) -- or
-    ``same`` encodes it like a blocking take."""
-    v = str(_get("ASYNC_DEVICE_CODEC") or "raw").lower()
+    v = str(_tuned("async_device_codec")).lower()
     return v if v in ("raw", "same") else "raw"
 
 
 def plan_cache_enabled() -> bool:
-    """Reuse a take's plan for the next take of the same device-resident
-    tensors (``engine/plan_cache.py``)."""
-    return _get_bool("PLAN_CACHE", True)
+    return bool(_tuned("plan_cache"))
 
 
 def native_restore_enabled() -> bool:
     """Reads whose bytes all land in HBM go through ONE native job per device
-    (engine/native_restore.py, csrc/hsrestore.hip): pread -> pinned slots ->
+    (engine/native_restore.py, csrc/hsrestore.cpp): pread -> pinned slots ->
     SDMA uploads -> GPU decode / region copy, no Python per blob."""
     return _get_bool("NATIVE_RESTORE", True)
 
 
 def restore_prewarm_enabled() -> bool:
-    """A restore into HBM fills the native job's pinned slots and device
-    rings on a thread while it plans its reads (engine/native_restore.py
-    prewarm_for)."""
-    return _get_bool("RESTORE_PREWARM", True)
+    return bool(_tuned("restore_prewarm"))
 
 
 def restore_plan_cache_enabled() -> bool:
-    """A restore of the same snapshot into the same device tensors reuses the
-    previous restore's native plan (engine/restore_cache.py)."""
-    return _get_bool("RESTORE_PLAN_CACHE", True)
+    return bool(_tuned("restore_plan_cache"))
 
 
 def native_io_numa_local() -> bool:
-    """The native restore's reader threads run on the CPUs of their GPU's
-    NUMA node (the process's own mask is left alone): unbound, one rank's
-    W = 8 share restored in 42 ms, bound in 29 (profiles/r4/restore_native/)."""
-    return _get_bool("NATIVE_IO_NUMA_LOCAL", True)
+    return bool(_tuned("native_io_numa_local"))
 
 
 def get_restore_slot_bytes() -> int:
-    """Pinned slot size of the native restore = the largest SDMA upload: 8
-    MiB uploads ran the link at 38 GB/s, 32 MiB at 45; a request costs the
-    engine a fixed ~0.1 ms (profiles/r4/restore_native/)."""
-    return max(1 << 20, _get_int("RESTORE_SLOT_BYTES", 128 << 20))
+    return max(1 << 20, int(_tuned("restore_slot_bytes")))
 
 
 def get_restore_first_bytes() -> int:
-    """The job's first upload is at most this large: the link starts once it
-    is read, not once a whole slot is."""
-    return max(1 << 20, _get_int("RESTORE_FIRST_BYTES", 16 << 20))
+    return max(1 << 20, int(_tuned("restore_first_bytes")))
 
 
 def get_restore_piece_bytes() -> int:
-    """Bytes one reader ``pread``s at a time: several readers fill a slot."""
-    return max(256 << 10, _get_int("RESTORE_PIECE_BYTES", 4 << 20))
+    return max(256 << 10, int(_tuned("restore_piece_bytes")))
 
 
 def get_restore_sdma_engine() -> int:
-    """SDMA engine of the native restore's uploads: -1 = the one ROCr picks
-    per request, -2 = the lowest engine ROCr reports free for host -> device
-    copies, k = engine k (when free)."""
-    return _get_int("RESTORE_SDMA_ENGINE", -1)
+    return int(_tuned("restore_sdma_engine"))
 
 
 def get_restore_slots() -> int:
-    return max(2, _get_int("RESTORE_SLOTS", 6))
+    return max(2, int(_tuned("restore_slots")))
 
 
 def get_restore_readers() -> int:
     """pread threads of the native restore (page-cache copies of ~8 GB/s
-    each feed a 57 GB/s link): ``HIPSNAPSHOT_RESTORE_READERS``, else the I/O
-    thread count."""
-    v = _get("RESTORE_READERS")
-    return max(1, int(v)) if v is not None else max(4, min(12, get_io_threads()))
+    each feed a 57 GB/s link)."""
+    v = int(_tuned("restore_readers"))
+    return max(1, v) if v > 0 else max(4, min(12, get_io_threads()))
 
 
 def get_restore_device_budget() -> int:
     """HBM of each of the native restore's two rings (uncached upload
-    targets, decode scratch): blobs in flight between their first read and
-    the end of their decode / copy kernels."""
-    return max(4 << 20, _get_int("RESTORE_DEVICE_BUDGET", 2 << 30))
+    targets, decode scratch)."""
+    return max(4 << 20, int(_tuned("restore_device_budget")))
 
 
 def get_restore_keep_bytes() -> int:
-    """Idle restore blocks kept per pool after a restore: the rings of the
-    next restore then allocate nothing."""
-    return max(0, _get_int("RESTORE_KEEP_BYTES", (2 << 30) + (256 << 20)))
+    return max(0, int(_tuned("restore_keep_bytes")))
 
 
 def get_stage_threads() -> int:
-    return _get_int("STAGE_THREADS", 4)
+    return int(_tuned("stage_threads"))
 
 
 def use_direct_io() -> bool:
+    """O_DIRECT for blob files (take writes and the native drain): no CPU copy
+    into the page cache, at the storage device's write rate."""
     return _get_bool("FS_DIRECT_IO", False)
 
 
@@ -550,7 +513,7 @@ def hbm_staging_max_bytes() -> int:
 
 
 def slab_align() -> int:
-    return max(1, _get_int("SLAB_ALIGN", 256))
+    return max(1, int(_tuned("slab_align")))
 
 
 def trust_object_payloads() -> bool:
@@ -558,7 +521,32 @@ def trust_object_payloads() -> bool:
 
 
 def use_gpu_gather_for_slabs() -> bool:
-    return _get_bool("GPU_SLAB_GATHER", True)
+    return bool(_tuned("gpu_slab_gather"))
+
+
+def pinned_pool_max_bytes() -> int:
+    """Cap of the pinned host pool (bytes kept registered across takes)."""
+    return _get_int("PINNED_POOL_MAX_BYTES", 64 << 30)
+
+
+def fp8_format() -> str:
+    """Layout of ``quantize=`` blobs: ``mx`` (default: e4m3fn + E8M0 scale
+    per 32 elements), ``block`` (fp32 scale per 128), ``hadamard32`` (32-wide
+    Hadamard rotation on the matrix cores, then fp32-scale blocks)."""
+    v = str(_get("FP8_FORMAT") or "mx").strip().lower()
+    return v if v in ("mx", "block", "hadamard32") else "mx"
+
+
+def plan_settings() -> tuple:
+    """The configuration a take plan or a restore plan depends on (the plan
+    caches' key: engine/plan_cache.py, engine/restore_cache.py) -- values,
+    not every environment variable: a change of tracing or I/O thread count
+    keeps the plans."""
+    return (get_max_chunk_size_bytes(), get_max_shard_size_bytes(),
+            get_slab_size_threshold_bytes(), is_batching_disabled(), get_compression(),
+            checksum_enabled(), async_hbm_staging_enabled(), hbm_staging_reserve_bytes(),
+            hbm_staging_max_bytes(), native_drain_enabled(), native_restore_enabled(),
+            use_direct_io(), fp8_format(), tuple(sorted(vars(TUNING).items())))
 
 
 @contextmanager
@@ -602,6 +590,42 @@ def override_is_batching_disabled(disabled: bool) -> Generator[None, None, None]
 
 
 @contextmanager
+def override_tuning(**values: Any) -> Generator[None, None, None]:
+    old = {k: vars(TUNING).get(k, _MISSING) for k in values}
+    for k, v in values.items():
+        if not hasattr(_Tuning, k):
+            raise AttributeError(f"no tuning constant {k!r}")
+        setattr(TUNING, k, v)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is _MISSING:
+                delattr(TUNING, k)
+            else:
+                setattr(TUNING, k, v)
+
+
+_MISSING = object()
+
+
+@contextmanager
 def override_knob(name: str, value: Any) -> Generator[None, None, None]:
-    with _override_env_var(name, value):
+    """An environment knob (``ENV_KNOBS``) or, by its upper-case name, a
+    ``TUNING`` constant."""
+    if name in ENV_KNOBS:
+        with _override_env_var(name, value):
+            yield
+        return
+    attr = name.lower()
+    if not hasattr(_Tuning, attr):
+        raise KeyError(f"unknown knob {name!r}")
+    cur = getattr(TUNING, attr)
+    if isinstance(cur, bool) or (cur is None and str(value) in ("0", "1")):
+        value = str(value).strip().lower() in ("1", "true", "yes", "on")
+    elif isinstance(cur, int):
+        value = int(value)
+    elif isinstance(cur, float):
+        value = float(value)
+    with override_tuning(**{attr: value}):
         yield

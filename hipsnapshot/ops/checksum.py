@@ -80,7 +80,7 @@ def device_hash_start(dev: int, slot: int, ptr: int, nbytes: int,
                       after_slot: int = -1, max_grid: Optional[int] = None) -> int:
     """Enqueue the hs64 partial sum of device bytes on stream (dev, slot),
     after the work queued on stream (dev, after_slot) if that is >= 0, on at
-    most ``max_grid`` workgroups (default ``HIPSNAPSHOT_HASH_GRID``; 0 = the
+    most ``max_grid`` workgroups (default ``knobs.TUNING.hash_grid``; 0 = the
     whole chip).  Returns the handle ``device_hash_result`` takes."""
     import ctypes
 

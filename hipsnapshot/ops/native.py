@@ -246,8 +246,9 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_pinned_stats", None, [ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_pinned_trim", c_uint64, [])
         _declare(lib, "hsg_pinned_set_limit", None, [c_uint64])
-        lim = os.environ.get("HIPSNAPSHOT_PINNED_POOL_MAX_BYTES")
-        lib.hsg_pinned_set_limit(int(lim) if lim else 64 << 30)
+        from .. import knobs
+
+        lib.hsg_pinned_set_limit(knobs.pinned_pool_max_bytes())
         _declare(lib, "hsg_memcpy", c_int,
                  [c_int, c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_int, c_int])
         _declare(lib, "hsg_stream_join", c_int, [c_int, c_int, c_void_p])
@@ -838,6 +839,10 @@ class NativeDrain:
         err = c_int(0)
         flags = self.flags(fsync, hash_blobs, direct, hash_high_priority, nice) | \
             (max(0, min(parked_writers, 255)) << 16)
+        # boost() (any thread) and wait() (the drain's thread) both use the
+        # handle: hsg_drain_wait frees the job, so a boost must never run
+        # concurrently with or after it
+        self._lock = threading.Lock()
         self._h = lib.hsg_drain_start(dev, n, self._srcs, self._sizes, self._paths,
                                       slot_bytes, nslots, nwriters, flags, max_hash_grid,
                                       ctypes.byref(err))
@@ -855,9 +860,9 @@ class NativeDrain:
 
     def boost(self) -> None:
         """Start the parked writers (call while the job runs)."""
-        h = self._h
-        if h:
-            require_gpu_lib().hsg_drain_boost(h)
+        with self._lock:
+            if self._h:
+                require_gpu_lib().hsg_drain_boost(self._h)
 
     STATS = ("slot_wait", "hash_collect", "hash_launch", "sdma_submit", "sdma_wait", "pwrite",
              "close", "open", "wall")
@@ -870,7 +875,8 @@ class NativeDrain:
         written = c_uint64(0)
         msg = ctypes.create_string_buffer(256)
         st = (ctypes.c_double * len(self.STATS))()
-        h, self._h = self._h, None
+        with self._lock:
+            h, self._h = self._h, None
         r = lib.hsg_drain_wait(h, sums, ctypes.byref(written), msg, st)
         self.stats = {k: round(v, 4) for k, v in zip(self.STATS, st)}
         if r != 0:

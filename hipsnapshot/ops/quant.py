@@ -11,7 +11,7 @@ layout::
 
 blob = ``[fp8 payload (P bytes)][B fp32 scales]``.
 
-rotation ``"hadamard32"`` (opt-in, ``HIPSNAPSHOT_FP8_ROTATION=hadamard32``): the flat
+rotation ``"hadamard32"`` (opt-in, ``HIPSNAPSHOT_FP8_FORMAT=hadamard32``): the flat
 tensor is cut into groups of 32 elements and each group is multiplied by the
 32x32 Sylvester Hadamard matrix H (+-1 entries) before quantization; restore
 computes ``(Y' H) / 32``.  The rotation spreads outliers over the group; for
@@ -34,7 +34,7 @@ converts to OCP e4m3fn natively).
 Scale rule (both): ``scale = amax / 448`` (correctly rounded; 1 when the block
 is all zeros), ``q = e4m3fn(clamp(y / scale))`` with round-to-nearest-even.
 
-MX layout (default for un-rotated tensors; ``HIPSNAPSHOT_FP8_SCALE=fp32``
+MX layout (default for un-rotated tensors; ``HIPSNAPSHOT_FP8_FORMAT=block``
 selects the fp32-scale layout above)::
 
     {"format": "fp8_e4m3fn_mx", "block": 32, "scale": "e8m0", "rotation": "none",
@@ -82,15 +82,17 @@ def default_rotation() -> str:
     # Student-t(2) weights the rotated L2 error is ~1.6x the plain one, so the
     # rotation is opt-in; it pays when a block's dynamic range exceeds e4m3's
     # ~2^15 (values far below amax would otherwise fall into subnormals).
-    r = os.environ.get("HIPSNAPSHOT_FP8_ROTATION", "none").lower()
-    return r if r in ("hadamard32", "none") else "none"
+    from .. import knobs
+
+    return "hadamard32" if knobs.fp8_format() == "hadamard32" else "none"
 
 
 def default_scale() -> str:
-    """``e8m0`` (MX, default) or ``fp32`` (``HIPSNAPSHOT_FP8_SCALE``) for
-    un-rotated quantization."""
-    v = os.environ.get("HIPSNAPSHOT_FP8_SCALE", "e8m0").lower()
-    return v if v in ("e8m0", "fp32") else "e8m0"
+    """``e8m0`` (MX, default) or ``fp32`` (``HIPSNAPSHOT_FP8_FORMAT=block``)
+    for un-rotated quantization."""
+    from .. import knobs
+
+    return "fp32" if knobs.fp8_format() == "block" else "e8m0"
 
 
 MX_BLOCK = 32

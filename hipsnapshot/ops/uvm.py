@@ -34,7 +34,7 @@ def is_uvm_tensor(t: torch.Tensor) -> bool:
 def residency(t: torch.Tensor) -> str:
     """Where a managed tensor's pages live: ``"host"`` / ``"device"`` when
     advised or prefetched (``place``); never-placed pages are in host DRAM
-    unless XNACK migrates them (``HIPSNAPSHOT_UVM_ASSUME_HOST``), else
+    unless XNACK migrates them (``knobs.uvm_assume_host``), else
     ``"unknown"``.  Not a managed tensor: ``"not_managed"`` (the range query
     is only valid on managed memory)."""
     if not is_uvm_tensor(t):

@@ -25,6 +25,14 @@ fits a fixed 64 KiB frame (header with the true length + bytes), and falls
 back to a second round only for the ranks' overflow -- halving the
 latency-bound collective count of a take (10 + K object collectives,
 SURVEY 3.5).  Results are identical to torch's.
+
+World size 1: the reference issues every collective whenever a process group
+is given (`/root/reference/torchsnapshot/pg_wrapper.py:42-56`).  ``Comm``
+skips them for a one-rank group (nothing to exchange) unless
+``HIPSNAPSHOT_FORCE_COLLECTIVES=1`` (or ``Comm(pg, force=True)``): then a
+one-rank RCCL group runs the same framed all-gather, device broadcast and
+device barrier as an N-rank one -- the GPU tests use it so every RCCL code
+path has executed on the MI355X before a multi-GPU job relies on it.
 """
 
 from __future__ import annotations
@@ -37,6 +45,8 @@ from typing import Any, Dict, List, Optional
 
 import torch
 import torch.distributed as dist
+
+from .. import knobs
 
 _FRAME = 64 * 1024
 _HDR = struct.Struct("<q")
@@ -56,10 +66,18 @@ def _side_stream(dev: int) -> "torch.cuda.Stream":
 
 
 class Comm:
-    def __init__(self, pg: Optional[dist.ProcessGroup] = None) -> None:
+    def __init__(self, pg: Optional[dist.ProcessGroup] = None,
+                 force: Optional[bool] = None) -> None:
         if pg is None and dist.is_available() and dist.is_initialized():
             pg = dist.group.WORLD
         self.pg = pg
+        self.force = knobs.force_collectives() if force is None else bool(force)
+
+    def solo(self) -> bool:
+        """No collective is issued: no process group, or a one-rank group
+        outside forced mode.  Callers that skip a collective (or a store
+        barrier) at world size 1 must test this, not the world size."""
+        return self.pg is None or (not self.force and self.get_world_size() == 1)
 
     # -- topology ----------------------------------------------------------
 
@@ -88,7 +106,7 @@ class Comm:
     # -- collectives -------------------------------------------------------
 
     def barrier(self) -> None:
-        if self.pg is None or self.get_world_size() == 1:
+        if self.solo():
             return
         if "nccl" in str(self.backend()):
             with self._on_side_stream():
@@ -97,7 +115,7 @@ class Comm:
             dist.barrier(group=self.pg)
 
     def broadcast_object_list(self, obj_list: List[Any], src: int = 0) -> None:
-        if self.pg is None or self.get_world_size() == 1:
+        if self.solo():
             return
         with self._on_side_stream():
             dist.broadcast_object_list(obj_list, src=dist.get_global_rank(self.pg, src)
@@ -107,8 +125,7 @@ class Comm:
     def all_gather_object(self, obj_list: List[Any], obj: Any, frame: int = _FRAME) -> None:
         """``frame``: bytes per rank of the first (usually only) round; small
         payloads (the coalesce gather) pass a smaller one."""
-        ws = self.get_world_size()
-        if self.pg is None or ws == 1:
+        if self.solo():
             obj_list[0] = obj
             return
         with self._on_side_stream():
@@ -151,7 +168,7 @@ class Comm:
 
     def scatter_object_list(self, output_list: List[Any], input_list: Optional[List[Any]],
                             src: int = 0) -> None:
-        if self.pg is None or self.get_world_size() == 1:
+        if self.solo():
             output_list[0] = input_list[0] if input_list else None
             return
         # RCCL has no scatter of objects: broadcast the whole list, keep ours

@@ -75,8 +75,7 @@ def partition_write_reqs(entries: Dict[str, Entry], write_reqs: Dict[str, List[W
     if not set(write_reqs).issubset(entries):
         raise RuntimeError("Not all entries associated with the write reqs are passed in. "
                            f"Missing: {set(write_reqs) - set(entries)}.")
-    if os.environ.get("TORCH_SNAPSHOT_DISABLE_PARTITIONER") or \
-            os.environ.get("HIPSNAPSHOT_DISABLE_PARTITIONER"):
+    if os.environ.get("TORCH_SNAPSHOT_DISABLE_PARTITIONER"):
         # every rank writes its own copy of the replicated state, but only
         # rank 0's copy is referenced by the manifest (others are skipped).
         if pg.get_rank() == 0:

@@ -23,7 +23,7 @@ the most loaded ranks to the least loaded ones before staging:
    location does not depend on the writer); its checksum is recorded by the
    rank that wrote it.
 
-CPU tensors can be moved too (``HIPSNAPSHOT_REBALANCE_HOST=1``; tests use
+CPU tensors can be moved too (``knobs.TUNING.rebalance_host``; tests use
 it with gloo).  Async takes keep their blobs: the frozen arena is drained
 without collectives.
 """
@@ -151,7 +151,7 @@ def _blob_bytes(wr: WriteReq) -> Tuple[torch.Tensor, object]:
 
 def rebalance(write_reqs: List[WriteReq], comm: Comm) -> List[WriteReq]:
     ws = comm.get_world_size()
-    if ws == 1 or not knobs.rebalance_enabled():
+    if comm.solo() or not knobs.rebalance_enabled():
         return write_reqs
     host_ok = knobs.rebalance_host()
     mine = []
@@ -172,8 +172,7 @@ def rebalance(write_reqs: List[WriteReq], comm: Comm) -> List[WriteReq]:
     rank = comm.get_rank()
     logger.info(f"rebalance: {len(moves)} blob(s), "
                 f"{sum(m[3] for m in moves) / 1e9:.2f} GB over xGMI")
-    ops, keep, launches, outgoing, incoming = [], [], [], set(), []
-    pg = comm.pg
+    sends, recvs, keep, launches, outgoing, incoming = [], [], [], [], set(), []
     for src, idx, dst, n, path in moves:
         if rank == src:
             buf, ka = _blob_bytes(write_reqs[idx])
@@ -181,27 +180,43 @@ def rebalance(write_reqs: List[WriteReq], comm: Comm) -> List[WriteReq]:
             if ka is not None:
                 launches.append(ka)
             outgoing.add(idx)
-            ops.append(dist.P2POp(dist.isend, buf, dist.get_global_rank(pg, dst)
-                                  if pg is not dist.group.WORLD else dst, group=pg))
+            sends.append((buf, dst))
         elif rank == dst:
             dev = torch.device("cuda", torch.cuda.current_device()) if on_dev[(src, idx)] \
                 else torch.device("cpu")
             buf = torch.empty(n, dtype=torch.uint8, device=dev)
             incoming.append((path, buf))
-            ops.append(dist.P2POp(dist.irecv, buf, dist.get_global_rank(pg, src)
-                                  if pg is not dist.group.WORLD else src, group=pg))
+            recvs.append((buf, src))
     if keep and any(b.is_cuda for b in keep):
         # every gather launch (and the producers queued before it on this
         # stream) must be done before a send reads its buffer and before its
         # pinned descriptor stage goes back to the pool
         torch.cuda.current_stream().synchronize()
     launches.clear()
-    if ops:
-        if "nccl" in str(comm.backend()):
-            works = dist.batch_isend_irecv(ops)  # one NCCL group: no ordering deadlock
-        else:
-            works = [op.op(op.tensor, op.peer, group=op.group) for op in ops]
-        for w in works:
-            w.wait()
+    p2p_exchange(sends, recvs, comm)
     kept = [wr for i, wr in enumerate(write_reqs) if i not in outgoing]
     return kept + [WriteReq(path=p, buffer_stager=ReceivedBlobStager(b)) for p, b in incoming]
+
+
+def p2p_exchange(sends: Sequence[Tuple[torch.Tensor, int]],
+                 recvs: Sequence[Tuple[torch.Tensor, int]], comm: Comm) -> None:
+    """Post every send ``(tensor, dst)`` and receive ``(tensor, src)`` (ranks
+    relative to ``comm.pg``) and wait for all of them.  RCCL: one
+    ``batch_isend_irecv`` group (device buffers over xGMI; no ordering
+    deadlock, and a rank may be its own peer); CPU backends: plain
+    isend/irecv."""
+    pg = comm.pg
+
+    def peer(r: int) -> int:
+        return dist.get_global_rank(pg, r) if pg is not dist.group.WORLD else r
+
+    ops = [dist.P2POp(dist.isend, t, peer(d), group=pg) for t, d in sends] + \
+          [dist.P2POp(dist.irecv, t, peer(s), group=pg) for t, s in recvs]
+    if not ops:
+        return
+    if "nccl" in str(comm.backend()):
+        works = dist.batch_isend_irecv(ops)
+    else:
+        works = [op.op(op.tensor, op.peer, group=op.group) for op in ops]
+    for w in works:
+        w.wait()

@@ -55,7 +55,6 @@ from .engine import native_restore, restore_cache, staging
 from .engine.scheduler import (
     PendingIOWork,
     get_process_memory_budget_bytes,
-    order_reads_for_pipeline,
     _budget_cache,
     sync_execute_read_reqs,
     sync_execute_write_reqs,
@@ -274,9 +273,8 @@ class Snapshot:
         loop = asyncio.new_event_loop()
         comm = Comm(pg)
         t0 = time.monotonic()
-        with timeline.span("coalesce"):
-            path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
-        storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
+        path, rep, keys, nonce, storage = cls._open_and_coalesce(
+            path, comm, app_state, replicated, loop, storage_options)
         progress: Dict[str, Any] = {}
         try:
             with roctx_range("hipsnapshot.take.plan_and_stage"):
@@ -294,7 +292,7 @@ class Snapshot:
                 if comm.get_rank() == 0:
                     with timeline.span("write_metadata", "commit"):
                         cls._write_snapshot_metadata(metadata, storage, loop)
-                if comm.get_world_size() > 1:
+                if not comm.solo():
                     # take() returns on every rank only once the snapshot is
                     # committed: a rank may read it right away (the reference
                     # returns before rank 0 has written the metadata)
@@ -349,10 +347,8 @@ class Snapshot:
         comm = Comm(pg)
         t0 = time.monotonic()
         tp0 = time.perf_counter()
-        with timeline.span("coalesce"):
-            path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
-        with timeline.span("storage_open"):
-            storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
+        path, rep, keys, nonce, storage = cls._open_and_coalesce(
+            path, comm, app_state, replicated, loop, storage_options)
         progress: Dict[str, Any] = {}
         try:
             pending, metadata = cls._take_impl(path, app_state, rep, keys, comm, storage, loop,
@@ -382,6 +378,36 @@ class Snapshot:
         timeline.add("unblock", "phase", tp0, time.perf_counter())
         timeline.dump("async_take", comm.get_rank())
         return ps
+
+    @classmethod
+    def _open_and_coalesce(cls, path: str, comm: Comm, app_state: AppState,
+                           replicated: Optional[List[str]], loop: asyncio.AbstractEventLoop,
+                           storage_options: Optional[Dict[str, Any]]):
+        """Commit rule (reference `snapshot.py:226-234`): a snapshot exists
+        iff its ``.snapshot_metadata`` exists.  A take into a path that holds
+        a committed snapshot overwrites its blobs, so rank 0 removes the old
+        commit (``_uncommit``) BEFORE it contributes to the coalesce gather:
+        no rank can finish that collective -- and so write its first blob --
+        while the old metadata still names the blobs being rewritten.  (Rank
+        0's path is the snapshot's path, so it can open storage first.)"""
+        storage = None
+        try:
+            if comm.get_rank() == 0:
+                with timeline.span("storage_open"):
+                    storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
+                with timeline.span("uncommit"):
+                    cls._uncommit(storage, loop)
+            with timeline.span("coalesce"):
+                path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
+            if storage is None:
+                with timeline.span("storage_open"):
+                    storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
+        except BaseException:
+            if storage is not None:
+                storage.sync_close(loop)
+            loop.close()
+            raise
+        return path, rep, keys, nonce, storage
 
     @staticmethod
     def _uncommit(storage: StoragePlugin, loop: asyncio.AbstractEventLoop) -> None:
@@ -413,9 +439,6 @@ class Snapshot:
                    compression: Optional[str] = None,
                    progress: Optional[Dict[str, Any]] = None,
                    ) -> Tuple[PendingIOWork, SnapshotMetadata]:
-        if comm.get_rank() == 0:
-            with timeline.span("uncommit"):
-                cls._uncommit(storage, loop)
         app_state = dict(app_state)
         rng_item = cls._pop_rng_state(app_state)
         manifest: Dict[str, Entry] = {}
@@ -447,7 +470,7 @@ class Snapshot:
             rep_paths = cls._calculate_replicated_entries(flattened, replicated, comm)
         from .engine import plan_cache
         from .format.serialization import Serializer
-        from .io.compression import plan_compression, resolve
+        from .io.compression import host_requested, plan_compression, resolve
 
         comp = resolve(compression)
         if is_async and comp != "none" and knobs.async_device_codec() == "raw" \
@@ -467,8 +490,9 @@ class Snapshot:
                     everything = dict(app_state)
                     if rng_item is not None:
                         everything[rng_item[0]] = rng_item[1]
-                    cache_key = plan_cache.settings_key(everything, rank, comm.get_world_size(),
-                                                        is_async, quantize, comp)
+                    cache_key = plan_cache.settings_key(
+                        everything, rank, comm.get_world_size(), is_async, quantize,
+                        comp + ("+host" if host_requested(compression) else ""))
                     plan = plan_cache.lookup(cache_key, resident)
                     if progress is not None and plan is not None:
                         # owned by this take from here on: a failure anywhere
@@ -514,7 +538,7 @@ class Snapshot:
                     name_prefix=f"r{rank}" if plan is None else f"r{rank}v")
         if comp == "hsz1":
             with timeline.span("plan_compression"):
-                plan_compression(write_reqs)
+                plan_compression(write_reqs, include_host=host_requested(compression))
         if plan is not None:
             object_entries = {k: plan.entries[k] if k in plan.entries else object_entries[k]
                               for k in flattened
@@ -558,7 +582,7 @@ class Snapshot:
             for wr in write_reqs:
                 (deferred if is_deferrable(wr) else now).append(wr)
             write_reqs = now
-        if not is_async and comm.get_world_size() > 1 and knobs.rebalance_enabled():
+        if not is_async and not comm.solo() and knobs.rebalance_enabled():
             # uneven device loads: move whole blobs to idle ranks over xGMI
             # (a collective: before the background metadata gather starts)
             from .parallel.rebalance import rebalance
@@ -681,7 +705,6 @@ class Snapshot:
         with timeline.span("batch_reads", n=len(reads)):
             if not knobs.is_batching_disabled():
                 reads = batch_read_requests(reads)
-            reads = order_reads_for_pipeline(reads)
         native_jobs, py_reads = native_restore.split(reads, storage, budget)
         with timeline.span("read_pipeline", n=len(reads)):
             sync_execute_read_reqs(py_reads, storage, budget, comm.get_rank(), loop,
@@ -830,7 +853,7 @@ class Snapshot:
         comm.all_gather_object(gathered, mine, frame=4096)
         # per-key barriers only when some rank's state_dict() may run a
         # collective (every rank sees the same gathered flags)
-        comm.state_dict_barriers = ws > 1 and not all(g[5] for g in gathered)
+        comm.state_dict_barriers = not comm.solo() and not all(g[5] for g in gathered)
         root_path = gathered[0][0]
         if root_path != path:
             logger.warning(f"Rank {rank} specified a path ({path}) different from rank 0 "
@@ -863,7 +886,7 @@ class Snapshot:
         mine = sorted(p for p, v in flattened.items()
                       if not is_sharded(v) and any(fnmatch.fnmatch(p, g) for g in replicated))
         ws = comm.get_world_size()
-        if ws == 1 or not replicated:
+        if comm.solo() or not replicated:
             # ``replicated`` is the cross-rank intersection from _coalesce, so
             # every rank takes this early exit together (no collective needed)
             return set(mine)
@@ -1100,7 +1123,7 @@ def _report_async_failure(comm: Comm, path: str, nonce: str, exc: BaseException)
     publish the error on the async commit barrier so the leader fails in
     ``arrive`` and every peer in ``depart``.  Only an EXISTING store is used
     (creating one is collective and the peers are not in a collective)."""
-    if comm.get_world_size() <= 1:
+    if comm.solo():
         return
     store = existing_store(comm)
     if store is None:
@@ -1133,7 +1156,7 @@ class PendingSnapshot:
         self.stats: Dict[str, float] = {}
         self._go = threading.Event()  # set by async_take once it is returning
         self._gc_after = False  # run the new plan's full GC pass after the commit
-        store = get_or_create_store(comm) if comm.get_world_size() > 1 else None
+        store = None if comm.solo() else get_or_create_store(comm)
         self._pending_io_work = pending_io_work
         self.thread = threading.Thread(
             target=self._complete_snapshot, name="hipsnapshot-commit",

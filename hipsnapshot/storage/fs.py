@@ -104,8 +104,8 @@ class FSStoragePlugin(StoragePlugin):
     def native_drain_root(self):
         """(root, fsync, O_DIRECT) for the native drain of an async take's
         frozen blobs (engine/native_drain.py).  O_DIRECT when this plugin
-        writes O_DIRECT or ``HIPSNAPSHOT_DRAIN_DIRECT_IO`` asks for it."""
-        return self.root, self.fsync, self.direct_io or knobs.drain_direct_io()
+        writes O_DIRECT (``direct_io`` storage option / ``HIPSNAPSHOT_FS_DIRECT_IO``)."""
+        return self.root, self.fsync, self.direct_io
 
     def native_read_root(self) -> str:
         """Root of the blobs for the native restore (engine/native_restore.py)."""

@@ -135,7 +135,7 @@ def describe(devices: List[int]) -> List[dict]:
 # memcpy takes a large share of the core's issue slots.  ``async_take`` notes
 # the core its caller runs on; the native drain's threads are created with an
 # affinity mask that excludes that core's hardware threads, or every CPU of
-# its L3 domain (``HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE`` = core (default) / l3
+# its L3 domain (``knobs.TUNING.drain_avoid_caller_core`` = core (default) / l3
 # / 0).
 
 _caller_cpu: List[Optional[int]] = [None]

@@ -200,8 +200,7 @@ class GcWatch:
 
 @contextlib.contextmanager
 def paused_gc(defer_plan_gc: Optional[list] = None):
-    """Suspend Python's cyclic GC for a bounded critical section (and, with
-    ``HIPSNAPSHOT_GIL_SWITCH_US``, shorten the GIL switch interval for it).
+    """Suspend Python's cyclic GC for a bounded critical section.
 
     Planning a snapshot allocates tens of thousands of small objects (entries,
     requests, futures); in a training process with a large heap that triggers
@@ -210,7 +209,7 @@ def paused_gc(defer_plan_gc: Optional[list] = None):
     Garbage created meanwhile is collected after the section.
 
     A take that built (and cached) a new take plan ends with one full
-    collection (``HIPSNAPSHOT_GC_AFTER_PLAN``, default on).  The plan's
+    collection (``knobs.TUNING.gc_after_plan``, default on).  The plan's
     objects are long-lived; CPython runs a full pass once the objects that
     survived into the oldest generation since the last full pass reach 25 %
     of those counted by it, and a training loop allocates almost nothing
@@ -224,21 +223,14 @@ def paused_gc(defer_plan_gc: Optional[list] = None):
     off the unblock path (while a GPU-bound training step waits on the
     device with the GIL released)."""
     import gc
-    import sys
 
     from .. import knobs
 
     was = gc.isenabled()
     gc.disable()
-    us = knobs.get_gil_switch_us()
-    prev = sys.getswitchinterval()
-    if us > 0:
-        sys.setswitchinterval(us * 1e-6)
     try:
         yield
     finally:
-        if us > 0:
-            sys.setswitchinterval(prev)
         if was:
             gc.enable()
             from ..engine import plan_cache

@@ -137,7 +137,7 @@ def verify_snapshot(path: str, storage_options: Optional[Dict[str, Any]] = None,
         storage.sync_close(loop)
         loop.close()
     report.seconds = time.monotonic() - t0
-    if ws > 1:
+    if comm is not None and not comm.solo():
         parts: List[Any] = [None] * ws
         comm.all_gather_object(parts, report)
         merged = VerifyReport(path=path, has_checksums=all(p.has_checksums for p in parts))

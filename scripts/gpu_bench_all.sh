@@ -2,8 +2,8 @@
 # All BASELINE configs that fit one MI355X. Each step bounded; stop at first failure.
 set -o pipefail
 mkdir -p gpurun_out/benches
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 R=gpurun_out/benches
 run() { name=$1; shift; echo "== $name"; timeout -k 10 ${T:-420} "$@" > $R/$name.json 2> $R/$name.err || { echo "FAIL $name"; tail -20 $R/$name.err; exit 1; }; cat $R/$name.json; }
 run ddp_20gb python benchmarks/ddp/main.py --repeats 3 --torch-save

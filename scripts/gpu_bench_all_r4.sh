@@ -4,8 +4,8 @@
 set -o pipefail
 R=gpurun_out/benches_r4
 mkdir -p $R
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 run() { name=$1; shift; echo "== $name"; timeout -k 10 ${T:-420} "$@" > $R/$name.json 2> $R/$name.err || { echo "FAIL $name"; tail -20 $R/$name.err; exit 1; }; tail -1 $R/$name.json | cut -c1-700; }
 run ddp_20gb python benchmarks/ddp/main.py --repeats 3
 run fsdp python benchmarks/fsdp/main.py

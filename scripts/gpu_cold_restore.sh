@@ -2,8 +2,8 @@
 # restore in a fresh process (restart case), then the same with a phase timeline
 set -o pipefail
 out=gpurun_out/cold_restore; mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 timeout -k 10 400 python benchmarks/cold_restore/main.py > $out/cold.json 2> $out/cold.err \
     || { echo COLD_FAIL; tail -30 $out/cold.err; exit 1; }
 cat $out/cold.json

@@ -3,7 +3,7 @@
 # ranks (sharing the GPU), restored by 4 ranks and by 1 rank, checksums compared.
 set -o pipefail
 mkdir -p gpurun_out/elastic
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD HSBENCH_DIR=$PWD/bench_tmp
 mkdir -p bench_tmp
 run() { local n=$1; shift; timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
     --master-addr 127.0.0.1 --master-port $((29700 + n)) benchmarks/elastic/main.py --backend gloo "$@"; }

@@ -4,8 +4,8 @@
 set -o pipefail
 out=gpurun_out/native_restore
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 timeout -k 10 300 python -u -m pytest tests/test_native_restore.py -x -v --timeout 120 \
     --timeout-method thread > $out/pytest_native.log 2>&1 \
     || { echo NATIVE_TESTS_FAIL; tail -60 $out/pytest_native.log; exit 1; }

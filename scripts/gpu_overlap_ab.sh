@@ -3,8 +3,8 @@
 set -o pipefail
 out=gpurun_out/overlap_ab
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 K=${KNOB:-HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE}
 for i in $(seq 1 ${N:-3}); do
   for v in ${VALS:-1 0}; do

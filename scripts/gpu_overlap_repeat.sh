@@ -3,8 +3,8 @@
 # per-step slowdown while an async snapshot drains)
 set -o pipefail
 mkdir -p gpurun_out/overlap_rep
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 for i in $(seq 1 ${N:-6}); do
   timeout -k 10 280 python benchmarks/train_overlap/main.py --seq 2048 --compression hsz1 \
       > gpurun_out/overlap_rep/run_$i.json 2> gpurun_out/overlap_rep/run_$i.err \

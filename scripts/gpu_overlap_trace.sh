@@ -6,8 +6,8 @@
 set -o pipefail
 out=gpurun_out/ovtrace
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 tr=/tmp/ovtrace_$$
 SEQ=${SEQ:-512}

@@ -4,8 +4,8 @@
 set -o pipefail
 out=gpurun_out/prewarm_ab
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 timeout -k 10 400 python -u -m pytest tests/test_native_restore.py -x -q -m gpu --timeout 120 \
     --timeout-method thread > $out/tests.log 2>&1 || { echo TEST_FAIL; tail -30 $out/tests.log; exit 1; }
 tail -1 $out/tests.log

@@ -3,8 +3,8 @@
 # native restore), then a kernel-trace-only pass of the W = 8 share restore.
 set -o pipefail
 mkdir -p gpurun_out/prof_r4
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
     -d gpurun_out/prof_r4/bench -o bench -- python3 bench.py --steps 2 --warmup 1 --async-iters 1 \

@@ -5,8 +5,8 @@ set -o pipefail
 bash scripts/gpu_fp8.sh || exit 1
 out=gpurun_out/rank_share
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 timeout -k 10 300 python benchmarks/rank_share/main.py --world 8 --restore-iters 5 \
     > $out/w8.json 2> $out/w8.err || { echo FAIL w8; tail -20 $out/w8.err; exit 1; }
 tail -1 $out/w8.json

@@ -4,8 +4,8 @@
 set -o pipefail
 out=gpurun_out/rank_share
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 for w in ${WS:-8 4 2 1}; do
   for c in ${COMP:-hsz1 none}; do
     timeout -k 10 240 python benchmarks/rank_share/main.py --world $w --compression $c \

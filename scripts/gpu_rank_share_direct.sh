@@ -4,8 +4,8 @@
 set -o pipefail
 out=gpurun_out/rank_share_direct
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 for mode in buffered direct buffered direct; do
   if [ $mode = direct ]; then export HIPSNAPSHOT_FS_DIRECT_IO=1; else unset HIPSNAPSHOT_FS_DIRECT_IO; fi
   timeout -k 10 300 python benchmarks/rank_share/main.py --world 8 --host-siblings 7 --steps 6 --warmup 2 \

@@ -4,8 +4,8 @@
 set -o pipefail
 out=gpurun_out/rs_restore_tl
 rm -rf $out; mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 W=${W:-8}
 HIPSNAPSHOT_TIMELINE=$PWD/$out/t timeout -k 10 240 python benchmarks/rank_share/main.py --world $W \
     --steps 2 --warmup 1 --async-iters 1 --restore-iters ${RESTORE_ITERS:-4} \

@@ -4,8 +4,8 @@
 # replicas + DDP buckets fit one card) and the elastic 8 -> 4 restore.
 set -o pipefail
 mkdir -p gpurun_out
-export PYTHONUNBUFFERED=1 HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 N=${N:-8}
 timeout -k 10 1000 python bench.py --gpus $N --backend gloo --steps 2 --warmup 1 \
     --async-iters 2 --restore-iters 2 --raw-steps 1 --fresh-steps 0 --ddp-steps 0 \

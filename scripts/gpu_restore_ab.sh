@@ -4,8 +4,8 @@
 set -o pipefail
 out=gpurun_out/restore_ab
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 for kv in ${ABS:-HIPSNAPSHOT_STAGE_THREADS=4,8}; do
   n=${kv%%=*}
   timeout -k 10 300 python benchmarks/rank_share/main.py --world ${W:-8} --steps 4 --warmup 2 \

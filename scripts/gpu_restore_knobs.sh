@@ -4,8 +4,8 @@
 set -o pipefail
 out=gpurun_out/restore_knobs
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 i=0
 for ab in ${ABS:-HIPSNAPSHOT_NATIVE_RESTORE=1,0 HIPSNAPSHOT_RESTORE_READERS=4,8,12 HIPSNAPSHOT_RESTORE_SLOT_BYTES=4194304,16777216,33554432}; do
   i=$((i+1))

@@ -7,8 +7,8 @@ set -o pipefail
 
 out=gpurun_out/restore_probe
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 run() {  # name, env..., args...
   local name=$1; shift
   timeout -k 10 300 env "$@" > $out/$name.json 2> $out/$name.err || { echo FAIL $name; tail -20 $out/$name.err; return 1; }

@@ -4,8 +4,8 @@
 set -o pipefail
 out=gpurun_out/restore_tl
 mkdir -p $out
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 HIPSNAPSHOT_TIMELINE=$PWD/$out/t timeout -k 10 300 python bench.py --steps 2 --warmup 1 \
     --async-iters 1 --restore-iters ${RESTORE_ITERS:-3} --raw-steps 0 ${BENCH_ARGS:-} \
     > $out/bench.json 2> $out/bench.err || { echo FAIL; tail -20 $out/bench.err; exit 1; }

@@ -2,8 +2,8 @@
 # full GPU suite, smoke, headline bench, train-overlap benchmark (hsz1 + raw)
 set -o pipefail
 mkdir -p gpurun_out/overlap
-export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HIPSNAPSHOT_BENCH_DIR=$PWD/bench_tmp
-mkdir -p $HIPSNAPSHOT_BENCH_DIR
+export PYTHONUNBUFFERED=1 PYTHONPATH=$PWD:$PYTHONPATH HSBENCH_DIR=$PWD/bench_tmp
+mkdir -p $HSBENCH_DIR
 TESTS=1 STEPS=5 bash scripts/gpu_check.sh || exit 1
 for c in hsz1 none; do
 timeout -k 10 600 python benchmarks/train_overlap/main.py --seq 2048 --compression $c \

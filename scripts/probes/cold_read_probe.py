@@ -27,7 +27,7 @@ if mode == "alloc":
         print(json.dumps({what: round((time.perf_counter() - t0) * 1e3, 2)}), flush=True)
     sys.exit(0)
 t = torch.randn(50000, 50000, device=dev)
-root = os.path.join(os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"), "cold_read_probe")
+root = os.path.join(os.environ.get("HSBENCH_DIR", "/tmp"), "cold_read_probe")
 shutil.rmtree(root, ignore_errors=True)
 Snapshot.take(root, {"sd": StateDict(t=t)})
 import cProfile  # noqa: E402

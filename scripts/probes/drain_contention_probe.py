@@ -31,7 +31,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gb", type=float, default=8.0)
     ap.add_argument("--blob-mb", type=int, default=96)
-    ap.add_argument("--dir", default=os.path.join(os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"),
+    ap.add_argument("--dir", default=os.path.join(os.environ.get("HSBENCH_DIR", "/tmp"),
                                                   "drain_probe"))
     ap.add_argument("--gemm", type=int, default=8192)
     args = ap.parse_args()

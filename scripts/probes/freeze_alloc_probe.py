@@ -42,7 +42,7 @@ dist.init_process_group("nccl", rank=0, world_size=1)
 torch.cuda.set_device(0)
 model = build_fsdp_llama(LlamaConfig.llama3_8b(), torch.device("cuda:0"), torch.bfloat16,
                          mesh=init_device_mesh("cuda", (1,)))
-path = os.path.join(os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"), "probe")
+path = os.path.join(os.environ.get("HSBENCH_DIR", "/tmp"), "probe")
 nbytes = 16060522496
 state("after model")
 a = timed_alloc(nbytes, "fresh process")

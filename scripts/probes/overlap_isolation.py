@@ -186,7 +186,7 @@ def main() -> None:
                     choices=["none", "take_hsz1", "take_raw", "d2h", "write", "encode",
                              "encode_capped"])
     ap.add_argument("--out", default="gpurun_out/iso")
-    ap.add_argument("--dir", default=os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"))
+    ap.add_argument("--dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     ap.add_argument("--seconds", type=float, default=6.0)
     ap.add_argument("--lead", type=float, default=1.0)
     ap.add_argument("--seq", type=int, default=2048)

@@ -26,7 +26,7 @@ for i in range(32):
         leaves[f"l{i}.{n}"] = torch.randn(*shape, device=dev, generator=g).bfloat16()
 leaves["norm"] = torch.randn(256, device=dev, generator=g).bfloat16()
 leaves["out"] = torch.randn(4096, 256, device=dev, generator=g).bfloat16()
-root = os.path.join(os.environ.get("HIPSNAPSHOT_BENCH_DIR", "/tmp"), "restore_plan_profile")
+root = os.path.join(os.environ.get("HSBENCH_DIR", "/tmp"), "restore_plan_profile")
 comp = os.environ.get("COMPRESSION", "hsz1")
 Snapshot.take(root, {"m": StateDict(**leaves)}, compression=comp)
 torch.cuda.synchronize()

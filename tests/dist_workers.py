@@ -516,3 +516,149 @@ def rebalance_take(path: str):
     assert out["r"] == rank
     for i in range(n):
         assert torch.equal(out[f"t{i}"], sd[f"t{i}"]), i
+
+
+def _register_guarded_fs(delay_s: float) -> None:
+    """``guardfs://``: the FS plugin, except that writing a blob while the
+    path still holds a ``.snapshot_metadata`` raises (a crash there would
+    leave a committed snapshot with torn blobs) and rank 0's delete of the
+    old metadata is delayed, so a rank that wrote before the uncommit would
+    be caught."""
+    from hipsnapshot.storage import fs as fsmod
+    from hipsnapshot.storage.registry import register_storage_plugin
+
+    class GuardedFS(fsmod.FSStoragePlugin):
+        def _committed(self) -> bool:
+            return os.path.exists(os.path.join(self.root, ".snapshot_metadata"))
+
+        async def write(self, write_io):
+            if write_io.path != ".snapshot_metadata" and self._committed():
+                raise AssertionError(f"rank {dist.get_rank()} wrote {write_io.path} "
+                                     "while the previous commit still existed")
+            return await super().write(write_io)
+
+        async def delete(self, path):
+            if path == ".snapshot_metadata":
+                time.sleep(delay_s)
+            return await super().delete(path)
+
+    register_storage_plugin("guardfs", lambda p, o: GuardedFS(root=p, storage_options=o))
+
+
+def rewrite_never_overlaps_commit(path: str, delay_s: float = 1.0):
+    """take / async_take into a path that holds a committed snapshot: every
+    rank's blob writes start only after rank 0 removed the old commit."""
+    from hipsnapshot.knobs import override_is_batching_disabled
+
+    _register_guarded_fs(delay_s)
+    rank = dist.get_rank()
+    sd = StateDict({f"w{i}": torch.full((256 + 64 * i,), float(rank + i)) for i in range(4)})
+    app = {"sd": sd}
+    with override_is_batching_disabled(True):  # one write per tensor
+        Snapshot.take(path, app)
+        dist.barrier()
+        for i in range(2):
+            sd[f"w{i}"] += 1.0
+            Snapshot.take("guardfs://" + path, app)
+            pending = Snapshot.async_take("guardfs://" + path, app)
+            pending.wait()
+    out = StateDict({f"w{i}": torch.zeros(256 + 64 * i) for i in range(4)})
+    Snapshot(path).restore({"sd": out})
+    for k in out:
+        assert torch.equal(out[k], sd[k]), k
+
+
+def forced_collectives(path: str, out_json: str, use_cuda: bool):
+    """``HIPSNAPSHOT_FORCE_COLLECTIVES=1`` in a one-rank group: every Comm
+    collective (framed all-gather incl. its overflow round, broadcast,
+    barrier, scatter), the store bootstrap broadcast, a self point-to-point
+    exchange (RCCL), and a whole take / async_take / restore (the sync
+    take's metadata gather runs on its helper thread beside staging) really
+    issue their collectives.  Writes what it observed to ``out_json`` so the
+    RCCL and gloo runs can be compared."""
+    import json
+
+    from hipsnapshot.parallel.comm import Comm
+    from hipsnapshot.parallel.rebalance import p2p_exchange
+    from hipsnapshot.parallel.store import create_store
+
+    os.environ["HIPSNAPSHOT_FORCE_COLLECTIVES"] = "1"
+    comm = Comm()
+    assert comm.force and not comm.solo() and comm.get_world_size() == 1
+    rank = comm.get_rank()
+    nccl = "nccl" in str(comm.backend())
+    res = {"backend": "nccl" if nccl else "gloo"}
+    small = [None]
+    comm.all_gather_object(small, {"rank": rank, "s": "x" * 100})
+    res["small"] = small
+    big_payload = bytes(range(256)) * 1024  # 256 KiB: the 64 KiB frame overflows
+    big = [None]
+    comm.all_gather_object(big, big_payload)
+    assert big[0] == big_payload
+    res["big_len"] = len(big[0])
+    objs = ["some/path", {"x": 3}] if rank == 0 else [None, None]
+    comm.broadcast_object_list(objs, src=0)
+    res["bcast"] = objs
+    comm.barrier()
+    out = [None]
+    comm.scatter_object_list(out, [["mine", rank]], src=0)
+    res["scatter"] = out
+    store = create_store(comm)  # rank 0 broadcasts the address: a collective
+    store.set("forced_k", "v")
+    res["store"] = store.get("forced_k").decode()
+    if nccl:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        src = torch.arange(1 << 20, dtype=torch.int32, device=dev)
+        dst = torch.empty_like(src)
+        p2p_exchange([(src, 0)], [(dst, 0)], comm)  # a rank is its own peer
+        torch.cuda.synchronize()
+        assert torch.equal(src, dst)
+    if use_cuda:
+        from torch.distributed.device_mesh import init_device_mesh
+
+        from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+
+        mesh = init_device_mesh("cuda", (1,))
+        torch.manual_seed(0)
+        m = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cuda", torch.cuda.current_device()),
+                             torch.bfloat16, mesh=mesh)
+
+        def full(mod):
+            return {k: v.full_tensor().clone() for k, v in mod.state_dict().items()}
+
+        def zero(mod):
+            for p in mod.parameters():
+                p._local_tensor.zero_()
+    else:
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.Linear(128, 8))
+
+        def full(mod):
+            return {k: v.clone() for k, v in mod.state_dict().items()}
+
+        def zero(mod):
+            with torch.no_grad():
+                for p in mod.parameters():
+                    p.zero_()
+    ref = full(m)
+    extra = StateDict(step=7)
+    app = {"model": m, "extra": extra}
+    s1 = Snapshot.take(path, app, replicated=["extra/**"])
+    pending = Snapshot.async_take(path + "_a", app)
+    s2 = pending.wait()
+    keys = {}
+    for tag, snap in (("take", s1), ("async", s2)):
+        zero(m)
+        extra["step"] = -1
+        Snapshot(snap.path).restore(app)
+        if use_cuda:
+            torch.cuda.synchronize()
+        got = full(m)
+        for k, v in ref.items():
+            assert torch.equal(got[k], v), (tag, k)
+        assert extra["step"] == 7
+        keys[tag] = sorted(Snapshot(snap.path).get_manifest().keys())
+    res["manifest_keys"] = keys
+    res["sha"] = {k: float(v.float().sum().item()) for k, v in sorted(ref.items())}
+    with open(out_json, "w") as f:
+        json.dump(res, f, sort_keys=True)

@@ -24,7 +24,7 @@ def _run(args, env_extra, timeout=120):
 
 
 def test_launcher_forwards_rank0_json():
-    p, _ = _run(["--gpus", "3"], {"HIPSNAPSHOT_BENCH_SELFTEST": "ok"})
+    p, _ = _run(["--gpus", "3"], {"HSBENCH_SELFTEST": "ok"})
     assert p.returncode == 0, p.stderr
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 3
@@ -33,7 +33,7 @@ def test_launcher_forwards_rank0_json():
 def test_launcher_propagates_rank_failure_and_stops_the_others():
     # rank 1 fails at once; ranks 0 and 2 would block forever (as in a
     # rendezvous waiting for rank 1): the launcher must end them and fail
-    p, dt = _run(["--gpus", "3"], {"HIPSNAPSHOT_BENCH_SELFTEST": "fail:1"})
+    p, dt = _run(["--gpus", "3"], {"HSBENCH_SELFTEST": "fail:1"})
     assert p.returncode == 3, (p.returncode, p.stderr)
     assert "rank 1 exited with 3" in p.stderr
     assert dt < 60
@@ -41,7 +41,7 @@ def test_launcher_propagates_rank_failure_and_stops_the_others():
 
 def test_launcher_timeout_fails_the_run():
     p, dt = _run(["--gpus", "2", "--launch-timeout", "3"],
-                 {"HIPSNAPSHOT_BENCH_SELFTEST": "fail:9"})
+                 {"HSBENCH_SELFTEST": "fail:9"})
     assert p.returncode == 124 and "timed out" in p.stderr
     assert dt < 60
 
@@ -49,7 +49,7 @@ def test_launcher_timeout_fails_the_run():
 def test_torchrun_world_size_mismatch_is_an_error():
     env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
                MASTER_ADDR="127.0.0.1", MASTER_PORT="29999")
-    env.pop("HIPSNAPSHOT_BENCH_SELFTEST", None)
+    env.pop("HSBENCH_SELFTEST", None)
     p = subprocess.run([sys.executable, BENCH, "--gpus", "2"], env=env, capture_output=True,
                        text=True, timeout=300)
     assert p.returncode == 2 and "WORLD_SIZE is 1" in p.stderr

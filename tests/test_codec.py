@@ -2,6 +2,8 @@
 
 import numpy as np
 import pytest
+
+from hipsnapshot import knobs
 import torch
 
 from hipsnapshot.ops import codec
@@ -196,7 +198,9 @@ def test_validate_offsets_rejects_corrupt_table():
 
 @pytest.fixture
 def host_compression(monkeypatch):
-    monkeypatch.setenv("HIPSNAPSHOT_COMPRESSION_HOST", "1")
+    # the takes below ask for compression="hsz1+host" (host tensors too);
+    # takes without compression= must stay uncompressed
+    monkeypatch.delenv("HIPSNAPSHOT_COMPRESSION", raising=False)
 
 
 def _weights(seed=0):
@@ -219,7 +223,7 @@ def test_snapshot_compressed_roundtrip(tmp_path, host_compression, batching):
 
     src = _weights()
     with override_is_batching_disabled(not batching):
-        snap = Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(**src)}, compression="hsz1")
+        snap = Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(**src)}, compression="hsz1+host")
         man = snap.get_manifest()
         assert man["0/sd/big_bf16"].codec["name"] == "hsz1"
         assert man["0/sd/big_bf16"].codec["w"] == 2
@@ -253,7 +257,7 @@ def test_snapshot_compressed_chunked_and_metadata_compat(tmp_path, host_compress
 
     t = (torch.randn(1000, 300) * 0.02).to(torch.bfloat16)
     with override_max_chunk_size_bytes(100_000):
-        Snapshot.take(str(tmp_path / "c"), {"sd": StateDict(t=t)}, compression="hsz1")
+        Snapshot.take(str(tmp_path / "c"), {"sd": StateDict(t=t)}, compression="hsz1+host")
     md = json.loads((tmp_path / "c" / ".snapshot_metadata").read_text())
     ent = md["manifest"]["0/sd/t"]
     assert ent["type"] == "ChunkedTensor" and len(ent["chunks"]) > 3
@@ -283,13 +287,12 @@ def _dtensor_worker(path: str, mode: str) -> None:
 
     from hipsnapshot import Snapshot, StateDict
 
-    os.environ["HIPSNAPSHOT_COMPRESSION_HOST"] = "1"
     mesh = init_device_mesh("cpu", (dist.get_world_size(),))
     torch.manual_seed(0)
     full = (torch.randn(640, 96) * 0.02).to(torch.bfloat16)
     if mode == "save":
         d = distribute_tensor(full, mesh, [Shard(0)])
-        Snapshot.take(path, {"sd": StateDict(w=d)}, compression="hsz1")
+        Snapshot.take(path, {"sd": StateDict(w=d)}, compression="hsz1+host")
     else:
         d = distribute_tensor(torch.zeros_like(full), mesh, [Shard(1)])
         Snapshot(path).restore({"sd": StateDict(w=d)})
@@ -330,7 +333,7 @@ def test_compressed_restore_with_split_head_read(tmp_path, host_compression, mon
     from hipsnapshot.knobs import override_is_batching_disabled
     from hipsnapshot.storage import fs as fs_mod
 
-    monkeypatch.setenv("HIPSNAPSHOT_READ_HEAD_BYTES", str(64 * 1024))
+    monkeypatch.setattr(knobs.TUNING, "read_head_bytes", 64 * 1024)
     ranges = []
     orig = fs_mod.FSStoragePlugin.read
 
@@ -341,7 +344,7 @@ def test_compressed_restore_with_split_head_read(tmp_path, host_compression, mon
     monkeypatch.setattr(fs_mod.FSStoragePlugin, "read", spy)
     src = _weights(3)
     with override_is_batching_disabled(not batching):
-        Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(**src)}, compression="hsz1")
+        Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(**src)}, compression="hsz1+host")
         out = StateDict(**{k: torch.zeros_like(v) for k, v in src.items()})
         Snapshot(str(tmp_path / "s")).restore({"sd": out})
     for k, v in src.items():
@@ -357,8 +360,8 @@ def test_compressed_restore_fails_when_rest_read_fails(tmp_path, host_compressio
     from hipsnapshot.storage import fs as fs_mod
 
     src = {"big_bf16": _weights(4)["big_bf16"]}
-    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(**src)}, compression="hsz1")
-    monkeypatch.setenv("HIPSNAPSHOT_READ_HEAD_BYTES", str(64 * 1024))
+    Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(**src)}, compression="hsz1+host")
+    monkeypatch.setattr(knobs.TUNING, "read_head_bytes", 64 * 1024)
     orig = fs_mod.FSStoragePlugin.read
 
     async def flaky(self, read_io):

@@ -111,3 +111,16 @@ def test_rebalance_plan_math():
         loads[dst] += n
     assert max(loads) - min(loads) <= 100 and loads[0] <= 350, (moves, loads)
     assert plan_moves([100, 100], [[(0, 10, "x")], []], 0.1, 4) == []
+
+
+def test_rewrite_of_committed_path_uncommits_before_any_blob_write(tmp_path):
+    # rank 0 deletes the old .snapshot_metadata before its part of the first
+    # collective; a blob written while it still exists fails the take
+    run_distributed(W.rewrite_never_overlaps_commit, 3, str(tmp_path / "rw"))
+
+
+def test_forced_collectives_at_world_size_one(tmp_path):
+    # HIPSNAPSHOT_FORCE_COLLECTIVES: a one-rank group issues every collective
+    # (the GPU suite runs the same worker on RCCL and compares)
+    run_distributed(W.forced_collectives, 1, str(tmp_path / "s"), str(tmp_path / "o.json"),
+                    False)

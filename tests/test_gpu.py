@@ -13,6 +13,7 @@ import torch
 
 from hipsnapshot import Snapshot, StateDict
 from hipsnapshot.knobs import override_knob, override_slab_size_threshold_bytes
+from hipsnapshot import knobs
 from hipsnapshot.ops import native
 from hipsnapshot.utils.test_utils import assert_state_dict_eq, run_distributed
 
@@ -271,7 +272,7 @@ def test_fp8_hadamard_snapshot_gpu(gpu, tmp_path):
     from hipsnapshot.utils.test_utils import env
 
     w = torch.randn(777, 333, device=gpu, dtype=torch.bfloat16)
-    with env(HIPSNAPSHOT_FP8_ROTATION="hadamard32"):
+    with env(HIPSNAPSHOT_FP8_FORMAT="hadamard32"):
         Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/*"])
     out = torch.zeros_like(w)
     Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=out)})
@@ -419,7 +420,7 @@ def test_fp8_quantized_save_gpu(gpu, tmp_path):
     from hipsnapshot.utils.test_utils import env
 
     w = torch.randn(1000, 333, device=gpu, dtype=torch.bfloat16)
-    with env(HIPSNAPSHOT_FP8_SCALE="fp32"):  # the fp32-scale layout (MX: test_mx8_*)
+    with env(HIPSNAPSHOT_FP8_FORMAT="block"):  # the fp32-scale layout (MX: test_mx8_*)
         Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/*"])
     out = torch.zeros_like(w)
     Snapshot(str(tmp_path / "s")).restore({"sd": StateDict(w=out)})
@@ -517,6 +518,45 @@ def _fsdp_gpu_worker(path):
 
 def test_fsdp2_rccl_single_rank(gpu, tmp_path):
     run_distributed(_fsdp_gpu_worker, 1, str(tmp_path / "f"), backend="nccl")
+
+
+def test_rccl_forced_collectives_match_gloo(gpu, tmp_path, monkeypatch):
+    """HIPSNAPSHOT_FORCE_COLLECTIVES: a one-rank RCCL group runs every
+    collective the planner and commit use -- framed all_gather_into_tensor
+    with its overflow round, broadcast with a device, barrier(device_ids),
+    scatter, the store bootstrap broadcast, the helper thread's manifest
+    gather, a self batch_isend_irecv -- around a whole FSDP2 take /
+    async_take / restore, with results identical to the gloo run of the
+    same worker.  The RCCL debug log must show the collectives ran."""
+    import json
+    import shutil
+
+    import dist_workers as W
+
+    logdir = tmp_path / "rccl"
+    logdir.mkdir()
+    monkeypatch.setenv("NCCL_DEBUG", "INFO")
+    monkeypatch.setenv("NCCL_DEBUG_SUBSYS", "INIT,COLL,P2P")
+    monkeypatch.setenv("NCCL_DEBUG_FILE", str(logdir / "rccl.%p.log"))
+    run_distributed(W.forced_collectives, 1, str(tmp_path / "n"), str(tmp_path / "n.json"),
+                    True, backend="nccl")
+    monkeypatch.delenv("NCCL_DEBUG")
+    run_distributed(W.forced_collectives, 1, str(tmp_path / "g"), str(tmp_path / "g.json"),
+                    True, backend="gloo")
+    rn = json.loads((tmp_path / "n.json").read_text())
+    rg = json.loads((tmp_path / "g.json").read_text())
+    assert rn.pop("backend") == "nccl" and rg.pop("backend") == "gloo"
+    assert rn == rg
+    log = "".join(f.read_text(errors="replace") for f in logdir.iterdir())
+    ops = {op: log.count(f"{op}: opCount") for op in ("AllGather", "Broadcast", "AllReduce")}
+    assert all(n > 0 for n in ops.values()), ops
+    art = os.environ.get("HSTEST_ARTIFACTS")
+    if art:  # the GPU runs keep the RCCL log (profiles/r5/rccl_forced/)
+        os.makedirs(art, exist_ok=True)
+        for f in logdir.iterdir():
+            shutil.copy(f, os.path.join(art, f.name))
+        with open(os.path.join(art, "rccl_forced_ops.json"), "w") as f:
+            json.dump(ops, f)
 
 
 def _multirank_gpu_worker(path, phase, compression=None):
@@ -704,15 +744,11 @@ def _corruptions(blob: bytes, w: int):
     return out
 
 
-@pytest.mark.parametrize("variant", ["staged", "staged-pf", "lds"])
 @pytest.mark.parametrize("w", [2, 4])
-def test_hsz_gpu_decode_rejects_corrupt_frames(gpu, w, variant, monkeypatch):
+def test_hsz_gpu_decode_rejects_corrupt_frames(gpu, w):
     """Every frame the host decoder rejects (-74) makes the GPU decode raise
-    too, instead of leaving the output unwritten; for each mode-2
-    decoder (HIPSNAPSHOT_HSZ_DECODE2)."""
+    too, instead of leaving the output unwritten."""
     from hipsnapshot.ops import codec
-
-    monkeypatch.setenv("HIPSNAPSHOT_HSZ_DECODE2", variant)
 
     g = torch.Generator().manual_seed(3)
     x = (torch.randn(3 * 65536 // w, generator=g) * 0.02)
@@ -735,15 +771,12 @@ def test_hsz_gpu_decode_rejects_corrupt_frames(gpu, w, variant, monkeypatch):
     assert out.cpu().numpy().tobytes() == raw
 
 
-@pytest.mark.parametrize("variant", ["staged", "staged-pf", "lds"])
 @pytest.mark.parametrize("w", [2, 4])
-def test_hsz_gpu_decode_variants_bit_exact(gpu, w, variant, monkeypatch):
-    """Each mode-2 decoder reproduces the input bit for bit: escapes (values
+def test_hsz_gpu_decode_bit_exact(gpu, w):
+    """The mode-2 decoder reproduces the input bit for bit: escapes (values
     outside the 15-entry dictionary), a short last frame with tail bytes, and
     an output that is not 16-B aligned (byte-store path)."""
     from hipsnapshot.ops import codec
-
-    monkeypatch.setenv("HIPSNAPSHOT_HSZ_DECODE2", variant)
     g = torch.Generator().manual_seed(11)
     n = (5 * 65536 + 4 * 1000 + 8) // w
     x = torch.randn(n, generator=g) * 0.02
@@ -1077,7 +1110,7 @@ def test_sdma_failure_falls_back_to_blit(gpu, tmp_path, monkeypatch, where):
 
         monkeypatch.setattr(native, "sdma_wait", wait_then_fail)
     else:
-        monkeypatch.setenv("HIPSNAPSHOT_ASYNC_DMA", "0")
+        monkeypatch.setattr(knobs.TUNING, "async_dma", False)
         monkeypatch.setattr(native, "sdma_d2h", broken)
     monkeypatch.setattr(staging, "_sdma_ok", {0: True})
     sd = StateDict(w=torch.randn(3000, 1000, device=gpu), b=torch.randn(77, device=gpu))
@@ -1158,7 +1191,7 @@ def test_gpu_compressed_restore_with_split_head_read(gpu, tmp_path, monkeypatch,
     (plain tensors) and through the scratch + region copy (slabs)."""
     from hipsnapshot.knobs import override_is_batching_disabled
 
-    monkeypatch.setenv("HIPSNAPSHOT_READ_HEAD_BYTES", str(64 * 1024))
+    monkeypatch.setattr(knobs.TUNING, "read_head_bytes", 64 * 1024)
     torch.manual_seed(5)
     sd = StateDict(
         w=(torch.randn(1500, 1000, device=gpu) * 0.02).to(torch.bfloat16),
@@ -1233,7 +1266,7 @@ def test_native_drain_matches_python_drain(gpu, tmp_path, fsync, direct, monkeyp
         import pathlib
 
         tmp_path = pathlib.Path(tmp_path)
-        monkeypatch.setenv("HIPSNAPSHOT_DRAIN_DIRECT_IO", "1")
+        monkeypatch.setenv("HIPSNAPSHOT_FS_DIRECT_IO", "1")
     try:
         _native_vs_python_drain(gpu, tmp_path, fsync, monkeypatch, native_drain,
                                 verify_snapshot)
@@ -1301,7 +1334,7 @@ def test_native_drain_rewrite_trims_and_async_codec_policy(gpu, tmp_path):
     """An async take into a path whose files are larger (an earlier take of a
     bigger state) leaves exactly the new bytes; compression='hsz1' async
     takes drain the frozen device state raw by default (natively) and encode
-    with HIPSNAPSHOT_ASYNC_DEVICE_CODEC=same."""
+    with knobs.TUNING.async_device_codec = "same"."""
     p = str(tmp_path / "s")
     w = torch.randn(4096, 1024, device=gpu)
     with override_slab_size_threshold_bytes(1 << 20):  # w is its own blob

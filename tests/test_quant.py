@@ -61,7 +61,8 @@ def test_rotation_error_tradeoff():
                                             ("hadamard32", "fp32")])
 def test_snapshot_fp8_formats(tmp_path, rotation, scale):
     w = torch.randn(257, 129)
-    with env(HIPSNAPSHOT_FP8_ROTATION=rotation, HIPSNAPSHOT_FP8_SCALE=scale):
+    fmt = "hadamard32" if rotation != "none" else ("block" if scale == "fp32" else "mx")
+    with env(HIPSNAPSHOT_FP8_FORMAT=fmt):
         Snapshot.take(str(tmp_path / "s"), {"sd": StateDict(w=w)}, quantize=["sd/w"])
     e = Snapshot(str(tmp_path / "s")).get_manifest()["0/sd/w"]
     assert e.quant["rotation"] == rotation

@@ -1,8 +1,8 @@
-"""Engine scheduling helpers: the shared host-memory gate and read ordering."""
+"""Engine scheduling helpers: the shared host-memory gate and I/O threads."""
 
 import asyncio
 
-from hipsnapshot.engine.scheduler import MemoryGate, execute_write_reqs, order_reads_for_pipeline
+from hipsnapshot.engine.scheduler import MemoryGate, execute_write_reqs
 from hipsnapshot.io_types import BufferConsumer, BufferStager, ReadReq, StagedBuffer, WriteReq
 from hipsnapshot.storage.memory import MemoryStoragePlugin
 
@@ -16,17 +16,6 @@ class _C(BufferConsumer):
 
     def get_consuming_cost_bytes(self):
         return self.n
-
-
-def test_read_order_small_lead_then_largest_first():
-    from hipsnapshot.knobs import override_knob
-
-    sizes = [300, 5 << 20, 100 << 20, 2 << 20, 400 << 20, 7]
-    reqs = [ReadReq(path=f"p{i}", buffer_consumer=_C(n)) for i, n in enumerate(sizes)]
-    assert order_reads_for_pipeline(reqs) == reqs  # default: manifest order
-    with override_knob("READ_ORDER", "pipeline"):
-        out = [r.buffer_consumer.n for r in order_reads_for_pipeline(reqs)]
-    assert out == [2 << 20, 400 << 20, 100 << 20, 5 << 20, 300, 7]
 
 
 def test_memory_gate_admission():

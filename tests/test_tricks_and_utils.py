@@ -339,8 +339,8 @@ def test_drain_threads_avoid_the_callers_core():
 def test_drain_avoid_knob_modes(monkeypatch):
     from hipsnapshot import knobs
 
+    assert knobs.drain_avoid_caller_core() == "core"  # default
     for v, want in (("1", "core"), ("core", "core"), ("l3", "l3"), ("0", ""), ("off", "")):
-        monkeypatch.setenv("HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE", v)
-        assert knobs.drain_avoid_caller_core() == want
-    monkeypatch.delenv("HIPSNAPSHOT_DRAIN_AVOID_CALLER_CORE")
+        with knobs.override_knob("DRAIN_AVOID_CALLER_CORE", v):
+            assert knobs.drain_avoid_caller_core() == want
     assert knobs.drain_avoid_caller_core() == "core"
