@@ -245,6 +245,9 @@ def main() -> None:
                          "(reference-format, uncompressed) blobs -> raw_GBps (0 = skip)")
     ap.add_argument("--restore-iters", type=int, default=3,
                     help="restores to time (median reported); each is checked bitwise")
+    ap.add_argument("--verify-iters", type=int, default=2,
+                    help="restores with verify=True (every blob checked against the take's "
+                         "checksums) -> restore_verify_GBps (0 = skip)")
     ap.add_argument("--fresh-steps", type=int, default=3,
                     help="takes to a NEW step_<i>/ directory each (as a training loop "
                          "writes them), timed one by one -> fresh_path_GBps (0 = skip)")
@@ -476,7 +479,6 @@ def main() -> None:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         restore_ok = bool(ok.item())
         restore_gbps = total_bytes / restore_s / 1e9
-        del refs
         restore_each = [round(total_bytes / t / 1e9, 2) for t in times]
         # the first restore plans from scratch, later ones of the same
         # snapshot into the same tensors reuse its plan (engine/restore_cache.py)
@@ -484,6 +486,26 @@ def main() -> None:
                         "restore_plan_cache": {k: restore_cache.stats[k] - rc0.get(k, 0)
                                                for k in ("hits", "misses", "stores")},
                         "native_restore_stats": dict(native_restore.last_stats)}
+        # the same restores with every blob checked against the take's hs64
+        # checksums (restore(verify=True): hashed in HBM inside the native job)
+        vtimes, vbad = [], 0
+        for _ in range(max(0, args.verify_iters)):
+            for _, p in named:
+                p._local_tensor.zero_()
+            barrier_sync()
+            tr = time.perf_counter()
+            Snapshot(path).restore(app_state, verify=True)
+            barrier_sync()
+            vtimes.append(time.perf_counter() - tr)
+            named = list(model.named_parameters())
+            vbad += sum(not torch.equal(r, p._local_tensor) for (_n, p), r in zip(named, refs))
+        del refs
+        if vtimes:
+            restore_info["restore_verify_bitwise_ok"] = vbad == 0
+            restore_info["restore_verify_GBps"] = round(
+                total_bytes / statistics.median(vtimes) / 1e9, 2)
+            restore_info["restore_verify_GBps_each"] = [round(total_bytes / t / 1e9, 2)
+                                                        for t in vtimes]
         log(f"restore: {restore_s:.3f}s ({restore_gbps:.2f} GB/s) ok={restore_ok} "
             f"each {restore_each} GB/s; {restore_info}")
 

@@ -1911,6 +1911,25 @@ int hsg_hash64(int dev, int slot, int after_slot, const void* p, uint64_t n,
   return 0;
 }
 
+// hs64's partial sum of device bytes [p, p + n) into the caller's device
+// accumulator `acc` (one u64, zeroed here), on the caller's `stream`: the
+// native restore hashes every uploaded blob on the stream that decodes it,
+// into one accumulator per blob of its own (no shared ring to outrun).
+int hsg_hash64_into(int dev, void* stream, const void* p, uint64_t n, uint64_t first_word,
+                    int max_grid, void* acc) {
+  HS_CHECK(hipSetDevice(dev));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto* a = static_cast<unsigned long long*>(acc);
+  HS_CHECK(hipMemsetAsync(a, 0, sizeof(unsigned long long), s));
+  const uint64_t words = n / 8 + 1;
+  int grid = static_cast<int>(std::min<uint64_t>((words + kBlock - 1) / kBlock, 256 * 8));
+  if (max_grid > 0) grid = std::min(grid, max_grid);
+  hipLaunchKernelGGL(hs_hash64, dim3(std::max(grid, 1)), dim3(kBlock), 0, s,
+                     static_cast<const uint8_t*>(p), n, first_word, a);
+  HS_CHECK(hipGetLastError());
+  return 0;
+}
+
 // The partial sum of hash `handle`, started on stream (dev, slot); waits for it.
 int hsg_hash64_result(int dev, int slot, int handle, uint64_t* out) {
   HS_CHECK(hipSetDevice(dev));

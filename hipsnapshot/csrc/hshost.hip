@@ -74,4 +74,13 @@ int hsg_rt_stream_sync(void* stream) {
   return hipStreamSynchronize(static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -1;
 }
 
+// Blocking device -> host copy of n bytes (small result arrays).
+int hsg_rt_memcpy_d2h(void* dst, const void* src, uint64_t n) {
+  if (hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return 0;
+}
+
 }  // extern "C"

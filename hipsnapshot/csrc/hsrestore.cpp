@@ -82,6 +82,9 @@ int hsg_rt_event_sync(void* ev);
 void hsg_rt_event_free(void* ev);
 int hsg_rt_stream_after(void* waiter, void* producer);
 int hsg_rt_stream_sync(void* stream);
+int hsg_rt_memcpy_d2h(void* dst, const void* src, uint64_t n);
+int hsg_hash64_into(int dev, void* stream, const void* p, uint64_t n, uint64_t first_word,
+                    int max_grid, void* acc);
 }
 
 namespace {
@@ -240,6 +243,7 @@ struct Item {
   uint64_t base_off = 0;   // region sources start here in the decoded / raw bytes
   int64_t desc_off = 0;    // first descriptor in the job's table
   int desc_n = 0;
+  bool hash = false;       // hs64 the uploaded (stored) bytes: restore(verify=True)
 
   // runtime
   std::mutex mu;
@@ -308,6 +312,9 @@ struct Job {
   uint64_t desc_size = 0;
   uint32_t* err_words = nullptr;  // host-mapped, one per item
   void* streams[2] = {nullptr, nullptr};
+  int hash_grid = 64;
+  uint64_t* hash_acc = nullptr;   // device: one hs64 partial sum per item
+
 
   std::vector<void*> slots;
   std::unique_ptr<SlotFill[]> fills;
@@ -592,6 +599,12 @@ bool hsz_header_ok(const Item& it, int* w, uint32_t* fb, uint32_t* nf) {
 int launch_item(Job* j, int i, void* s) {
   Item& it = j->items[i];
   char* base = static_cast<char*>(it.block);
+  // the stored bytes as they landed, before anything reads them
+  if (it.hash && hsg_hash64_into(j->dev, s, it.block, it.nbytes, 0, j->hash_grid,
+                                 j->hash_acc + i) != 0) {
+    j->fail(-EIO, i, "hash launch");
+    return -1;
+  }
   if (it.codec == kCodecHsz) {
     int w;
     uint32_t fb, nf;
@@ -750,6 +763,9 @@ extern "C" {
 // bytes, relative to base_off[i]) copy the bytes into their destinations.
 // Device work is ordered after every stream in `producers`.  `err_words`:
 // host-mapped uint32 per item (decoders flag corrupt frames there).
+// `hash_items` (nullable): items whose stored bytes are hs64-hashed in HBM
+// on their stream before anything reads them (grid <= `hash_grid`
+// workgroups); hsg_restore_wait returns the partial sums.
 // Returns a handle for hsg_restore_wait, or null with *err set.
 void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t* file_lo,
                         const uint64_t* nbytes, const int* codec, const uint64_t* logical,
@@ -757,7 +773,8 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
                         const int* desc_n, const void* descs, int64_t n_descs,
                         const uint64_t* producers, int n_producers, uint32_t* err_words,
                         uint64_t slot_bytes, uint64_t first_bytes, uint64_t piece_bytes,
-                        int nslots, int nreaders, uint64_t budget, int engine, int* err) {
+                        int nslots, int nreaders, uint64_t budget, int engine,
+                        const int* hash_items, int hash_grid, int* err) {
   *err = 0;
   if (hsg_rt_set_device(dev) != 0) {
     *err = -1;
@@ -790,6 +807,7 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
     it.base_off = base_off[i];
     it.desc_off = desc_off[i];
     it.desc_n = desc_n[i];
+    it.hash = hash_items != nullptr && hash_items[i] != 0;
     for (uint64_t off = 0; off < it.nbytes;) {
       const uint64_t cap = j->spans.empty() ? std::min(j->slot_bytes, first_bytes) : j->slot_bytes;
       const uint64_t n = std::min(cap, it.nbytes - off);
@@ -805,6 +823,7 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
       return nullptr;
     }
   }
+  j->hash_grid = hash_grid;
   // persistent streams (creating one costs ~1 ms of HIP runtime time)
   for (int s = 0; s < 2; ++s) {
     j->streams[s] = hsg_copy_stream(dev, kRestoreSlot + s);
@@ -861,11 +880,15 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   nslots = std::max(nslots, 2);
   j->fills.reset(new SlotFill[nslots]);
   j->slots.assign(nslots, nullptr);
+  bool any_hash = false;
+  for (const Item& it : j->items) any_hash |= it.hash;
+  if (any_hash) j->hash_acc = static_cast<uint64_t*>(hsg_rt_dev_alloc(dev, 8 * uint64_t(n), 0));
   // two slots now, the rest from a helper thread while the readers start:
   // a first use of pinned memory in the process registers it (~10 ms/GiB)
   for (int s = 0; s < 2; ++s) {
-    void* p = hsg_pinned_acquire(j->slot_bytes);
+    void* p = (any_hash && !j->hash_acc) ? nullptr : hsg_pinned_acquire(j->slot_bytes);
     if (!p) {
+      hsg_rt_dev_free(j->hash_acc);
       for (void* q : j->slots)
         if (q) hsg_pinned_release(q);
       g_upload_pool.release(j->up_base);
@@ -908,15 +931,24 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
 // Wait for the restore (blocking; Python calls it without the GIL).  Returns
 // 0 or the first error (negative errno); *err_item = the item it concerns
 // (-1: none); `msg` (>= 320 bytes) its text; `stats` (kNumStats doubles:
-// seconds) where the time went; *bytes_read the bytes read from files.
+// seconds) where the time went; *bytes_read the bytes read from files;
+// `sums` (n entries, nullable) the hs64 partial sums of the hashed items'
+// stored bytes (0 for the others).
 // Everything launched has finished when this returns (decode error words
 // are final).  Frees the job: call exactly once per handle.
 int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
-                     uint64_t* bytes_read) {
+                     uint64_t* bytes_read, uint64_t* sums) {
   Job* j = static_cast<Job*>(handle);
   for (auto& t : j->threads) t.join();
   for (int s = 0; s < 2; ++s) {
     if (hsg_rt_stream_sync(j->streams[s]) != 0) j->fail(-EIO, -1, "device work");
+  }
+  if (j->hash_acc) {
+    const size_t n = j->items.size();
+    if (sums && hsg_rt_memcpy_d2h(sums, j->hash_acc, 8 * n) != 0)
+      j->fail(-EIO, -1, "hash results");
+    hsg_rt_dev_free(j->hash_acc);
+    j->hash_acc = nullptr;
   }
   j->add(kWall, j->t_start);
   for (auto& it : j->items) {
@@ -983,6 +1015,11 @@ int hsg_restore_prewarm(int dev, uint64_t up_bytes, uint64_t sc_bytes, uint64_t 
 // bytes remain in each (per call; -1 device = all).  Returns bytes freed.
 uint64_t hsg_restore_trim(int dev, uint64_t keep) {
   return g_upload_pool.trim(dev, keep) + g_scratch_pool.trim(dev, keep);
+}
+
+// The same per pool: uncached upload blocks / plain scratch blocks.
+uint64_t hsg_restore_trim_pools(int dev, uint64_t keep_upload, uint64_t keep_scratch) {
+  return g_upload_pool.trim(dev, keep_upload) + g_scratch_pool.trim(dev, keep_scratch);
 }
 
 }  // extern "C"

@@ -284,16 +284,42 @@ def _join_prewarm() -> None:
         t.join()
 
 
-def run(jobs: Dict[int, list], budget: Optional[int] = None) -> int:
+def _hash_plan(entries, verifier) -> Optional[List[bool]]:
+    """Which items the job hashes (``restore(verify=True)``): those that read
+    a whole blob (HSZ1 items always do); the blobs of the others are noted
+    for a full read at the end (engine/blob_verify.py)."""
+    if verifier is None:
+        return None
+    out = []
+    for rr, item, _p in entries:
+        whole = item[3] == _HSZ or (item[1] == 0 and _file_size(item[0]) == item[2])
+        if not whole:
+            verifier.note_partial(rr.path)
+        out.append(whole)
+    return out
+
+
+def _file_size(path: str) -> Optional[int]:
+    try:
+        return os.path.getsize(path)
+    except OSError:
+        return None
+
+
+def run(jobs: Dict[int, list], budget: Optional[int] = None, verifier=None) -> int:
     """Run the planned jobs (blocking; call off the event loop); returns the
-    logical bytes restored.  Raises ``CorruptBlobError`` for rejected frames,
-    ``OSError`` / ``HipError`` for other failures."""
+    logical bytes restored.  Raises ``CorruptBlobError`` for rejected frames
+    (and, with a ``verifier``, for blobs whose stored bytes do not match the
+    take's checksums), ``OSError`` / ``HipError`` for other failures."""
+    from ..ops import checksum
+
     _join_prewarm()
     total = 0
     slot, first, nslots = sizing(budget)
     for dev, entries in jobs.items():
         t0 = time.perf_counter()
         items = [e[1] for e in entries]
+        hashed = _hash_plan(entries, verifier)
         prods = sorted({p for e in entries for p in e[2]})
         from ..utils.affinity import gpu_node_mask, threads_with_mask
 
@@ -304,7 +330,8 @@ def run(jobs: Dict[int, list], budget: Optional[int] = None) -> int:
             job = native.NativeRestore(dev, items, prods, slot, knobs.get_restore_piece_bytes(),
                                        nslots, knobs.get_restore_readers(),
                                        knobs.get_restore_device_budget(),
-                                       knobs.get_restore_sdma_engine(), first)
+                                       knobs.get_restore_sdma_engine(), first,
+                                       hash_items=hashed, hash_grid=knobs.get_hash_grid())
         t2 = time.perf_counter()
         rc, item, msg = job.wait()
         t3 = time.perf_counter()
@@ -332,5 +359,9 @@ def run(jobs: Dict[int, list], budget: Optional[int] = None) -> int:
             if rc < 0 and -rc in errno.errorcode:
                 raise OSError(-rc, msg)
             raise native.HipError(f"native restore failed ({rc}): {msg}")
+        if hashed:
+            for (rr, item, _p), h, s in zip(entries, hashed, job.sums):
+                if h:
+                    verifier.check_sum(rr.path, checksum.finish(s, item[2]), item[2])
         total += nbytes
     return total

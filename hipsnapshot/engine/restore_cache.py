@@ -133,16 +133,17 @@ def clear() -> None:
         _plans.clear()
 
 
-def run(plan: RestorePlan, budget: Optional[int] = None) -> int:
+def run(plan: RestorePlan, budget: Optional[int] = None, verifier=None) -> int:
     """Run a recorded plan's native jobs, ordered after the callers' current
-    streams on each device; returns the logical bytes restored."""
+    streams on each device; returns the logical bytes restored.  ``verifier``:
+    hash the whole blobs in the job (the caller finishes the partial ones)."""
     from . import native_restore
 
     jobs = {}
     for dev, entries in plan.jobs.items():
         prod = [int(torch.cuda.current_stream(dev).cuda_stream)]
         jobs[dev] = [(_Path(path), item, prod) for path, item in entries]
-    return native_restore.run(jobs, budget)
+    return native_restore.run(jobs, budget, verifier)
 
 
 class _Path:

@@ -591,11 +591,14 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                             memory_budget_bytes: int, rank: int,
                             consume_threads: Optional[int] = None,
                             io_concurrency: Optional[int] = None,
-                            native_jobs: Optional[dict] = None) -> PipelineStats:
+                            native_jobs: Optional[dict] = None,
+                            verifier=None) -> PipelineStats:
     """Run ``read_reqs``.  Reads whose bytes all land in HBM go to one native
     job per device (engine/native_restore.py) beside the Python pipeline for
     the rest; ``native_jobs``: a split the caller already made
-    (``native_restore.split``), ``read_reqs`` then being the Python part."""
+    (``native_restore.split``), ``read_reqs`` then being the Python part.
+    ``verifier`` (engine/blob_verify.py): check every blob read against the
+    take's checksums."""
     from . import native_restore
 
     if native_jobs is None:
@@ -603,10 +606,10 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
     native_fut = None
     if native_jobs:
         native_fut = asyncio.get_running_loop().run_in_executor(
-            aux_pool(), native_restore.run, native_jobs, memory_budget_bytes)
+            aux_pool(), native_restore.run, native_jobs, memory_budget_bytes, verifier)
     try:
         stats = await _execute_python_reads(read_reqs, storage, memory_budget_bytes, rank,
-                                            consume_threads, io_concurrency) \
+                                            consume_threads, io_concurrency, verifier) \
             if read_reqs or not native_jobs else PipelineStats()
     finally:
         if native_fut is not None:
@@ -617,13 +620,16 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
             raise native_bytes[0]
         stats.bytes_written += native_bytes[0]
         stats.n_reqs += sum(len(v) for v in native_jobs.values())
+    if verifier is not None:
+        await verifier.finish(storage)
     return stats
 
 
 async def _execute_python_reads(read_reqs: List[ReadReq], storage: StoragePlugin,
                                 memory_budget_bytes: int, rank: int,
                                 consume_threads: Optional[int] = None,
-                                io_concurrency: Optional[int] = None) -> PipelineStats:
+                                io_concurrency: Optional[int] = None,
+                                verifier=None) -> PipelineStats:
     consume_threads = consume_threads or knobs.get_stage_threads()
     io_concurrency = io_concurrency or knobs.get_io_threads()
     # reads are split across all I/O workers by the native engine, so a few
@@ -697,6 +703,8 @@ async def _execute_python_reads(read_reqs: List[ReadReq], storage: StoragePlugin
                                 None if t.cancelled() or t.exception() is None
                                 else t.exception()))
                 else:
+                    if verifier is not None:
+                        verifier.note_partial(rr.path)
                     head_io = ReadIO(path=rr.path, byte_range=(0, hsz.payload_start(nf)))
                     await storage.read(head_io)
                     header = hsz.parse_header(head_io.data())
@@ -725,6 +733,15 @@ async def _execute_python_reads(read_reqs: List[ReadReq], storage: StoragePlugin
         stats.bytes_written += hi - lo
         try:
             await rr.buffer_consumer.consume_buffer(span, executor)
+            if rest_task is not None:
+                await asyncio.gather(rest_task, return_exceptions=True)
+            if verifier is not None and stored is not None and (
+                    rest_task is None or (not rest_task.cancelled()
+                                          and rest_task.exception() is None)):
+                # the whole stored blob sits in ``full``: hash it before the
+                # buffer goes back to the pool
+                await asyncio.get_running_loop().run_in_executor(
+                    aux_pool(), verifier.check_host, rr.path, full.addr, stored)
         finally:
             if rest_task is not None:
                 await asyncio.gather(rest_task, return_exceptions=True)
@@ -761,6 +778,8 @@ async def _execute_python_reads(read_reqs: List[ReadReq], storage: StoragePlugin
             data = read_io.data()
             nb = memoryview(data).nbytes
             timeline.add("read", "io", t_r, t_c, path=rr.path, bytes=nb)
+            if verifier is not None:
+                await _verify_raw_read(verifier, storage, rr, data, nb)
             stats.bytes_written += nb
             await rr.buffer_consumer.consume_buffer(dest if dest is not None else data,
                                                     executor)
@@ -806,13 +825,28 @@ async def _execute_python_reads(read_reqs: List[ReadReq], storage: StoragePlugin
     return stats
 
 
+async def _verify_raw_read(verifier, storage: StoragePlugin, rr: ReadReq, data, nb: int) -> None:
+    from ..io_types import buffer_address
+    from .blob_verify import whole_read
+
+    stored = None
+    if rr.byte_range is not None and rr.byte_range[0] == 0:
+        stored = await storage.size(rr.path)
+    if whole_read(rr, stored):
+        mv = memoryview(data).cast("B")
+        await asyncio.get_running_loop().run_in_executor(
+            aux_pool(), verifier.check_host, rr.path, buffer_address(mv) if nb else 0, nb)
+    else:
+        verifier.note_partial(rr.path)
+
+
 def sync_execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
                            memory_budget_bytes: int, rank: int,
                            event_loop: asyncio.AbstractEventLoop,
-                           native_jobs: Optional[dict] = None) -> PipelineStats:
+                           native_jobs: Optional[dict] = None, verifier=None) -> PipelineStats:
     return run_sync(event_loop,
         execute_read_reqs(read_reqs, storage, memory_budget_bytes, rank,
-                          native_jobs=native_jobs))
+                          native_jobs=native_jobs, verifier=verifier))
 
 
 def hostname() -> str:

@@ -285,10 +285,11 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_int, c_int, P(c_char_p), P(c_uint64), P(c_uint64), P(c_int), P(c_uint64),
                   P(c_uint64), P(c_uint64), P(c_int64), P(c_int), c_void_p, c_int64,
                   P(c_uint64), c_int, c_void_p, c_uint64, c_uint64, c_uint64, c_int, c_int,
-                  c_uint64, c_int, P(c_int)])
+                  c_uint64, c_int, P(c_int), c_int, P(c_int)])
         _declare(lib, "hsg_restore_wait", c_int,
-                 [c_void_p, P(c_int), c_char_p, P(ctypes.c_double), P(c_uint64)])
+                 [c_void_p, P(c_int), c_char_p, P(ctypes.c_double), P(c_uint64), P(c_uint64)])
         _declare(lib, "hsg_restore_trim", c_uint64, [c_int, c_uint64])
+        _declare(lib, "hsg_restore_trim_pools", c_uint64, [c_int, c_uint64, c_uint64])
         _declare(lib, "hsg_restore_prewarm", c_int,
                  [c_int, c_uint64, c_uint64, c_uint64, c_int, c_uint64])
         _declare(lib, "hsg_sdma_h2d_submit", c_int,
@@ -896,14 +897,18 @@ class NativeRestore:
     ``items``: (path, file_lo, nbytes, codec (0 raw / 1 hsz1), logical,
     direct device address or 0, base_off, descriptor rows (packed
     COPY_DESC_DTYPE array whose ``src`` are offsets)).  ``producers``:
-    stream handles the device work is ordered after."""
+    stream handles the device work is ordered after.  ``hash_items``: per
+    item, hs64 its stored bytes in HBM before they are decoded / copied
+    (``restore(verify=True)``); ``wait`` then fills ``self.sums`` (partial
+    sums, ``checksum.finish`` them with the item's byte count)."""
 
     STATS = ("read", "slot_wait", "budget_wait", "alloc", "submit", "upload_wait", "launch",
              "retire_wait", "first_upload", "upload_busy", "wall")
 
     def __init__(self, dev: int, items: Sequence[tuple], producers: Sequence[int],
                  slot_bytes: int, piece_bytes: int, nslots: int, nreaders: int,
-                 budget: int, engine: int = -1, first_bytes: int = 16 << 20) -> None:
+                 budget: int, engine: int = -1, first_bytes: int = 16 << 20,
+                 hash_items: Optional[Sequence[bool]] = None, hash_grid: int = 64) -> None:
         import torch
 
         lib = require_gpu_lib()
@@ -932,12 +937,14 @@ class NativeRestore:
         # one host-mapped word per item: the decoder flags corrupt frames there
         # (pinned arrays are reused: a hipHostMalloc per restore costs ~1 ms)
         self.err_words = _take_err_words(m)
+        self._hash = (c_int * m)(*[int(bool(h)) for h in hash_items]) if hash_items else None
+        self.sums: List[int] = []
         err = c_int(0)
         self._h = lib.hsg_restore_start(
             dev, n, self._paths, self._lo, self._nb, self._codec, self._logical, self._direct,
             self._base, self._doff, self._dn, self._descs.ctypes.data, k, self._prod,
             len(producers), self.err_words.data_ptr(), slot_bytes, first_bytes, piece_bytes,
-            nslots, nreaders, budget, engine, ctypes.byref(err))
+            nslots, nreaders, budget, engine, self._hash, hash_grid, ctypes.byref(err))
         if not self._h:
             raise HipError(f"hsg_restore_start failed ({err.value})")
 
@@ -950,8 +957,11 @@ class NativeRestore:
         msg = ctypes.create_string_buffer(320)
         st = (ctypes.c_double * len(self.STATS))()
         nread = c_uint64(0)
+        sums = (c_uint64 * max(self.n, 1))() if self._hash is not None else None
         h, self._h = self._h, None
-        r = lib.hsg_restore_wait(h, ctypes.byref(item), msg, st, ctypes.byref(nread))
+        r = lib.hsg_restore_wait(h, ctypes.byref(item), msg, st, ctypes.byref(nread), sums)
+        if sums is not None:
+            self.sums = list(sums[: self.n])
         self.stats = {k: round(v, 5) for k, v in zip(self.STATS, st)}
         self.bytes_read = int(nread.value)
         return int(r), (int(item.value) if item.value >= 0 else None), \

@@ -625,19 +625,29 @@ class Snapshot:
 
     # --------------------------------------------------------------- restore
 
-    def restore(self, app_state: AppState) -> None:
-        """Restore ``app_state`` in place from this snapshot."""
+    def restore(self, app_state: AppState, verify: bool = False) -> None:
+        """Restore ``app_state`` in place from this snapshot.
+
+        ``verify``: check every blob read against the checksums the take
+        recorded (engine/blob_verify.py) and raise ``CorruptBlobError``
+        naming the first blob that does not match."""
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.restore")
         with paused_gc():
-            self._restore(app_state)
+            self._restore(app_state, verify)
 
-    def _restore(self, app_state: AppState) -> None:
+    def _restore(self, app_state: AppState, verify: bool = False) -> None:
         self._validate_app_state(app_state)
         _numa_bind_once()
         loop = asyncio.new_event_loop()
         comm = Comm(self.pg)
         storage = url_to_storage_plugin_in_event_loop(self.path, loop, self._storage_options)
         try:
+            verifier = None
+            if verify:
+                from .engine.blob_verify import RestoreVerifier
+
+                verifier = run_sync(loop, RestoreVerifier.load(storage,
+                                                               self.metadata.world_size))
             app_state = dict(app_state)
             rng_item = self._pop_rng_state(app_state)
             gathered: List[Any] = [None] * comm.get_world_size()
@@ -646,17 +656,17 @@ class Snapshot:
             knobs.set_local_ranks_hint([g[1] for g in gathered].count(socket.gethostname()))
             for key in keys:
                 with timeline.span("load_stateful", key=key):
-                    self._load_stateful(key, app_state.get(key), storage, comm, loop)
+                    self._load_stateful(key, app_state.get(key), storage, comm, loop, verifier)
                 comm.barrier()
             if rng_item is not None:
-                self._load_stateful(rng_item[0], rng_item[1], storage, comm, loop)
+                self._load_stateful(rng_item[0], rng_item[1], storage, comm, loop, verifier)
         finally:
             storage.sync_close(loop)
             loop.close()
         timeline.dump("restore", comm.get_rank())
 
     def _load_stateful(self, key: str, stateful: Optional[Stateful], storage: StoragePlugin,
-                       comm: Comm, loop: asyncio.AbstractEventLoop) -> None:
+                       comm: Comm, loop: asyncio.AbstractEventLoop, verifier=None) -> None:
         if stateful is None:
             return
         with timeline.span("restore_plan_view"):
@@ -684,7 +694,9 @@ class Snapshot:
             plan = restore_cache.lookup(cache_key)
             if plan is not None:
                 with timeline.span("read_pipeline", cached=True):
-                    restore_cache.run(plan, get_process_memory_budget_bytes(comm))
+                    restore_cache.run(plan, get_process_memory_budget_bytes(comm), verifier)
+                    if verifier is not None:
+                        run_sync(loop, verifier.finish(storage))
                 return
         budget = get_process_memory_budget_bytes(comm)
         # the native job's pinned slots / device rings fill beside the planning
@@ -708,7 +720,7 @@ class Snapshot:
         native_jobs, py_reads = native_restore.split(reads, storage, budget)
         with timeline.span("read_pipeline", n=len(reads)):
             sync_execute_read_reqs(py_reads, storage, budget, comm.get_rank(), loop,
-                                   native_jobs=native_jobs)
+                                   native_jobs=native_jobs, verifier=verifier)
         native_restore.join_prewarm()
         with timeline.span("load_state_dict", n=len(futs)):
             objs = {k: f.obj for k, f in futs.items()}
@@ -762,12 +774,13 @@ class Snapshot:
                                distributed=distributed, pg=self.pg)
 
     def read_object(self, path: str, obj_out: Optional[T] = None,
-                    memory_budget_bytes: Optional[int] = None) -> T:
+                    memory_budget_bytes: Optional[int] = None, verify: bool = False) -> T:
         """Read one persisted object by manifest path ``RANK/STATEFUL/KEY/...``.
 
         Tensor/ShardedTensor/DTensor ``obj_out`` are filled in place (sharded
         entries need an ``obj_out``); with ``memory_budget_bytes`` large
-        tensors are read in tiles that never exceed it.
+        tensors are read in tiles that never exceed it.  ``verify``: as for
+        ``restore``.
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.read_object")
         rank_str, unranked = path.split("/", 1)
@@ -792,9 +805,15 @@ class Snapshot:
                                       trust_objects=self.trust_objects)
             if not knobs.is_batching_disabled():
                 reads = batch_read_requests(reads)
+            verifier = None
+            if verify:
+                from .engine.blob_verify import RestoreVerifier
+
+                verifier = run_sync(loop, RestoreVerifier.load(storage,
+                                                               self.metadata.world_size))
             sync_execute_read_reqs(reads, storage,
                                    memory_budget_bytes or knobs.MAX_PER_RANK_MEMORY_BUDGET_BYTES,
-                                   Comm(self.pg).get_rank(), loop)
+                                   Comm(self.pg).get_rank(), loop, verifier=verifier)
         finally:
             storage.sync_close(loop)
             loop.close()

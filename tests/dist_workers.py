@@ -164,7 +164,9 @@ def fsdp_restore(path: str):
     orig = nn.Module.load_state_dict
     nn.Module.load_state_dict = lambda self, *a, **k: calls.append(1) or orig(self, *a, **k)
     try:
-        Snapshot(path).restore({"model": model})
+        # verified: the shard blobs of every saving rank (their checksum
+        # files), whole or as byte ranges of another world size's shards
+        Snapshot(path).restore({"model": model}, verify=True)
     finally:
         nn.Module.load_state_dict = orig
     assert not calls
@@ -173,7 +175,7 @@ def fsdp_restore(path: str):
         assert torch.equal(v.full_tensor(), ref[k]), k
     # read_object of a sharded entry into a plain tensor (whole global tensor)
     w = torch.zeros_like(ref["layers.0.attention.wq.weight"])
-    Snapshot(path).read_object("0/model/layers.0.attention.wq.weight", obj_out=w)
+    Snapshot(path).read_object("0/model/layers.0.attention.wq.weight", obj_out=w, verify=True)
     assert torch.equal(w, ref["layers.0.attention.wq.weight"])
 
 

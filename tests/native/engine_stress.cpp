@@ -109,6 +109,7 @@ struct RestorePlan {
   std::vector<std::vector<uint8_t>> expected;  // what they must hold
   std::vector<std::string> files;
   std::vector<std::vector<uint8_t>> file_data;
+  std::vector<int> hash;                       // items hashed in the job
   int first_hsz = -1;
 };
 
@@ -163,6 +164,7 @@ void add_item(RestorePlan& p, uint64_t L, int kind) {
     }
   }
   p.dn.push_back(n);
+  p.hash.push_back(int(rnd(0, 2) == 0));
 }
 
 int run_restore(RestorePlan& p, uint64_t slot, uint64_t first, uint64_t piece, int nslots,
@@ -172,6 +174,8 @@ int run_restore(RestorePlan& p, uint64_t slot, uint64_t first, uint64_t piece, i
   std::vector<const char*> cpaths;
   for (auto& s : p.paths) cpaths.push_back(s.c_str());
   std::vector<uint32_t> err_words(std::max(n, 1), 0);
+  std::vector<uint64_t> sums(std::max(n, 1), 0);
+  p.hash.resize(n, 0);
   std::vector<uint64_t> producers;
   for (int k = int(rnd(0, 2)); k > 0; --k) producers.push_back(reinterpret_cast<uint64_t>(stub::new_stream()));
   int err = 0;
@@ -179,7 +183,8 @@ int run_restore(RestorePlan& p, uint64_t slot, uint64_t first, uint64_t piece, i
                               p.logical.data(), p.direct.data(), p.base_off.data(), p.doff.data(),
                               p.dn.data(), p.descs.data(), int64_t(p.descs.size()),
                               producers.data(), int(producers.size()), err_words.data(), slot,
-                              first, piece, nslots, readers, budget, -1, &err);
+                              first, piece, nslots, readers, budget, -1, p.hash.data(), 64,
+                              &err);
   if (!h) {
     *msg = "start failed " + std::to_string(err);
     return -1000 + err;
@@ -188,9 +193,18 @@ int run_restore(RestorePlan& p, uint64_t slot, uint64_t first, uint64_t piece, i
   char text[320];
   double stats[16];
   uint64_t nread = 0;
-  const int rc = hsg_restore_wait(h, &item, text, stats, &nread);
+  const int rc = hsg_restore_wait(h, &item, text, stats, &nread, sums.data());
   *msg = text;
-  for (int i = 0; rc == 0 && i < n; ++i) CHECK(err_words[i] == 0, "decode flagged item %d", i);
+  for (int i = 0; rc == 0 && i < n; ++i) {
+    CHECK(err_words[i] == 0, "decode flagged item %d", i);
+    if (!p.hash[i]) continue;
+    // the hash covers the stored bytes of the item as read from its file
+    const std::vector<uint8_t>* file = nullptr;
+    for (size_t f = 0; f < p.files.size(); ++f)
+      if (p.files[f] == p.paths[i]) file = &p.file_data[f];
+    CHECK(file, "item %d file", i);
+    CHECK(sums[i] == stub::hash_bytes(file->data() + p.lo[i], p.nb[i]), "item %d hash", i);
+  }
   return rc;
 }
 

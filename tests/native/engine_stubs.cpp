@@ -292,6 +292,11 @@ int hsg_rt_stream_sync(void* stream) {
   return 0;
 }
 
+int hsg_rt_memcpy_d2h(void* dst, const void* src, uint64_t n) {
+  memcpy(dst, src, n);
+  return 0;
+}
+
 // ---- streams, pinned memory (hsgpu.hip) -----------------------------------------
 
 void* hsg_copy_stream(int dev, int slot) {
@@ -379,6 +384,15 @@ int hsg_hash64(int dev, int slot, int after_slot, const void* p, uint64_t n, uin
   const uint64_t h = new_handle(f);
   static_cast<Queue*>(hsg_copy_stream(dev, slot))->push([=] { f->set(0, hash_bytes(p, n)); });
   *handle = int(h);
+  return 0;
+}
+
+int hsg_hash64_into(int dev, void* stream, const void* p, uint64_t n, uint64_t first_word,
+                    int max_grid, void* acc) {
+  (void)dev;
+  (void)first_word;
+  (void)max_grid;
+  stream_of(stream)->push([=] { *static_cast<uint64_t*>(acc) = hash_bytes(p, n); });
   return 0;
 }
 

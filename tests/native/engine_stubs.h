@@ -38,9 +38,10 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
                         const int* desc_n, const void* descs, int64_t n_descs,
                         const uint64_t* producers, int n_producers, uint32_t* err_words,
                         uint64_t slot_bytes, uint64_t first_bytes, uint64_t piece_bytes,
-                        int nslots, int nreaders, uint64_t budget, int engine, int* err);
+                        int nslots, int nreaders, uint64_t budget, int engine,
+                        const int* hash_items, int hash_grid, int* err);
 int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
-                     uint64_t* bytes_read);
+                     uint64_t* bytes_read, uint64_t* sums);
 int hsg_restore_prewarm(int dev, uint64_t up_bytes, uint64_t sc_bytes, uint64_t slot_bytes,
                         int nslots, uint64_t table_bytes);
 uint64_t hsg_restore_trim(int dev, uint64_t keep);

@@ -1425,3 +1425,48 @@ def test_rebalance_blob_bytes_two_slabs_busy_stream(gpu):
             src = m._source_view().reshape(-1).view(torch.uint8)
             want[lo:lo + src.numel()] = src
         assert torch.equal(buf, want)
+
+
+@pytest.mark.parametrize("comp", ["none", "hsz1"])
+def test_native_restore_verify_flags_flipped_byte(gpu, tmp_path, comp):
+    """restore(verify=True) into HBM: the native job hashes every whole blob
+    in HBM right after its upload.  A byte flipped in a raw blob, or in an
+    HSZ1 blob's low-byte plane (which the frame checks do not cover), fails
+    the verified restore; the default restore is unchanged (and wrong)."""
+    from hipsnapshot.engine import native_restore
+    from hipsnapshot.ops import codec
+    from hipsnapshot.ops.native import CorruptBlobError
+
+    p = str(tmp_path / "s")
+    torch.manual_seed(7)
+    w = (torch.randn(2048, 1024, device=gpu) * 0.02).to(torch.bfloat16)
+    b = torch.randn(3000, device=gpu)
+    with override_slab_size_threshold_bytes(1 << 20):  # w is its own blob
+        Snapshot.take(p, {"sd": StateDict(w=w, b=b)}, compression=comp)
+    snap = Snapshot(p)
+    entry = snap.get_manifest()["0/sd/w"]
+    assert bool(entry.codec) == (comp == "hsz1")
+    ow, ob = torch.zeros_like(w), torch.zeros_like(b)
+    snap.restore({"sd": StateDict(w=ow, b=ob)}, verify=True)
+    torch.cuda.synchronize()
+    assert torch.equal(ow, w) and torch.equal(ob, b)
+    assert native_restore.last_stats.get("items", 0) >= 1  # the native job ran
+    blob = os.path.join(p, entry.location)
+    if comp == "hsz1":
+        with open(blob, "rb") as f:
+            hdr = codec.parse_header(f.read())
+        off = hdr.offsets[1] - 8  # the end of frame 0: its low-byte plane
+    else:
+        off = (entry.byte_range[0] if entry.byte_range else 0) + 4097
+    with open(blob, "r+b") as f:
+        f.seek(off)
+        c = f.read(1)
+        f.seek(off)
+        f.write(bytes([c[0] ^ 0x20]))
+    ow.zero_()
+    Snapshot(p).restore({"sd": StateDict(w=ow, b=ob)})
+    torch.cuda.synchronize()
+    assert not torch.equal(ow, w)
+    with pytest.raises(CorruptBlobError, match=entry.location):
+        Snapshot(p).restore({"sd": StateDict(w=torch.zeros_like(w), b=torch.zeros_like(b))},
+                            verify=True)

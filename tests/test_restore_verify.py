@@ -1,0 +1,98 @@
+"""restore(verify=True) / read_object(verify=True): every blob a restore reads
+is checked against the take's hs64 checksums (engine/blob_verify.py)."""
+
+import os
+
+import pytest
+import torch
+
+from hipsnapshot import Snapshot, StateDict
+from hipsnapshot.knobs import override_is_batching_disabled, override_slab_size_threshold_bytes
+from hipsnapshot.ops.native import CorruptBlobError
+
+
+def _flip(path: str, offset: int) -> None:
+    with open(path, "r+b") as f:
+        f.seek(offset)
+        b = f.read(1)
+        f.seek(offset)
+        f.write(bytes([b[0] ^ 0x10]))
+
+
+def _state(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return StateDict(w=torch.randn(300, 200, generator=g), b=torch.randn(77, generator=g),
+                     step=3)
+
+
+@pytest.mark.parametrize("batching", [True, False])
+def test_flipped_raw_byte_fails_verified_restore_only(tmp_path, batching):
+    p = str(tmp_path / "s")
+    src = _state()
+    with override_is_batching_disabled(not batching):
+        Snapshot.take(p, {"sd": src})
+        snap = Snapshot(p)
+        entry = snap.get_manifest()["0/sd/w"]
+        blob = os.path.join(p, entry.location)
+        lo = entry.byte_range[0] if entry.byte_range else 0
+        out = _state(1)
+        snap.restore({"sd": out}, verify=True)  # intact: passes
+        assert torch.equal(out["w"], src["w"])
+        _flip(blob, lo + 1234)
+        out = _state(1)
+        Snapshot(p).restore({"sd": out})  # default path: unchanged (no check)
+        assert not torch.equal(out["w"], src["w"])
+        with pytest.raises(CorruptBlobError, match=entry.location):
+            Snapshot(p).restore({"sd": _state(1)}, verify=True)
+
+
+def test_partial_reads_verify_the_whole_blob(tmp_path):
+    """read_object with a memory budget reads byte ranges of the blob: the
+    blob is hashed in full at the end, so a flip outside the ranges read is
+    still found."""
+    p = str(tmp_path / "s")
+    src = _state()
+    with override_slab_size_threshold_bytes(1):
+        Snapshot.take(p, {"sd": src})
+    entry = Snapshot(p).get_manifest()["0/sd/w"]
+    out = torch.zeros_like(src["w"])
+    Snapshot(p).read_object("0/sd/w", obj_out=out, memory_budget_bytes=4096, verify=True)
+    assert torch.equal(out, src["w"])
+    _flip(os.path.join(p, entry.location), 17)
+    with pytest.raises(CorruptBlobError):
+        Snapshot(p).read_object("0/sd/w", obj_out=torch.zeros_like(src["w"]),
+                                memory_budget_bytes=4096, verify=True)
+
+
+def test_flipped_low_byte_plane_of_hsz1_blob(tmp_path):
+    """HSZ1 frame checks validate the container, not the stored low bytes: a
+    flip there restores silently unless the checksum is checked."""
+    from hipsnapshot.ops import codec
+
+    p = str(tmp_path / "s")
+    g = torch.Generator().manual_seed(4)
+    w = (torch.randn(700, 1000, generator=g) * 0.02).to(torch.bfloat16)
+    with override_slab_size_threshold_bytes(1):
+        Snapshot.take(p, {"sd": StateDict(w=w)}, compression="hsz1+host")
+    entry = Snapshot(p).get_manifest()["0/sd/w"]
+    assert entry.codec
+    blob = os.path.join(p, entry.location)
+    with open(blob, "rb") as f:
+        raw = f.read()
+    hdr = codec.parse_header(raw)
+    # the last bytes of the first frame: its low-byte plane
+    _flip(blob, hdr.offsets[1] - 8)
+    out = torch.zeros_like(w)
+    Snapshot(p).restore({"sd": StateDict(w=out)})
+    assert not torch.equal(out, w)  # decodes "fine", wrong values
+    with pytest.raises(CorruptBlobError, match=entry.location):
+        Snapshot(p).restore({"sd": StateDict(w=torch.zeros_like(w))}, verify=True)
+
+
+def test_verify_needs_checksums(tmp_path, monkeypatch):
+    p = str(tmp_path / "s")
+    monkeypatch.setenv("HIPSNAPSHOT_CHECKSUM", "0")
+    Snapshot.take(p, {"sd": _state()})
+    monkeypatch.delenv("HIPSNAPSHOT_CHECKSUM")
+    with pytest.raises(RuntimeError, match="no blob checksums"):
+        Snapshot(p).restore({"sd": _state(1)}, verify=True)
