@@ -164,6 +164,12 @@ def sizing(budget: Optional[int]) -> Tuple[int, int, int]:
     return slot, min(first, slot), n
 
 
+def pinned_bytes(budget: Optional[int] = None) -> int:
+    """Pinned host memory one job holds: its slots and its copy-table stage."""
+    slot, _first, n = sizing(budget)
+    return n * slot + table_bytes(slot)
+
+
 def split(read_reqs: List[ReadReq], storage: StoragePlugin, budget: Optional[int] = None
           ) -> Tuple[Dict[int, list], List[ReadReq]]:
     """({device: [(read req, item)], ...} for native jobs, the Python part);

@@ -604,11 +604,17 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
     if native_jobs is None:
         native_jobs, read_reqs = native_restore.split(read_reqs, storage, memory_budget_bytes)
     native_fut = None
+    py_budget = memory_budget_bytes
     if native_jobs:
         native_fut = asyncio.get_running_loop().run_in_executor(
             aux_pool(), native_restore.run, native_jobs, memory_budget_bytes, verifier)
+        # the job's pinned slots count against the same host budget as the
+        # Python part running beside it (a mixed restore pinned
+        # ~1.5x the budget); one oversized read still runs (MemoryGate)
+        py_budget = max(1, memory_budget_bytes - len(native_jobs) *
+                        native_restore.pinned_bytes(memory_budget_bytes))
     try:
-        stats = await _execute_python_reads(read_reqs, storage, memory_budget_bytes, rank,
+        stats = await _execute_python_reads(read_reqs, storage, py_budget, rank,
                                             consume_threads, io_concurrency, verifier) \
             if read_reqs or not native_jobs else PipelineStats()
     finally:

@@ -39,7 +39,11 @@ _tls = threading.local()
 _slot_lock = threading.Lock()
 _next_slot = [0]
 NUM_COPY_SLOTS = 4
-_HASH_SLOT_BASE = 64  # hash streams: slots 64.. (copy slots stay below)
+# stream slots: copy 0..63, decode / scatter 64..127, hash 128..191 -- the
+# ranges never overlap whatever the staging thread count
+_MAX_COPY_SLOTS = 64
+_DECODE_SLOT_BASE = 64
+_HASH_SLOT_BASE = 128
 
 
 def copy_slot() -> int:
@@ -50,7 +54,7 @@ def copy_slot() -> int:
     if s is None:
         from .. import knobs
 
-        n = max(NUM_COPY_SLOTS, min(_HASH_SLOT_BASE, knobs.get_stage_threads()))
+        n = max(NUM_COPY_SLOTS, min(_MAX_COPY_SLOTS, knobs.get_stage_threads()))
         with _slot_lock:
             s = _next_slot[0] % n
             _next_slot[0] += 1
@@ -61,9 +65,6 @@ def copy_slot() -> int:
 def hash_slot(slot: int) -> int:
     """The stream that hashes blobs beside copy slot ``slot``'s DMAs."""
     return _HASH_SLOT_BASE + slot
-
-
-_DECODE_SLOT_BASE = 32  # decode / scatter streams of the restore: slots 32..
 
 
 def decode_slot(slot: int) -> int:

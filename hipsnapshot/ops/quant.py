@@ -20,7 +20,11 @@ e4m3 that only pays when a block's dynamic range exceeds the format's (see
 matrix cores.  bf16 / f16 tensors are rotated by ``v_mfma_f32_32x32x16_{bf16,f16}``
 (``hs_fp8_hadamard_quant16``: 2 MFMAs per 1024 elements; the MFMA sums 16 exact
 products in its own order, so a code can differ from the fp32 reference by one
-fp8 ulp -- tests bound it); fp32 tensors use ``v_mfma_f32_32x32x2_f32``
+fp8 ulp -- tests bound it.  So a bf16 / f16 tensor's rotated blob is NOT
+byte-reproducible across devices: quantized on the GPU and on the CPU it can
+give different codes, blob bytes and checksums.  Nothing depends on the two
+matching -- a checksum is of the bytes actually written, and replicated
+entries are deduplicated by manifest, not by blob contents); fp32 tensors use ``v_mfma_f32_32x32x2_f32``
 (exact f32 k-ordered FMA chains, ``hs_fp8_hadamard_quant``), bit-identical to
 the torch reference below, which uses the same sequential k order.  Every
 dequantization runs on ``v_mfma_f32_32x32x16_bf16`` over the codes widened to

@@ -266,3 +266,18 @@ def hsz_deep_tree_frame(n: int = 65536) -> bytes:
         pos += c
     lo = np.random.default_rng(5).integers(0, 256, n, dtype=np.uint8)
     return np.stack([lo, hi], 1).reshape(-1).tobytes()
+
+
+def low_byte_offset(blob_bytes: bytes) -> int:
+    """File offset of a byte in frame 0's low-byte plane of an HSZ1 blob
+    (stored verbatim: a flip there decodes without error, to a wrong value)."""
+    from hipsnapshot.ops import codec
+
+    hdr = codec.parse_header(blob_bytes)
+    mode = codec.frame_modes(blob_bytes)[0]
+    lo = hdr.offsets[0] + 32
+    if mode == 1:
+        n = min(hdr.frame_bytes, hdr.logical_size) // hdr.elem_width
+        lo += (n + 1) // 2
+    assert mode in (1, 2), mode
+    return lo + 100

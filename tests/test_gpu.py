@@ -1453,9 +1453,10 @@ def test_native_restore_verify_flags_flipped_byte(gpu, tmp_path, comp):
     assert native_restore.last_stats.get("items", 0) >= 1  # the native job ran
     blob = os.path.join(p, entry.location)
     if comp == "hsz1":
+        from hipsnapshot.utils.test_utils import low_byte_offset
+
         with open(blob, "rb") as f:
-            hdr = codec.parse_header(f.read())
-        off = hdr.offsets[1] - 8  # the end of frame 0: its low-byte plane
+            off = low_byte_offset(f.read())
     else:
         off = (entry.byte_range[0] if entry.byte_range else 0) + 4097
     with open(blob, "r+b") as f:

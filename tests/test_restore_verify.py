@@ -77,11 +77,10 @@ def test_flipped_low_byte_plane_of_hsz1_blob(tmp_path):
     entry = Snapshot(p).get_manifest()["0/sd/w"]
     assert entry.codec
     blob = os.path.join(p, entry.location)
+    from hipsnapshot.utils.test_utils import low_byte_offset
+
     with open(blob, "rb") as f:
-        raw = f.read()
-    hdr = codec.parse_header(raw)
-    # the last bytes of the first frame: its low-byte plane
-    _flip(blob, hdr.offsets[1] - 8)
+        _flip(blob, low_byte_offset(f.read()))
     out = torch.zeros_like(w)
     Snapshot(p).restore({"sd": StateDict(w=out)})
     assert not torch.equal(out, w)  # decodes "fine", wrong values

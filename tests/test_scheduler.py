@@ -203,3 +203,28 @@ def test_io_threads_respect_cgroup_cpu_quota(tmp_path, monkeypatch):
         assert knobs.get_io_threads() == 16  # 2 x 256 / 8, capped
     finally:
         knobs._local_ranks_hint[0] = old
+
+
+def test_mixed_restore_budget_counts_the_native_jobs_pinned_slots(monkeypatch):
+    """A restore whose HBM reads go to the native job and whose host reads
+    stay in the Python pipeline: the Python part gets the host budget minus
+    the job's pinned slots (it used to get all of it)."""
+    from hipsnapshot.engine import native_restore, scheduler
+
+    seen = {}
+
+    async def fake_python(read_reqs, storage, budget, rank, *a, **k):
+        seen["budget"] = budget
+        return scheduler.PipelineStats()
+
+    monkeypatch.setattr(native_restore, "split", lambda reqs, st, b: ({0: [("rr", None, [])]},
+                                                                      list(reqs)))
+    monkeypatch.setattr(native_restore, "run", lambda jobs, budget, verifier=None: 0)
+    monkeypatch.setattr(scheduler, "_execute_python_reads", fake_python)
+    budget = 1 << 30
+    reqs = [ReadReq(path="x", buffer_consumer=_C(10))]
+    asyncio.run(scheduler.execute_read_reqs(reqs, MemoryStoragePlugin(root="m"), budget, 0))
+    assert seen["budget"] == budget - native_restore.pinned_bytes(budget)
+    small = 4 << 20
+    asyncio.run(scheduler.execute_read_reqs(reqs, MemoryStoragePlugin(root="m"), small, 0))
+    assert seen["budget"] >= 1 and native_restore.pinned_bytes(small) <= small
