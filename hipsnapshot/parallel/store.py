@@ -12,6 +12,12 @@ trainer's RCCL calls), so ranks synchronise through c10d ``Store`` keys:
   two snapshots to the same path never see each other's stale keys (the
   reference keyed by path only), and ``depart`` marks the barrier departed
   (reference set ``arrived`` again, Appendix C #5).
+* A barrier leaves no keys behind: the leader deletes the peers' keys once it
+  has read them in ``arrive``, and the last peer to read the leader's key in
+  ``depart`` deletes it (a counter key says which peer is last).  Every
+  ``async_take`` of a long job used to add ~2 x world size keys to the default
+  c10d store for good.  Keys of a barrier that failed are left (they carry
+  the error).
 """
 
 from __future__ import annotations
@@ -98,6 +104,13 @@ class LinearBarrier:
     def _key(self, rank: int) -> str:
         return f"{self.prefix}_{rank}"
 
+    def _delete(self, keys) -> None:
+        for k in keys:
+            try:
+                self.store.delete_key(k)
+            except Exception:  # noqa: BLE001 - a store without delete: keys stay
+                return
+
     def arrive(self, timeout: timedelta) -> None:
         if self.arrived:
             raise RuntimeError("Can't call .arrive() multiple times on a barrier.")
@@ -117,6 +130,7 @@ class LinearBarrier:
                 msg = err.decode() if isinstance(err, bytes) else str(err)
                 self.report_error(msg)
                 raise RuntimeError(msg)
+        self._delete(peers)
 
     def depart(self, timeout: timedelta) -> None:
         if not self.arrived:
@@ -132,6 +146,9 @@ class LinearBarrier:
         err = self.store.get(lk)
         if len(err) != 0:
             raise RuntimeError(err.decode() if isinstance(err, bytes) else str(err))
+        done = f"{self.prefix}_departed"
+        if self.store.add(done, 1) == self.world_size - 1:  # the last peer out
+            self._delete([lk, done])
 
     def report_error(self, err: str) -> None:
         self._errored = True

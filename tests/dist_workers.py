@@ -272,10 +272,21 @@ def linear_barrier(prefix: str, skip_arrive_rank: int = -1, error_rank: int = -1
         return
     if rank == skip_arrive_rank:
         return
+    clean_run = error_rank < 0 and skip_arrive_rank < 0
+    if clean_run:
+        n0 = store.num_keys()
+        dist.barrier()
     try:
         b.arrive(timeout=timedelta(seconds=3))
         b.depart(timeout=timedelta(seconds=3))
         assert error_rank < 0 and skip_arrive_rank < 0
+        dist.barrier()
+        # the barrier cleaned up after itself (num_keys also counts the
+        # c10d barrier's own bookkeeping keys: compare after a barrier each)
+        assert store.num_keys() <= n0 + 2, (store.num_keys(), n0)
+        for r in range(ws):
+            assert not store.check([f"{prefix}_{r}"]), r
+        assert not store.check([f"{prefix}_departed"])
     except RuntimeError as e:
         assert error_rank >= 0 or skip_arrive_rank >= 0, e
         if error_rank >= 0:
