@@ -10,6 +10,7 @@ import sys as _sys
 import torch as _torch  # noqa: F401  (load torch's HIP runtime before our .so)
 
 from .engine.hbm_staging import release_hbm_arena
+from .engine.native_restore import release_restore_memory
 from .snapshot import PendingSnapshot, Snapshot
 from .stateful import AppState, RNGState, StateDict, Stateful
 from .version import __hipsnapshot_version__, __version__
@@ -41,6 +42,7 @@ __all__ = [
     "RNGState",
     "AppState",
     "release_hbm_arena",
+    "release_restore_memory",
     "__version__",
     "__hipsnapshot_version__",
 ]

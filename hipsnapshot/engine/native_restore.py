@@ -251,10 +251,15 @@ def _has_codec(entry, depth: int = 0) -> bool:
     return False
 
 
-def prewarm_for(leaves, entries, budget: Optional[int] = None) -> None:
+def prewarm_for(leaves, entries, budget: Optional[int] = None,
+                storage: Optional[StoragePlugin] = None) -> None:
     """``prewarm_async`` for a restore into ``leaves`` (the stateful's
     tensors / DTensors) of manifest ``entries``: the device and bytes are
-    those of the HBM destinations."""
+    those of the HBM destinations.  Nothing is warmed when ``storage`` is
+    not one a native job reads (S3, GCS, memory): its reads take the Python
+    pipeline and the pools would only hold idle HBM."""
+    if storage is not None and _root(storage) is None:
+        return
     try:
         from torch.distributed.tensor import DTensor
     except Exception:  # pragma: no cover
@@ -275,6 +280,23 @@ def prewarm_for(leaves, entries, budget: Optional[int] = None) -> None:
         return
     dev, nbytes = max(per_dev.items(), key=lambda kv: kv[1])
     prewarm_async(dev, nbytes, any(_has_codec(e) for e in entries), budget)
+
+
+def release_restore_memory() -> int:
+    """Free every idle block of the native restore's device pools (the
+    upload / scratch rings a restore keeps for the next one, up to 2 x
+    2.25 GiB of HBM outside torch's caching allocator).  Call it when no
+    restore is running on this GPU -- from any process (see
+    ``knobs.TUNING.restore_keep_bytes``).  Returns the bytes freed."""
+    _join_prewarm()
+    if not native.gpu_available():
+        return 0
+    import torch
+
+    freed = 0
+    for dev in range(torch.cuda.device_count()):
+        freed += native.restore_trim(dev, 0)
+    return freed
 
 
 def join_prewarm() -> None:

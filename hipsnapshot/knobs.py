@@ -213,8 +213,13 @@ class _Tuning:
     restore_readers = 0        # 0: max(4, min(12, I/O threads))
     restore_device_budget = 2 << 30
     # idle restore blocks kept per pool after a restore (HBM outside torch's
-    # allocator): none, so training after a restore has all of it
-    restore_keep_bytes = 0
+    # allocator): the two 2 GiB rings.  Trimming them to 0 after every job
+    # was measured in round 5: alone on a GPU it restored bitwise, but with 4
+    # processes restoring on one GPU it gave wrong bytes and device-work
+    # errors (profiles/r5/trim/); released pool memory is reused at once by
+    # the other processes' uncached SDMA targets.  ``release_restore_memory()``
+    # frees them on request.
+    restore_keep_bytes = (2 << 30) + (256 << 20)
     # -- distributed -------------------------------------------------------------------
     rebalance_host = False     # let the rebalancer move host blobs too (gloo tests)
     rebalance_min_gain = 0.1

@@ -700,7 +700,7 @@ class Snapshot:
                 return
         budget = get_process_memory_budget_bytes(comm)
         # the native job's pinned slots / device rings fill beside the planning
-        native_restore.prewarm_for(flat.values(), manifest.values(), budget)
+        native_restore.prewarm_for(flat.values(), manifest.values(), budget, storage)
         containers: Dict[str, Entry] = {}
         reads: List[ReadReq] = []
         futs = {}
