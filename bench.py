@@ -275,6 +275,9 @@ def main() -> None:
     ap.add_argument("--launch-timeout", type=float, default=3600.0,
                     help="self-launched ranks (--gpus N > 1 without torchrun): seconds before "
                          "every rank is stopped and the run fails")
+    ap.add_argument("--no-plan-gc", action="store_true",
+                    help="A/B probe: skip the full GC pass after a take that built a plan "
+                         "(knobs.TUNING.gc_after_plan)")
     args = ap.parse_args()
 
     torchrun = "RANK" in os.environ and "WORLD_SIZE" in os.environ
@@ -320,6 +323,10 @@ def main() -> None:
     from hipsnapshot.ops import native
 
     native.require_gpu_lib()  # the HIP data plane must be the one running
+    if args.no_plan_gc:
+        from hipsnapshot import knobs
+
+        knobs.TUNING.gc_after_plan = False
     cfg = {"llama3_8b": LlamaConfig.llama3_8b, "llama3_70b": LlamaConfig.llama3_70b,
            "tiny": LlamaConfig.tiny}[args.model]()
     from torch.distributed.device_mesh import init_device_mesh

@@ -35,6 +35,10 @@ def main():
     ap.add_argument("--uvm-place", default=None, choices=["host", "device"],
                     help="advise + prefetch the UVM tables to host DRAM or HBM first")
     ap.add_argument("--work-dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
+    ap.add_argument("--host-siblings", type=int, default=0,
+                    help="K host-only processes replaying the other ranks' host work (one "
+                         "staging pass + the same blob bytes written) with every timed take: "
+                         "one rank's share of a (K+1)-GPU node sharing this host")
     ap.add_argument("--single-path", action="store_true",
                     help="every take rewrites ONE snapshot path (100 GB runs: one copy on storage)")
     args = ap.parse_args()
@@ -69,10 +73,25 @@ def main():
                                else (root + "/warm", root + "/sync", root + "/async"))
     Snapshot.take(p_warm, {"model": model})
     sync(dev)
+    sib = None
+    if args.host_siblings > 0:
+        from common import Siblings
+        from hipsnapshot import knobs
+
+        knobs.set_local_ranks_hint(args.host_siblings + 1)
+        # what one sibling rank writes per take: this rank's blob sizes
+        sizes = [os.path.getsize(os.path.join(dp, f)) for dp, _, fs in os.walk(p_warm)
+                 for f in fs if not f.startswith(".")]
+        sib = Siblings(args.host_siblings, sizes, os.path.join(root, "siblings"), True)
+    sib_ms = []
     with Timer() as t:
+        if sib is not None:
+            sib.go()
         Snapshot.take(p_sync, {"model": model})
         sync(dev)
     sync_s = max_over_ranks(t.s, dev)
+    if sib is not None:
+        sib_ms.append(max(x[0] for x in sib.wait()) * 1e3)
     sync(dev)
     # the first async_take of a state builds its plan: untimed, reported as cold
     with Timer() as tc:
@@ -81,13 +100,20 @@ def main():
     sync(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    with Timer() as tu:
-        pending = Snapshot.async_take(p_async, {"model": model})
-    e1.record()
-    e1.synchronize()
+    with Timer() as ta:
+        with Timer() as tu:
+            if sib is not None:
+                sib.go()
+            pending = Snapshot.async_take(p_async, {"model": model})
+        e1.record()
+        e1.synchronize()
+        pending.wait()
     freeze_ms = e0.elapsed_time(e1)  # the trainer stream's busy time (HBM freeze)
     unblock = max_over_ranks(tu.s, dev)
-    pending.wait()
+    async_total = max_over_ranks(ta.s, dev)
+    if sib is not None:
+        sib_ms.append(max(x[0] for x in sib.wait()) * 1e3)
+        sib.stop()
     sync(dev)
     restore_s = None
     if os.environ.get("DLRM_RESTORE", "1") == "1":
@@ -109,6 +135,9 @@ def main():
           "world_size": ws, "bytes": nbytes,
           "sync_take_s": round(sync_s, 3), "sync_GBps": round(nbytes / sync_s / 1e9, 2),
           "async_unblock_ms": round(unblock * 1e3, 1), "freeze_gpu_ms": round(freeze_ms, 2),
+          "async_total_s": round(async_total, 3),
+          "async_GBps": round(nbytes / async_total / 1e9, 2),
+          "host_siblings": args.host_siblings, "sibling_take_ms": [round(x, 1) for x in sib_ms],
           "cold_async_total_s": round(cold_s, 3), "single_path": args.single_path,
           "uvm_residency": residency, "uvm_place": args.uvm_place,
           "restore_s": round(restore_s, 3) if restore_s else None,

@@ -261,7 +261,7 @@ class Snapshot:
         bf16, ~0.84x for fp32); default from ``HIPSNAPSHOT_COMPRESSION`` ("none").
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.take")
-        with paused_gc():
+        with paused_gc(plan_gc=False):
             return cls._take(path, app_state, pg, replicated, storage_options,
                              _custom_tensor_prepare_func, quantize, compression)
 

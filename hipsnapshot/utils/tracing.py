@@ -199,7 +199,7 @@ class GcWatch:
 
 
 @contextlib.contextmanager
-def paused_gc(defer_plan_gc: Optional[list] = None):
+def paused_gc(defer_plan_gc: Optional[list] = None, plan_gc: bool = True):
     """Suspend Python's cyclic GC for a bounded critical section.
 
     Planning a snapshot allocates tens of thousands of small objects (entries,
@@ -221,7 +221,13 @@ def paused_gc(defer_plan_gc: Optional[list] = None):
     ``defer_plan_gc`` (a list): instead of collecting, append True to it --
     ``async_take`` runs that pass in its commit thread once the drain is done,
     off the unblock path (while a GPU-bound training step waits on the
-    device with the GIL released)."""
+    device with the GIL released).
+
+    ``plan_gc=False`` (blocking takes): no forced pass.  It is the process's
+    first full collection -- 140 ms with torch loaded, whatever the plan --
+    and a one-time cost either way; forced, it made the first blocking take
+    of the Llama-3-8B bench 0.38 s instead of 0.24 s, and without it no full
+    pass fell into a later timed take or restore (profiles/r5/cold_take/)."""
     import gc
 
     from .. import knobs
@@ -235,7 +241,7 @@ def paused_gc(defer_plan_gc: Optional[list] = None):
             gc.enable()
             from ..engine import plan_cache
 
-            if plan_cache.take_stored_flag() and knobs.gc_after_plan():
+            if plan_cache.take_stored_flag() and knobs.gc_after_plan() and plan_gc:
                 if defer_plan_gc is not None:
                     defer_plan_gc.append(True)
                 else:
