@@ -82,7 +82,8 @@ def main():
         # what one sibling rank writes per take: this rank's blob sizes
         sizes = [os.path.getsize(os.path.join(dp, f)) for dp, _, fs in os.walk(p_warm)
                  for f in fs if not f.startswith(".")]
-        sib = Siblings(args.host_siblings, sizes, os.path.join(root, "siblings"), True)
+        sib_root = os.environ.get("HSBENCH_SIBLING_DIR") or os.path.join(root, "siblings")
+        sib = Siblings(args.host_siblings, sizes, sib_root, True)
     sib_ms = []
     with Timer() as t:
         if sib is not None:
