@@ -1,7 +1,7 @@
 """Native drain of an async take's frozen HBM arena to the local FS.
 
 ``DeferredIOWork`` (engine/scheduler.py) hands every eligible deferred write
-to ONE ``native.NativeDrain`` call (csrc/hsdrain.hip): SDMA copies arena ->
+to ONE ``native.NativeDrain`` call (csrc/hsdrain.cpp): SDMA copies arena ->
 pinned slots -> ``pwrite``, per-blob hs64 hashes on the GPU, optional
 fdatasync -- in native threads, so the training loop keeps the GIL and the
 compute units while a checkpoint drains.  Eligible: a raw blob (no HSZ1

@@ -1,7 +1,7 @@
 """Native restore of local-FS blobs whose bytes all land in HBM.
 
 ``execute_read_reqs`` (engine/scheduler.py) hands every eligible read to ONE
-``native.NativeRestore`` job per device (csrc/hsrestore.hip): reader threads
+``native.NativeRestore`` job per device (csrc/hsrestore.cpp): reader threads
 ``pread`` the blobs from the page cache into pinned slots and queue their
 SDMA uploads back to back, the completion thread launches each blob's HSZ1
 decode and ONE region-copy kernel as soon as its bytes have landed -- no
@@ -199,7 +199,7 @@ _prewarm_lock = threading.Lock()
 
 
 def table_bytes(slot: int) -> int:
-    """The job's copy-table ring size (csrc/hsrestore.hip kTables)."""
+    """The job's copy-table ring size (csrc/hsrestore.cpp kTables)."""
     return min(32 << 20, max(1 << 20, slot // 4))
 
 

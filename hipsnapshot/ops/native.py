@@ -823,7 +823,7 @@ def mx8_dequantize(dev: int, q: torch.Tensor, scales: torch.Tensor, dst: torch.T
 
 
 class NativeDrain:
-    """``hsg_drain_start`` / ``hsg_drain_wait`` (csrc/hsdrain.hip): device
+    """``hsg_drain_start`` / ``hsg_drain_wait`` (csrc/hsdrain.cpp): device
     byte ranges -> files, entirely in native threads (SDMA copies through
     pinned slots, pwrite, optional fdatasync and GPU hs64 hashing)."""
 
@@ -889,7 +889,7 @@ class NativeDrain:
 
 
 class NativeRestore:
-    """``hsg_restore_start`` / ``hsg_restore_wait`` (csrc/hsrestore.hip):
+    """``hsg_restore_start`` / ``hsg_restore_wait`` (csrc/hsrestore.cpp):
     file byte ranges (raw, or whole HSZ1 blobs) -> HBM destinations in
     native threads: pread into pinned slots, SDMA uploads into uncached
     blocks, GPU decode and ONE region-copy launch per item.

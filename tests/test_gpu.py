@@ -1210,7 +1210,7 @@ def test_gpu_compressed_restore_with_split_head_read(gpu, tmp_path, monkeypatch,
         assert torch.equal(sd[k], v), k
 
 
-# ---- native drain of an async take (csrc/hsdrain.hip) ---------------------------
+# ---- native drain of an async take (csrc/hsdrain.cpp) ---------------------------
 
 def _drain_state(gpu):
     torch.manual_seed(11)

@@ -1,4 +1,4 @@
-"""Native restore (engine/native_restore.py, csrc/hsrestore.hip): every read
+"""Native restore (engine/native_restore.py, csrc/hsrestore.cpp): every read
 whose bytes land in HBM goes through one native job; the results must equal
 the Python pipeline's bit for bit, for raw and HSZ1 blobs, batched slabs,
 strided / narrowed / cast destinations and resharded DTensors; corrupt or
