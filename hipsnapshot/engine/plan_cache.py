@@ -126,6 +126,48 @@ def fast_signatures(resident: Dict[str, Any]) -> Optional[tuple]:
     return tuple(out)
 
 
+def capture(resident: Dict[str, Any]) -> Optional[tuple]:
+    """What a plan must remember of its leaves, taken once when it is
+    stored (~1 us per leaf; the full ``signatures`` cost ~4 us): the leaf
+    object's id, its local tensor's address / shape / strides / dtype /
+    device and, for a DTensor, its (immutable) spec object -- from which the
+    full signature is derived only when a later take presents new leaf
+    objects.  None when a leaf needs the full signature (ShardedTensor)."""
+    out = []
+    for v in resident.values():
+        lt = getattr(v, "_local_tensor", None)
+        if lt is not None:
+            out.append((id(v), lt.data_ptr(), lt.shape, lt.stride(), lt.dtype, lt.device,
+                        v._spec))
+        elif ShardedTensor is not None and isinstance(v, ShardedTensor):
+            return None
+        else:
+            out.append((id(v), v.data_ptr(), v.shape, v.stride(), v.dtype, v.device, None))
+    return tuple(out)
+
+
+def _same_objects(a: tuple, b: tuple) -> bool:
+    """The same leaf objects pointing at the same memory in the same layout."""
+    return len(a) == len(b) and all(x[:6] == y[:6] and x[6] is y[6] for x, y in zip(a, b))
+
+
+def _same_layout(a: tuple, b: tuple) -> bool:
+    """Possibly other leaf objects, over the same memory, shapes and
+    sharding (``signatures`` equality, from captured facts)."""
+    if len(a) != len(b):
+        return False
+    for x, y in zip(a, b):
+        if x[1:6] != y[1:6]:
+            return False
+        sx, sy = x[6], y[6]
+        if (sx is None) != (sy is None):
+            return False
+        if sx is not None and (tuple(sx.placements) != tuple(sy.placements)
+                               or sx.mesh is not sy.mesh or tuple(sx.shape) != tuple(sy.shape)):
+            return False
+    return True
+
+
 def settings_key(app_state: Dict[str, Any], rank: int, world_size: int, is_async: bool,
                  quantize, compression: str) -> tuple:
     """Everything besides the leaves that shapes a plan.  The app-state KEYS
@@ -152,11 +194,12 @@ def _tensor_stagers(write_reqs: List[WriteReq]) -> Iterator[Any]:
 
 
 class TakePlan:
-    def __init__(self, key: tuple, sigs: tuple, keep: List[Any], entries: Dict[str, Entry],
-                 write_reqs: List[WriteReq], fast: Optional[tuple] = None) -> None:
+    def __init__(self, key: tuple, sigs: Optional[tuple], keep: List[Any],
+                 entries: Dict[str, Entry], write_reqs: List[WriteReq],
+                 cap: Optional[tuple] = None) -> None:
         self.key = key
-        self.sigs = sigs
-        self.fast = fast
+        self.sigs = sigs  # full signatures, only when ``capture`` cannot describe a leaf
+        self.cap = cap
         self.keep = keep          # the leaves: their addresses stay reserved
         self.entries = entries    # logical path -> final Entry (batched / compressed)
         self.write_reqs = write_reqs
@@ -181,13 +224,16 @@ def lookup(key: tuple, resident: Dict[str, Any]) -> Optional[TakePlan]:
         if p is None or p.busy:
             stats["misses"] += 1
             return None
-    fast = fast_signatures(resident)
-    if fast is None or fast != p.fast:
+    if p.cap is not None:
+        cur = capture(resident)
         # new leaf objects (e.g. views a state_dict creates on every call):
         # compare what they point at
-        if signatures(resident) != p.sigs:
-            stats["misses"] += 1
-            return None
+        ok = cur is not None and (_same_objects(cur, p.cap) or _same_layout(cur, p.cap))
+    else:
+        ok = signatures(resident) == p.sigs
+    if not ok:
+        stats["misses"] += 1
+        return None
     with _lock:
         if p.busy or _plans.get(key) is not p:
             stats["misses"] += 1
@@ -204,8 +250,8 @@ def store(key: tuple, resident: Dict[str, Any], object_entries: Dict[str, Entry]
     caller's take is using it), or None when it cannot be cached.  ``owners``:
     the app-state objects the resident leaves come from -- the plan is
     dropped (and its tensors released) when any of them is collected."""
-    sigs = signatures(resident)
-    fast = fast_signatures(resident)
+    cap = capture(resident)
+    sigs = signatures(resident) if cap is None else None
     entries = {k: object_entries[k] for k in resident if k in object_entries}
     if len(entries) != len(resident):
         return None
@@ -225,7 +271,7 @@ def store(key: tuple, resident: Dict[str, Any], object_entries: Dict[str, Entry]
     for v in resident.values():
         if DTensor is not None and isinstance(v, DTensor):
             keep.append(v.device_mesh)
-    plan = TakePlan(key, sigs, keep, entries, mine, fast)
+    plan = TakePlan(key, sigs, keep, entries, mine, cap)
     plan.owner_ids = {id(v) for v in owners}
     for v in owners:
         if id(v) in _watched:
