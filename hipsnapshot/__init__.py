@@ -11,6 +11,7 @@ import torch as _torch  # noqa: F401  (load torch's HIP runtime before our .so)
 
 from .engine.hbm_staging import release_hbm_arena
 from .engine.native_restore import release_restore_memory
+from .storage.fs import release_file_mappings
 from .snapshot import PendingSnapshot, Snapshot
 from .stateful import AppState, RNGState, StateDict, Stateful
 from .version import __hipsnapshot_version__, __version__
@@ -43,6 +44,7 @@ __all__ = [
     "AppState",
     "release_hbm_arena",
     "release_restore_memory",
+    "release_file_mappings",
     "__version__",
     "__hipsnapshot_version__",
 ]

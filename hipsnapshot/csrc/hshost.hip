@@ -74,6 +74,24 @@ int hsg_rt_stream_sync(void* stream) {
   return hipStreamSynchronize(static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -1;
 }
 
+// Register / unregister host memory (a file mapping: csrc/hsfmap.cpp) so the
+// SDMA engines can write it.
+int hsg_rt_host_register(void* p, uint64_t n) {
+  if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return 0;
+}
+
+int hsg_rt_host_unregister(void* p) {
+  if (hipHostUnregister(p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return 0;
+}
+
 // Blocking device -> host copy of n bytes (small result arrays).
 int hsg_rt_memcpy_d2h(void* dst, const void* src, uint64_t n) {
   if (hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) != hipSuccess) {

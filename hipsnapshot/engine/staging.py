@@ -25,7 +25,7 @@ from __future__ import annotations
 import threading
 import time
 from contextlib import contextmanager
-from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -209,6 +209,39 @@ def producer_stream_handle(t: torch.Tensor) -> Optional[int]:
 def _pinned_staged(nbytes: int) -> Tuple[native.PinnedBuffer, StagedBuffer]:
     pb = native.PinnedBuffer(nbytes)
     return pb, StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
+
+
+_dest = threading.local()
+
+
+@contextmanager
+def blob_destination(provider: Optional[Callable[[int], Optional[StagedBuffer]]]) -> Iterator[None]:
+    """While one blob is staged on this thread, ``provider(nbytes)`` may hand
+    out the host destination of its bytes -- a GPU-writable mapping of the
+    file the blob goes to (``FSStoragePlugin.mapped_dest``) -- in place of a
+    pinned block.  Asked at most once, by the copy that produces the blob's
+    final bytes (``_dest_staged``)."""
+    prev = getattr(_dest, "fn", None)
+    _dest.fn = provider
+    try:
+        yield
+    finally:
+        _dest.fn = prev
+
+
+def _dest_staged(nbytes: int) -> StagedBuffer:
+    """The final host buffer of a blob of ``nbytes`` that a DMA engine fills:
+    the destination file's own pages when the storage offers them
+    (``blob_destination``), else a pinned block."""
+    fn = getattr(_dest, "fn", None)
+    if fn is not None and nbytes:
+        _dest.fn = None
+        t_s = time.perf_counter()
+        staged = fn(nbytes)
+        if staged is not None:
+            timeline.add("fmap", "stage", t_s, time.perf_counter(), bytes=nbytes)
+            return staged
+    return _pinned_staged(nbytes)[1]
 
 
 _sdma_ok: dict = {}
@@ -411,7 +444,10 @@ def d2h_tensor(t: torch.Tensor, producer: Optional[int],
         timeline.add("uvm_host_view", "d2h", t_s, time.perf_counter(), bytes=staged.nbytes)
         return staged
     nbytes = t.numel() * t.element_size()
-    pb, staged = _pinned_staged(nbytes)
+    if t.is_contiguous():
+        pb, staged = None, _dest_staged(nbytes)
+    else:  # packed by a kernel storing into the (device-mapped) pinned block
+        pb, staged = _pinned_staged(nbytes)
     if nbytes == 0:
         return staged
     dev = device_of(t)
@@ -513,7 +549,7 @@ def _encode_device_to_host(dev: int, slot: int, src_u8: torch.Tensor, codec: dic
         t_l = time.perf_counter()
         nbytes = _read_u64_device(dev, slot, total.data_ptr())
     t_n = time.perf_counter()
-    pb, staged = _pinned_staged(nbytes)
+    staged = _dest_staged(nbytes)
     t_p = time.perf_counter()
     timeline.add("enc_alloc", "enc", t_s, t_a)
     timeline.add("enc_launch", "enc", t_a, t_l)
@@ -648,8 +684,10 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
     """
     if codec is not None and members:
         return _gather_encoded(members, total_bytes, producers, codec)
-    pb, staged = _pinned_staged(total_bytes)
-    if total_bytes == 0 or not members:
+    if not via_device_slab or not members:
+        return _gather_into_host(members, total_bytes, producers)
+    staged = _dest_staged(total_bytes)
+    if total_bytes == 0:
         return staged
     dev = device_of(members[0][0])
     slot = copy_slot()
@@ -658,29 +696,51 @@ def gather_to_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int
     try:
         for producer in producers:
             native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
-        slab = None
-        if via_device_slab:
-            try:
-                slab = torch.empty(total_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
-                _join_current_stream(dev, slot)
-            except torch.cuda.OutOfMemoryError:
-                slab = None
-        base = slab.data_ptr() if slab is not None else pb.ptr
+        try:
+            slab = torch.empty(total_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+        except torch.cuda.OutOfMemoryError:
+            staged.release()
+            return _gather_into_host(members, total_bytes, producers)
+        _join_current_stream(dev, slot)
         batch = native.CopyBatch()
-        _add_members_zero_gaps(batch, members, base, dev)
+        _add_members_zero_gaps(batch, members, slab.data_ptr(), dev)
         keep = batch.launch(dev, stream, sync=False)
-        if slab is not None:
-            hs = None
-            if _checksums():
-                hs = checksum.device_hash_start(dev, hash_slot(slot), slab.data_ptr(),
-                                                total_bytes, slot)
-            d2h_staged(dev, slot, staged, slab.data_ptr(), total_bytes, [slab], hs)
-        else:
-            native.stream_sync(dev, slot)  # the kernel wrote host memory directly
+        hs = None
+        if _checksums():
+            hs = checksum.device_hash_start(dev, hash_slot(slot), slab.data_ptr(),
+                                            total_bytes, slot)
+        d2h_staged(dev, slot, staged, slab.data_ptr(), total_bytes, [slab], hs)
         if keep is not None:
             # the gather kernel is done: submitting the copy waited for it
             keep[0].release()
         del slab
+    except BaseException:
+        staged.release()
+        raise
+    timeline.add("gather_d2h", "d2h", t_s, time.perf_counter(), bytes=total_bytes,
+                 members=len(members), slot=slot)
+    return staged
+
+
+def _gather_into_host(members: Sequence[Tuple[torch.Tensor, int]], total_bytes: int,
+                      producers: Sequence[int]) -> StagedBuffer:
+    """No HBM for a device slab: the gather kernel stores the members over
+    PCIe straight into a (device-mapped) pinned block."""
+    pb, staged = _pinned_staged(total_bytes)
+    if total_bytes == 0 or not members:
+        return staged
+    dev = device_of(members[0][0])
+    slot = copy_slot()
+    t_s = time.perf_counter()
+    try:
+        for producer in producers:
+            native.memcpy(dev, slot, 0, 0, 0, native.D2H, producer, sync=False)
+        batch = native.CopyBatch()
+        _add_members_zero_gaps(batch, members, pb.ptr, dev)
+        keep = batch.launch(dev, native.copy_stream(dev, slot), sync=False)
+        native.stream_sync(dev, slot)
+        if keep is not None:
+            keep[0].release()
     except BaseException:
         staged.release()
         raise

@@ -39,7 +39,7 @@ def buffer_address(buf) -> int:
 class StagedBuffer:
     """Bytes ready for storage: ``view`` + raw ``addr`` + release hook."""
 
-    __slots__ = ("view", "addr", "_release", "keepalive", "checksum", "ready")
+    __slots__ = ("view", "addr", "_release", "keepalive", "checksum", "ready", "mapped")
 
     def __init__(self, view: BufferType, addr: Optional[int] = None,
                  release: Optional[Callable[[], None]] = None, keepalive: Any = None) -> None:
@@ -56,6 +56,10 @@ class StagedBuffer:
         # set when the bytes are still arriving (asynchronous SDMA copy):
         # call it (blocking, once) before reading the buffer
         self.ready: Optional[Callable[[], None]] = None
+        # the bytes ARE the destination file's pages (a GPU-writable mapping
+        # the storage plugin handed out, ``mapped_dest``): the plugin's write
+        # only has to commit them
+        self.mapped: Any = None
 
     @property
     def nbytes(self) -> int:
@@ -207,6 +211,8 @@ class WriteIO:
     path: str
     buf: BufferType
     addr: Optional[int] = None
+    # ``StagedBuffer.mapped`` of a buffer the plugin's ``mapped_dest`` handed out
+    mapped: Any = None
 
 
 @dataclass

@@ -220,6 +220,11 @@ class _Tuning:
     # the other processes' uncached SDMA targets.  ``release_restore_memory()``
     # frees them on request.
     restore_keep_bytes = (2 << 30) + (256 << 20)
+    # -- file mappings (csrc/hsfmap.cpp) ------------------------------------------------
+    # a blocking take that rewrites an existing file of the blob's exact size
+    # DMAs into the file's page-cache pages (no pinned copy, no pwrite copy)
+    file_map = True
+    file_map_max_bytes = 64 << 30  # mapped (pinned page-cache) bytes kept per process
     # -- distributed -------------------------------------------------------------------
     rebalance_host = False     # let the rebalancer move host blobs too (gloo tests)
     rebalance_min_gain = 0.1

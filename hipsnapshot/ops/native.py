@@ -316,6 +316,13 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_sdma_d2h_submit", c_int,
                  [c_int, c_void_p, c_void_p, c_uint64, c_void_p, ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_sdma_wait", c_int, [c_uint64])
+        _declare(lib, "hsg_fmap_acquire", c_void_p, [c_char_p, c_uint64])
+        _declare(lib, "hsg_fmap_commit", c_int, [c_void_p, c_int])
+        _declare(lib, "hsg_fmap_abandon", None, [c_void_p])
+        _declare(lib, "hsg_fmap_release", c_uint64, [c_int])
+        _declare(lib, "hsg_fmap_prune", c_uint64, [])
+        _declare(lib, "hsg_fmap_set_budget", None, [c_uint64])
+        _declare(lib, "hsg_fmap_stats", None, [P(c_uint64)])
         _declare(lib, "hsg_hsz_meta_bytes", c_uint64, [ctypes.c_uint32])
         _declare(lib, "hsg_hsz_encode", c_int,
                  [c_int, c_void_p, c_uint64, c_int, ctypes.c_uint32, c_void_p, c_void_p,
@@ -354,6 +361,58 @@ def _check(rc: int, what: str) -> None:
         lib = _load_hsgpu()
         msg = lib.hsg_last_error().decode() if lib is not None else "?"
         raise HipError(f"{what} failed ({rc}): {msg}")
+
+
+# ---- GPU-writable file mappings (csrc/hsfmap.cpp) -------------------------
+
+_fmap_budget_set = None
+
+
+def fmap_acquire(path: str, nbytes: int) -> Optional[int]:
+    """Address of a GPU-writable mapping of the existing file ``path`` when it
+    is exactly ``nbytes`` long (busy until ``fmap_commit`` / ``fmap_abandon``),
+    else None."""
+    global _fmap_budget_set
+    lib = require_gpu_lib()
+    from .. import knobs
+
+    budget = knobs.TUNING.file_map_max_bytes
+    if _fmap_budget_set != budget:
+        lib.hsg_fmap_set_budget(budget)
+        _fmap_budget_set = budget
+    p = lib.hsg_fmap_acquire(os.fsencode(path), nbytes)
+    return int(p) if p else None
+
+
+def fmap_commit(addr: int, sync: bool) -> int:
+    """Mark the mapping's pages dirty after the copy into it (optionally
+    fdatasync); 0 or -errno."""
+    return int(require_gpu_lib().hsg_fmap_commit(c_void_p(addr), 1 if sync else 0))
+
+
+def fmap_abandon(addr: int) -> None:
+    require_gpu_lib().hsg_fmap_abandon(c_void_p(addr))
+
+
+def fmap_prune() -> int:
+    """Drop idle mappings of files that were deleted, replaced or resized."""
+    lib = _load_hsgpu()
+    return int(lib.hsg_fmap_prune()) if lib is not None else 0
+
+
+def fmap_release(all_mappings: bool = False) -> int:
+    """Unmap idle mappings (``all_mappings``: every one; no copy may be in
+    flight).  Returns the bytes released."""
+    lib = _load_hsgpu()
+    return int(lib.hsg_fmap_release(1 if all_mappings else 0)) if lib is not None else 0
+
+
+def fmap_stats() -> dict:
+    lib = _load_hsgpu()
+    out = (c_uint64 * 6)()
+    if lib is not None:
+        lib.hsg_fmap_stats(out)
+    return dict(zip(("bytes", "mappings", "hits", "maps", "drops", "misses"), map(int, out)))
 
 
 # ---- pinned host memory ---------------------------------------------------

@@ -63,7 +63,8 @@ def test_hsz_decoder_fuzz_under_asan(tmp_path):
 ENGINE_SRC = [os.path.join(ROOT, "tests", "native", "engine_stress.cpp"),
               os.path.join(ROOT, "tests", "native", "engine_stubs.cpp"),
               os.path.join(ROOT, "hipsnapshot", "csrc", "hsrestore.cpp"),
-              os.path.join(ROOT, "hipsnapshot", "csrc", "hsdrain.cpp")]
+              os.path.join(ROOT, "hipsnapshot", "csrc", "hsdrain.cpp"),
+              os.path.join(ROOT, "hipsnapshot", "csrc", "hsfmap.cpp")]
 SAN_ENV = dict(ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", TSAN_OPTIONS="halt_on_error=1",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
 
@@ -84,7 +85,8 @@ def _build_engine_stress(tmp_path, san, sources=None):
     return exe
 
 
-@pytest.mark.parametrize("mode,rounds", [("restore", 24), ("drain", 24), ("ringwrap", 1)])
+@pytest.mark.parametrize("mode,rounds", [("restore", 24), ("drain", 24), ("ringwrap", 1),
+                                         ("fmap", 10)])
 @pytest.mark.parametrize("san", ["thread", "address,undefined"])
 def test_native_engines_under_sanitizer(tmp_path, san, mode, rounds):
     """csrc/hsrestore.cpp and csrc/hsdrain.cpp (host code: readers,
@@ -92,7 +94,8 @@ def test_native_engines_under_sanitizer(tmp_path, san, mode, rounds):
     writers and parked writers) driven by tests/native/engine_stress.cpp over
     CPU stand-ins of every device hook (random completion delays, injected
     upload / copy / file / memory failures, budgets below one blob, the
-    c026ee7 ring wrap)."""
+    c026ee7 ring wrap) and csrc/hsfmap.cpp (the file-mapping cache under
+    concurrent map / commit / abandon / replace / prune / evict)."""
     exe = _build_engine_stress(tmp_path, san)
     if san == "thread":
         rounds = max(1, rounds // 2)  # ~5x slower under TSan
@@ -112,7 +115,7 @@ def test_ring_wrap_regression_hangs_without_the_fix(tmp_path):
     assert src.count(fix) == 1
     reverted = tmp_path / "hsrestore_reverted.cpp"
     reverted.write_text(src.replace(fix, ""))
-    exe = _build_engine_stress(tmp_path, "", ENGINE_SRC[:2] + [str(reverted), ENGINE_SRC[3]])
+    exe = _build_engine_stress(tmp_path, "", ENGINE_SRC[:2] + [str(reverted)] + ENGINE_SRC[3:])
     proc = subprocess.Popen([exe, "ringwrap", str(tmp_path / "rw")], stdout=subprocess.PIPE,
                             stderr=subprocess.PIPE)
     try:
