@@ -27,10 +27,12 @@ import ctypes
 import errno
 import os
 import shutil
+import time
 from typing import Any, Dict, Optional
 
 from .. import knobs
 from ..io_types import ReadIO, StagedBuffer, StoragePlugin, WriteIO, buffer_address
+from ..utils.tracing import timeline
 
 try:
     from ..ops import native as _native
@@ -146,8 +148,11 @@ class FSStoragePlugin(StoragePlugin):
             # the bytes are already in the file's pages: dirty them for writeback
             path = self._abs(write_io.path)
             n = memoryview(write_io.buf).nbytes
+            t_s = time.perf_counter()
             rc = await _uncancellable(asyncio.get_running_loop().run_in_executor(
                 None, write_io.mapped.commit, self.fsync))
+            timeline.add("fmap_commit", "io", t_s, time.perf_counter(), path=write_io.path,
+                         bytes=n)
             if rc < 0:
                 raise OSError(-rc, os.strerror(-rc), path)
             self.bytes_written += n
