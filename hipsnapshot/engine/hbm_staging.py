@@ -59,11 +59,25 @@ def _retire_launches() -> None:
     _live_launches[:] = [kd for kd in _live_launches if not kd[1].query()]
 
 
+_TYPES: Optional[tuple] = None
+
+
+def _types() -> tuple:
+    """(TensorBufferStager, GPUBatchedBufferStager, ObjectBufferStager),
+    imported once: these run per write request on the unblock path."""
+    global _TYPES
+    if _TYPES is None:
+        from ..io.batcher import GPUBatchedBufferStager
+        from ..io.object import ObjectBufferStager
+        from ..io.tensor import TensorBufferStager
+
+        _TYPES = (TensorBufferStager, GPUBatchedBufferStager, ObjectBufferStager)
+    return _TYPES
+
+
 def _cuda_sources(wr: WriteReq):
     """The stagers whose CUDA tensors a write request reads (empty if none)."""
-    from ..io.batcher import GPUBatchedBufferStager
-    from ..io.tensor import TensorBufferStager
-
+    TensorBufferStager, GPUBatchedBufferStager, _ = _types()
     st = wr.buffer_stager
     if isinstance(st, TensorBufferStager) and st.tensor.is_cuda \
             and st._tensor_prepare_func is None:
@@ -83,10 +97,8 @@ def _region(wr: WriteReq, sts) -> Tuple[int, List[int], int]:
     request.  The region holds the blob exactly as it goes to storage: a
     tensor's C-order bytes, or a device slab with every member at its slab
     offset (the gaps are zero-filled by the freeze)."""
-    from ..io.batcher import GPUBatchedBufferStager
-
     st = wr.buffer_stager
-    if isinstance(st, GPUBatchedBufferStager):
+    if isinstance(st, _types()[1]):
         offs = [lo for (lo, _hi), _m in st.members]
         return (st.total + _ALIGN - 1) // _ALIGN * _ALIGN, offs, st.total
     t = sts[0].tensor
@@ -308,7 +320,7 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
                 for st, mo in zip(sts, moffs):
                     if mo > end:  # slab gap: zeros, as the slab gather writes them
                         batch.add_bytes(zero, base + off + end, mo - end)
-                    t = st.tensor.detach()
+                    t = st.tensor  # (only its pointer and layout are read: no detach)
                     if t.numel():
                         batch.add_tensor(t, base + off + mo)
                     placed.append((st, off + mo))
@@ -355,10 +367,7 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
 def is_deferrable(wr: WriteReq) -> bool:
     """A write whose bytes are already captured (frozen HBM copy or eagerly
     serialized object) can run entirely after ``async_take`` returns."""
-    from ..io.batcher import GPUBatchedBufferStager
-    from ..io.object import ObjectBufferStager
-    from ..io.tensor import TensorBufferStager
-
+    TensorBufferStager, GPUBatchedBufferStager, ObjectBufferStager = _types()
     st = wr.buffer_stager
     if isinstance(st, ObjectBufferStager):
         return True

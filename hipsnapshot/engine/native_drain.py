@@ -67,7 +67,7 @@ def _root(storage: StoragePlugin):
 
 
 def eligible(wr: WriteReq, storage: StoragePlugin) -> bool:
-    from ..format.serialization import Serializer
+    from ..format.serialization import SER
     from ..io.batcher import GPUBatchedBufferStager
     from ..io.tensor import TensorBufferStager
 
@@ -75,7 +75,7 @@ def eligible(wr: WriteReq, storage: StoragePlugin) -> bool:
     if getattr(st, "frozen_region", None) is None or getattr(st, "codec", None) is not None:
         return False
     if isinstance(st, TensorBufferStager):
-        if st.entry.serializer != Serializer.BUFFER_PROTOCOL.value or \
+        if st.entry.serializer != SER.BUFFER_PROTOCOL or \
                 st._tensor_prepare_func is not None:
             return False
     elif not isinstance(st, GPUBatchedBufferStager):

@@ -174,21 +174,33 @@ def settings_key(app_state: Dict[str, Any], rank: int, world_size: int, is_async
     are part of it, not the objects: ``{"model": m, "progress": StateDict(
     step=i)}`` rebuilt for every take must still reuse the model's plan (the
     leaf signatures establish that the model's tensors are the same)."""
-    from .. import knobs
-
     return (tuple(sorted(app_state)), rank, world_size, bool(is_async),
             tuple(quantize or ()), compression, knobs.plan_settings())
 
 
-def _tensor_stagers(write_reqs: List[WriteReq]) -> Iterator[Any]:
-    from ..io.batcher import BatchedBufferStager, GPUBatchedBufferStager
-    from ..io.tensor import TensorBufferStager
+_STAGER_TYPES: Optional[tuple] = None
 
+
+def _stager_types() -> tuple:
+    """(single-tensor stager, slab stagers); imported once (io imports this
+    package: a function-level import on every call cost ~1 us each, ~0.9 ms
+    of a cold async_take's unblock over its ~430 calls)."""
+    global _STAGER_TYPES
+    if _STAGER_TYPES is None:
+        from ..io.batcher import BatchedBufferStager, GPUBatchedBufferStager
+        from ..io.tensor import TensorBufferStager
+
+        _STAGER_TYPES = (TensorBufferStager, (GPUBatchedBufferStager, BatchedBufferStager))
+    return _STAGER_TYPES
+
+
+def _tensor_stagers(write_reqs: List[WriteReq]) -> Iterator[Any]:
+    single, slabs = _stager_types()
     for wr in write_reqs:
         st = wr.buffer_stager
-        if isinstance(st, TensorBufferStager):
+        if isinstance(st, single):
             yield st
-        elif isinstance(st, (GPUBatchedBufferStager, BatchedBufferStager)):
+        elif isinstance(st, slabs):
             for _, m in st.members:
                 yield m
 

@@ -38,6 +38,7 @@ from ..ops import checksum
 from ..io_types import (ReadIO, ReadReq, StagedBuffer, StoragePlugin, WriteIO, WriteReq, as_staged,
                         run_sync)
 from ..utils.tracing import timeline
+from . import native_drain  # (on first use it cost the first async_take's unblock ~1 ms)
 
 logger = logging.getLogger(__name__)
 
@@ -513,16 +514,12 @@ class DeferredIOWork:
         self.rank = rank
         self.stats = first.stats
         self._second: Optional[PendingIOWork] = None
-        from .native_drain import Booster
-
-        self.booster = Booster()  # PendingSnapshot.wait() -> all drain writers
+        self.booster = native_drain.Booster()  # PendingSnapshot.wait() -> all drain writers
 
     def boost(self) -> None:
         self.booster.boost()
 
     async def complete(self) -> None:
-        from . import native_drain
-
         native_reqs, py_reqs = native_drain.split(self.deferred, self.storage)
         native_out: Dict[str, Any] = {}
         native_fut: List[Any] = []  # the native drain's executor future

@@ -36,6 +36,18 @@ class Serializer(Enum):
     FP8_BLOCK = "hipsnapshot_fp8_block"
 
 
+class SER:
+    """``Serializer`` values as plain class attributes: ``Serializer.X.value``
+    goes through an enum descriptor (~0.7 us), several times per leaf while a
+    take is planned."""
+
+    TORCH_SAVE = Serializer.TORCH_SAVE.value
+    BUFFER_PROTOCOL = Serializer.BUFFER_PROTOCOL.value
+    PER_TENSOR_QTENSOR = Serializer.PER_TENSOR_QTENSOR.value
+    PER_CHANNEL_QTENSOR = Serializer.PER_CHANNEL_QTENSOR.value
+    FP8_BLOCK = Serializer.FP8_BLOCK.value
+
+
 _DTYPE_STRING_PAIRS: List[tuple] = [
     (torch.float64, "torch.float64", 8),
     (torch.float32, "torch.float32", 4),
@@ -102,8 +114,11 @@ def dtype_to_element_size(dtype: torch.dtype) -> int:
         raise ValueError(f"Unsupported dtype {dtype}. {_supported_msg()}") from None
 
 
+_BUFFER_PROTOCOL_SET = frozenset(BUFFER_PROTOCOL_SUPPORTED_DTYPES)
+
+
 def is_buffer_protocol_dtype(dtype: torch.dtype) -> bool:
-    return dtype in BUFFER_PROTOCOL_SUPPORTED_DTYPES
+    return dtype in _BUFFER_PROTOCOL_SET
 
 
 def tensor_nbytes(shape, dtype: torch.dtype) -> int:

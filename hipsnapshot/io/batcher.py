@@ -33,7 +33,7 @@ from .. import knobs
 from ..engine import staging
 from ..utils.tracing import timeline
 from ..format.manifest import Entry, iter_tensor_entries
-from ..format.serialization import Serializer, string_to_dtype
+from ..format.serialization import SER, string_to_dtype
 from ..io_types import (BufferConsumer, BufferStager, CompressedSpan, ReadReq, StagedBuffer,
                         WriteReq)
 from .tensor import TensorBufferConsumer, TensorBufferStager, run_in_executor, tensor_nbytes_from_entry
@@ -41,7 +41,7 @@ from .tensor import TensorBufferConsumer, TensorBufferStager, run_in_executor, t
 
 def is_batchable(stager: BufferStager) -> bool:
     return (isinstance(stager, TensorBufferStager)
-            and stager.entry.serializer == Serializer.BUFFER_PROTOCOL.value
+            and stager.entry.serializer == SER.BUFFER_PROTOCOL
             and stager._tensor_prepare_func is None)
 
 
@@ -157,7 +157,7 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
     threshold = slab_size_threshold_bytes or knobs.get_slab_size_threshold_bytes()
     align = knobs.slab_align()
     out: List[WriteReq] = []
-    slabs: Dict[Optional[torch.device], List[Slab]] = {}
+    slabs: Dict[int, List[Slab]] = {}
     relocation: Dict[str, Tuple[str, int, int]] = {}
     # Tail taper: slabs are staged after the big blobs (largest first), and
     # one file is written by one thread at ~10-15 GB/s (buffered writes to a
@@ -169,39 +169,41 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
     # equal-sized slabs the last big writes outlived the staging by ~4 ms:
     # the taper takes 1/8 off one rank's take at 8 GPUs (profiles/rank_share/).
     floor = min(threshold, max(threshold // 16, 8 << 20))  # smaller slabs gain nothing
-    remaining: Dict[Optional[torch.device], int] = defaultdict(int)
-    info = []  # (batchable below threshold?, nbytes, device) once per request
+    # keyed by CUDA device index (-1: host): t.device builds a torch.device
+    # object per call
+    remaining: Dict[int, int] = defaultdict(int)
+    info = []  # (batchable below threshold?, nbytes, device index) once per request
     for wr in write_reqs:
         st = wr.buffer_stager
         if is_batchable(st):
             t = st.tensor
             nb = t.numel() * t.element_size()
             if nb < threshold:
-                dev = t.device if t.is_cuda else None
-                remaining[dev] += nb
-                info.append((True, nb, dev))
+                di = t.get_device() if t.is_cuda else -1
+                remaining[di] += nb
+                info.append((True, nb, di))
                 continue
-        info.append((False, 0, None))
-    for wr, (small, nbytes, dev) in zip(write_reqs, info):
+        info.append((False, 0, -1))
+
+    def _new_slab(di: int, k: int) -> Slab:
+        dev = torch.device("cuda", di) if di >= 0 else None
+        if name_prefix is None:
+            return Slab(dev)
+        return Slab(dev, f"{name_prefix}_{f'cuda{di}' if di >= 0 else 'cpu'}_{k}")
+
+    for wr, (small, nbytes, di) in zip(write_reqs, info):
         if not small:
             out.append(wr)
             continue
         st = wr.buffer_stager
-        left = remaining[dev]  # batchable bytes on this device not placed yet
-        remaining[dev] -= nbytes
+        left = remaining[di]  # batchable bytes on this device not placed yet
+        remaining[di] -= nbytes
         cap = threshold if left > 8 * threshold else max(floor, min(threshold, left // 8))
-
-        def _new_slab(k: int) -> Slab:
-            if name_prefix is None:
-                return Slab(dev)
-            tag = f"cuda{dev.index}" if dev is not None else "cpu"
-            return Slab(dev, f"{name_prefix}_{tag}_{k}")
-
-        lst = slabs.get(dev)
+        lst = slabs.get(di)
         if lst is None:
-            lst = slabs[dev] = [_new_slab(0)]
+            lst = slabs[di] = [_new_slab(di, 0)]
         if lst[-1].members and _align(lst[-1].sz_bytes, align) + nbytes >= cap:
-            lst.append(_new_slab(len(lst)))
+            lst.append(_new_slab(di, len(lst)))
         lo, hi = lst[-1].add(nbytes, st, align)
         relocation[wr.path] = (lst[-1].location, lo, hi)
     for lst in slabs.values():

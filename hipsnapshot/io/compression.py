@@ -20,7 +20,7 @@ from typing import List, Optional
 
 import torch
 
-from ..format.serialization import Serializer
+from ..format.serialization import SER
 from ..io_types import WriteReq
 from ..ops import codec as hsz
 
@@ -58,7 +58,7 @@ def _float_stager(st, include_host: bool) -> Optional[int]:
 
     if not isinstance(st, TensorBufferStager):
         return None
-    if st.entry.serializer != Serializer.BUFFER_PROTOCOL.value or st._tensor_prepare_func:
+    if st.entry.serializer != SER.BUFFER_PROTOCOL or st._tensor_prepare_func:
         return None
     t = st.tensor
     if not t.is_cuda and not include_host:

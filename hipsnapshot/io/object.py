@@ -19,7 +19,7 @@ from typing import Any, List, Optional, Tuple
 
 from .. import knobs
 from ..format.manifest import ObjectEntry
-from ..format.serialization import Serializer, torch_load_from_bytes, torch_save_as_bytes
+from ..format.serialization import SER, torch_load_from_bytes, torch_save_as_bytes
 from ..io_types import BufferConsumer, BufferStager, Future, ReadReq, WriteReq
 
 
@@ -74,7 +74,7 @@ class ObjectIOPreparer:
     @staticmethod
     def prepare_write(storage_path: str, obj: Any) -> Tuple[ObjectEntry, List[WriteReq]]:
         t = type(obj)
-        entry = ObjectEntry(location=storage_path, serializer=Serializer.TORCH_SAVE.value,
+        entry = ObjectEntry(location=storage_path, serializer=SER.TORCH_SAVE,
                             obj_type=f"{t.__module__}.{t.__qualname__}", replicated=False)
         return entry, [WriteReq(path=storage_path, buffer_stager=ObjectBufferStager(obj))]
 

@@ -34,7 +34,7 @@ from typing import Any, List, Optional, Sequence, Tuple
 import torch
 
 from ..format.manifest import Shard, ShardedTensorEntry, TensorEntry
-from ..format.serialization import Serializer, string_to_dtype
+from ..format.serialization import SER, string_to_dtype
 from ..io_types import BufferConsumer, CompressedSpan, Future, ReadReq, StagedBuffer, WriteReq
 from ..knobs import get_max_shard_size_bytes
 from ..engine import staging
@@ -79,11 +79,26 @@ class LocalBox:
         self.tensor = tensor
         self.sharding_dim = sharding_dim
 
+    @classmethod
+    def of_ints(cls, offsets: List[int], sizes: List[int], tensor, sharding_dim: int) -> "LocalBox":
+        """From lists of Python ints (a cached DTensor layout): copied, not
+        converted."""
+        b = cls.__new__(cls)
+        b.offsets = list(offsets)
+        b.sizes = list(sizes)
+        b.tensor = tensor
+        b.sharding_dim = sharding_dim
+        return b
+
 
 # DTensorSpec (hashable, hash cached by torch) -> (skip, boxes, sharding dim):
 # the same layouts recur every snapshot of a training job, and FSDP2 state
 # dicts share one spec object per parameter.
 _LAYOUT_CACHE: dict = {}
+# (id(spec), for_write) -> (spec, has Partial, layout): the same spec OBJECT
+# recurs, and an identity hit skips the spec's __eq__ (~3 us a leaf) behind
+# the equality-keyed cache.  Holding the spec keeps its id from being reused.
+_LAYOUT_BY_ID: dict = {}
 
 
 def _shard_dim_of(p, ndim: int) -> Optional[int]:
@@ -213,25 +228,38 @@ def _dtensor_layout(dt, for_write: bool):
 
 
 def _dtensor_boxes(dt, for_write: bool) -> List[LocalBox]:
-    placements = dt.placements
-    if any(isinstance(p, Partial) for p in placements):
+    spec = dt._spec
+    key = (id(spec), for_write)
+    ent = _LAYOUT_BY_ID.get(key)
+    if ent is None or ent[0] is not spec:
+        partial = any(isinstance(p, Partial) for p in spec.placements)
+        ent = (spec, partial, None if partial else _dtensor_layout(dt, for_write))
+        if len(_LAYOUT_BY_ID) > 65536:
+            _LAYOUT_BY_ID.clear()
+        _LAYOUT_BY_ID[key] = ent
+    if ent[1]:
+        placements = dt.placements
         dt = dt.redistribute(dt.device_mesh,
                              [Replicate() if isinstance(p, Partial) else p for p in placements])
-    skip, boxes, sdim = _dtensor_layout(dt, for_write)
+        layout = _dtensor_layout(dt, for_write)
+    else:
+        layout = ent[2]
+    skip, boxes, sdim = layout
     if skip:
         return []
     local = dt._local_tensor
     if local.dim() == 0:
         return [LocalBox([], [], local, 0)]
     out = []
+    shape = local.shape
     for lo, go, sz in boxes:
-        if any(s == 0 for s in sz):
+        if 0 in sz:
             continue
         view = local
         for d, (o, s) in enumerate(zip(lo, sz)):
-            if o or s != view.shape[d]:
+            if o or s != shape[d]:
                 view = view.narrow(d, o, s)
-        out.append(LocalBox(go, sz, view, sdim))
+        out.append(LocalBox.of_ints(go, sz, view, sdim))
     return out
 
 
@@ -309,10 +337,14 @@ class ShardedTensorIOPreparer:
         shards, reqs = [], []
         max_shard = max_shard_size_bytes or get_max_shard_size_bytes()
         for box in local_boxes(obj, for_write=True):
-            pieces = cls.subdivide_shard(box.tensor, box.offsets, box.sizes, box.sharding_dim,
-                                         max_shard)
+            t = box.tensor
+            if t.numel() * t.element_size() <= max_shard:
+                pieces = ((t, box.offsets, box.sizes),)  # (the common case)
+            else:
+                pieces = cls.subdivide_shard(t, box.offsets, box.sizes, box.sharding_dim,
+                                             max_shard)
             for t, offs, sizes in pieces:
-                suffix = "_".join(str(i) for i in offs)
+                suffix = "_".join(map(str, offs))
                 entry, wrs = TensorIOPreparer.prepare_write(
                     storage_path=f"{storage_path}_{suffix}", tensor=t,
                     is_async_snapshot=is_async_snapshot,
@@ -383,7 +415,7 @@ class ShardedTensorBufferConsumer(BufferConsumer):
     def __init__(self, regions: List[Region], entry: TensorEntry) -> None:
         self.regions = regions
         self.entry = entry
-        self._gpu = (entry.serializer == Serializer.BUFFER_PROTOCOL.value
+        self._gpu = (entry.serializer == SER.BUFFER_PROTOCOL
                      and all(r.dst.is_cuda for r in regions) and len(regions) > 0
                      and len({r.dst.device for r in regions}) == 1)
         self.producer = staging.producer_stream_handle(regions[0].dst) if self._gpu else None
@@ -453,7 +485,7 @@ class ShardedTensorBufferConsumer(BufferConsumer):
 
     def get_consuming_cost_bytes(self) -> int:
         n = tensor_nbytes_from_entry(self.entry)
-        return 2 * n if self.entry.serializer == Serializer.TORCH_SAVE.value else n
+        return 2 * n if self.entry.serializer == SER.TORCH_SAVE else n
 
     def device_regions(self, base: int):
         if not self._gpu:

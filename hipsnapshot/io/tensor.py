@@ -29,7 +29,7 @@ import torch
 from ..format.manifest import ChunkedTensorEntry, TensorEntry
 from ..format.serialization import (
     SUPPORTED_QUANTIZED_DTYPES,
-    Serializer,
+    SER,
     dtype_to_element_size,
     dtype_to_string,
     is_buffer_protocol_dtype,
@@ -80,7 +80,7 @@ class TensorIOPreparer:
                 "_tensor_prepare_func shouldn't change the tensor's shape "
                 f"(changed from {tensor.shape} to {proc.shape}).")
         quant = None
-        if serializer == Serializer.FP8_BLOCK.value:
+        if serializer == SER.FP8_BLOCK:
             from ..ops.quant import fp8_entry_quant_info, fp8_supported
 
             if not fp8_supported(proc):
@@ -88,8 +88,8 @@ class TensorIOPreparer:
             else:
                 quant = fp8_entry_quant_info(proc)
         if serializer is None:
-            serializer = (Serializer.BUFFER_PROTOCOL.value if is_buffer_protocol_dtype(proc.dtype)
-                          else Serializer.TORCH_SAVE.value)
+            serializer = (SER.BUFFER_PROTOCOL if is_buffer_protocol_dtype(proc.dtype)
+                          else SER.TORCH_SAVE)
         entry = TensorEntry(location=storage_path, serializer=serializer,
                             dtype=dtype_to_string(proc.dtype), shape=list(proc.shape),
                             replicated=False, quant=quant)
@@ -103,7 +103,7 @@ class TensorIOPreparer:
                      buffer_size_limit_bytes: Optional[int] = None
                      ) -> Tuple[List[ReadReq], Future]:
         if tensor_out is None or not cls.can_load_inplace(entry, tensor_out):
-            if entry.serializer == Serializer.TORCH_SAVE.value:
+            if entry.serializer == SER.TORCH_SAVE:
                 # the payload carries its own tensor (quantized params etc.):
                 # hand the loaded object out instead of pre-allocating
                 fut = Future()
@@ -111,7 +111,7 @@ class TensorIOPreparer:
                 return [ReadReq(path=entry.location, byte_range=entry.byte_range_tuple,
                                 buffer_consumer=consumer, codec=entry.codec)], fut
             tensor_out = cls.empty_tensor_from_entry(entry)
-        if entry.serializer == Serializer.BUFFER_PROTOCOL.value and entry.codec is None:
+        if entry.serializer == SER.BUFFER_PROTOCOL and entry.codec is None:
             if buffer_size_limit_bytes is not None:
                 return cls.prepare_read_tiled(entry, tensor_out, buffer_size_limit_bytes)
             if tensor_nbytes_from_entry(entry) > AUTO_TILE_THRESHOLD_BYTES:
@@ -240,7 +240,7 @@ class TensorBufferStager(BufferStager):
 
     def _stage_source(self, t: torch.Tensor):
         ser = self.entry.serializer
-        if ser == Serializer.BUFFER_PROTOCOL.value:
+        if ser == SER.BUFFER_PROTOCOL:
             if t.is_cuda:
                 return self._d2h(t)
             # async snapshots must not alias live host memory (Appendix C #1);
@@ -252,11 +252,11 @@ class TensorBufferStager(BufferStager):
             if self.codec is not None:
                 return self._encode_host(t)
             return staging.cpu_tensor_bytes(t, copy)
-        if ser == Serializer.FP8_BLOCK.value:
+        if ser == SER.FP8_BLOCK:
             from ..ops.quant import stage_fp8
 
             return stage_fp8(t, self.entry, self.producer)
-        if ser == Serializer.TORCH_SAVE.value:
+        if ser == SER.TORCH_SAVE:
             return _torch_save_tensor(t)
         raise ValueError(f"Unrecognized serializer: {ser}.")
 
@@ -276,7 +276,7 @@ class TensorBufferStager(BufferStager):
 
     def get_staging_cost_bytes(self) -> int:
         n = tensor_nbytes_from_entry(self.entry)
-        return 2 * n if self.entry.serializer == Serializer.TORCH_SAVE.value else n
+        return 2 * n if self.entry.serializer == SER.TORCH_SAVE else n
 
 
 def _torch_save_tensor(t: torch.Tensor) -> bytes:
@@ -289,20 +289,20 @@ def _torch_save_tensor(t: torch.Tensor) -> bytes:
 
 
 def deserialize_tensor(buf, entry: TensorEntry) -> torch.Tensor:
-    if entry.serializer == Serializer.TORCH_SAVE.value:
+    if entry.serializer == SER.TORCH_SAVE:
         # tensor payloads (complex / quantized dtypes) load weights-only
         return torch_load_from_bytes(buf, trusted=False)
-    if entry.serializer == Serializer.BUFFER_PROTOCOL.value:
+    if entry.serializer == SER.BUFFER_PROTOCOL:
         return tensor_from_bytes(buf, string_to_dtype(entry.dtype), entry.shape)
-    if entry.serializer == Serializer.FP8_BLOCK.value:
+    if entry.serializer == SER.FP8_BLOCK:
         from ..ops.quant import dequantize_host_fp8
 
         return dequantize_host_fp8(buf, entry)
-    if entry.serializer == Serializer.PER_TENSOR_QTENSOR.value:
+    if entry.serializer == SER.PER_TENSOR_QTENSOR:
         from ..format.serialization import per_tensor_qtensor_from_bytes
 
         return per_tensor_qtensor_from_bytes(buf)
-    if entry.serializer == Serializer.PER_CHANNEL_QTENSOR.value:
+    if entry.serializer == SER.PER_CHANNEL_QTENSOR:
         from ..format.serialization import per_channel_qtensor_from_bytes
 
         return per_channel_qtensor_from_bytes(buf)
@@ -323,7 +323,7 @@ class TensorBufferConsumer(BufferConsumer):
 
     def _fp8_on_device(self) -> bool:
         t = self.tensor
-        return (t is not None and t.is_cuda and self.entry.serializer == Serializer.FP8_BLOCK.value
+        return (t is not None and t.is_cuda and self.entry.serializer == SER.FP8_BLOCK
                 and t.is_contiguous() and t.dtype == string_to_dtype(self.entry.dtype))
 
     def get_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
@@ -332,7 +332,7 @@ class TensorBufferConsumer(BufferConsumer):
 
             pb = native.PinnedBuffer(nbytes)
             return StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
-        if self.entry.serializer != Serializer.BUFFER_PROTOCOL.value or self.tensor is None:
+        if self.entry.serializer != SER.BUFFER_PROTOCOL or self.tensor is None:
             return None
         t = self.tensor
         if (not t.is_cuda and t.dtype == string_to_dtype(self.entry.dtype)
@@ -356,7 +356,7 @@ class TensorBufferConsumer(BufferConsumer):
 
     def get_compressed_read_dest(self, nbytes: int) -> Optional[StagedBuffer]:
         t = self.tensor
-        if t is not None and t.is_cuda and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value:
+        if t is not None and t.is_cuda and self.entry.serializer == SER.BUFFER_PROTOCOL:
             from ..ops import native
 
             pb = native.PinnedBuffer(nbytes)
@@ -372,7 +372,7 @@ class TensorBufferConsumer(BufferConsumer):
         t = self.tensor
         if isinstance(buf, CompressedSpan):
             if (t is not None and t.is_cuda
-                    and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value):
+                    and self.entry.serializer == SER.BUFFER_PROTOCOL):
                 staging.scatter_compressed(
                     buf, [(string_to_dtype(self.entry.dtype), self.entry.shape, 0, None, t)],
                     staging.device_of(t), self.producer)
@@ -395,7 +395,7 @@ class TensorBufferConsumer(BufferConsumer):
             dequantize_device(blob, self.entry, t)
             torch.cuda.current_stream(t.device).synchronize()
             return
-        if (t.is_cuda and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value):
+        if (t.is_cuda and self.entry.serializer == SER.BUFFER_PROTOCOL):
             staging.h2d_into(t, staging.host_buffer_addr(buf), self._nbytes(),
                              string_to_dtype(self.entry.dtype), self.entry.shape, self.producer)
             return
@@ -404,13 +404,13 @@ class TensorBufferConsumer(BufferConsumer):
 
     def get_consuming_cost_bytes(self) -> int:
         n = self._nbytes()
-        return 2 * n if self.entry.serializer == Serializer.TORCH_SAVE.value else n
+        return 2 * n if self.entry.serializer == SER.TORCH_SAVE else n
 
     def device_regions(self, base: int):
         """Scatter regions for a merged (batched) GPU restore, or None."""
         t = self.tensor
         if (t is not None and t.is_cuda
-                and self.entry.serializer == Serializer.BUFFER_PROTOCOL.value and t.dim() <= 8 and list(t.shape) == list(self.entry.shape)):
+                and self.entry.serializer == SER.BUFFER_PROTOCOL and t.dim() <= 8 and list(t.shape) == list(self.entry.shape)):
             return [(string_to_dtype(self.entry.dtype), self.entry.shape, base, None, t)]
         return None
 

@@ -745,6 +745,20 @@ class CopyBatch:
         if not n:
             return arr
         cols = list(zip(*self.rows))
+        if all(d == 1 for d in cols[3]):
+            # every row one run (contiguous copies: a freeze of a model's
+            # tensors): fill column 0 of the shape/stride tables directly
+            for field, v in (("src", cols[0]), ("dst", cols[1])):
+                arr[field] = np.asarray(v, dtype=np.uint64)
+            arr["numel"] = cols[2]
+            arr["ndim"] = 1
+            arr["src_dtype"] = cols[4]
+            arr["dst_dtype"] = cols[5]
+            arr["flags"] = cols[6]
+            arr["sizes"][:, 0] = [z[0] for z in cols[7]]
+            arr["src_strides"][:, 0] = [a[0] for a in cols[8]]
+            arr["dst_strides"][:, 0] = [b[0] for b in cols[9]]
+            return arr
         arr["src"] = np.asarray(cols[0], dtype=np.uint64)
         arr["dst"] = np.asarray(cols[1], dtype=np.uint64)
         arr["numel"] = cols[2]

@@ -32,6 +32,7 @@ from __future__ import annotations
 import asyncio
 import copy
 import fnmatch
+import functools
 import itertools
 import json
 import logging
@@ -373,7 +374,8 @@ class Snapshot:
             ps = PendingSnapshot(path=path, pending_io_work=pending, comm=comm, metadata=metadata,
                                  storage=storage, event_loop=loop,
                                  storage_options=storage_options, nonce=nonce,
-                                 plan=progress.get("plan"))
+                                 plan=progress.get("plan"),
+                                 plan_store=progress.get("plan_store"))
         TakeStats.last = {"unblock_s": time.monotonic() - t0}
         timeline.add("unblock", "phase", tp0, time.perf_counter())
         timeline.dump("async_take", comm.get_rank())
@@ -548,7 +550,17 @@ class Snapshot:
             prefixes = {k: flat_prefix(k) for k in everything}
             owners = [everything[k] for k, pre in prefixes.items()
                       if any(r == pre or r.startswith(pre + "/") for r in resident)]
-            plan = plan_cache.store(cache_key, resident, object_entries, write_reqs, owners)
+            if is_async:
+                # stored by the commit thread, off the unblock path (~0.4 ms of
+                # a cold async_take); the plan serves the NEXT take either way
+                if progress is not None:
+                    progress["plan_store"] = functools.partial(
+                        plan_cache.store, cache_key, resident, object_entries, write_reqs,
+                        owners)
+            else:
+                with timeline.span("plan_store"):
+                    plan = plan_cache.store(cache_key, resident, object_entries, write_reqs,
+                                            owners)
         if progress is not None:
             progress["plan"] = plan
         manifest.update(primitives)
@@ -578,10 +590,11 @@ class Snapshot:
                 progress["arenas"] = list({
                     id(r[0]): r[0] for r in (getattr(wr.buffer_stager, "frozen_region", None)
                                              for wr in write_reqs) if r is not None}.values())
-            now: List[WriteReq] = []
-            for wr in write_reqs:
-                (deferred if is_deferrable(wr) else now).append(wr)
-            write_reqs = now
+            with timeline.span("split_deferred"):
+                now: List[WriteReq] = []
+                for wr in write_reqs:
+                    (deferred if is_deferrable(wr) else now).append(wr)
+                write_reqs = now
         if not is_async and not comm.solo() and knobs.rebalance_enabled():
             # uneven device loads: move whole blobs to idle ranks over xGMI
             # (a collective: before the background metadata gather starts)
@@ -620,7 +633,8 @@ class Snapshot:
         if deferred:
             from .engine.scheduler import DeferredIOWork
 
-            pending = DeferredIOWork(pending, deferred, storage, budget, rank)
+            with timeline.span("deferred_init"):
+                pending = DeferredIOWork(pending, deferred, storage, budget, rank)
         return pending, metadata
 
     # --------------------------------------------------------------- restore
@@ -1166,7 +1180,7 @@ class PendingSnapshot:
                  metadata: SnapshotMetadata, storage: StoragePlugin,
                  event_loop: asyncio.AbstractEventLoop,
                  storage_options: Optional[Dict[str, Any]] = None, nonce: str = "",
-                 plan=None) -> None:
+                 plan=None, plan_store=None) -> None:
         self.path = path
         self.pg = comm.pg
         self.exc_info = None
@@ -1181,15 +1195,30 @@ class PendingSnapshot:
             target=self._complete_snapshot, name="hipsnapshot-commit",
             kwargs=dict(path=path, rank=comm.get_rank(), world_size=comm.get_world_size(),
                         pending_io_work=pending_io_work, metadata=metadata, storage=storage,
-                        event_loop=event_loop, store=store, nonce=nonce, plan=plan))
+                        event_loop=event_loop, store=store, nonce=nonce, plan=plan,
+                        plan_store=plan_store))
         self.thread.start()
 
     def _complete_snapshot(self, path: str, rank: int, world_size: int,
                            pending_io_work: PendingIOWork, metadata: SnapshotMetadata,
                            storage: StoragePlugin, event_loop: asyncio.AbstractEventLoop,
-                           store, nonce: str, plan=None) -> None:
+                           store, nonce: str, plan=None, plan_store=None) -> None:
         # WARNING: no collectives in this thread
         self._go.wait()
+        if plan_store is not None:
+            # a new take plan, cached here instead of on the unblock path
+            from .engine import plan_cache
+
+            try:
+                with timeline.span("plan_store", "commit"):
+                    plan = plan_store()
+            except Exception as e:  # noqa: BLE001 - an uncached plan is only not reused
+                logger.debug(f"take plan not cached: {e}")
+                plan = None
+            if isinstance(metadata, _DeferredMetadata):
+                metadata.plan = plan
+            if plan_cache.take_stored_flag() and knobs.gc_after_plan():
+                self._gc_after = True  # its one full GC pass, after the commit
         barrier = None
         if store is not None:
             barrier = _commit_barrier(store, path, nonce, rank, world_size)
