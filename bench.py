@@ -595,6 +595,12 @@ def main() -> None:
         if rank == 0:
             shutil.rmtree(path + "_async", ignore_errors=True)
         fdir = os.path.join(root, "fresh")
+        # untimed: write back what the earlier sections left dirty.  New
+        # files need new page-cache pages, and under a cgroup's dirty limit
+        # the first fresh take otherwise paid for that writeback (1.6-2.6 s
+        # instead of 0.2 s after the GPU test suite ran in the same box call)
+        os.sync()
+        dist.barrier()
         Snapshot.take(os.path.join(fdir, "warm"), app_state, storage_options=opts,
                       compression=args.compression)
         fresh_each = []

@@ -157,8 +157,6 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
     threshold = slab_size_threshold_bytes or knobs.get_slab_size_threshold_bytes()
     align = knobs.slab_align()
     out: List[WriteReq] = []
-    slabs: Dict[int, List[Slab]] = {}
-    relocation: Dict[str, Tuple[str, int, int]] = {}
     # Tail taper: slabs are staged after the big blobs (largest first), and
     # one file is written by one thread at ~10-15 GB/s (buffered writes to a
     # file serialize on its inode lock), while the DMA feeding the writes runs
@@ -169,21 +167,22 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
     # equal-sized slabs the last big writes outlived the staging by ~4 ms:
     # the taper takes 1/8 off one rank's take at 8 GPUs (profiles/rank_share/).
     floor = min(threshold, max(threshold // 16, 8 << 20))  # smaller slabs gain nothing
-    # keyed by CUDA device index (-1: host): t.device builds a torch.device
-    # object per call
-    remaining: Dict[int, int] = defaultdict(int)
-    info = []  # (batchable below threshold?, nbytes, device index) once per request
+    # batchable bytes per CUDA device index (-1: host) not placed yet
+    remaining: Dict[int, int] = {}
+    small = []  # (write request, stager, bytes, device index), in plan order
+    bp = SER.BUFFER_PROTOCOL
     for wr in write_reqs:
         st = wr.buffer_stager
-        if is_batchable(st):
+        if isinstance(st, TensorBufferStager) and st.entry.serializer == bp \
+                and st._tensor_prepare_func is None:
             t = st.tensor
             nb = t.numel() * t.element_size()
             if nb < threshold:
-                di = t.get_device() if t.is_cuda else -1
-                remaining[di] += nb
-                info.append((True, nb, di))
+                di = t.get_device()  # -1 for host tensors
+                remaining[di] = remaining.get(di, 0) + nb
+                small.append((wr, st, nb, di))
                 continue
-        info.append((False, 0, -1))
+        out.append(wr)
 
     def _new_slab(di: int, k: int) -> Slab:
         dev = torch.device("cuda", di) if di >= 0 else None
@@ -191,35 +190,37 @@ def batch_write_requests(entries: List[Entry], write_reqs: List[WriteReq],
             return Slab(dev)
         return Slab(dev, f"{name_prefix}_{f'cuda{di}' if di >= 0 else 'cpu'}_{k}")
 
-    for wr, (small, nbytes, di) in zip(write_reqs, info):
-        if not small:
-            out.append(wr)
-            continue
-        st = wr.buffer_stager
-        left = remaining[di]  # batchable bytes on this device not placed yet
-        remaining[di] -= nbytes
+    slabs: Dict[int, List[Slab]] = {}
+    moved = []  # (write request, stager, slab location, lo, hi)
+    for wr, st, nb, di in small:
+        left = remaining[di]
+        remaining[di] = left - nb
         cap = threshold if left > 8 * threshold else max(floor, min(threshold, left // 8))
         lst = slabs.get(di)
         if lst is None:
             lst = slabs[di] = [_new_slab(di, 0)]
-        if lst[-1].members and _align(lst[-1].sz_bytes, align) + nbytes >= cap:
-            lst.append(_new_slab(di, len(lst)))
-        lo, hi = lst[-1].add(nbytes, st, align)
-        relocation[wr.path] = (lst[-1].location, lo, hi)
+        slab = lst[-1]
+        if slab.members and _align(slab.sz_bytes, align) + nb >= cap:
+            slab = _new_slab(di, len(lst))
+            lst.append(slab)
+        lo, hi = slab.add(nb, st, align)
+        moved.append((wr, st, slab.location, lo, hi))
     for lst in slabs.values():
         for slab in lst:
             if slab.members:
                 out.append(WriteReq(path=slab.location, buffer_stager=slab.build()))
-    by_location = {}
-    for e in entries:
-        for te in iter_tensor_entries(e):
-            by_location[te.location] = te
-    for loc, (new_loc, lo, hi) in relocation.items():
-        if loc not in by_location:
-            raise RuntimeError(
-                f"The tensor entry with the location {loc} is not passed to batch_write.")
-        by_location[loc].location = new_loc
-        by_location[loc].byte_range = [lo, hi]
+    by_location = None
+    for wr, st, new_loc, lo, hi in moved:
+        te = st.entry  # the manifest's entry object (the preparers share it)
+        if te.location != wr.path:
+            if by_location is None:
+                by_location = {te.location: te for e in entries for te in iter_tensor_entries(e)}
+            te = by_location.get(wr.path)
+            if te is None:
+                raise RuntimeError(
+                    f"The tensor entry with the location {wr.path} is not passed to batch_write.")
+        te.location = new_loc
+        te.byte_range = [lo, hi]
     return entries, out
 
 
