@@ -32,6 +32,8 @@ def main() -> int:
         got = last_json(p)
         for key, rule in metrics.items():
             v = got.get(key)
+            if isinstance(v, list):  # per-iteration values: the worst one counts
+                v = (min(v) if "min" in rule else max(v)) if v else None
             ok = v is not None and (v >= rule["min"] if "min" in rule else v <= rule["max"])
             bad += not ok
             bound = f">= {rule['min']}" if "min" in rule else f"<= {rule['max']}"
