@@ -128,6 +128,42 @@ def _state_dict_view(stateful: Any) -> Any:
     return sd
 
 
+def _materialize_optimizer_state(optim: "torch.optim.Optimizer") -> bool:
+    """Create a fresh optimizer's state tensors so sharded (DTensor) state can
+    be restored into them.
+
+    A snapshot's sharded optimizer state is read into tensors of the current
+    layout, and a fresh optimizer has none: it creates them at its first
+    step.  That step is run here with zero gradients and a zero learning
+    rate. The parameters do not move (lr 0 scales every update and the
+    decoupled weight decay to nothing), and the state appears in the
+    parameters' own sharding, as after a training step.  The restore then
+    overwrites every value.  Skipped, returning False, when a parameter
+    already holds a gradient."""
+    params = [p for g in optim.param_groups for p in g["params"]]
+    if any(p.grad is not None for p in params):
+        return False
+    saved = []
+    for g in optim.param_groups:
+        lr = g.get("lr")
+        saved.append(lr)
+        if lr is not None:
+            g["lr"] = torch.zeros_like(lr) if isinstance(lr, torch.Tensor) else 0.0
+    try:
+        with torch.no_grad():
+            for p in params:
+                if p.requires_grad:
+                    p.grad = torch.zeros_like(p)
+        optim.step()
+    finally:
+        for p in params:
+            p.grad = None
+        for g, lr in zip(optim.param_groups, saved):
+            if lr is not None:
+                g["lr"] = lr
+    return True
+
+
 _PLAIN_SD_CLASS: Dict[type, bool] = {}
 
 
@@ -760,6 +796,11 @@ class Snapshot:
         with timeline.span("restore_plan_view"):
             with timeline.span("manifest_for_rank"):
                 manifest, merged = get_manifest_for_rank(self.metadata, comm.get_rank())
+            if isinstance(stateful, torch.optim.Optimizer) and not stateful.state:
+                state_pre = flat_prefix(key) + "/state/"
+                if any(k.startswith(state_pre) and isinstance(e, ShardedTensorEntry)
+                       for k, e in manifest.items()):
+                    _materialize_optimizer_state(stateful)
             with timeline.span("state_dict_view"):
                 _, flat = flatten(_state_dict_view(stateful), prefix=key)
         with timeline.span("restore_filter"):

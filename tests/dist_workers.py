@@ -179,6 +179,58 @@ def fsdp_restore(path: str):
     assert torch.equal(w, ref["layers.0.attention.wq.weight"])
 
 
+def _fsdp_adamw(seed: int):
+    from torch.distributed.device_mesh import init_device_mesh
+    from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+
+    mesh = init_device_mesh("cpu", (dist.get_world_size(),))
+    torch.manual_seed(seed)
+    model = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cpu"), torch.float32, mesh=mesh)
+    return model, torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=0.1)
+
+
+def _full_optim_state(optim):
+    out = {}
+    for i, st in optim.state_dict()["state"].items():
+        for name, v in st.items():
+            out[(i, name)] = v.full_tensor() if hasattr(v, "full_tensor") else v.clone()
+    return out
+
+
+def fsdp_optim_take(path: str):
+    """FSDP2 + AdamW after two steps: model and (sharded) optimizer state."""
+    model, optim = _fsdp_adamw(0)
+    for _ in range(2):
+        tokens = torch.randint(0, 256, (2, 16))
+        model(tokens).float().logsumexp(-1).mean().backward()
+        optim.step()
+        optim.zero_grad()
+    Snapshot.take(path, {"model": model, "optim": optim})
+    ref = {"model": {k: v.full_tensor() for k, v in model.state_dict().items()},
+           "optim": _full_optim_state(optim)}
+    if dist.get_rank() == 0:
+        torch.save(ref, path + "_ref.pt")
+
+
+def fsdp_optim_restore_fresh(path: str):
+    """A fresh process (any world size) restores into a model and an AdamW
+    that never stepped: the sharded optimizer state has no tensors to land in
+    until hipsnapshot materializes them; the parameters must come out as
+    saved, not moved by that zero step."""
+    model, optim = _fsdp_adamw(1)
+    assert not optim.state
+    Snapshot(path).restore({"model": model, "optim": optim})
+    ref = torch.load(path + "_ref.pt", weights_only=True)
+    for k, v in model.state_dict().items():
+        assert torch.equal(v.full_tensor(), ref["model"][k]), k
+    got = _full_optim_state(optim)
+    assert set(got) == set(ref["optim"])
+    for k, v in got.items():
+        assert torch.equal(v, ref["optim"][k]), k
+    assert all(p.grad is None for p in model.parameters())
+    assert optim.param_groups[0]["lr"] == 1e-3
+
+
 class FaultyPlugin:
     pass
 

@@ -41,6 +41,13 @@ def test_fsdp2_dtensor_resharding(tmp_path, save_ws, load_ws):
     run_distributed(W.fsdp_restore, load_ws, p)
 
 
+@pytest.mark.parametrize("load_ws", [1, 2])
+def test_fsdp2_optimizer_state_restores_into_a_fresh_optimizer(tmp_path, load_ws):
+    p = str(tmp_path / "opt")
+    run_distributed(W.fsdp_optim_take, 2, p)
+    run_distributed(W.fsdp_optim_restore_fresh, load_ws, p)
+
+
 def test_fsdp2_takes_reuse_plan_on_every_rank(tmp_path):
     run_distributed(W.fsdp_take_reusing_plan, 2, str(tmp_path / "pc"))
 
