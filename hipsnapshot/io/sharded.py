@@ -27,9 +27,8 @@ from __future__ import annotations
 
 import logging
 import math
-from collections import OrderedDict
 from concurrent.futures import Executor
-from typing import Any, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -370,20 +369,24 @@ class ShardedTensorIOPreparer:
                 f"The shape of obj_out ({out_shape}) is different from the shape of the "
                 f"persisted sharded tensor ({gshape}). Only the overlapping part will be loaded.")
         boxes = local_boxes(obj_out, for_write=False)
-        groups: "OrderedDict[tuple, List[Region]]" = OrderedDict()
-        entries = {}
+        groups: Dict[tuple, list] = {}  # (location, byte range) -> [entry, regions]
         for shard in entry.shards:
-            key = (shard.tensor.location, shard.tensor.byte_range_tuple)
+            te = shard.tensor
+            g = None
             for box in boxes:
                 nar = overlap_narrows(shard.offsets, shard.sizes, box.offsets, box.sizes)
                 if nar is None:
                     continue
-                groups.setdefault(key, []).append(Region(box.tensor, nar))
-                entries[key] = shard.tensor
-        reqs = [ReadReq(path=entries[k].location, byte_range=entries[k].byte_range_tuple,
-                        buffer_consumer=ShardedTensorBufferConsumer(regions, entries[k]),
-                        codec=entries[k].codec)
-                for k, regions in groups.items()]
+                if g is None:
+                    key = (te.location, te.byte_range_tuple)
+                    g = groups.get(key)
+                    if g is None:
+                        g = groups[key] = [te, key[1], []]
+                g[0] = te
+                g[2].append(Region(box.tensor, nar))
+        reqs = [ReadReq(path=te.location, byte_range=br,
+                        buffer_consumer=ShardedTensorBufferConsumer(regions, te), codec=te.codec)
+                for te, br, regions in groups.values()]
         return reqs, Future(obj=obj_out)
 
 
