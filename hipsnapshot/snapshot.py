@@ -155,6 +155,10 @@ def _materialize_optimizer_state(optim: "torch.optim.Optimizer") -> bool:
                 if p.requires_grad:
                     p.grad = torch.zeros_like(p)
         optim.step()
+    except Exception as e:  # noqa: BLE001 - e.g. an optimizer whose step needs a closure
+        logger.warning(f"could not create {type(optim).__name__} state before restoring "
+                       f"it: {e}")
+        return False
     finally:
         for p in params:
             p.grad = None
