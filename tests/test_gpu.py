@@ -520,6 +520,48 @@ def test_fsdp2_rccl_single_rank(gpu, tmp_path):
     run_distributed(_fsdp_gpu_worker, 1, str(tmp_path / "f"), backend="nccl")
 
 
+def _fsdp_gpu_optim_worker(path):
+    """FSDP2 + AdamW in HBM: an async take after training steps, restored
+    into a fresh model and a fresh AdamW (no state tensors yet: created by a
+    zero step, then filled by the native restore job)."""
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+
+    from hipsnapshot.models.llama import LlamaConfig, build_fsdp_llama
+
+    mesh = init_device_mesh("cuda", (dist.get_world_size(),))
+
+    def build(seed):
+        torch.manual_seed(seed)
+        m = build_fsdp_llama(LlamaConfig.tiny(), torch.device("cuda", 0), torch.float32,
+                             mesh=mesh)
+        return m, torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=0.1)
+
+    m, opt = build(0)
+    for _ in range(2):
+        m(torch.randint(0, 256, (2, 16), device="cuda")).float().logsumexp(-1).mean().backward()
+        opt.step()
+        opt.zero_grad()
+    ref_m = {k: v.full_tensor().clone() for k, v in m.state_dict().items()}
+    ref_o = {(i, n): (v.full_tensor() if hasattr(v, "full_tensor") else v).clone()
+             for i, st in opt.state_dict()["state"].items() for n, v in st.items()}
+    Snapshot.async_take(path, {"model": m, "optim": opt}).wait()
+    m2, opt2 = build(1)
+    Snapshot(path).restore({"model": m2, "optim": opt2}, verify=True)
+    torch.cuda.synchronize()
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v.full_tensor(), ref_m[k]), k
+    got = {(i, n): (v.full_tensor() if hasattr(v, "full_tensor") else v)
+           for i, st in opt2.state_dict()["state"].items() for n, v in st.items()}
+    assert set(got) == set(ref_o)
+    for k, v in got.items():
+        assert torch.equal(v.cpu(), ref_o[k].cpu()), k
+
+
+def test_fsdp2_adamw_restores_into_fresh_optimizer(gpu, tmp_path):
+    run_distributed(_fsdp_gpu_optim_worker, 1, str(tmp_path / "o"), backend="nccl")
+
+
 def test_rccl_forced_collectives_match_gloo(gpu, tmp_path, monkeypatch):
     """HIPSNAPSHOT_FORCE_COLLECTIVES: a one-rank RCCL group runs every
     collective the planner and commit use -- framed all_gather_into_tensor
