@@ -910,10 +910,11 @@ class Snapshot:
                     memory_budget_bytes: Optional[int] = None, verify: bool = False) -> T:
         """Read one persisted object by manifest path ``RANK/STATEFUL/KEY/...``.
 
-        Tensor/ShardedTensor/DTensor ``obj_out`` are filled in place (sharded
-        entries need an ``obj_out``); with ``memory_budget_bytes`` large
-        tensors are read in tiles that never exceed it.  ``verify``: as for
-        ``restore``.
+        Tensor/ShardedTensor/DTensor ``obj_out`` are filled in place; with
+        ``memory_budget_bytes`` large tensors are read in tiles that never
+        exceed it.  ``verify``: as for ``restore``.  A sharded entry read
+        without a tensor ``obj_out`` comes back whole, as a host tensor of its
+        global shape (the reference requires an ``obj_out`` there).
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.read_object")
         rank_str, unranked = path.split("/", 1)
@@ -930,6 +931,12 @@ class Snapshot:
         entry = merged.get(unranked) or manifest[unranked]
         if isinstance(entry, PrimitiveEntry):
             return entry.get_value()
+        if isinstance(entry, ShardedTensorEntry) and entry.shards and \
+                not isinstance(obj_out, torch.Tensor) and not is_sharded(obj_out):
+            from .format.serialization import string_to_dtype
+
+            obj_out = torch.empty(entry.global_shape(),
+                                  dtype=string_to_dtype(entry.shards[0].tensor.dtype))
         loop = asyncio.new_event_loop()
         storage = url_to_storage_plugin_in_event_loop(self.path, loop, self._storage_options)
         try:

@@ -95,3 +95,30 @@ def test_verify_needs_checksums(tmp_path, monkeypatch):
     monkeypatch.delenv("HIPSNAPSHOT_CHECKSUM")
     with pytest.raises(RuntimeError, match="no blob checksums"):
         Snapshot(p).restore({"sd": _state(1)}, verify=True)
+
+
+def test_read_object_of_a_sharded_entry_without_obj_out(tmp_path):
+    """A sharded entry comes back whole (global shape, host tensor) when no
+    tensor obj_out is given."""
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import Shard, distribute_tensor
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29591")
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        mesh = init_device_mesh("cpu", (1,))
+        full = torch.randn(37, 11)
+        dt = distribute_tensor(full, mesh, [Shard(0)])
+        p = str(tmp_path / "s")
+        Snapshot.take(p, {"sd": StateDict(w=dt)})
+        got = Snapshot(p).read_object("0/sd/w", verify=True)
+        assert isinstance(got, torch.Tensor) and torch.equal(got, full)
+        got = Snapshot(p).read_object("0/sd/w", memory_budget_bytes=512)
+        assert torch.equal(got, full)
+    finally:
+        if own:
+            dist.destroy_process_group()
