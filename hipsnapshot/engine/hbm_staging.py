@@ -165,6 +165,8 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
     freeze launch's descriptor table are cached on it)."""
     if not native.gpu_available():
         return {}
+    if plan is not None:
+        plan.mutated = True  # its stagers are re-pointed at the arena below
     for wr in write_reqs:
         # a previous take's region (reused plan) never carries over
         wr.buffer_stager.__dict__.pop("frozen_region", None)

@@ -218,14 +218,35 @@ class TakePlan:
         self.json: Dict[str, str] = {}  # logical path -> entry JSON (metadata gather)
         self.owner_ids: set = set()  # ids of the app-state objects behind the leaves
         self.busy = True
+        # stagers changed since the last reset (an async take's HBM freeze
+        # re-points them); a blocking take leaves them as planned
+        self.mutated = True
+        self._streams: Optional[tuple] = None  # producer streams at the last reset
+        self._devices: tuple = ()
+
+    def _current_streams(self) -> tuple:
+        return tuple(int(torch.cuda.current_stream(d).cuda_stream) for d in self._devices)
 
     def reset(self) -> None:
-        """Stagers back to their planned state, producer = current stream."""
+        """Stagers back to their planned state, producer = current stream.
+        Skipped when nothing changed them since the last reset and the
+        devices' current streams are the same (every blocking take: ~0.35 ms
+        of the 291 Llama-3-8B stagers)."""
+        if not self.mutated and self._streams is not None and \
+                self._current_streams() == self._streams:
+            return
         from . import staging
 
+        devs = set()
         with staging.plan_scope():
             for st in _tensor_stagers(self.write_reqs):
                 st.reset_for_reuse()
+                t = st.tensor
+                if t.is_cuda:
+                    devs.add(t.get_device())
+        self._devices = tuple(sorted(devs))
+        self._streams = self._current_streams()
+        self.mutated = False
 
 
 def lookup(key: tuple, resident: Dict[str, Any]) -> Optional[TakePlan]:

@@ -24,7 +24,9 @@ from .manifest import DictEntry, Entry, ListEntry, Manifest, OrderedDictEntry
 
 
 def encode_key(s: str) -> str:
-    return s.replace("%", "%25").replace("/", "%2F")
+    if "%" in s or "/" in s:
+        return s.replace("%", "%25").replace("/", "%2F")
+    return s  # (the common key: nothing to escape)
 
 
 def decode_key(s: str) -> str:

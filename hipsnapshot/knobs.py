@@ -118,6 +118,18 @@ def _cgroup_cpu_quota(root: str = "/sys/fs/cgroup") -> Optional[float]:
         return None
 
 
+_quota_seen: list = [None, None]  # (quota function, its value): read once per process
+
+
+def _cpu_quota() -> Optional[float]:
+    """``_cgroup_cpu_quota()``, read once: every take asks for it (I/O thread
+    count) and the two cgroup file reads cost ~0.1 ms each."""
+    fn = _cgroup_cpu_quota
+    if _quota_seen[0] is not fn:
+        _quota_seen[:] = [fn, fn()]
+    return _quota_seen[1]
+
+
 def available_cpus() -> int:
     """CPUs this process can actually use: its affinity mask, capped by the
     cgroup's CPU quota.  (A GPU box here shows 256 CPUs in the mask and a
@@ -127,7 +139,7 @@ def available_cpus() -> int:
         cpus = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):  # pragma: no cover - non-Linux
         cpus = os.cpu_count() or 16
-    quota = _cgroup_cpu_quota()
+    quota = _cpu_quota()
     if quota is not None:
         cpus = min(cpus, max(1, int(math.ceil(quota))))
     return cpus

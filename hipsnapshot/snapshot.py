@@ -123,7 +123,8 @@ def _state_dict_view(stateful: Any) -> Any:
     if sd is None:
         sd = stateful.state_dict(keep_vars=True)
     for k, v in sd.items():
-        if isinstance(v, torch.Tensor) and v.requires_grad and not isinstance(v, DTensor):
+        if type(v) is not DTensor and isinstance(v, torch.Tensor) and v.requires_grad \
+                and not isinstance(v, DTensor):
             sd[k] = v.detach()
     return sd
 
