@@ -1980,6 +1980,16 @@ int hsg_sync_stream_handle(void* stream) {
 
 uint64_t hsg_desc_size() { return sizeof(CopyDesc); }
 
+// Load this library's code object on `dev` now (the runtime loads it at the
+// first kernel launch otherwise: ~3 ms that fell into the first async_take's
+// freeze launch).  Called from a helper thread while a first take plans.
+int hsg_prewarm_module(int dev) {
+  HS_CHECK(hipSetDevice(dev));
+  hipFuncAttributes attr;
+  HS_CHECK(hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&hs_copy_nd)));
+  return 0;
+}
+
 // Batched strided copy / cast.  `descs` is a host array of `n` CopyDesc (see
 // hipsnapshot/ops/native.py for the packing); `scratch` is a device (or
 // host-mapped) workspace of at least hsg_copy_workspace_bytes() bytes used for

@@ -33,6 +33,7 @@ scales with the bytes that did NOT fit, instead of falling back wholesale.
 from __future__ import annotations
 
 import logging
+import time
 import weakref
 from collections import defaultdict
 from typing import Dict, List, Optional, Tuple
@@ -117,14 +118,32 @@ def _cached_unused(dev: int) -> int:
         return torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
 
 
-_zero_pages: Dict[int, torch.Tensor] = {}
+ZERO_PAGE = 4096
+_zero_page: list = []  # [PinnedBuffer]: kept for the life of the process
 
 
-def _zeros(dev: int) -> torch.Tensor:
-    z = _zero_pages.get(dev)
-    if z is None:
-        z = _zero_pages[dev] = torch.zeros(4096, dtype=torch.uint8, device=f"cuda:{dev}")
-    return z
+def zero_page_ptr() -> int:
+    """Address of ZERO_PAGE zero bytes the copy kernel reads slab gaps from:
+    a pinned host block (device-mapped), zeroed by the CPU.  (A torch.zeros
+    on the device was the first launch of torch's fill kernel in some
+    processes: 15 ms of a cold async_take, spent loading its code object.)"""
+    if not _zero_page:
+        import ctypes
+
+        pb = native.PinnedBuffer(ZERO_PAGE)
+        ctypes.memset(pb.ptr, 0, ZERO_PAGE)
+        _zero_page.append(pb)
+    return _zero_page[0].ptr
+
+
+def add_zero_fill(batch, dst: int, nbytes: int) -> None:
+    """Zero ``nbytes`` at device address ``dst`` within ``batch``'s launch."""
+    zero = zero_page_ptr()
+    while nbytes > 0:
+        n = min(nbytes, ZERO_PAGE)
+        batch.add_bytes(zero, dst, n)
+        dst += n
+        nbytes -= n
 
 
 def _layout(write_reqs: List[WriteReq]) -> Dict[int, list]:
@@ -171,7 +190,8 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
         # a previous take's region (reused plan) never carries over
         wr.buffer_stager.__dict__.pop("frozen_region", None)
         wr.buffer_stager.__dict__.pop("frozen_event", None)
-    by_dev = _plan_layout(write_reqs, plan) if plan is not None else _layout(write_reqs)
+    with timeline.span("freeze_layout"):
+        by_dev = _plan_layout(write_reqs, plan) if plan is not None else _layout(write_reqs)
     launch_cache = plan.freeze_layout["launch"] if plan is not None else None
     frozen = {}
     cap = knobs.hbm_staging_max_bytes()
@@ -187,11 +207,13 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
                 continue
             frozen[dev] = want
             continue
-        free, _ = torch.cuda.mem_get_info(dev)
-        # blocks torch's caching allocator holds but does not use are free
-        # for the arena too (the allocator releases them and retries when a
-        # fresh allocation does not fit) -- a trainer's cache is often tens of GB
-        cached = _cached_unused(dev)
+        with timeline.span("freeze_room"):
+            free, _ = torch.cuda.mem_get_info(dev)
+            # blocks torch's caching allocator holds but does not use are free
+            # for the arena too (the allocator releases them and retries when
+            # a fresh allocation does not fit) -- a trainer's cache is often
+            # tens of GB
+            cached = _cached_unused(dev)
         kept = _kept.get(dev)
         kept_bytes = kept[0].numel() if kept is not None and not kept[1] else 0
         room = min(free + max(cached, 0) + kept_bytes - knobs.hbm_staging_reserve_bytes(), cap)
@@ -325,7 +347,6 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
                 wr.buffer_stager.frozen_region = (arena, off, blob)
         else:
             batch = native.CopyBatch()
-            zero = _zeros(dev).data_ptr()
             placed = []  # (stager, arena offset)
             regions = []  # (write request, arena offset, blob bytes)
             off = 0
@@ -333,7 +354,7 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
                 end = 0
                 for st, mo in zip(sts, moffs):
                     if mo > end:  # slab gap: zeros, as the slab gather writes them
-                        batch.add_bytes(zero, base + off + end, mo - end)
+                        add_zero_fill(batch, base + off + end, mo - end)
                     t = st.tensor  # (only its pointer and layout are read: no detach)
                     if t.numel():
                         batch.add_tensor(t, base + off + mo)
@@ -347,6 +368,7 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
             if launch_cache is not None:
                 launch_cache[dev] = (key, arr, placed, regions)
         sts_all = [st for st, _ in placed]
+        t_ev = time.perf_counter()
         # producers may differ from the current stream: order after them
         for p in {st.producer for st in sts_all if st.producer is not None}:
             if p != stream.cuda_stream:
@@ -361,6 +383,7 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
         done = torch.cuda.Event(enable_timing=True)
         done.record(stream)
         _last_freeze[dev] = (t_start, done)
+        timeline.add("freeze_events", "stage", t_ev, time.perf_counter())
     _live_launches.append((keep, done))
     done_keep = (keep, done)
     if is_kept(arena):

@@ -660,14 +660,12 @@ def _add_members_zero_gaps(batch, members, base: int, dev: int) -> None:
     """Slab members at their offsets, and zeros in the alignment gaps between
     them (same launch): a slab's padding never carries stale HBM bytes, and
     every drain path writes identical blobs."""
-    from .hbm_staging import _zeros
+    from .hbm_staging import add_zero_fill
 
-    zero = None
     end = 0
     for t, off in sorted(members, key=lambda m: m[1]):
         if off > end:
-            zero = zero or _zeros(dev).data_ptr()
-            batch.add_bytes(zero, base + end, off - end)
+            add_zero_fill(batch, base + end, off - end)
         batch.add_tensor(t, base + off)
         end = max(end, off + t.numel() * t.element_size())
 

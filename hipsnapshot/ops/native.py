@@ -256,6 +256,7 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_copy_stream", c_void_p, [c_int, c_int])
         _declare(lib, "hsg_sync_stream_handle", c_int, [c_void_p])
         _declare(lib, "hsg_desc_size", c_uint64, [])
+        _declare(lib, "hsg_prewarm_module", c_int, [c_int])
         _declare(lib, "hsg_copy_workspace_bytes", c_uint64, [c_void_p, c_int])
         _declare(lib, "hsg_copy_nd", c_int,
                  [c_int, c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_int])
@@ -361,6 +362,22 @@ def _check(rc: int, what: str) -> None:
         lib = _load_hsgpu()
         msg = lib.hsg_last_error().decode() if lib is not None else "?"
         raise HipError(f"{what} failed ({rc}): {msg}")
+
+
+_prewarmed: set = set()
+
+
+def prewarm_module(dev: int, pool) -> None:
+    """Load the HIP code object of ``_hsgpu.so`` on ``dev`` on a thread of
+    ``pool`` while the caller goes on planning.  The library is opened here
+    (Python work under the GIL), the load itself runs in the ctypes call,
+    which releases the GIL."""
+    if dev in _prewarmed:
+        return
+    _prewarmed.add(dev)
+    lib = _load_hsgpu()
+    if lib is not None:
+        pool.submit(lib.hsg_prewarm_module, dev)
 
 
 # ---- GPU-writable file mappings (csrc/hsfmap.cpp) -------------------------

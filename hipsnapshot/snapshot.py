@@ -457,12 +457,15 @@ class Snapshot:
     @classmethod
     def _async_take(cls, path, app_state, pg, replicated, storage_options,
                     _custom_tensor_prepare_func, quantize, compression) -> "PendingSnapshot":
+        t_in = time.perf_counter()
         cls._validate_app_state(app_state)
-        _numa_bind_once()
+        with timeline.span("first_use"):
+            _numa_bind_once()
         loop = asyncio.new_event_loop()
         comm = Comm(pg)
         t0 = time.monotonic()
         tp0 = time.perf_counter()
+        timeline.add("async_setup", "phase", t_in, tp0)
         path, rep, keys, nonce, storage = cls._open_and_coalesce(
             path, comm, app_state, replicated, loop, storage_options)
         progress: Dict[str, Any] = {}
@@ -1170,7 +1173,15 @@ def _numa_bind_once() -> None:
     _numa_done[0] = True
     # one commit thread up front: starting it in the first async_take cost
     # that take's unblock ~0.2 ms
-    _commit_pool().submit(int)
+    pool = _commit_pool()
+    if torch.cuda.is_initialized():
+        # the data plane's code object loads on that thread while this take
+        # plans, not at its first kernel launch (~3 ms of a first async_take)
+        from .ops import native
+
+        native.prewarm_module(torch.cuda.current_device(), pool)
+    else:
+        pool.submit(int)
     if os.environ.get("HIPSNAPSHOT_NUMA_BIND") and torch.cuda.is_available():
         from .utils.affinity import maybe_bind_from_env
 

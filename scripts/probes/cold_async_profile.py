@@ -33,7 +33,8 @@ model = build_fsdp_llama(LlamaConfig.llama3_8b(), torch.device("cuda", 0), torch
                          mesh=init_device_mesh("cuda", (1,)))
 torch.cuda.synchronize()
 D = os.environ.get("HSBENCH_DIR", "/tmp")
-Snapshot.take(os.path.join(D, "c"), {"model": model}, compression="hsz1")
+if "--async-first" not in sys.argv:  # (the bench's order: a blocking take first)
+    Snapshot.take(os.path.join(D, "c"), {"model": model}, compression="hsz1")
 torch.cuda.synchronize()
 prof = "--profile" in sys.argv
 if os.environ.get("PROBE_TL"):
