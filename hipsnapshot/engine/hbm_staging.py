@@ -194,6 +194,16 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
         by_dev = _plan_layout(write_reqs, plan) if plan is not None else _layout(write_reqs)
     launch_cache = plan.freeze_layout["launch"] if plan is not None else None
     frozen = {}
+    placed: set = set()  # ids of the stagers re-pointed at an arena below
+    try:
+        _freeze_devices(by_dev, launch_cache, frozen, placed)
+    finally:
+        if plan is not None and plan.pending_reset:
+            plan.reset_except(placed)
+    return frozen
+
+
+def _freeze_devices(by_dev, launch_cache, frozen: Dict[int, int], placed: set) -> None:
     cap = knobs.hbm_staging_max_bytes()
     for dev, reqs in by_dev.items():
         want = sum(r[0] for r in reqs)
@@ -201,7 +211,7 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
         if kept is not None and not kept[1] and kept[0].numel() >= want and want <= cap:
             # the idle kept arena holds everything: no room estimate needed
             try:
-                _freeze(dev, reqs, want, launch_cache)
+                _freeze(dev, reqs, want, launch_cache, placed)
             except torch.cuda.OutOfMemoryError:
                 logger.info(f"HBM staging on cuda:{dev}: arena of {want} B not allocatable")
                 continue
@@ -230,13 +240,13 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
             logger.info(f"HBM staging on cuda:{dev}: {total} of {want} B frozen, the rest "
                         "is staged to host before async_take returns")
         try:
-            _freeze(dev, chosen, total, launch_cache if len(chosen) == len(reqs) else None)
+            _freeze(dev, chosen, total, launch_cache if len(chosen) == len(reqs) else None,
+                    placed)
         except torch.cuda.OutOfMemoryError:
             # fragmentation: the estimate above was optimistic -> host path
             logger.info(f"HBM staging on cuda:{dev}: arena of {total} B not allocatable")
             continue
         frozen[dev] = total
-    return frozen
 
 
 # Arena kept between async takes (knobs.TUNING.hbm_arena_keep): device ->
@@ -329,7 +339,8 @@ def release_hbm_arena() -> int:
     return freed
 
 
-def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -> None:
+def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None,
+            placed_ids: Optional[set] = None) -> None:
     _retire_launches()
     stream = torch.cuda.current_stream(dev)
     with torch.cuda.device(dev):
@@ -390,6 +401,8 @@ def _freeze(dev: int, chosen, total: int, launch_cache: Optional[dict] = None) -
         holders = _holders.setdefault(base, weakref.WeakSet())
         holders.update(st for st, _ in placed)
         holders.update(r[0].buffer_stager for r in regions)
+    if placed_ids is not None:
+        placed_ids.update(id(st) for st, _ in placed)
     for st, o in placed:
         st.frozen_at = (arena, o)  # _source() views the arena from now on
         st.producer = None  # ordering is carried by wait_event

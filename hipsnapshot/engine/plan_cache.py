@@ -221,6 +221,9 @@ class TakePlan:
         # stagers changed since the last reset (an async take's HBM freeze
         # re-points them); a blocking take leaves them as planned
         self.mutated = True
+        # an async take's freeze resets only the stagers it does not re-point
+        # (``lookup(defer_reset=True)``, ``reset_except``)
+        self.pending_reset = False
         self._streams: Optional[tuple] = None  # producer streams at the last reset
         self._devices: tuple = ()
 
@@ -247,11 +250,26 @@ class TakePlan:
         self._devices = tuple(sorted(devs))
         self._streams = self._current_streams()
         self.mutated = False
+        self.pending_reset = False
+
+    def reset_except(self, keep: set) -> None:
+        """Reset every stager whose id is not in ``keep`` (the ones an HBM
+        freeze just re-pointed at its arena, which it set up completely)."""
+        from . import staging
+
+        with staging.plan_scope():
+            for st in _tensor_stagers(self.write_reqs):
+                if id(st) not in keep:
+                    st.reset_for_reuse()
+        self.pending_reset = False
 
 
-def lookup(key: tuple, resident: Dict[str, Any]) -> Optional[TakePlan]:
+def lookup(key: tuple, resident: Dict[str, Any], defer_reset: bool = False
+           ) -> Optional[TakePlan]:
     """The cached plan for ``key`` if every resident leaf still matches it
-    (marked busy for the caller's take), else None."""
+    (marked busy for the caller's take), else None.  ``defer_reset``: the
+    take freezes the plan's device state next; the freeze resets only the
+    stagers it does not re-point (~0.5 ms of every warm async unblock)."""
     with _lock:
         p = _plans.get(key)
         if p is None or p.busy:
@@ -273,7 +291,10 @@ def lookup(key: tuple, resident: Dict[str, Any]) -> Optional[TakePlan]:
             return None
         p.busy = True
         stats["hits"] += 1
-    p.reset()
+    if defer_reset and p.mutated:
+        p.pending_reset = True
+    else:
+        p.reset()
     return p
 
 

@@ -76,7 +76,7 @@ from .io.batcher import batch_read_requests, batch_write_requests
 from .io.preparer import prepare_read, prepare_write
 from .io.sharded import is_sharded
 from .io_types import ReadIO, ReadReq, StoragePlugin, WriteIO, WriteReq, run_sync
-from .ops import checksum
+from .ops import checksum, native
 from .parallel.comm import Comm
 from .parallel.elasticity import get_manifest_for_rank, handle_sharded_tensor_elasticity
 from .parallel.partitioner import consolidate_replicated_entries, partition_write_reqs
@@ -613,7 +613,12 @@ class Snapshot:
                     cache_key = plan_cache.settings_key(
                         everything, rank, comm.get_world_size(), is_async, quantize,
                         comp + ("+host" if host_requested(compression) else ""))
-                    plan = plan_cache.lookup(cache_key, resident)
+                    # an async take's HBM freeze re-points the plan's
+                    # stagers itself: it resets only the others
+                    plan = plan_cache.lookup(
+                        cache_key, resident,
+                        defer_reset=is_async and knobs.async_hbm_staging_enabled()
+                        and native.gpu_available())
                     if progress is not None and plan is not None:
                         # owned by this take from here on: a failure anywhere
                         # below must release it (``_release_plan``)
@@ -1177,8 +1182,6 @@ def _numa_bind_once() -> None:
     if torch.cuda.is_initialized():
         # the data plane's code object loads on that thread while this take
         # plans, not at its first kernel launch (~3 ms of a first async_take)
-        from .ops import native
-
         native.prewarm_module(torch.cuda.current_device(), pool)
     else:
         pool.submit(int)
