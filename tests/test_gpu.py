@@ -1131,6 +1131,52 @@ def test_plan_reuse_gpu_sync_and_async(gpu, tmp_path):
     plan_cache.clear()
 
 
+def test_reused_async_plan_full_then_partial_then_full_freeze(gpu, tmp_path, monkeypatch):
+    """Warm async takes reset only the stagers their freeze does not
+    re-point (plan_cache.lookup(defer_reset=True)): a take whose freeze is
+    partial (HBM short) must stage the rest from the live tensors -- not
+    from the previous take's arena -- and the next full freeze must cover
+    everything again.  Tensors change right after every unblock."""
+    from hipsnapshot.engine import hbm_staging, plan_cache
+
+    plan_cache.clear()
+    hbm_staging.release_hbm_arena()
+    torch.manual_seed(3)
+    sd = StateDict(**{f"big{i}": torch.randn(1 << 20, device=gpu) for i in range(6)},
+                   **{f"small{i}": torch.randn(1000 + i, device=gpu) for i in range(8)})
+    reserve = knobs.hbm_staging_reserve_bytes()
+    real_info = torch.cuda.mem_get_info
+    refs = []
+    for i, mode in enumerate(["full", "full", "partial", "full"]):
+        for v in sd.values():
+            v.add_(1)
+        refs.append({k: v.clone() for k, v in sd.items()})
+        if mode == "partial":
+            hbm_staging.release_hbm_arena()
+            # room for ~2 of the 4 MiB tensors
+            monkeypatch.setattr(torch.cuda, "mem_get_info",
+                                lambda d=None: (reserve + (9 << 20), real_info(d)[1]))
+            monkeypatch.setattr(hbm_staging, "_cached_unused", lambda d: 0)
+        else:
+            monkeypatch.setattr(torch.cuda, "mem_get_info", real_info)
+            monkeypatch.undo()
+        p = Snapshot.async_take(str(tmp_path / f"a{i}"), {"sd": sd})
+        for v in sd.values():  # after unblock: must not leak into the snapshot
+            v.mul_(-7)
+        p.wait()
+        for k, v in refs[-1].items():
+            sd[k].copy_(v)
+    monkeypatch.undo()
+    assert plan_cache.stats["hits"] >= 3
+    for i, ref in enumerate(refs):
+        out = StateDict(**{k: torch.zeros_like(v) for k, v in ref.items()})
+        Snapshot(str(tmp_path / f"a{i}")).restore({"sd": out})
+        torch.cuda.synchronize()
+        for k in ref:
+            assert torch.equal(out[k], ref[k]), (i, k)
+    plan_cache.clear()
+
+
 @pytest.mark.parametrize("where", ["submit", "wait", "blocking"])
 def test_sdma_failure_falls_back_to_blit(gpu, tmp_path, monkeypatch, where):
     """An SDMA copy that fails to start (submit / blocking call) or that the
