@@ -1146,27 +1146,42 @@ def test_reused_async_plan_full_then_partial_then_full_freeze(gpu, tmp_path, mon
                    **{f"small{i}": torch.randn(1000 + i, device=gpu) for i in range(8)})
     reserve = knobs.hbm_staging_reserve_bytes()
     real_info = torch.cuda.mem_get_info
+    real_freeze = hbm_staging.freeze_device_state
+    frozen_bytes = []
+
+    def spy(write_reqs, plan=None):
+        out = real_freeze(write_reqs, plan)
+        frozen_bytes.append(sum(out.values()))
+        return out
+
+    hbm_staging.freeze_device_state = spy
     refs = []
-    for i, mode in enumerate(["full", "full", "partial", "full"]):
-        for v in sd.values():
-            v.add_(1)
-        refs.append({k: v.clone() for k, v in sd.items()})
-        if mode == "partial":
-            hbm_staging.release_hbm_arena()
-            # room for ~2 of the 4 MiB tensors
-            monkeypatch.setattr(torch.cuda, "mem_get_info",
-                                lambda d=None: (reserve + (9 << 20), real_info(d)[1]))
-            monkeypatch.setattr(hbm_staging, "_cached_unused", lambda d: 0)
-        else:
-            monkeypatch.setattr(torch.cuda, "mem_get_info", real_info)
-            monkeypatch.undo()
-        p = Snapshot.async_take(str(tmp_path / f"a{i}"), {"sd": sd})
-        for v in sd.values():  # after unblock: must not leak into the snapshot
-            v.mul_(-7)
-        p.wait()
-        for k, v in refs[-1].items():
-            sd[k].copy_(v)
-    monkeypatch.undo()
+    try:
+        for i, mode in enumerate(["full", "full", "partial", "full"]):
+            for v in sd.values():
+                v.add_(1)
+            refs.append({k: v.clone() for k, v in sd.items()})
+            if mode == "partial":
+                hbm_staging.release_hbm_arena()
+                # room for ~2 of the 4 MiB tensors
+                monkeypatch.setattr(torch.cuda, "mem_get_info",
+                                    lambda d=None: (reserve + (9 << 20), real_info(d)[1]))
+                monkeypatch.setattr(hbm_staging, "_cached_unused", lambda d: 0)
+            else:
+                monkeypatch.setattr(torch.cuda, "mem_get_info", real_info)
+                monkeypatch.undo()
+            p = Snapshot.async_take(str(tmp_path / f"a{i}"), {"sd": sd})
+            for v in sd.values():  # after unblock: must not leak into the snapshot
+                v.mul_(-7)
+            p.wait()
+            for k, v in refs[-1].items():
+                sd[k].copy_(v)
+    finally:
+        monkeypatch.undo()
+        hbm_staging.freeze_device_state = real_freeze
+    # the third take froze part of the state, the others all of it
+    assert frozen_bytes[2] < frozen_bytes[1] == frozen_bytes[3], frozen_bytes
+    assert frozen_bytes[2] > 0, frozen_bytes
     assert plan_cache.stats["hits"] >= 3
     for i, ref in enumerate(refs):
         out = StateDict(**{k: torch.zeros_like(v) for k, v in ref.items()})
