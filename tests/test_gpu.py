@@ -1162,8 +1162,12 @@ def test_reused_async_plan_full_then_partial_then_full_freeze(gpu, tmp_path, mon
                 v.add_(1)
             refs.append({k: v.clone() for k, v in sd.items()})
             if mode == "partial":
-                hbm_staging.release_hbm_arena()
-                # room for ~2 of the 4 MiB tensors
+                # the kept arena (which the previous take's stagers still
+                # point into) counts as busy -- a drain still reading it --
+                # so this take freezes into a new, smaller arena: room for
+                # ~2 of the 4 MiB tensors
+                for k in hbm_staging._kept.values():
+                    k[1] = True
                 monkeypatch.setattr(torch.cuda, "mem_get_info",
                                     lambda d=None: (reserve + (9 << 20), real_info(d)[1]))
                 monkeypatch.setattr(hbm_staging, "_cached_unused", lambda d: 0)
@@ -1174,6 +1178,8 @@ def test_reused_async_plan_full_then_partial_then_full_freeze(gpu, tmp_path, mon
             for v in sd.values():  # after unblock: must not leak into the snapshot
                 v.mul_(-7)
             p.wait()
+            for k in hbm_staging._kept.values():
+                k[1] = False
             for k, v in refs[-1].items():
                 sd[k].copy_(v)
     finally:
