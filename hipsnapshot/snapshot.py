@@ -155,7 +155,13 @@ def _materialize_optimizer_state(optim: "torch.optim.Optimizer") -> bool:
             for p in params:
                 if p.requires_grad:
                     p.grad = torch.zeros_like(p)
-        optim.step()
+        # the class's own step, without the registered step hooks (an EMA or
+        # a logger hooked on steps must not see this one)
+        raw = getattr(type(optim).step, "__wrapped__", None)
+        if raw is not None:
+            raw(optim)
+        else:
+            optim.step()
     except Exception as e:  # noqa: BLE001 - e.g. an optimizer whose step needs a closure
         logger.warning(f"could not create {type(optim).__name__} state before restoring "
                        f"it: {e}")

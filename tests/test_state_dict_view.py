@@ -89,3 +89,21 @@ def test_state_dict_view_detaches_plain_parameters():
     sd = _state_dict_view(m)
     assert not sd["0.lin.weight"].requires_grad
     assert sd["0.lin.weight"].data_ptr() == m[0].lin.weight.data_ptr()
+
+
+def test_optimizer_state_materialized_without_moving_params_or_hooks():
+    from hipsnapshot.snapshot import _materialize_optimizer_state
+
+    m = nn.Linear(4, 4)
+    opt = torch.optim.AdamW(m.parameters(), lr=0.1, weight_decay=0.5)
+    seen = []
+    opt.register_step_post_hook(lambda *a: seen.append(1))
+    w = m.weight.detach().clone()
+    assert _materialize_optimizer_state(opt)
+    assert len(opt.state) == 2 and not seen
+    assert torch.equal(m.weight, w) and m.weight.grad is None
+    assert opt.param_groups[0]["lr"] == 0.1
+    # a parameter holding a gradient: left alone
+    m2 = nn.Linear(2, 2)
+    m2.weight.grad = torch.ones_like(m2.weight)
+    assert not _materialize_optimizer_state(torch.optim.SGD(m2.parameters(), lr=1.0))
