@@ -253,12 +253,15 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                              io_concurrency: Optional[int] = None,
                              gate: Optional[MemoryGate] = None,
                              background: bool = False,
-                             wait_copies: bool = False) -> PendingIOWork:
+                             wait_copies: bool = False,
+                             first_staged: Optional[threading.Event] = None) -> PendingIOWork:
     """``background``: the pipeline runs while the caller keeps using the GPU
     (async-take drain); its staging kernels get a capped grid.
     ``wait_copies``: return only once every staged buffer's asynchronous
     device copy (and on-device hash) has finished, i.e. nothing reads the
-    source tensors any more (async take from live, un-frozen tensors)."""
+    source tensors any more (async take from live, un-frozen tensors).
+    ``first_staged``: set once the first buffer is staged (its copy is
+    queued), so helper work that needs the GIL can wait for it."""
     stage_threads = stage_threads or knobs.get_stage_threads()
     io_concurrency = io_concurrency or knobs.get_io_threads()
     executor = _acquire_pool("stage_bg" if background else "stage", stage_threads, rank)
@@ -282,6 +285,8 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
     def _staged(wr: WriteReq, buf: StagedBuffer, cost: int, t_s: float) -> None:
         timeline.add("stage", "stage", t_s, time.perf_counter(), path=wr.path,
                      bytes=buf.nbytes)
+        if first_staged is not None:
+            first_staged.set()
         stats.bytes_staged += buf.nbytes
         copy = None
         if buf.ready is not None:
@@ -578,10 +583,15 @@ class DeferredIOWork:
 def sync_execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                             memory_budget_bytes: int, rank: int,
                             event_loop: asyncio.AbstractEventLoop,
-                            wait_copies: bool = False) -> PendingIOWork:
-    return run_sync(event_loop,
-        execute_write_reqs(write_reqs, storage, memory_budget_bytes, rank,
-                           wait_copies=wait_copies))
+                            wait_copies: bool = False,
+                            first_staged: Optional[threading.Event] = None) -> PendingIOWork:
+    try:
+        return run_sync(event_loop,
+            execute_write_reqs(write_reqs, storage, memory_budget_bytes, rank,
+                               wait_copies=wait_copies, first_staged=first_staged))
+    finally:
+        if first_staged is not None:
+            first_staged.set()
 
 
 def _expected_read_bytes(rr: ReadReq) -> Optional[int]:

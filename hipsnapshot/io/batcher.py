@@ -125,6 +125,7 @@ class GPUBatchedBufferStager(BufferStager):
         self.members = members
         self.total = total
         self.codec: Optional[dict] = None  # HSZ1 info when the slab is compressed
+        self._pack_cache: dict = {}  # the gather launch's descriptor table (plan reuse)
 
     thread_staging = True
 
@@ -144,7 +145,7 @@ class GPUBatchedBufferStager(BufferStager):
         timeline.add("slab_sources", "stage", t0, time.perf_counter(), n=len(pairs))
         return staging.gather_to_host(pairs, self.total, producers,
                                       via_device_slab=knobs.use_gpu_gather_for_slabs(),
-                                      codec=self.codec)
+                                      codec=self.codec, pack_cache=self._pack_cache)
 
     def get_staging_cost_bytes(self) -> int:
         return self.total
