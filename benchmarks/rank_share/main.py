@@ -215,9 +215,10 @@ def main() -> None:
         "share_GBps": round(share / med / 1e9, 2),
         "ideal_aggregate_GBps": round(args.world * share / med / 1e9, 1),
         # the first async_take of the state builds its plan: reported apart
-        "unblock_ms_median": round(statistics.median(unblock[1:] or unblock) * 1e3, 2),
+        "unblock_ms_median": (round(statistics.median(unblock[1:] or unblock) * 1e3, 2)
+                              if unblock else None),
         "cold_unblock_ms": round(unblock[0] * 1e3, 2) if unblock else None,
-        "async_total_ms_median": round(statistics.median(total) * 1e3, 2),
+        "async_total_ms_median": round(statistics.median(total) * 1e3, 2) if total else None,
         "restore_ms_median": round(statistics.median(rtimes) * 1e3, 2),
         "restore_bitwise_ok": ok,
         "native_restore_stats": _native_restore_stats(),

@@ -188,6 +188,9 @@ class _Tuning:
     dma_inflight = 8           # SDMA device -> host copies in flight per device
     serial_encode = True       # staging threads take turns on a device's HSZ1 encodes
     thread_staging = True      # long-running staging threads pull requests
+    # the first blob is staged before the other workers start (rank share
+    # A/B: 28.5 vs 28.8 ms, scripts/gpu_r5_z.sh; the first DMA starts sooner)
+    stage_head_alone = True
     # checksum launch width: a full-chip hash slows the concurrent SDMA copies
     # (scripts/probes/hash_probe.py); blobs only need hashing at PCIe rate
     hash_grid = 64
