@@ -141,8 +141,28 @@ def describe(devices: List[int]) -> List[dict]:
 _caller_cpu: List[Optional[int]] = [None]
 
 
+_getcpu: list = []
+
+
 def current_cpu() -> Optional[int]:
-    """The CPU the calling thread last ran on (/proc/thread-self/stat)."""
+    """The CPU the calling thread last ran on: glibc's ``sched_getcpu`` (a
+    vDSO call), else /proc/thread-self/stat (a file read on every
+    ``async_take``)."""
+    if not _getcpu:
+        try:
+            import ctypes
+
+            fn = ctypes.CDLL(None, use_errno=True).sched_getcpu
+            fn.restype = ctypes.c_int
+            fn.argtypes = []
+            _getcpu.append(fn)
+        except (OSError, AttributeError):
+            _getcpu.append(None)
+    fn = _getcpu[0]
+    if fn is not None:
+        c = fn()
+        if c >= 0:
+            return c
     try:
         with open("/proc/thread-self/stat") as f:
             stat = f.read()
