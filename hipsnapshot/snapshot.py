@@ -952,10 +952,11 @@ class Snapshot:
             return entry.get_value()
         if isinstance(entry, ShardedTensorEntry) and entry.shards and \
                 not isinstance(obj_out, torch.Tensor) and not is_sharded(obj_out):
-            from .format.serialization import string_to_dtype
+            from .format.serialization import SUPPORTED_QUANTIZED_DTYPES, string_to_dtype
 
-            obj_out = torch.empty(entry.global_shape(),
-                                  dtype=string_to_dtype(entry.shards[0].tensor.dtype))
+            dtype = string_to_dtype(entry.shards[0].tensor.dtype)
+            if dtype not in SUPPORTED_QUANTIZED_DTYPES:  # (those need an obj_out)
+                obj_out = torch.empty(entry.global_shape(), dtype=dtype)
         loop = asyncio.new_event_loop()
         storage = url_to_storage_plugin_in_event_loop(self.path, loop, self._storage_options)
         try:
