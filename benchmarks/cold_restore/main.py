@@ -68,14 +68,32 @@ def _child(args) -> None:
         refs = [p._local_tensor.clone() for _, p in named]
         times = []
         ok = True
-        for _ in range(args.restores):
+        prof_out = os.environ.get("HSBENCH_PROFILE")  # cProfile of each restore
+        for i in range(args.restores):
             for _, p in named:
                 p._local_tensor.zero_()
             torch.cuda.synchronize()
+            prof = None
+            if prof_out:
+                import cProfile
+
+                prof = cProfile.Profile()
+                prof.enable()
             t = time.perf_counter()
             Snapshot(args.path).restore(app_state)
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t)
+            if prof is not None:
+                import io
+                import pstats
+
+                prof.disable()
+                buf = io.StringIO()
+                st = pstats.Stats(prof, stream=buf)
+                st.sort_stats("cumulative").print_stats(60)
+                st.sort_stats("tottime").print_stats(40)
+                with open(f"{prof_out}.restore{i}.txt", "w") as f:
+                    f.write(buf.getvalue())
             named = list(model.named_parameters())
             ok = ok and all(torch.equal(r, p._local_tensor) for (_, p), r in zip(named, refs))
         out.update({"restore_s_each": [round(x, 4) for x in times],
