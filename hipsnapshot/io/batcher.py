@@ -33,10 +33,10 @@ from .. import knobs
 from ..engine import staging
 from ..utils.tracing import timeline
 from ..format.manifest import Entry, iter_tensor_entries
-from ..format.serialization import SER, string_to_dtype
+from ..format.serialization import SER
 from ..io_types import (BufferConsumer, BufferStager, CompressedSpan, ReadReq, StagedBuffer,
                         WriteReq)
-from .tensor import TensorBufferConsumer, TensorBufferStager, run_in_executor, tensor_nbytes_from_entry
+from .tensor import TensorBufferStager, run_in_executor
 
 
 def is_batchable(stager: BufferStager) -> bool:
