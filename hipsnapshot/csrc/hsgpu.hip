@@ -1694,6 +1694,27 @@ uint64_t hsg_pinned_trim() {
   return freed;
 }
 
+int hsg_restore_idle_blocks(int dev, uint64_t* ptrs, uint64_t* sizes, int max);
+
+// Test hook: overwrite every idle block of the restore's device pools (on
+// `dev`) and of the pinned host pool with `byte`, so a test can show that no
+// restore reads bytes an earlier one left behind.  Returns the blocks written.
+int hsg_poison_idle_pools(int dev, int byte) {
+  std::vector<uint64_t> ptrs(4096), sizes(4096);
+  const int n = hsg_restore_idle_blocks(dev, ptrs.data(), sizes.data(), 4096);
+  HS_CHECK(hipSetDevice(dev));
+  for (int i = 0; i < n; ++i)
+    HS_CHECK(hipMemset(reinterpret_cast<void*>(ptrs[i]), byte, sizes[i]));
+  HS_CHECK(hipDeviceSynchronize());
+  int m = 0;
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  for (auto& kv : g_pool.free_blocks) {
+    std::memset(kv.second, byte, kv.first);
+    ++m;
+  }
+  return n + m;
+}
+
 // ---- DMA copies on side streams --------------------------------------------
 
 // Copy `n` bytes between host and device on copy stream (dev, slot), ordered

@@ -152,6 +152,21 @@ struct DevPool {
     live.erase(it);
   }
 
+  // idle blocks of `dev`: (address, bytes) pairs, at most `max`
+  int idle(int dev, uint64_t* ptrs, uint64_t* sizes, int max) {
+    std::lock_guard<std::mutex> g(mu);
+    int n = 0;
+    auto it = free_blocks.find(dev);
+    if (it == free_blocks.end()) return 0;
+    for (auto& kv : it->second) {
+      if (n >= max) break;
+      ptrs[n] = reinterpret_cast<uint64_t>(kv.second);
+      sizes[n] = kv.first;
+      ++n;
+    }
+    return n;
+  }
+
   // free idle blocks of `dev` (-1: all devices) until at most `keep` idle
   // bytes remain (largest first); returns the bytes freed
   uint64_t trim(int dev, uint64_t keep) {
@@ -1015,6 +1030,14 @@ int hsg_restore_prewarm(int dev, uint64_t up_bytes, uint64_t sc_bytes, uint64_t 
 // bytes remain in each (per call; -1 device = all).  Returns bytes freed.
 uint64_t hsg_restore_trim(int dev, uint64_t keep) {
   return g_upload_pool.trim(dev, keep) + g_scratch_pool.trim(dev, keep);
+}
+
+// The idle blocks of both pools on `dev` (upload first), at most `max`
+// (address, bytes) pairs; returns how many.  For tests that overwrite what a
+// restore left in them (a later restore must not depend on those bytes).
+int hsg_restore_idle_blocks(int dev, uint64_t* ptrs, uint64_t* sizes, int max) {
+  const int n = g_upload_pool.idle(dev, ptrs, sizes, max);
+  return n + g_scratch_pool.idle(dev, ptrs + n, sizes + n, max - n);
 }
 
 // The same per pool: uncached upload blocks / plain scratch blocks.

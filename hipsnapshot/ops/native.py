@@ -291,6 +291,7 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_void_p, P(c_int), c_char_p, P(ctypes.c_double), P(c_uint64), P(c_uint64)])
         _declare(lib, "hsg_restore_trim", c_uint64, [c_int, c_uint64])
         _declare(lib, "hsg_restore_trim_pools", c_uint64, [c_int, c_uint64, c_uint64])
+        _declare(lib, "hsg_poison_idle_pools", c_int, [c_int, c_int])
         _declare(lib, "hsg_restore_prewarm", c_int,
                  [c_int, c_uint64, c_uint64, c_uint64, c_int, c_uint64])
         _declare(lib, "hsg_sdma_h2d_submit", c_int,
@@ -1087,6 +1088,14 @@ def _give_err_words(t: torch.Tensor) -> None:
     with _err_words_lock:
         if len(_err_words_free) < 8:
             _err_words_free.append(t)
+
+
+def poison_idle_pools(dev: int, byte: int) -> int:
+    """Test hook: fill every idle restore device block on ``dev`` and every
+    idle pinned host block with ``byte``; returns the blocks written."""
+    r = int(require_gpu_lib().hsg_poison_idle_pools(dev, byte))
+    _check(min(r, 0), "hsg_poison_idle_pools")
+    return r
 
 
 def restore_trim(dev: int, keep_bytes: int) -> int:

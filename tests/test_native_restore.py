@@ -306,3 +306,77 @@ def test_native_and_python_reads_in_one_restore(gpu, tmp_path):
     assert native_restore.last_stats.get("items", 0) >= 1
     assert torch.equal(dst["gpu"], src["gpu"]) and torch.equal(dst["cpu"], src["cpu"])
     assert dst["obj"] == src["obj"]
+
+
+@pytest.mark.parametrize("compression", ["none", "hsz1"])
+def test_restore_never_reads_bytes_an_earlier_restore_left(gpu, tmp_path, compression):
+    """Every idle block of the restore's device pools and of the pinned host
+    pool is overwritten between restores of the same snapshot: a job that
+    read a byte it had not written (upload / decode / copy-table space, or a
+    pinned slot) would only be right because the previous restore left the
+    same bytes there (round-5 trim A/B: wrong bytes once another process got
+    the freed HBM)."""
+    from hipsnapshot.engine import native_restore
+    from hipsnapshot.ops import native
+
+    src = _state(gpu)
+    path = str(tmp_path / "s")
+    Snapshot.take(path, {"sd": src}, compression=compression)
+    dev = torch.cuda.current_device()
+    for i, byte in enumerate((0xA5, 0x00, 0xFF, 0x7F)):
+        dst = _zeros_like_state(src)
+        native_restore.last_stats.clear()
+        Snapshot(path).restore({"sd": dst}, verify=(i % 2 == 1))
+        torch.cuda.synchronize()
+        assert native_restore.last_stats.get("items", 0) > 0
+        _eq(dst, src)
+        assert native.poison_idle_pools(dev, byte) > 0
+    # budgeted reads: 1 MiB pinned slots, many pieces per blob
+    for name in ("big", "w", "h"):
+        for byte in (0x5A, 0xC3):
+            out = torch.zeros_like(src[name])
+            native.poison_idle_pools(dev, byte)
+            Snapshot(path).read_object(f"0/sd/{name}", obj_out=out, memory_budget_bytes=2048)
+            torch.cuda.synchronize()
+            assert torch.equal(out, src[name]), (name, byte)
+
+
+def test_resharded_restore_never_reads_stale_pool_bytes(gpu, tmp_path):
+    from hipsnapshot.utils.test_utils import run_distributed
+
+    run_distributed(_poison_reshard_worker, 2, str(tmp_path), timeout=600)
+
+
+def _poison_reshard_worker(root):
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import DTensor, Shard
+
+    from hipsnapshot.ops import native
+
+    rank = dist.get_rank()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    mesh = init_device_mesh("cuda", (2,))  # both ranks on this GPU
+
+    def dt(local, dim):
+        return DTensor.from_local(local, mesh, [Shard(dim)], run_check=False)
+
+    g = torch.Generator(device=dev).manual_seed(7)
+    full = (torch.randn(512, 384, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    want = full[:, rank * 192:(rank + 1) * 192]
+    for comp in ("none", "hsz1"):
+        path = os.path.join(root, comp)
+        Snapshot.take(path, {"sd": StateDict(x=dt(full[rank * 256:(rank + 1) * 256].clone(), 0))},
+                      compression=comp)
+        for byte in (0xA5, 0xFF, 0x00):
+            native.poison_idle_pools(0, byte)
+            loc = torch.zeros(512, 192, device=dev, dtype=torch.bfloat16)
+            Snapshot(path).restore({"sd": StateDict(x=dt(loc, 1))})
+            torch.cuda.synchronize()
+            assert torch.equal(loc, want), (comp, byte)
+            out = torch.zeros(512, 384, device=dev, dtype=torch.bfloat16)
+            native.poison_idle_pools(0, byte ^ 0x3C)
+            Snapshot(path).read_object("0/sd/x", obj_out=out, memory_budget_bytes=2048)
+            torch.cuda.synchronize()
+            assert torch.equal(out, full), (comp, byte, "read_object")
