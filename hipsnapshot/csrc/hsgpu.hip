@@ -1727,6 +1727,10 @@ int hsg_poison_idle_pools(int dev, int byte) {
 // hipDeviceMallocUncached memory, cached per device by size (best fit up to
 // 2x, 2 MiB granules): the restore's encoded frames are uploaded into it by
 // SDMA and read once by the decode kernel, never through a stale L2 line.
+extern "C" void* hsg_rt_vmm_alloc(int dev, uint64_t nbytes, int uncached);
+extern "C" int hsg_rt_vmm_free(void* p);
+extern "C" const char* hsg_rt_last_error();
+
 struct UncachedPool {
   std::mutex mu;
   std::map<int, std::multimap<size_t, void*>> free_blocks;  // dev -> size -> block
@@ -1749,10 +1753,11 @@ void* hsg_uncached_acquire(int dev, uint64_t nbytes) {
       return p;
     }
   }
-  if (hipSetDevice(dev) != hipSuccess) return nullptr;
-  void* p = nullptr;
-  hipError_t e = hipExtMallocWithFlags(&p, want, hipDeviceMallocUncached);
-  if (e != hipSuccess) {
+  // hsg_rt_vmm_alloc (hshost.hip): a freed block's address is never handed
+  // out again (re-used addresses of freed uncached blocks were written
+  // through stale translations, profiles/r6/trim/)
+  void* p = hsg_rt_vmm_alloc(dev, want, 1);
+  if (p == nullptr) {
     // drop this device's idle blocks and retry once
     std::vector<void*> drop;
     {
@@ -1761,10 +1766,10 @@ void* hsg_uncached_acquire(int dev, uint64_t nbytes) {
       for (auto& kv : fl) { drop.push_back(kv.second); g_upool.cached_bytes -= kv.first; }
       fl.clear();
     }
-    for (void* q : drop) (void)hipFree(q);
-    e = hipExtMallocWithFlags(&p, want, hipDeviceMallocUncached);
-    if (e != hipSuccess) {
-      set_err("hipExtMallocWithFlags(uncached)", e);
+    for (void* q : drop) (void)hsg_rt_vmm_free(q);
+    p = hsg_rt_vmm_alloc(dev, want, 1);
+    if (p == nullptr) {
+      snprintf(g_err, sizeof(g_err), "uncached block of %zu bytes: %s", want, hsg_rt_last_error());
       return nullptr;
     }
   }
@@ -1798,10 +1803,7 @@ uint64_t hsg_uncached_trim() {
     }
     g_upool.cached_bytes -= freed;
   }
-  for (auto& d : drop) {
-    (void)hipSetDevice(d.first);
-    (void)hipFree(d.second);
-  }
+  for (auto& d : drop) (void)hsg_rt_vmm_free(d.second);
   return freed;
 }
 

@@ -75,8 +75,9 @@ int hsg_copy_nd(int dev, const void* descs, int n, void* workspace, uint64_t ws_
 uint64_t hsg_desc_size();
 void* hsg_copy_stream(int dev, int slot);
 int hsg_rt_set_device(int dev);
-void* hsg_rt_dev_alloc(int dev, uint64_t nbytes, int uncached);
-void hsg_rt_dev_free(void* p);
+void* hsg_rt_vmm_alloc(int dev, uint64_t nbytes, int uncached);
+int hsg_rt_vmm_free(void* p);
+uint64_t hsg_rt_vmm_retired_bytes();
 void* hsg_rt_event_record(void* stream);
 int hsg_rt_event_sync(void* ev);
 void hsg_rt_event_free(void* ev);
@@ -85,6 +86,8 @@ int hsg_rt_stream_sync(void* stream);
 int hsg_rt_memcpy_d2h(void* dst, const void* src, uint64_t n);
 int hsg_hash64_into(int dev, void* stream, const void* p, uint64_t n, uint64_t first_word,
                     int max_grid, void* acc);
+const char* hsg_rt_last_error();
+void hsg_rt_trace(const char* what, const void* p, uint64_t n, int kind);
 }
 
 namespace {
@@ -106,7 +109,17 @@ uint64_t align16(uint64_t n) { return (n + 15) & ~uint64_t(15); }
 // ---- device block pools (uncached upload targets, plain scratch) -----------
 //
 // Cached per device by size (best fit up to 2x, 2 MiB granules) across
-// restores; hsg_restore_trim() frees the idle ones.
+// restores; hsg_restore_trim() frees the idle ones.  Blocks come from
+// hsg_rt_vmm_alloc (hshost.hip): a freed block's virtual range is never
+// handed out again.  With hipMalloc / hipExtMallocWithFlags blocks, freeing
+// uncached and plain blocks let the runtime hand a freed address out again as
+// the other kind, and kernels then wrote through the address's old
+// translation: wrong bytes and hipErrorIllegalAddress faults whenever the
+// pools were trimmed (profiles/r6/trim/).
+//
+// Freed ranges stay reserved (virtual address space only); past this many
+// bytes of them a trim keeps its blocks instead.
+constexpr uint64_t kMaxRetiredVa = uint64_t(64) << 40;
 struct DevPool {
   std::mutex mu;
   std::map<int, std::multimap<uint64_t, void*>> free_blocks;
@@ -126,13 +139,14 @@ struct DevPool {
         void* p = it->second;
         live[p] = {dev, it->first};
         idle_bytes -= it->first;
+        hsg_rt_trace("reuse", p, it->first, uncached);
         fl.erase(it);
         return p;
       }
     }
     void* p = nullptr;
     for (int attempt = 0; attempt < 2; ++attempt) {
-      p = hsg_rt_dev_alloc(dev, want, uncached);
+      p = hsg_rt_vmm_alloc(dev, want, uncached);
       if (p) break;
       if (attempt == 0) trim(dev, 0);  // drop this device's idle blocks and retry
     }
@@ -172,6 +186,7 @@ struct DevPool {
   uint64_t trim(int dev, uint64_t keep) {
     std::vector<void*> drop;
     uint64_t freed = 0;
+    if (hsg_rt_vmm_retired_bytes() > kMaxRetiredVa) return 0;
     {
       std::lock_guard<std::mutex> g(mu);
       for (auto& dv : free_blocks) {
@@ -186,7 +201,7 @@ struct DevPool {
         }
       }
     }
-    for (void* q : drop) hsg_rt_dev_free(q);
+    for (void* q : drop) (void)hsg_rt_vmm_free(q);
     return freed;
   }
 };
@@ -383,9 +398,10 @@ struct Job {
     if (err.compare_exchange_strong(expected, code)) {
       std::lock_guard<std::mutex> g(mu);
       err_item = item;
-      snprintf(errmsg, sizeof(errmsg), "%s %s: %s", what,
+      snprintf(errmsg, sizeof(errmsg), "%s %s: %s%s%s", what,
                item >= 0 ? items[item].path.c_str() : "",
-               code < 0 && code > -4096 ? strerror(-code) : "error");
+               code < 0 && code > -4096 ? strerror(-code) : "error",
+               code == -EIO ? " -- " : "", code == -EIO ? hsg_rt_last_error() : "");
     }
     cv.notify_all();
   }
@@ -553,6 +569,7 @@ void reader_thread(Job* j) {
     }
     t0 = now_ns();
     uint64_t h = 0;
+    hsg_rt_trace("upload", static_cast<char*>(it.block) + f.off, f.n, i);
     const int r = hsg_sdma_h2d_submit_on(j->dev, static_cast<char*>(it.block) + f.off, sp, f.n,
                                          j->engine, &h);
     if (!j->first_upload.exchange(true)) j->ns[kFirstUpload].store(now_ns() - j->t_start);
@@ -897,13 +914,13 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
   j->slots.assign(nslots, nullptr);
   bool any_hash = false;
   for (const Item& it : j->items) any_hash |= it.hash;
-  if (any_hash) j->hash_acc = static_cast<uint64_t*>(hsg_rt_dev_alloc(dev, 8 * uint64_t(n), 0));
+  if (any_hash) j->hash_acc = static_cast<uint64_t*>(g_scratch_pool.acquire(dev, 8 * uint64_t(n)));
   // two slots now, the rest from a helper thread while the readers start:
   // a first use of pinned memory in the process registers it (~10 ms/GiB)
   for (int s = 0; s < 2; ++s) {
     void* p = (any_hash && !j->hash_acc) ? nullptr : hsg_pinned_acquire(j->slot_bytes);
     if (!p) {
-      hsg_rt_dev_free(j->hash_acc);
+      g_scratch_pool.release(j->hash_acc);
       for (void* q : j->slots)
         if (q) hsg_pinned_release(q);
       g_upload_pool.release(j->up_base);
@@ -918,6 +935,7 @@ void* hsg_restore_start(int dev, int n, const char* const* paths, const uint64_t
     j->free_slots.push_back(1 - s);
   }
   j->t_start = now_ns();
+  hsg_rt_trace("job-start", j, uint64_t(n), dev);
   if (nslots > 2)
     j->threads.emplace_back([j, nslots] {
       for (int s = 2; s < nslots && !j->err.load(); ++s) {
@@ -962,7 +980,7 @@ int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
     const size_t n = j->items.size();
     if (sums && hsg_rt_memcpy_d2h(sums, j->hash_acc, 8 * n) != 0)
       j->fail(-EIO, -1, "hash results");
-    hsg_rt_dev_free(j->hash_acc);
+    g_scratch_pool.release(j->hash_acc);
     j->hash_acc = nullptr;
   }
   j->add(kWall, j->t_start);
@@ -980,6 +998,7 @@ int hsg_restore_wait(void* handle, int* err_item, char* msg, double* stats,
     for (int k = 0; k < kNumStats; ++k) stats[k] = 1e-9 * double(j->ns[k].load());
   if (bytes_read) *bytes_read = j->bytes_read.load();
   const int e = j->err.load();
+  hsg_rt_trace("job-end", j, uint64_t(-e), j->err_item);
   if (err_item) *err_item = j->err_item;
   if (msg) snprintf(msg, 320, "%s", j->errmsg);
   delete j;

@@ -7,9 +7,15 @@ dicts are ``DTensor``s, so both map to the same ``ShardedTensorEntry``:
 write
   every local shard (global offsets/sizes) is subdivided along its sharding
   dim into <= ``max_shard_size`` pieces stored at
-  ``sharded/<logical_path>_<off0>_<off1>...``.  For a DTensor, ranks whose
-  coordinate along a ``Replicate`` mesh dim is not 0 write nothing (HSDP /
-  replicated DTensors are saved once); ``Partial`` is reduced first.  Any
+  ``sharded/<logical_path>_<off0>_<off1>...``.  A DTensor replicated R ways
+  (``Replicate`` mesh dims: HSDP, DTensor DDP) is saved once, its write load
+  spread over the R replicas: each box of >= ``replica_split_min_bytes`` is
+  cut into R row ranges, replica j writing range j; a smaller box goes whole
+  to one replica picked by a hash of its position.  Every rank computes the
+  same plan from its mesh coordinate, without a collective (the reference
+  balances replicated blobs through its partitioner,
+  `/root/reference/torchsnapshot/partitioner.py:42-79`).  ``Partial`` is
+  reduced first.  Any
   mesh rank and any mix of ``Shard`` / ``_StridedShard`` placements (FSDP2 x
   TP) is decomposed into the global boxes the local tensor holds
   (``dim_index_runs``): a strided layout saves several boxes per rank.
@@ -205,19 +211,65 @@ def _implicit_replica(mesh) -> bool:
     return False
 
 
+def replica_index(mesh_shape: Sequence[int], coord: Sequence[int],
+                  placements: Sequence[Any]) -> Tuple[int, int]:
+    """(this rank's index among the replicas of its boxes, replica count):
+    mixed radix over the ``Replicate`` mesh dims."""
+    j, r = 0, 1
+    for mdim, p in enumerate(placements):
+        if isinstance(p, Replicate) and int(mesh_shape[mdim]) > 1:
+            j = j * int(mesh_shape[mdim]) + int(coord[mdim])
+            r *= int(mesh_shape[mdim])
+    return j, r
+
+
+def _box_owner(go: Sequence[int], sz: Sequence[int], shape: Sequence[int], r: int) -> int:
+    """The replica that writes a small box whole (the same on every rank)."""
+    import zlib
+
+    return zlib.crc32(repr((list(go), list(sz), list(shape))).encode()) % r
+
+
+def split_for_replicas(boxes, j: int, r: int, itemsize: int, shape: Sequence[int],
+                       min_split_bytes: int):
+    """The part of ``boxes`` (``(local_offsets, global_offsets, sizes)``)
+    replica ``j`` of ``r`` writes: a box of >= ``min_split_bytes`` with at
+    least ``r`` rows is cut into ``r`` near-equal row ranges (range ``j`` is
+    this replica's); a smaller box is written whole by ``_box_owner``."""
+    if r <= 1:
+        return list(boxes)
+    out = []
+    for lo, go, sz in boxes:
+        n = itemsize
+        for s in sz:
+            n *= int(s)
+        if sz and int(sz[0]) >= r and n >= min_split_bytes:
+            a, b = int(sz[0]) * j // r, int(sz[0]) * (j + 1) // r
+            if b > a:
+                out.append(([lo[0] + a] + list(lo[1:]), [go[0] + a] + list(go[1:]),
+                            [b - a] + list(sz[1:])))
+        elif _box_owner(go, sz, shape, r) == j:
+            out.append((lo, go, sz))
+    return out
+
+
 def _dtensor_layout(dt, for_write: bool):
-    key = (dt._spec, for_write)
+    from .. import knobs
+
+    key = (dt._spec, for_write, knobs.TUNING.replica_split_min_bytes)
     hit = _LAYOUT_CACHE.get(key)
     if hit is not None:
         return hit
     placements = list(dt.placements)
     mesh = dt.device_mesh
     coord = mesh.get_coordinate()
-    skip = coord is None or (for_write and (any(
-        isinstance(p, Replicate) and coord[mdim] != 0 for mdim, p in enumerate(placements))
-        or _implicit_replica(mesh)))
+    skip = coord is None or (for_write and _implicit_replica(mesh))
     boxes = [] if coord is None else runs_to_boxes(
         dim_index_runs(dt.shape, mesh.shape, coord, placements))
+    if for_write and not skip:
+        j, r = replica_index(mesh.shape, coord, placements)
+        boxes = split_for_replicas(boxes, j, r, dt.element_size(), list(dt.shape),
+                                   knobs.TUNING.replica_split_min_bytes)
     sdim = next((d for d in (_shard_dim_of(p, dt.dim()) for p in placements) if d is not None), 0)
     hit = (skip, boxes, sdim)
     if len(_LAYOUT_CACHE) > 65536:
@@ -227,8 +279,10 @@ def _dtensor_layout(dt, for_write: bool):
 
 
 def _dtensor_boxes(dt, for_write: bool) -> List[LocalBox]:
+    from .. import knobs
+
     spec = dt._spec
-    key = (id(spec), for_write)
+    key = (id(spec), for_write, knobs.TUNING.replica_split_min_bytes)
     ent = _LAYOUT_BY_ID.get(key)
     if ent is None or ent[0] is not spec:
         partial = any(isinstance(p, Partial) for p in spec.placements)

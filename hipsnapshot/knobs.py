@@ -246,6 +246,10 @@ class _Tuning:
     file_map = False
     file_map_max_bytes = 64 << 30  # mapped (pinned page-cache) bytes kept per process
     # -- distributed -------------------------------------------------------------------
+    # a DTensor box replicated R ways (HSDP, DTensor DDP) at least this large
+    # is written as R row ranges, one per replica; smaller boxes go whole to
+    # one replica chosen by a hash of their position (io/sharded.py)
+    replica_split_min_bytes = 1 << 20
     rebalance_host = False     # let the rebalancer move host blobs too (gloo tests)
     rebalance_min_gain = 0.1
     # -- UVM ------------------------------------------------------------------------------

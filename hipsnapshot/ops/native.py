@@ -313,6 +313,13 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_uncached_acquire", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_uncached_release", c_int, [c_void_p])
         _declare(lib, "hsg_uncached_trim", c_uint64, [])
+        _declare(lib, "hsg_rt_dev_alloc", c_void_p, [c_int, c_uint64, c_int])
+        _declare(lib, "hsg_rt_dev_free", None, [c_void_p])
+        _declare(lib, "hsg_rt_memcpy_d2h", c_int, [c_void_p, c_void_p, c_uint64])
+        _declare(lib, "hsg_rt_last_error", c_char_p, [])
+        _declare(lib, "hsg_rt_vmm_alloc", c_void_p, [c_int, c_uint64, c_int])
+        _declare(lib, "hsg_rt_vmm_free", c_int, [c_void_p])
+        _declare(lib, "hsg_rt_vmm_retired_bytes", c_uint64, [])
         _declare(lib, "hsg_sdma_d2h", c_int,
                  [c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p])
         _declare(lib, "hsg_sdma_d2h_submit", c_int,

@@ -16,6 +16,8 @@
 
 #include "engine_stubs.h"
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -238,6 +240,15 @@ extern "C" {
 
 int hsg_rt_set_device(int dev) { return dev == 0 ? 0 : -1; }
 
+const char* hsg_rt_last_error() { return "stub"; }
+
+void hsg_rt_trace(const char* what, const void* p, uint64_t n, int kind) {
+  (void)what;
+  (void)p;
+  (void)n;
+  (void)kind;
+}
+
 void* hsg_rt_dev_alloc(int dev, uint64_t nbytes, int uncached) {
   (void)dev;
   (void)uncached;
@@ -264,6 +275,54 @@ void hsg_rt_dev_free(void* p) {
   }
   free(p);
 }
+
+// The engines' pools allocate through the VMM hooks (hshost.hip), whose
+// promise is that a freed block's address range is never handed out again.
+// The stand-in keeps it: blocks are anonymous mappings, and a free replaces
+// the range with an inaccessible reservation -- the memory goes back, the
+// addresses stay taken, and any later use of the block (a kernel or copy the
+// engine still had queued on it) faults at once, as a GPU access to an
+// unmapped range does.
+void* hsg_rt_vmm_alloc(int dev, uint64_t nbytes, int uncached) {
+  (void)dev;
+  (void)uncached;
+  const uint64_t n = (std::max<uint64_t>(nbytes, 1) + 4095) / 4096 * 4096;
+  if (dev_live.load() + n > dev_cap.load()) return nullptr;
+  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return nullptr;
+  dev_live.fetch_add(n);
+  std::lock_guard<std::mutex> g(g_mu);
+  ensure();
+  (*g_dev_sizes)[p] = n;
+  return p;
+}
+
+std::atomic<uint64_t> g_vmm_retired{0};
+
+int hsg_rt_vmm_free(void* p) {
+  uint64_t n = 0;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    ensure();
+    auto it = g_dev_sizes->find(p);
+    if (it == g_dev_sizes->end()) {
+      fprintf(stderr, "stub: vmm free of %p, which is not a live block\n", p);
+      abort();
+    }
+    n = it->second;
+    g_dev_sizes->erase(it);
+  }
+  void* q = mmap(p, n, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
+  if (q != p) {
+    fprintf(stderr, "stub: retiring %p failed\n", p);
+    abort();
+  }
+  dev_live.fetch_sub(n);
+  g_vmm_retired.fetch_add(n);
+  return 0;
+}
+
+uint64_t hsg_rt_vmm_retired_bytes() { return g_vmm_retired.load(); }
 
 struct StubEvent {
   std::shared_ptr<Flag> f;

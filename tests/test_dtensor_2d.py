@@ -267,8 +267,8 @@ def test_fsdp_over_tp_save_and_reshard_gpu(gpu, tmp_path):
 
 
 def _hsdp_worker(tmp: str):
-    """HSDP: (replicate=2, shard=2) mesh -- replicas write nothing; restore
-    into a 1-D (4,) FSDP mesh."""
+    """HSDP: (replicate=2, shard=2) mesh -- each box is saved once (small
+    boxes whole, by one replica); restore into a 1-D (4,) FSDP mesh."""
     import torch.distributed as dist
     from torch.distributed.device_mesh import init_device_mesh
     from torch.distributed.tensor import Replicate, Shard, distribute_tensor
@@ -298,3 +298,54 @@ def _hsdp_worker(tmp: str):
 @pytest.mark.multiproc
 def test_hsdp_and_block_layouts(tmp_path):
     run_distributed(_hsdp_worker, 4, str(tmp_path))
+
+
+def _hsdp_balance_worker(tmp: str, shape):
+    """HSDP on a ``shape`` = (replicas, shards) mesh: every rank writes about
+    the same bytes (the replicas split each box by rows), and the snapshot
+    restores bitwise into the same mesh and into a 1-D FSDP mesh."""
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import Replicate, Shard, distribute_tensor
+
+    from hipsnapshot import Snapshot, StateDict
+    from hipsnapshot.snapshot import TakeStats
+
+    mesh = init_device_mesh("cpu", tuple(shape), mesh_dim_names=("rep", "shard"))
+    gen = torch.Generator().manual_seed(7)
+    full = {f"w{i}": torch.randn(2048 + 8 * i, 512, generator=gen) for i in range(6)}
+    full.update({f"norm{i}": torch.randn(512, generator=gen) for i in range(4)})
+    full["emb"] = torch.randn(4099, 256, generator=gen).to(torch.bfloat16)
+    dts = {k: distribute_tensor(v, mesh, [Replicate(), Shard(0)]) for k, v in full.items()}
+    Snapshot.take(f"{tmp}/hsdp", {"m": StateDict(**dts)})
+    written = [None] * dist.get_world_size()
+    dist.all_gather_object(written, TakeStats.last["bytes"])
+    total = sum(v.numel() * v.element_size() for v in full.values())
+    assert abs(sum(written) - total) <= 0.01 * total, (written, total)
+    mean = sum(written) / len(written)
+    assert max(written) / mean <= 1.10, written
+    # every element saved exactly once
+    man = Snapshot(f"{tmp}/hsdp").get_manifest()
+    for k, v in full.items():
+        cover = torch.zeros(v.shape, dtype=torch.int32)
+        for mk, e in man.items():
+            if mk.endswith(f"/m/{k}"):
+                for s in e.shards:
+                    cover[tuple(slice(o, o + z) for o, z in zip(s.offsets, s.sizes))] += 1
+        assert bool((cover == 1).all()), k
+    same = {k: distribute_tensor(torch.zeros_like(v), mesh, [Replicate(), Shard(0)])
+            for k, v in full.items()}
+    Snapshot(f"{tmp}/hsdp").restore({"m": StateDict(**same)})
+    m1 = init_device_mesh("cpu", (dist.get_world_size(),))
+    flat = {k: distribute_tensor(torch.zeros_like(v), m1, [Shard(0)]) for k, v in full.items()}
+    Snapshot(f"{tmp}/hsdp").restore({"m": StateDict(**flat)})
+    for k, v in full.items():
+        assert torch.equal(same[k].full_tensor(), v), k
+        assert torch.equal(flat[k].full_tensor(), v), k
+
+
+@pytest.mark.multiproc
+@pytest.mark.parametrize("shape", [(2, 2), (2, 4)], ids=["2x2", "2x4"])
+def test_hsdp_write_load_is_balanced(tmp_path, shape):
+    run_distributed(_hsdp_balance_worker, shape[0] * shape[1], str(tmp_path), list(shape),
+                    timeout=300)

@@ -380,3 +380,68 @@ def _poison_reshard_worker(root):
             Snapshot(path).read_object("0/sd/x", obj_out=out, memory_budget_bytes=2048)
             torch.cuda.synchronize()
             assert torch.equal(out, full), (comp, byte, "read_object")
+
+
+def test_pools_trimmed_to_zero_four_processes_bitwise(gpu, tmp_path):
+    """The round-5 failure: 4 processes restoring on one GPU with the restore
+    pools freed after EVERY job (and ``release_restore_memory()`` between
+    reads) got wrong bytes and hipErrorIllegalAddress faults, because a freed
+    hipMalloc / hipExtMallocWithFlags address came back as the other kind of
+    block and kernels wrote through its old translation
+    (profiles/r6/trim/).  The pools now allocate through the VMM hooks, whose
+    freed addresses are never handed out again: every read is bitwise, with
+    and without ``verify``, whole and in 2 KiB tiles."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    import test_dtensor_2d as T
+
+    from hipsnapshot.utils.test_utils import run_distributed
+
+    run_distributed(T._save_worker, 4, str(tmp_path), "cuda:0", timeout=600)
+    run_distributed(_trim_zero_worker, 4, str(tmp_path), timeout=600)
+
+
+def _trim_zero_worker(tmp):
+    from hipsnapshot import release_restore_memory
+    from hipsnapshot.knobs import override_tuning
+    from hipsnapshot.ops import native
+
+    ref = torch.load(f"{tmp}/ref.pt", weights_only=True)
+    names = ("layers.0.attention.wq.weight", "layers.1.feed_forward.w2.weight",
+             "tok_embeddings.weight")
+    with override_tuning(restore_keep_bytes=0):
+        for it in range(4):
+            for name in names:
+                for budget in (None, 2048):
+                    out = torch.zeros_like(ref[f"m/{name}"]).to("cuda:0")
+                    Snapshot(f"{tmp}/async").read_object(f"0/model/{name}", obj_out=out,
+                                                         memory_budget_bytes=budget,
+                                                         verify=bool(it % 2))
+                    torch.cuda.synchronize()
+                    assert torch.equal(out.cpu(), ref[f"m/{name}"]), (it, name, budget)
+            release_restore_memory()
+    assert native.require_gpu_lib().hsg_rt_vmm_retired_bytes() > 0  # the pools were freed
+
+
+def test_vmm_blocks_survive_mixed_churn_across_processes(gpu, tmp_path):
+    """The hook the pools allocate through, outside the engine: 4 processes
+    allocate an uncached and a plain block, SDMA-upload a tagged pattern,
+    copy it through both with the copy kernel, read it back and free both,
+    300 times each.  With hipMalloc / hipExtMallocWithFlags the same loop
+    returned wrong or foreign words in 117 of 1200 iterations (466 of 600 in
+    one process); with the VMM blocks none (scripts/probes/pool_churn_mp.py,
+    profiles/r6/trim/)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "churn.json"
+    proc = subprocess.run([sys.executable, os.path.join(root, "scripts/probes/pool_churn_mp.py"),
+                           "--mode", "both", "--alloc", "vmm", "--procs", "4", "--iters", "300",
+                           "--out", str(out)], capture_output=True, text=True, timeout=300)
+    assert proc.returncode == 0, proc.stderr[-2000:]
+    res = json.load(open(out))
+    assert res["errors"] == 0 and res["bad_iters"] == 0, json.dumps(res)[:2000]
+    assert all(r["iters"] == 300 for r in res["ranks"])

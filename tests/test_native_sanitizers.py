@@ -86,7 +86,7 @@ def _build_engine_stress(tmp_path, san, sources=None):
 
 
 @pytest.mark.parametrize("mode,rounds", [("restore", 24), ("drain", 24), ("ringwrap", 1),
-                                         ("fmap", 10)])
+                                         ("fmap", 10), ("restore-trim", 16)])
 @pytest.mark.parametrize("san", ["thread", "address,undefined"])
 def test_native_engines_under_sanitizer(tmp_path, san, mode, rounds):
     """csrc/hsrestore.cpp and csrc/hsdrain.cpp (host code: readers,
@@ -94,8 +94,10 @@ def test_native_engines_under_sanitizer(tmp_path, san, mode, rounds):
     writers and parked writers) driven by tests/native/engine_stress.cpp over
     CPU stand-ins of every device hook (random completion delays, injected
     upload / copy / file / memory failures, budgets below one blob, the
-    c026ee7 ring wrap) and csrc/hsfmap.cpp (the file-mapping cache under
-    concurrent map / commit / abandon / replace / prune / evict)."""
+    c026ee7 ring wrap), concurrent restores on the shared pools while
+    another thread frees every idle block (restore-trim), and csrc/hsfmap.cpp
+    (the file-mapping cache under concurrent map / commit / abandon /
+    replace / prune / evict)."""
     exe = _build_engine_stress(tmp_path, san)
     if san == "thread":
         rounds = max(1, rounds // 2)  # ~5x slower under TSan
