@@ -305,11 +305,12 @@ def main() -> None:
     gpu_index = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(gpu_index)
     dev = torch.device("cuda", gpu_index)
+    numa_rep = None
     if not args.no_numa_bind:
         # before any I/O-engine / staging thread exists: they inherit it
         from hipsnapshot.utils.affinity import bind_to_gpu_numa
 
-        rep = bind_to_gpu_numa(gpu_index)
+        rep = numa_rep = bind_to_gpu_numa(gpu_index)
         if local_rank == 0:
             print(f"numa: {rep}", file=sys.stderr, flush=True)
     if args.backend == "nccl":
@@ -389,6 +390,14 @@ def main() -> None:
     dist.all_gather_object(per_rank, (statistics.mean(my_step_s) * 1e3, my_stored))
     rank_take_ms = sorted(r[0] for r in per_rank)
     rank_stored = [r[1] for r in per_rank]
+    # one more (untimed) take with its phases captured on every rank: what a
+    # multi-GPU curve needs to be attributed without another run
+    from hipsnapshot.utils import rank_diag
+
+    barrier_sync()
+    my_diag = rank_diag.measure(lambda: Snapshot.take(path, app_state, storage_options=opts,
+                                                      compression=args.compression))
+    my_diag["numa"] = numa_rep
 
     # async_take: time-to-unblock
     # time_to_unblock: host time until async_take returns.  The HBM freeze
@@ -443,6 +452,9 @@ def main() -> None:
         log(f"async {i}: unblock {unblock[-1]:.1f} ms (stream free at {unblock_gpu[-1]:.1f} ms, "
             f"freeze kernel {freeze[-1]:.2f} ms), total {drain[-1]:.1f} ms")
 
+    from hipsnapshot import memory_held
+
+    held_after_takes = memory_held(gpu_index)  # between checkpoints: what stays
     stored = 0
     if rank == 0:
         for r, _, fs in os.walk(path):
@@ -489,6 +501,7 @@ def main() -> None:
         restore_each = [round(total_bytes / t / 1e9, 2) for t in times]
         # the first restore plans from scratch, later ones of the same
         # snapshot into the same tensors reuse its plan (engine/restore_cache.py)
+        my_diag["native_restore_stats"] = dict(native_restore.last_stats)
         restore_info = {"restore_cold_GBps": restore_each[0],
                         "restore_plan_cache": {k: restore_cache.stats[k] - rc0.get(k, 0)
                                                for k in ("hits", "misses", "stores")},
@@ -728,6 +741,9 @@ def main() -> None:
             shutil.rmtree(dpath, ignore_errors=True)
         dist.barrier()
 
+    all_diag = [None] * world
+    dist.all_gather_object(all_diag, my_diag)
+    held_after_restore = memory_held(gpu_index)
     if rank == 0:
         out = {
             "metric": "checkpoint save GB/s + time-to-unblock, Llama-3-8B FSDP",
@@ -800,6 +816,16 @@ def main() -> None:
                              "no published number for 2/4 GPUs",
             **ddp_llama,
             **elastic,
+            # what rank 0 holds between checkpoints (engine/memory.py): after
+            # the async takes (arena, pools, pinned) and after the restores
+            "hbm_held_between_takes_bytes": held_after_takes["hbm_held_bytes"],
+            "pinned_held_bytes": held_after_takes["pinned_held_bytes"],
+            "memory_held_after_takes": held_after_takes,
+            "memory_held_after_restore": held_after_restore,
+            # one untimed take per rank with its phases captured
+            # (utils/rank_diag.py), and the one-line skew summary
+            "rank_skew": rank_diag.skew(all_diag),
+            "rank_diag": all_diag,
         }
         print(json.dumps(out), flush=True)
     dist.barrier()

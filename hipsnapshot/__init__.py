@@ -10,6 +10,8 @@ import sys as _sys
 import torch as _torch  # noqa: F401  (load torch's HIP runtime before our .so)
 
 from .engine.hbm_staging import release_hbm_arena
+from .engine.memory import held as memory_held
+from .engine.memory import release_idle as release_snapshot_memory
 from .engine.native_restore import release_restore_memory
 from .storage.fs import release_file_mappings
 from .snapshot import PendingSnapshot, Snapshot
@@ -44,6 +46,8 @@ __all__ = [
     "AppState",
     "release_hbm_arena",
     "release_restore_memory",
+    "release_snapshot_memory",
+    "memory_held",
     "release_file_mappings",
     "__version__",
     "__hipsnapshot_version__",

@@ -1779,6 +1779,12 @@ void* hsg_uncached_acquire(int dev, uint64_t nbytes) {
   return p;
 }
 
+// Bytes the uncached pool holds (idle + in use, every device).
+uint64_t hsg_uncached_bytes() {
+  std::lock_guard<std::mutex> g(g_upool.mu);
+  return g_upool.cached_bytes;
+}
+
 int hsg_uncached_release(void* p) {
   std::lock_guard<std::mutex> g(g_upool.mu);
   auto it = g_upool.live.find(p);

@@ -166,6 +166,20 @@ struct DevPool {
     live.erase(it);
   }
 
+  // bytes of `dev`'s blocks (-1: every device): idle ones, ones in use
+  void bytes(int dev, uint64_t* idle_out, uint64_t* live_out) {
+    std::lock_guard<std::mutex> g(mu);
+    uint64_t idle = 0, used = 0;
+    for (auto& dv : free_blocks) {
+      if (dev >= 0 && dv.first != dev) continue;
+      for (auto& kv : dv.second) idle += kv.first;
+    }
+    for (auto& kv : live)
+      if (dev < 0 || kv.second.first == dev) used += kv.second.second;
+    *idle_out = idle;
+    *live_out = used;
+  }
+
   // idle blocks of `dev`: (address, bytes) pairs, at most `max`
   int idle(int dev, uint64_t* ptrs, uint64_t* sizes, int max) {
     std::lock_guard<std::mutex> g(mu);
@@ -1057,6 +1071,13 @@ uint64_t hsg_restore_trim(int dev, uint64_t keep) {
 int hsg_restore_idle_blocks(int dev, uint64_t* ptrs, uint64_t* sizes, int max) {
   const int n = g_upload_pool.idle(dev, ptrs, sizes, max);
   return n + g_scratch_pool.idle(dev, ptrs + n, sizes + n, max - n);
+}
+
+// Device bytes the restore pools hold on `dev` (-1: all devices): out[0..3] =
+// upload idle, upload in use, scratch idle, scratch in use.
+void hsg_restore_pool_bytes(int dev, uint64_t* out) {
+  g_upload_pool.bytes(dev, out, out + 1);
+  g_scratch_pool.bytes(dev, out + 2, out + 3);
 }
 
 // The same per pool: uncached upload blocks / plain scratch blocks.

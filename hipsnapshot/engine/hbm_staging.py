@@ -320,11 +320,16 @@ def is_kept(arena: torch.Tensor) -> bool:
 
 
 def arena_done(arenas) -> None:
-    """The drain of these arenas finished: a kept arena may be reused."""
+    """The drain of these arenas finished: a kept arena may be reused -- or
+    is dropped when the trainer's headroom fell below the reserve
+    (engine/memory.py)."""
+    from . import memory
+
     for a in arenas:
-        for k in _kept.values():
+        for dev, k in list(_kept.items()):
             if k[1] and a.data_ptr() == k[0].data_ptr():
                 k[1] = False
+                memory.settle_arena(dev)
 
 
 def release_hbm_arena() -> int:

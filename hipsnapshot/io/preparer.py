@@ -107,10 +107,12 @@ def _write_sharded(obj, path, is_async, prepare_func, serializer, max_chunk, max
 
 
 def _write_tensor(obj, path, is_async, prepare_func, serializer, max_chunk, max_shard):
-    if obj.numel() * obj.element_size() > (max_chunk or get_max_chunk_size_bytes()):
+    max_chunk = max_chunk or get_max_chunk_size_bytes()
+    if obj.numel() * obj.element_size() > max_chunk:
         return ChunkedTensorIOPreparer.prepare_write(
             storage_path=path, tensor=obj,
-            chunking_instruction=ChunkedTensorIOPreparer.chunk_tensor(obj),
+            chunking_instruction=ChunkedTensorIOPreparer.chunk_tensor(obj,
+                                                                      chunk_sz_bytes=max_chunk),
             is_async_snapshot=is_async, _tensor_prepare_func=prepare_func,
             serializer=serializer)
     return TensorIOPreparer.prepare_write(

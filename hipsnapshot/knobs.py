@@ -201,7 +201,13 @@ class _Tuning:
     # async takes drain the frozen device state raw: the encoder on the CUs
     # beside a training step cost +30 % step time (profiles/overlap_iso/)
     async_device_codec = "raw"
-    hbm_arena_keep = True      # release_hbm_arena() frees the async-take arena
+    # the async-take arena is kept for the next take while the device keeps
+    # HBM_STAGING_RESERVE_BYTES of headroom (engine/memory.py);
+    # release_hbm_arena() frees it on request
+    hbm_arena_keep = True
+    # idle pinned pool blocks are unregistered after this long without a
+    # snapshot operation (0: never)
+    pinned_idle_trim_s = 300.0
     # -- native drain (csrc/hsdrain.cpp) -----------------------------------------
     # 16 slots of 64 MiB drain the 16 GB Llama-3-8B arena at the PCIe rate
     # (profiles/r3/s2/drain_sizing/)
@@ -250,6 +256,9 @@ class _Tuning:
     # is written as R row ranges, one per replica; smaller boxes go whole to
     # one replica chosen by a hash of their position (io/sharded.py)
     replica_split_min_bytes = 1 << 20
+    # replicated (DDP) tensors are chunked so each rank's share is >= this
+    # many partitioner units (parallel/partitioner.py replicated_chunk_bytes)
+    replicated_units_per_rank = 16
     rebalance_host = False     # let the rebalancer move host blobs too (gloo tests)
     rebalance_min_gain = 0.1
     # -- UVM ------------------------------------------------------------------------------
@@ -559,7 +568,9 @@ def use_gpu_gather_for_slabs() -> bool:
 
 
 def pinned_pool_max_bytes() -> int:
-    """Cap of the pinned host pool (bytes kept registered across takes)."""
+    """Cap of the pinned host pool (bytes kept registered across takes)
+    until the first snapshot operation; from then on, unless this knob is
+    set, the rank's host memory budget (engine/memory.py pinned_cap_bytes)."""
     return _get_int("PINNED_POOL_MAX_BYTES", 64 << 30)
 
 

@@ -291,6 +291,8 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_void_p, P(c_int), c_char_p, P(ctypes.c_double), P(c_uint64), P(c_uint64)])
         _declare(lib, "hsg_restore_trim", c_uint64, [c_int, c_uint64])
         _declare(lib, "hsg_restore_trim_pools", c_uint64, [c_int, c_uint64, c_uint64])
+        _declare(lib, "hsg_restore_pool_bytes", None, [c_int, P(c_uint64)])
+        _declare(lib, "hsg_uncached_bytes", c_uint64, [])
         _declare(lib, "hsg_poison_idle_pools", c_int, [c_int, c_int])
         _declare(lib, "hsg_restore_prewarm", c_int,
                  [c_int, c_uint64, c_uint64, c_uint64, c_int, c_uint64])
@@ -1103,6 +1105,18 @@ def poison_idle_pools(dev: int, byte: int) -> int:
     r = int(require_gpu_lib().hsg_poison_idle_pools(dev, byte))
     _check(min(r, 0), "hsg_poison_idle_pools")
     return r
+
+
+def restore_pool_bytes(dev: int = -1) -> Dict[str, int]:
+    """Device bytes the native restore's pools hold (``dev`` -1: all)."""
+    out = (c_uint64 * 4)()
+    require_gpu_lib().hsg_restore_pool_bytes(dev, out)
+    return {"upload_idle": int(out[0]), "upload_live": int(out[1]),
+            "scratch_idle": int(out[2]), "scratch_live": int(out[3])}
+
+
+def uncached_pool_bytes() -> int:
+    return int(require_gpu_lib().hsg_uncached_bytes())
 
 
 def restore_trim(dev: int, keep_bytes: int) -> int:

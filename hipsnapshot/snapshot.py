@@ -52,7 +52,7 @@ import torch.distributed as dist
 from torch.nn.parallel import DistributedDataParallel as DDP
 
 from . import knobs
-from .engine import native_restore, restore_cache, staging
+from .engine import memory, native_restore, restore_cache, staging
 from .engine.scheduler import (
     PendingIOWork,
     get_process_memory_budget_bytes,
@@ -79,7 +79,11 @@ from .io_types import ReadIO, ReadReq, StoragePlugin, WriteIO, WriteReq, run_syn
 from .ops import checksum, native
 from .parallel.comm import Comm
 from .parallel.elasticity import get_manifest_for_rank, handle_sharded_tensor_elasticity
-from .parallel.partitioner import consolidate_replicated_entries, partition_write_reqs
+from .parallel.partitioner import (
+    consolidate_replicated_entries,
+    partition_write_reqs,
+    replicated_chunk_bytes,
+)
 from .parallel.store import LinearBarrier, existing_store, get_or_create_store
 from .stateful import AppState, RNGState, Stateful
 from .storage.registry import url_to_storage_plugin_in_event_loop
@@ -383,9 +387,13 @@ class Snapshot:
         bf16, ~0.84x for fp32); default from ``HIPSNAPSHOT_COMPRESSION`` ("none").
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.take")
-        with paused_gc(plan_gc=False):
-            return cls._take(path, app_state, pg, replicated, storage_options,
-                             _custom_tensor_prepare_func, quantize, compression)
+        memory.op_begin(pg)
+        try:
+            with paused_gc(plan_gc=False):
+                return cls._take(path, app_state, pg, replicated, storage_options,
+                                 _custom_tensor_prepare_func, quantize, compression)
+        finally:
+            memory.op_end()
 
     @classmethod
     def _take(cls, path, app_state, pg, replicated, storage_options,
@@ -449,9 +457,13 @@ class Snapshot:
 
         note_caller_cpu()  # the drain's threads keep off this thread's core
         deferred_gc: list = []
-        with paused_gc(deferred_gc):
-            pending = cls._async_take(path, app_state, pg, replicated, storage_options,
-                                      _custom_tensor_prepare_func, quantize, compression)
+        memory.op_begin(pg)
+        try:
+            with paused_gc(deferred_gc):
+                pending = cls._async_take(path, app_state, pg, replicated, storage_options,
+                                          _custom_tensor_prepare_func, quantize, compression)
+        finally:
+            memory.op_end()
         # a new plan's one full GC pass runs in the commit thread after the
         # drain, not on the unblock path (utils/tracing.paused_gc)
         pending._gc_after = bool(deferred_gc)
@@ -636,6 +648,13 @@ class Snapshot:
         path_reqs: Dict[str, List[WriteReq]] = {}
         primitives: Dict[str, PrimitiveEntry] = {}
         max_chunk, max_shard = knobs.get_max_chunk_size_bytes(), knobs.get_max_shard_size_bytes()
+        rep_chunk = max_chunk
+        if rep_paths and comm.get_world_size() > 1:
+            # replicated tensors in units small enough to balance the ranks
+            rep_chunk = replicated_chunk_bytes(
+                sum(v.numel() * v.element_size() for k, v in to_plan.items()
+                    if k in rep_paths and isinstance(v, torch.Tensor) and not is_sharded(v)),
+                comm.get_world_size(), max_chunk, knobs.TUNING.replicated_units_per_rank)
         with staging.plan_scope():
             for logical, obj in to_plan.items():
                 ser = None
@@ -647,7 +666,8 @@ class Snapshot:
                     _tensor_prepare_func=(
                         (lambda t, tracing, _p=logical: prepare_func(_p, t, tracing))
                         if prepare_func is not None else None),
-                    serializer=ser, max_chunk_size_bytes=max_chunk,
+                    serializer=ser,
+                    max_chunk_size_bytes=rep_chunk if logical in rep_paths else max_chunk,
                     max_shard_size_bytes=max_shard)
                 if isinstance(entry, PrimitiveEntry):
                     primitives[logical] = entry
@@ -779,8 +799,15 @@ class Snapshot:
         recorded (engine/blob_verify.py) and raise ``CorruptBlobError``
         naming the first blob that does not match."""
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.restore")
-        with paused_gc():
-            self._restore(app_state, verify)
+        memory.op_begin(self.pg)
+        try:
+            with paused_gc():
+                self._restore(app_state, verify)
+        finally:
+            memory.op_end()
+            # the pools keep their rings for the next restore only while the
+            # trainer keeps its headroom (engine/memory.py)
+            memory.settle_restore_pools()
 
     def _restore(self, app_state: AppState, verify: bool = False) -> None:
         self._validate_app_state(app_state)
@@ -936,6 +963,15 @@ class Snapshot:
         global shape (the reference requires an ``obj_out`` there).
         """
         torch._C._log_api_usage_once("hipsnapshot.Snapshot.read_object")
+        memory.op_begin(self.pg)
+        try:
+            return self._read_object(path, obj_out, memory_budget_bytes, verify)
+        finally:
+            memory.op_end()
+            memory.settle_restore_pools()
+
+    def _read_object(self, path: str, obj_out: Optional[T], memory_budget_bytes: Optional[int],
+                     verify: bool) -> T:
         rank_str, unranked = path.split("/", 1)
         manifest, merged = get_manifest_for_rank(self.metadata, int(rank_str))
         if unranked not in merged and unranked not in manifest:

@@ -111,6 +111,23 @@ class Timeline:
         self.events: list = []
         self.t0 = time.perf_counter()
         self.counts: dict = {}
+        self._captured: Optional[list] = None
+
+    @contextlib.contextmanager
+    def capture(self):
+        """Record spans in memory for the duration, without writing trace
+        files: yields the list the events land in (``bench.py``'s per-rank
+        phase split)."""
+        saved = (self.prefix, self.events, self._captured)
+        out: list = []
+        self.prefix = self.prefix or "<capture>"
+        self.events = []
+        self._captured = out
+        try:
+            yield out
+        finally:
+            out.extend(self.events)
+            self.prefix, self.events, self._captured = saved
 
     @property
     def enabled(self) -> bool:
@@ -138,6 +155,10 @@ class Timeline:
             self.add(name, cat, t, time.perf_counter(), **args)
 
     def dump(self, op: str, rank: int) -> Optional[str]:
+        if self._captured is not None:
+            self._captured.extend(self.events)
+            self.events = []
+            return None
         if self.prefix is None or not self.events:
             return None
         import json

@@ -129,6 +129,8 @@ def worker(r, args, q):
         got = dest[:n].cpu().numpy().view(np.uint32)
         checks["T"] = classify(np, got, want, r, k)
         res["iters"] += 1
+        res.setdefault("log", []).append([k, hex(u), hex(s), sorted(kk for kk, v in checks.items()
+                                                                   if v)])
         if any(v is not None for v in checks.values()):
             res["bad_iters"] += 1
             if len(res["details"]) < 20:
@@ -141,6 +143,25 @@ def worker(r, args, q):
             free(p)
     res["seconds"] = round(time.time() - t0, 2)
     q.put(res)
+
+
+def previous_kind_table(ranks):
+    """Per block role (U uncached / S plain): how many iterations had a bad
+    check, split by what the block's address was last allocated as in this
+    process (same kind, the other kind, never).  A stale translation of a
+    re-used address shows as bad iterations in the "other" rows only."""
+    table = {}
+    for r in ranks:
+        last = {}
+        for k, u, s, bad in r.get("log", []):
+            for role, addr, kind in (("U", u, 1), ("S", s, 0)):
+                prev = last.get(addr)
+                key = f"{role}:{'never' if prev is None else 'same' if prev == kind else 'other'}"
+                row = table.setdefault(key, [0, 0])
+                row[0] += 1
+                row[1] += int(bool(bad))
+            last[u], last[s] = 1, 0
+    return {k: {"iters": v[0], "bad": v[1]} for k, v in sorted(table.items())}
 
 
 def main():
@@ -168,6 +189,7 @@ def main():
                "errors": sum(len(o["errors"]) for o in out),
                "exitcodes": [p.exitcode for p in ps],
                "ranks": sorted(out, key=lambda o: o["rank"])}
+    summary["by_previous_kind"] = previous_kind_table(summary["ranks"])
     print(json.dumps({k: v for k, v in summary.items() if k != "ranks"}), flush=True)
     if args.out:
         with open(args.out, "w") as f:
