@@ -13,7 +13,6 @@ from .engine.hbm_staging import release_hbm_arena
 from .engine.memory import held as memory_held
 from .engine.memory import release_idle as release_snapshot_memory
 from .engine.native_restore import release_restore_memory
-from .storage.fs import release_file_mappings
 from .snapshot import PendingSnapshot, Snapshot
 from .stateful import AppState, RNGState, StateDict, Stateful
 from .version import __hipsnapshot_version__, __version__
@@ -48,7 +47,6 @@ __all__ = [
     "release_restore_memory",
     "release_snapshot_memory",
     "memory_held",
-    "release_file_mappings",
     "__version__",
     "__hipsnapshot_version__",
 ]

@@ -56,8 +56,7 @@ def build_hsgpu(force: bool = False) -> str:
     # in hshost.hip); hipcc builds them as plain C++ into the same library
     srcs = [os.path.join(CSRC, "hsgpu.hip"), os.path.join(CSRC, "hsz.hip"),
             os.path.join(CSRC, "hsdma.hip"), os.path.join(CSRC, "hshost.hip"),
-            os.path.join(CSRC, "hsdrain.cpp"), os.path.join(CSRC, "hsrestore.cpp"),
-            os.path.join(CSRC, "hsfmap.cpp")]
+            os.path.join(CSRC, "hsdrain.cpp"), os.path.join(CSRC, "hsrestore.cpp")]
     if force or _stale(HSGPU_SO, srcs):
         hipcc = os.path.join(ROCM, "bin", "hipcc")
         if not os.path.exists(hipcc):

@@ -29,16 +29,13 @@ void note(const char* what, hipError_t e) {
   snprintf(g_rt_err, sizeof(g_rt_err), "%s: %s (%d)", what, hipGetErrorName(e), int(e));
 }
 
-// HIPSNAPSHOT_POOL_TRACE=1: one stderr line per device allocation and free of
-// the engines' pools (pid, microseconds, address, bytes, kind), so a failing
+// Pool trace (hsg_rt_set_trace(1), from Python native.set_pool_trace): one
+// stderr line per device allocation and free of the engines' pools and per
+// restore upload (pid, microseconds, address, bytes, kind), so a failing
 // multi-process restore can be laid against which process held which range.
-int trace_on() {
-  static const int on = [] {
-    const char* v = getenv("HIPSNAPSHOT_POOL_TRACE");
-    return v != nullptr && v[0] != '\0' && v[0] != '0';
-  }();
-  return on;
-}
+std::atomic<int> g_trace{0};
+
+int trace_on() { return g_trace.load(std::memory_order_relaxed); }
 
 uint64_t now_us() {
   return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::microseconds>(
@@ -52,6 +49,8 @@ extern "C" {
 const char* hsg_rt_last_error() { return g_rt_err; }
 
 int hsg_rt_trace_on() { return trace_on(); }
+
+void hsg_rt_set_trace(int on) { g_trace.store(on ? 1 : 0); }
 
 void hsg_rt_trace(const char* what, const void* p, uint64_t n, int kind) {
   if (!trace_on()) return;
@@ -228,24 +227,6 @@ int hsg_rt_stream_sync(void* stream) {
   if (e == hipSuccess) return 0;
   note("hipStreamSynchronize", e);
   return -1;
-}
-
-// Register / unregister host memory (a file mapping: csrc/hsfmap.cpp) so the
-// SDMA engines can write it.
-int hsg_rt_host_register(void* p, uint64_t n) {
-  if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) {
-    (void)hipGetLastError();
-    return -1;
-  }
-  return 0;
-}
-
-int hsg_rt_host_unregister(void* p) {
-  if (hipHostUnregister(p) != hipSuccess) {
-    (void)hipGetLastError();
-    return -1;
-  }
-  return 0;
 }
 
 // Blocking device -> host copy of n bytes (small result arrays).

@@ -322,8 +322,7 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                 if failure:  # the snapshot is failing: do not start more writes
                     return
                 t_w = time.perf_counter()
-                await storage.write(WriteIO(path=wr.path, buf=buf.view, addr=buf.addr,
-                                            mapped=buf.mapped))
+                await storage.write(WriteIO(path=wr.path, buf=buf.view, addr=buf.addr))
                 timeline.add("write", "io", t_w, time.perf_counter(), path=wr.path,
                              bytes=buf.nbytes)
             stats.bytes_written += buf.nbytes
@@ -349,12 +348,9 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
 
     if pending and knobs.thread_staging_enabled() and \
             all(getattr(wr.buffer_stager, "thread_staging", False) for wr in pending):
-        # a storage that maps its files for the DMA engines (FSStoragePlugin)
-        mapper = getattr(storage, "mapped_dest", None) if knobs.TUNING.file_map else None
         try:
             await _stage_on_threads(pending, stage_threads, executor, gate, failure,
-                                    lambda wr, buf, cost, t_s: _staged(wr, buf, cost, t_s),
-                                    mapper)
+                                    lambda wr, buf, cost, t_s: _staged(wr, buf, cost, t_s))
         except BaseException:
             gate.unsubscribe(wake)
             # writes already issued keep their buffers until the engine is done
@@ -435,8 +431,7 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
 
 
 async def _stage_on_threads(pending: deque, nthreads: int, executor: ThreadPoolExecutor,
-                            gate: MemoryGate, failure: List[BaseException], on_staged,
-                            mapper: Optional[Callable[[str, int], Any]] = None) -> None:
+                            gate: MemoryGate, failure: List[BaseException], on_staged) -> None:
     """Stage ``pending`` on ``nthreads`` long-running executor workers.
 
     Each worker takes the next request the memory gate admits, stages it
@@ -445,14 +440,9 @@ async def _stage_on_threads(pending: deque, nthreads: int, executor: ThreadPoolE
     staged buffer to the writer goes through the event loop.  With one
     round trip through the loop per request instead, the DMA engine sat idle
     for 0.7-1.4 ms between blobs whenever all workers waited for the loop
-    (17 % of a take of one rank's 8-GPU share, profiles/rank_share/).
-
-    ``mapper(path, nbytes)``: the storage's GPU-writable mapping of the blob's
-    file, offered to the stager as the blob's destination
-    (``staging.blob_destination``)."""
+    (17 % of a take of one rank's 8-GPU share, profiles/rank_share/)."""
     loop = asyncio.get_running_loop()
     cond = gate.cond
-    from .staging import blob_destination
 
     # The first blob is staged alone: with every worker starting at once they
     # share the GIL and the GPU's encoders, and the first DMA -- the start of
@@ -480,11 +470,7 @@ async def _stage_on_threads(pending: deque, nthreads: int, executor: ThreadPoolE
             t_s = time.perf_counter()
             timeline.add("admit", "stage", t_w, t_s)
             try:
-                if mapper is None:
-                    buf = as_staged(wr.buffer_stager.stage_buffer_sync())
-                else:
-                    with blob_destination(functools.partial(mapper, wr.path)):
-                        buf = as_staged(wr.buffer_stager.stage_buffer_sync())
+                buf = as_staged(wr.buffer_stager.stage_buffer_sync())
             except BaseException as e:  # noqa: BLE001 - reported by the caller
                 head.set()
                 with cond:

@@ -211,36 +211,8 @@ def _pinned_staged(nbytes: int) -> Tuple[native.PinnedBuffer, StagedBuffer]:
     return pb, StagedBuffer(pb.view, pb.ptr, release=pb.release, keepalive=pb)
 
 
-_dest = threading.local()
-
-
-@contextmanager
-def blob_destination(provider: Optional[Callable[[int], Optional[StagedBuffer]]]) -> Iterator[None]:
-    """While one blob is staged on this thread, ``provider(nbytes)`` may hand
-    out the host destination of its bytes -- a GPU-writable mapping of the
-    file the blob goes to (``FSStoragePlugin.mapped_dest``) -- in place of a
-    pinned block.  Asked at most once, by the copy that produces the blob's
-    final bytes (``_dest_staged``)."""
-    prev = getattr(_dest, "fn", None)
-    _dest.fn = provider
-    try:
-        yield
-    finally:
-        _dest.fn = prev
-
-
 def _dest_staged(nbytes: int) -> StagedBuffer:
-    """The final host buffer of a blob of ``nbytes`` that a DMA engine fills:
-    the destination file's own pages when the storage offers them
-    (``blob_destination``), else a pinned block."""
-    fn = getattr(_dest, "fn", None)
-    if fn is not None and nbytes:
-        _dest.fn = None
-        t_s = time.perf_counter()
-        staged = fn(nbytes)
-        if staged is not None:
-            timeline.add("fmap", "stage", t_s, time.perf_counter(), bytes=nbytes)
-            return staged
+    """The final host buffer of a blob of ``nbytes`` that a DMA engine fills."""
     return _pinned_staged(nbytes)[1]
 
 

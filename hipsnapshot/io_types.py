@@ -56,10 +56,6 @@ class StagedBuffer:
         # set when the bytes are still arriving (asynchronous SDMA copy):
         # call it (blocking, once) before reading the buffer
         self.ready: Optional[Callable[[], None]] = None
-        # the bytes ARE the destination file's pages (a GPU-writable mapping
-        # the storage plugin handed out, ``mapped_dest``): the plugin's write
-        # only has to commit them
-        self.mapped: Any = None
 
     @property
     def nbytes(self) -> int:
@@ -211,8 +207,6 @@ class WriteIO:
     path: str
     buf: BufferType
     addr: Optional[int] = None
-    # ``StagedBuffer.mapped`` of a buffer the plugin's ``mapped_dest`` handed out
-    mapped: Any = None
 
 
 @dataclass

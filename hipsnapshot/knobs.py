@@ -241,16 +241,6 @@ class _Tuning:
     # the other processes' uncached SDMA targets.  ``release_restore_memory()``
     # frees them on request.
     restore_keep_bytes = (2 << 30) + (256 << 20)
-    # -- file mappings (csrc/hsfmap.cpp) ------------------------------------------------
-    # a blocking take that rewrites an existing file of the blob's exact size
-    # DMAs into the file's page-cache pages (no pinned copy, no pwrite copy).
-    # Off: a reused mapping saves ~85 ms of CPU per GiB (commit 36 ms vs
-    # pwrite 720 ms per 8 GiB), but registering the mappings inside a process
-    # that holds the 8B model took 44.6 s of acquire time for 10.7 GB and
-    # stalled its SDMA copies for seconds (profiles/r5/filemap/): the headline
-    # fell from 80.5 to 43.9 GB/s.
-    file_map = False
-    file_map_max_bytes = 64 << 30  # mapped (pinned page-cache) bytes kept per process
     # -- distributed -------------------------------------------------------------------
     # a DTensor box replicated R ways (HSDP, DTensor DDP) at least this large
     # is written as R row ranges, one per replica; smaller boxes go whole to

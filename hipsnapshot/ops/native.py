@@ -319,6 +319,7 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_rt_dev_free", None, [c_void_p])
         _declare(lib, "hsg_rt_memcpy_d2h", c_int, [c_void_p, c_void_p, c_uint64])
         _declare(lib, "hsg_rt_last_error", c_char_p, [])
+        _declare(lib, "hsg_rt_set_trace", None, [c_int])
         _declare(lib, "hsg_rt_vmm_alloc", c_void_p, [c_int, c_uint64, c_int])
         _declare(lib, "hsg_rt_vmm_free", c_int, [c_void_p])
         _declare(lib, "hsg_rt_vmm_retired_bytes", c_uint64, [])
@@ -327,13 +328,6 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_sdma_d2h_submit", c_int,
                  [c_int, c_void_p, c_void_p, c_uint64, c_void_p, ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_sdma_wait", c_int, [c_uint64])
-        _declare(lib, "hsg_fmap_acquire", c_void_p, [c_char_p, c_uint64])
-        _declare(lib, "hsg_fmap_commit", c_int, [c_void_p, c_int])
-        _declare(lib, "hsg_fmap_abandon", None, [c_void_p])
-        _declare(lib, "hsg_fmap_release", c_uint64, [c_int])
-        _declare(lib, "hsg_fmap_prune", c_uint64, [])
-        _declare(lib, "hsg_fmap_set_budget", None, [c_uint64])
-        _declare(lib, "hsg_fmap_stats", None, [P(c_uint64)])
         _declare(lib, "hsg_hsz_meta_bytes", c_uint64, [ctypes.c_uint32])
         _declare(lib, "hsg_hsz_encode", c_int,
                  [c_int, c_void_p, c_uint64, c_int, ctypes.c_uint32, c_void_p, c_void_p,
@@ -389,60 +383,6 @@ def prewarm_module(dev: int, pool) -> None:
     if lib is not None:
         pool.submit(lib.hsg_prewarm_module, dev)
 
-
-# ---- GPU-writable file mappings (csrc/hsfmap.cpp) -------------------------
-
-_fmap_budget_set = None
-
-
-def fmap_acquire(path: str, nbytes: int) -> Optional[int]:
-    """Address of a GPU-writable mapping of the existing file ``path`` when it
-    is exactly ``nbytes`` long (busy until ``fmap_commit`` / ``fmap_abandon``),
-    else None."""
-    global _fmap_budget_set
-    lib = require_gpu_lib()
-    from .. import knobs
-
-    budget = knobs.TUNING.file_map_max_bytes
-    if _fmap_budget_set != budget:
-        lib.hsg_fmap_set_budget(budget)
-        _fmap_budget_set = budget
-    p = lib.hsg_fmap_acquire(os.fsencode(path), nbytes)
-    return int(p) if p else None
-
-
-def fmap_commit(addr: int, sync: bool) -> int:
-    """Mark the mapping's pages dirty after the copy into it (optionally
-    fdatasync); 0 or -errno."""
-    return int(require_gpu_lib().hsg_fmap_commit(c_void_p(addr), 1 if sync else 0))
-
-
-def fmap_abandon(addr: int) -> None:
-    require_gpu_lib().hsg_fmap_abandon(c_void_p(addr))
-
-
-def fmap_prune() -> int:
-    """Drop idle mappings of files that were deleted, replaced or resized."""
-    lib = _load_hsgpu()
-    return int(lib.hsg_fmap_prune()) if lib is not None else 0
-
-
-def fmap_release(all_mappings: bool = False) -> int:
-    """Unmap idle mappings (``all_mappings``: every one; no copy may be in
-    flight).  Returns the bytes released."""
-    lib = _load_hsgpu()
-    return int(lib.hsg_fmap_release(1 if all_mappings else 0)) if lib is not None else 0
-
-
-def fmap_stats() -> dict:
-    lib = _load_hsgpu()
-    out = (c_uint64 * 6)()
-    if lib is not None:
-        lib.hsg_fmap_stats(out)
-    return dict(zip(("bytes", "mappings", "hits", "maps", "drops", "misses"), map(int, out)))
-
-
-# ---- pinned host memory ---------------------------------------------------
 
 class PinnedBuffer:
     """A page-locked host block from the native caching pool.
@@ -1113,6 +1053,13 @@ def restore_pool_bytes(dev: int = -1) -> Dict[str, int]:
     require_gpu_lib().hsg_restore_pool_bytes(dev, out)
     return {"upload_idle": int(out[0]), "upload_live": int(out[1]),
             "scratch_idle": int(out[2]), "scratch_live": int(out[3])}
+
+
+def set_pool_trace(on: bool) -> None:
+    """Log every engine pool allocation / free / restore upload to stderr
+    (csrc/hshost.hip ``hsg_rt_trace``): a debugging aid for multi-process
+    restores (scripts/probes/trim_probe_diag.py --trace)."""
+    require_gpu_lib().hsg_rt_set_trace(1 if on else 0)
 
 
 def uncached_pool_bytes() -> int:

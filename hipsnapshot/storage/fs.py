@@ -8,12 +8,6 @@ staged buffer's address (pinned pool block or CPU tensor storage) and reports
 completion through an eventfd watched by the asyncio loop, so no Python thread
 and no intermediate ``bytes`` copy is involved.
 
-Rewrites of an existing blob file (same path, same size -- a training job
-checkpointing into the same directory) skip the pinned bounce buffer: the
-stager DMAs straight into the file's page-cache pages, mapped and registered
-with the GPU (``mapped_dest``, ``csrc/hsfmap.cpp``), and ``write`` only marks
-the pages dirty (and fdatasyncs with ``fsync``): no CPU copy of the bytes.
-
 storage_options:
   ``direct_io`` (bool)  O_DIRECT for the 4 KiB-aligned body (default: knob)
   ``fsync`` (bool)      fdatasync each blob (default: knob)
@@ -53,9 +47,7 @@ class FSStoragePlugin(StoragePlugin):
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._pending: Dict[int, tuple] = {}
         self._native_ok = True
-        self._pruned = False
         self.bytes_written = 0
-        self.bytes_mapped = 0  # of bytes_written: DMA'd into mapped file pages
         self.bytes_read = 0
 
     @property
@@ -122,42 +114,9 @@ class FSStoragePlugin(StoragePlugin):
         """Root of the blobs for the native restore (engine/native_restore.py)."""
         return self.root
 
-    def mapped_dest(self, path: str, nbytes: int) -> Optional[StagedBuffer]:
-        """The page-cache pages of blob file ``path``, mapped and registered for
-        the DMA engines, when it exists with exactly ``nbytes`` bytes (a
-        rewrite); None otherwise (new file, other size, O_DIRECT, no GPU).
-        Called on staging threads; ``write`` commits the buffer."""
-        if self.direct_io or not _fmap_usable():
-            return None
-        if not self._pruned:
-            self._pruned = True
-            _native.fmap_prune()  # mappings of files deleted since the last take
-        addr = _native.fmap_acquire(self._abs(path), nbytes)
-        if addr is None:
-            return None
-        m = _MappedFile(addr)
-        mv = memoryview((ctypes.c_char * nbytes).from_address(addr)).cast("B")
-        sb = StagedBuffer(mv, addr, release=m.abandon)
-        sb.mapped = m
-        return sb
-
     # -- StoragePlugin -------------------------------------------------------
 
     async def write(self, write_io: WriteIO) -> None:
-        if isinstance(write_io.mapped, _MappedFile):
-            # the bytes are already in the file's pages: dirty them for writeback
-            path = self._abs(write_io.path)
-            n = memoryview(write_io.buf).nbytes
-            t_s = time.perf_counter()
-            rc = await _uncancellable(asyncio.get_running_loop().run_in_executor(
-                None, write_io.mapped.commit, self.fsync))
-            timeline.add("fmap_commit", "io", t_s, time.perf_counter(), path=write_io.path,
-                         bytes=n)
-            if rc < 0:
-                raise OSError(-rc, os.strerror(-rc), path)
-            self.bytes_written += n
-            self.bytes_mapped += n
-            return
         path = self._abs(write_io.path)
         mv = memoryview(write_io.buf).cast("B")
         n = mv.nbytes
@@ -235,45 +194,6 @@ class FSStoragePlugin(StoragePlugin):
             _native.release_io_engine(self._engine, reusable=not self._pending)
             self._engine = None
             self._loop = None
-
-
-_fmap_ok: Optional[bool] = None
-
-
-def release_file_mappings() -> int:
-    """Unmap every idle blob-file mapping this process keeps for rewrites
-    (their page-cache pages stay pinned while mapped, up to
-    ``knobs.TUNING.file_map_max_bytes``).  Returns the bytes released."""
-    return _native.fmap_release(False) if _native is not None else 0
-
-
-def _fmap_usable() -> bool:
-    global _fmap_ok
-    if _fmap_ok is None:
-        _fmap_ok = bool(_native is not None and _native.gpu_available() and
-                        _native.hsgpu_loaded())
-    return _fmap_ok
-
-
-class _MappedFile:
-    """One acquired file mapping: committed by ``write`` or, if the blob never
-    got there (failed take), abandoned by the buffer's release."""
-
-    __slots__ = ("addr", "settled")
-
-    def __init__(self, addr: int) -> None:
-        self.addr = addr
-        self.settled = False
-
-    def commit(self, sync: bool) -> int:
-        rc = _native.fmap_commit(self.addr, sync)
-        self.settled = True
-        return rc
-
-    def abandon(self) -> None:
-        if not self.settled:
-            self.settled = True
-            _native.fmap_abandon(self.addr)
 
 
 async def _uncancellable(fut: "asyncio.Future[Any]") -> Any:

@@ -21,11 +21,6 @@
 //       thread, and the round-5 trim-to-0 after every job): every byte must
 //       arrive, and no freed block may be touched again (the stubs retire a
 //       freed block's addresses, so a late use faults)
-//   engine_stress fmap <dir> <rounds>     the file-mapping cache (csrc/hsfmap.cpp):
-//       writer threads map, fill and commit / abandon files while a mutator
-//       replaces, resizes and deletes them, a racer maps and abandons without
-//       the files' locks, and the budget / prune / release calls run
-//       concurrently; committed bytes must be the file's bytes
 //
 // Prints "ok" and exits 0 when every check held.
 
@@ -422,132 +417,6 @@ void drain_mode(const std::string& dir, int rounds) {
   }
 }
 
-void fmap_mode(const std::string& dir, int rounds) {
-  constexpr int kFiles = 12;
-  std::vector<std::string> paths;
-  std::vector<std::mutex> locks(kFiles);
-  for (int i = 0; i < kFiles; ++i) {
-    paths.push_back(dir + "/m" + std::to_string(i));
-    write_file(paths[i], random_bytes(rnd(1, 300 << 10)));
-  }
-  hsg_fmap_set_budget(1 << 20);  // a few files: mappings are evicted as others come
-  stub::fail_register_every.store(7);
-  std::atomic<bool> stop{false};
-  std::atomic<int> committed{0}, hits_seen{0};
-  auto file_size = [](const std::string& p) -> int64_t {
-    struct stat st;
-    return stat(p.c_str(), &st) == 0 ? int64_t(st.st_size) : -1;
-  };
-  // (the threads draw from their own generators: the global rng is not shared)
-  auto range = [](std::mt19937_64& r, uint64_t lo, uint64_t hi) { return lo + r() % (hi - lo + 1); };
-  auto bytes = [](std::mt19937_64& r, uint64_t n) {
-    std::vector<uint8_t> v(n);
-    for (auto& x : v) x = uint8_t(r() >> 13);
-    return v;
-  };
-  auto writer = [&](uint64_t seed) {
-    std::mt19937_64 r(seed);
-    for (int it = 0; it < rounds * 40; ++it) {
-      const int f = int(r() % kFiles);
-      std::lock_guard<std::mutex> lk(locks[f]);
-      const int64_t n = file_size(paths[f]);
-      if (n <= 0) continue;
-      const bool wrong = r() % 8 == 0;
-      void* a = hsg_fmap_acquire(paths[f].c_str(), uint64_t(n) + (wrong ? 1 : 0));
-      if (wrong) {
-        CHECK(a == nullptr, "mapped %s with the wrong size", paths[f].c_str());
-        continue;
-      }
-      if (!a) continue;  // racer holds it / registration failed
-      std::vector<uint8_t> data(n);
-      for (auto& b : data) b = uint8_t(r());
-      memcpy(a, data.data(), n);
-      if (r() % 5 == 0) {
-        hsg_fmap_abandon(a);
-        continue;
-      }
-      CHECK(hsg_fmap_commit(a, int(r() % 4 == 0)) == 0, "commit %s", paths[f].c_str());
-      // (the mapping is not ours after the commit: the racer may hold it now)
-      CHECK(read_file(paths[f]) == data, "%s: committed bytes differ", paths[f].c_str());
-      committed.fetch_add(1);
-    }
-  };
-  std::thread mutator([&] {
-    std::mt19937_64 r(99);
-    while (!stop.load()) {
-      const int f = int(r() % kFiles);
-      {
-        std::lock_guard<std::mutex> lk(locks[f]);
-        switch (r() % 4) {
-          case 0: {  // replaced by a new file (new inode), maybe of the same size
-            const int64_t n = file_size(paths[f]);
-            const uint64_t len = (n > 0 && r() % 2) ? uint64_t(n) : range(r, 1, 300 << 10);
-            write_file(paths[f] + ".tmp", bytes(r, len));
-            CHECK(rename((paths[f] + ".tmp").c_str(), paths[f].c_str()) == 0, "rename");
-            break;
-          }
-          case 1:  // resized in place
-            if (file_size(paths[f]) >= 0) CHECK(truncate(paths[f].c_str(), range(r, 1, 300 << 10)) == 0, "truncate");
-            break;
-          case 2:
-            unlink(paths[f].c_str());
-            break;
-          default:
-            if (file_size(paths[f]) < 0) write_file(paths[f], bytes(r, range(r, 1, 300 << 10)));
-        }
-      }
-      std::this_thread::sleep_for(std::chrono::microseconds(range(r, 50, 400)));
-    }
-  });
-  std::thread racer([&] {
-    std::mt19937_64 r(7);
-    while (!stop.load()) {
-      const int f = int(r() % kFiles);
-      const int64_t n = file_size(paths[f]);
-      if (n > 0) {
-        void* a = hsg_fmap_acquire(paths[f].c_str(), uint64_t(n));
-        if (a) hsg_fmap_abandon(a);
-      }
-      uint64_t st[6];
-      hsg_fmap_stats(st);
-      hits_seen.store(int(st[2]));
-      if (r() % 16 == 0) hsg_fmap_prune();
-      if (r() % 32 == 0) hsg_fmap_release(0);
-      if (r() % 32 == 0) hsg_fmap_set_budget(range(r, 256 << 10, 2 << 20));
-    }
-  });
-  std::vector<std::thread> ws;
-  for (int t = 0; t < 4; ++t) ws.emplace_back(writer, 1000 + t);
-  for (auto& t : ws) t.join();
-  stop.store(true);
-  mutator.join();
-  racer.join();
-  stub::fail_register_every.store(0);
-  CHECK(committed.load() > 0, "no mapped write committed");
-  // a rewrite of an unchanged file hits the cached mapping
-  hsg_fmap_set_budget(64 << 20);
-  write_file(paths[0], random_bytes(100000));
-  for (int k = 0; k < 3; ++k) {
-    void* a = hsg_fmap_acquire(paths[0].c_str(), 100000);
-    CHECK(a, "map %s", paths[0].c_str());
-    CHECK(hsg_fmap_acquire(paths[0].c_str(), 100000) == nullptr, "a busy mapping handed out twice");
-    CHECK(hsg_fmap_commit(a, 1) == 0, "commit");
-    CHECK(hsg_fmap_commit(a, 0) == -EINVAL, "second commit accepted");
-  }
-  uint64_t st[6];
-  hsg_fmap_stats(st);
-  CHECK(st[2] >= 2, "no cache hit (%llu)", (unsigned long long)st[2]);
-  unlink(paths[0].c_str());
-  CHECK(hsg_fmap_prune() >= 100000, "the deleted file's mapping was not pruned");
-  hsg_fmap_release(1);
-  hsg_fmap_stats(st);
-  CHECK(st[0] == 0 && st[1] == 0, "mappings left: %llu bytes", (unsigned long long)st[0]);
-  CHECK(stub::registered_live.load() == 0, "%d registrations left", stub::registered_live.load());
-  printf("fmap: %d commits, %llu hits, %llu maps, %llu drops, %llu misses\n", committed.load(),
-         (unsigned long long)st[2], (unsigned long long)st[3], (unsigned long long)st[4],
-         (unsigned long long)st[5]);
-}
-
 }  // namespace
 
 void restore_trim_mode(const std::string& dir, int rounds) {
@@ -606,8 +475,6 @@ int main(int argc, char** argv) {
     drain_mode(dir, rounds);
   else if (mode == "ringwrap")
     ringwrap_mode(dir);
-  else if (mode == "fmap")
-    fmap_mode(dir, rounds);
   else if (mode == "restore-trim")
     restore_trim_mode(dir, rounds);
   else

@@ -45,8 +45,6 @@ std::atomic<uint64_t> dev_live{0};
 std::atomic<int> pinned_live{0};
 std::atomic<int> corruption{0};
 std::atomic<int> max_delay_us{200};
-std::atomic<int> registered_live{0};
-std::atomic<int> fail_register_every{0};
 
 namespace {
 
@@ -351,37 +349,6 @@ int hsg_rt_stream_after(void* waiter, void* producer) {
 
 int hsg_rt_stream_sync(void* stream) {
   stream_of(stream)->sync();
-  return 0;
-}
-
-// Host registration: remembers each registered range so an unregister of an
-// address never registered (or twice) is caught.
-namespace {
-std::mutex g_reg_mu;
-std::map<void*, uint64_t> g_registered;
-std::atomic<uint64_t> g_registrations{0};
-}  // namespace
-
-int hsg_rt_host_register(void* p, uint64_t n) {
-  const int every = fail_register_every.load();
-  if (every > 0 && g_registrations.fetch_add(1) % uint64_t(every) == uint64_t(every - 1))
-    return -1;
-  std::lock_guard<std::mutex> g(g_reg_mu);
-  if (!g_registered.emplace(p, n).second) {
-    fprintf(stderr, "stub: %p registered twice\n", p);
-    abort();
-  }
-  registered_live.fetch_add(1);
-  return 0;
-}
-
-int hsg_rt_host_unregister(void* p) {
-  std::lock_guard<std::mutex> g(g_reg_mu);
-  if (g_registered.erase(p) != 1) {
-    fprintf(stderr, "stub: unregister of %p, which is not registered\n", p);
-    abort();
-  }
-  registered_live.fetch_sub(1);
   return 0;
 }
 

@@ -23,8 +23,6 @@ extern std::atomic<uint64_t> dev_cap;       // device allocations fail above thi
 extern std::atomic<uint64_t> dev_live;
 extern std::atomic<int> pinned_live;        // pinned blocks not released
 extern std::atomic<int> corruption;         // copy launches whose stage / workspace was reused early
-extern std::atomic<int> registered_live;    // host ranges registered and not yet unregistered
-extern std::atomic<int> fail_register_every; // every Nth host registration fails
 extern std::atomic<int> max_delay_us;       // random delay before each queued operation
 
 uint64_t hash_bytes(const void* p, uint64_t n);
@@ -56,11 +54,4 @@ int hsg_drain_wait(void* handle, uint64_t* sums, uint64_t* bytes_written, char* 
                    double* stats);
 int hsg_drain_pending(void* handle);
 
-void* hsg_fmap_acquire(const char* path, uint64_t nbytes);
-int hsg_fmap_commit(void* addr, int sync);
-void hsg_fmap_abandon(void* addr);
-uint64_t hsg_fmap_release(int all);
-uint64_t hsg_fmap_prune();
-void hsg_fmap_set_budget(uint64_t bytes);
-void hsg_fmap_stats(uint64_t* out);
 }

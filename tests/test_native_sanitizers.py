@@ -63,8 +63,7 @@ def test_hsz_decoder_fuzz_under_asan(tmp_path):
 ENGINE_SRC = [os.path.join(ROOT, "tests", "native", "engine_stress.cpp"),
               os.path.join(ROOT, "tests", "native", "engine_stubs.cpp"),
               os.path.join(ROOT, "hipsnapshot", "csrc", "hsrestore.cpp"),
-              os.path.join(ROOT, "hipsnapshot", "csrc", "hsdrain.cpp"),
-              os.path.join(ROOT, "hipsnapshot", "csrc", "hsfmap.cpp")]
+              os.path.join(ROOT, "hipsnapshot", "csrc", "hsdrain.cpp")]
 SAN_ENV = dict(ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", TSAN_OPTIONS="halt_on_error=1",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
 
@@ -86,7 +85,7 @@ def _build_engine_stress(tmp_path, san, sources=None):
 
 
 @pytest.mark.parametrize("mode,rounds", [("restore", 24), ("drain", 24), ("ringwrap", 1),
-                                         ("fmap", 10), ("restore-trim", 16)])
+                                         ("restore-trim", 16)])
 @pytest.mark.parametrize("san", ["thread", "address,undefined"])
 def test_native_engines_under_sanitizer(tmp_path, san, mode, rounds):
     """csrc/hsrestore.cpp and csrc/hsdrain.cpp (host code: readers,
@@ -95,9 +94,7 @@ def test_native_engines_under_sanitizer(tmp_path, san, mode, rounds):
     CPU stand-ins of every device hook (random completion delays, injected
     upload / copy / file / memory failures, budgets below one blob, the
     c026ee7 ring wrap), concurrent restores on the shared pools while
-    another thread frees every idle block (restore-trim), and csrc/hsfmap.cpp
-    (the file-mapping cache under concurrent map / commit / abandon /
-    replace / prune / evict)."""
+    another thread frees every idle block (restore-trim)."""
     exe = _build_engine_stress(tmp_path, san)
     if san == "thread":
         rounds = max(1, rounds // 2)  # ~5x slower under TSan
