@@ -41,6 +41,9 @@ def main():
                          "one rank's share of a (K+1)-GPU node sharing this host")
     ap.add_argument("--single-path", action="store_true",
                     help="every take rewrites ONE snapshot path (100 GB runs: one copy on storage)")
+    ap.add_argument("--sync-repeats", type=int, default=1,
+                    help="timed sync takes (the median is reported); each one's phase split, "
+                         "page-cache state and page faults go to sync_each")
     args = ap.parse_args()
     rank, ws, dev = init_dist()
     from torch.distributed.device_mesh import init_device_mesh
@@ -85,15 +88,30 @@ def main():
         sib_root = os.environ.get("HSBENCH_SIBLING_DIR") or os.path.join(root, "siblings")
         sib = Siblings(args.host_siblings, sizes, sib_root, True)
     sib_ms = []
-    with Timer() as t:
+    sync_each = []
+    from hipsnapshot.utils import rank_diag
+
+    for _ in range(max(1, args.sync_repeats)):
+        before = _host_state()
         if sib is not None:
             sib.go()
-        Snapshot.take(p_sync, {"model": model})
+        d = rank_diag.measure(lambda: (Snapshot.take(p_sync, {"model": model}), sync(dev)))
+        after = _host_state()
+        d["take_s"] = max_over_ranks(d["take_ms"] / 1e3, dev)
+        d["GBps"] = round(nbytes / d["take_s"] / 1e9, 2)
+        d["dirty_kB_before"], d["writeback_kB_before"] = before["Dirty"], before["Writeback"]
+        d["dirty_kB_after"] = after["Dirty"]
+        d["minflt"] = after["minflt"] - before["minflt"]
+        d["majflt"] = after["majflt"] - before["majflt"]
+        sync_each.append(d)
+        if sib is not None:
+            sib_ms.append(max(x[0] for x in sib.wait()) * 1e3)
         sync(dev)
-    sync_s = max_over_ranks(t.s, dev)
-    if sib is not None:
-        sib_ms.append(max(x[0] for x in sib.wait()) * 1e3)
-    sync(dev)
+    sync_s = sorted(x["take_s"] for x in sync_each)[len(sync_each) // 2]
+    uvm_numa = None
+    if args.uvm:
+        uvm_numa = _numa_pages([(t.data_ptr(), t.numel() * t.element_size()) for t in locals_
+                                if t.numel()])
     # the first async_take of a state builds its plan: untimed, reported as cold
     with Timer() as tc:
         Snapshot.async_take(p_async, {"model": model}).wait()
@@ -135,6 +153,9 @@ def main():
     emit({"bench": "dlrm_uvm" if args.uvm else "dlrm_hbm", "sharding": args.sharding,
           "world_size": ws, "bytes": nbytes,
           "sync_take_s": round(sync_s, 3), "sync_GBps": round(nbytes / sync_s / 1e9, 2),
+          "sync_GBps_each": [x["GBps"] for x in sync_each], "sync_each": sync_each,
+          "uvm_pages_per_numa_node": uvm_numa,
+          "writer_cpus": rank_diag.cpu_set(), "writer_cpu_nodes": _cpu_nodes(),
           "async_unblock_ms": round(unblock * 1e3, 1), "freeze_gpu_ms": round(freeze_ms, 2),
           "async_total_s": round(async_total, 3),
           "async_GBps": round(nbytes / async_total / 1e9, 2),
@@ -147,6 +168,75 @@ def main():
     if rank == 0:
         shutil.rmtree(root, ignore_errors=True)
     dist.destroy_process_group()
+
+
+def _host_state() -> dict:
+    """Page-cache dirt (kB) and this process's page faults so far."""
+    import resource
+
+    out = {"Dirty": None, "Writeback": None}
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                k, v = line.split(":", 1)
+                if k in out:
+                    out[k] = int(v.split()[0])
+    except OSError:
+        pass
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    out["minflt"], out["majflt"] = ru.ru_minflt, ru.ru_majflt
+    return out
+
+
+def _numa_pages(ranges) -> dict:
+    """Pages of the managed tables per NUMA node (/proc/self/numa_maps)."""
+    out: dict = {}
+    try:
+        with open("/proc/self/numa_maps") as f:
+            lines = f.readlines()
+    except OSError:
+        return out
+    for line in lines:
+        parts = line.split()
+        try:
+            start = int(parts[0], 16)
+        except (ValueError, IndexError):
+            continue
+        if not any(lo <= start < lo + n for lo, n in ranges):
+            continue
+        for p in parts[1:]:
+            if p.startswith("N") and "=" in p:
+                node, cnt = p[1:].split("=", 1)
+                out[f"N{node}"] = out.get(f"N{node}", 0) + int(cnt)
+    return out
+
+
+def _cpu_nodes() -> dict:
+    """NUMA node of each CPU this process may run on (count per node)."""
+    out: dict = {}
+    cpus = os.sched_getaffinity(0)
+    base = "/sys/devices/system/node"
+    try:
+        nodes = [d for d in os.listdir(base) if d.startswith("node")]
+    except OSError:
+        return out
+    for d in nodes:
+        try:
+            with open(f"{base}/{d}/cpulist") as f:
+                spec = f.read().strip()
+        except OSError:
+            continue
+        ids = set()
+        for part in spec.split(","):
+            if "-" in part:
+                a, b = part.split("-")
+                ids.update(range(int(a), int(b) + 1))
+            elif part:
+                ids.add(int(part))
+        n = len(ids & cpus)
+        if n:
+            out[d] = n
+    return out
 
 
 if __name__ == "__main__":

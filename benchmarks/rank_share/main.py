@@ -181,6 +181,11 @@ def main() -> None:
         unblock.append(time.perf_counter() - t0)
         pending.wait()
         total.append(time.perf_counter() - t0)
+    from hipsnapshot import memory_held
+    from hipsnapshot.utils import rank_diag
+
+    held_after_takes = memory_held(dev.index or 0)  # what stays between checkpoints
+    diag = rank_diag.measure(take)  # one more take with its phases captured
     refs = {k: v._local_tensor.clone() for k, v in params.items()}
     rtimes = []
     r_per_val = {v: [] for v in ab_vals}
@@ -222,6 +227,11 @@ def main() -> None:
         "restore_ms_median": round(statistics.median(rtimes) * 1e3, 2),
         "restore_bitwise_ok": ok,
         "native_restore_stats": _native_restore_stats(),
+        "hbm_held_between_takes_bytes": held_after_takes["hbm_held_bytes"],
+        "pinned_held_bytes": held_after_takes["pinned_held_bytes"],
+        "memory_held_after_takes": held_after_takes,
+        "memory_held_after_restore": memory_held(dev.index or 0),
+        "rank_diag": diag,
         "numa_bind": numa,
         # host CPU time (user + system, every thread of the process) per take
         # and per stored GB; the kernel's page-cache writeback threads are

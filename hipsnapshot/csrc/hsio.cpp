@@ -27,10 +27,12 @@
 #include <cstring>
 #include <deque>
 #include <fcntl.h>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <cstdlib>
+#include <sched.h>
 #include <sys/eventfd.h>
 #include <sys/resource.h>
 #include <sys/syscall.h>
@@ -48,6 +50,13 @@ constexpr int kFlagDirect = 1;   // try O_DIRECT for the aligned body
 constexpr int kFlagSync = 2;     // fdatasync before completing a write
 constexpr int kFlagMkdirs = 4;   // create parent directories
 constexpr int kFlagAppend = 8;   // write at offset without truncating
+// bits 16..23: NUMA node + 1 whose CPUs run the job (0: any).  A blob
+// written straight from host pages (a host-resident UVM table) is copied into
+// the page cache by the worker's CPU: a worker on the pages' node reads them
+// locally.  Unbound, the workers landed on either socket and an 8 GB DLRM
+// UVM save spread 36-69 GB/s; bound to the wrong node it ran 30-43
+// (profiles/r6/dlrm_var/).
+constexpr int kNodeShift = 16;
 constexpr size_t kAlign = 4096;
 constexpr size_t kMaxIo = size_t(1) << 30;  // keep single syscalls < 2 GiB
 
@@ -117,6 +126,8 @@ int64_t full_pread(int fd, char* p, size_t n, size_t off) {
 class Engine {
  public:
   explicit Engine(int nthreads) {
+    CPU_ZERO(&base_mask_);
+    have_base_ = ::sched_getaffinity(0, sizeof(base_mask_), &base_mask_) == 0;
     efd_ = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     if (nthreads < 1) nthreads = 1;
     for (int i = 0; i < nthreads; ++i)
@@ -198,6 +209,7 @@ class Engine {
         j = std::move(queue_.front());
         queue_.pop_front();
       }
+      PlaceFor(((j.flags >> kNodeShift) & 0xff) - 1);
       int64_t r = Execute(j);
       int64_t id = j.id;
       if (j.group) {
@@ -219,6 +231,52 @@ class Engine {
       uint64_t one = 1;
       (void)!::write(efd_, &one, sizeof(one));
     }
+  }
+
+  // Run this worker on `node`'s CPUs (within the engine's original mask), or
+  // back on the original mask for node -1.  Kept until a job asks otherwise.
+  void PlaceFor(int node) {
+    thread_local int placed = -1;
+    if (node == placed || !have_base_) return;
+    cpu_set_t m;
+    if (node < 0) {
+      m = base_mask_;
+    } else {
+      if (!NodeMask(node, &m)) return;
+      CPU_AND(&m, &m, &base_mask_);
+      if (CPU_COUNT(&m) == 0) return;
+    }
+    if (::sched_setaffinity(0, sizeof(m), &m) == 0) placed = node;
+  }
+
+  bool NodeMask(int node, cpu_set_t* out) {
+    std::lock_guard<std::mutex> g(nmu_);
+    auto it = node_masks_.find(node);
+    if (it == node_masks_.end()) {
+      cpu_set_t m;
+      CPU_ZERO(&m);
+      char path[96];
+      snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+      bool ok = false;
+      if (FILE* f = fopen(path, "r")) {
+        char buf[4096];
+        if (fgets(buf, sizeof(buf), f)) {
+          ok = true;
+          for (char* tok = strtok(buf, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+            int a = -1, b = -1;
+            if (sscanf(tok, "%d-%d", &a, &b) == 2) {
+              for (int c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(c, &m);
+            } else if (sscanf(tok, "%d", &a) == 1 && a >= 0 && a < CPU_SETSIZE) {
+              CPU_SET(a, &m);
+            }
+          }
+        }
+        fclose(f);
+      }
+      it = node_masks_.emplace(node, std::make_pair(ok, m)).first;
+    }
+    *out = it->second.second;
+    return it->second.first;
   }
 
   int MkdirsFor(const std::string& path) {
@@ -340,6 +398,10 @@ class Engine {
   std::deque<Completion> done_;
   std::mutex dmu_;
   std::unordered_set<std::string> dirs_;
+  cpu_set_t base_mask_;  // the creating thread's CPUs (the workers' default)
+  bool have_base_ = false;
+  std::mutex nmu_;
+  std::map<int, std::pair<bool, cpu_set_t>> node_masks_;
   int efd_ = -1;
 };
 

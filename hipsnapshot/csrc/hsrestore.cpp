@@ -112,9 +112,8 @@ uint64_t align16(uint64_t n) { return (n + 15) & ~uint64_t(15); }
 // restores; hsg_restore_trim() frees the idle ones.  Blocks come from
 // hsg_rt_vmm_alloc (hshost.hip): a freed block's virtual range is never
 // handed out again.  With hipMalloc / hipExtMallocWithFlags blocks, freeing
-// uncached and plain blocks let the runtime hand a freed address out again as
-// the other kind, and kernels then wrote through the address's old
-// translation: wrong bytes and hipErrorIllegalAddress faults whenever the
+// uncached and plain blocks left the process's next blocks used through stale
+// translations: wrong bytes and hipErrorIllegalAddress faults whenever the
 // pools were trimmed (profiles/r6/trim/).
 //
 // Freed ranges stay reserved (virtual address space only); past this many

@@ -322,7 +322,8 @@ async def execute_write_reqs(write_reqs: List[WriteReq], storage: StoragePlugin,
                 if failure:  # the snapshot is failing: do not start more writes
                     return
                 t_w = time.perf_counter()
-                await storage.write(WriteIO(path=wr.path, buf=buf.view, addr=buf.addr))
+                await storage.write(WriteIO(path=wr.path, buf=buf.view, addr=buf.addr,
+                                            numa_node=buf.numa_node))
                 timeline.add("write", "io", t_w, time.perf_counter(), path=wr.path,
                              bytes=buf.nbytes)
             stats.bytes_written += buf.nbytes

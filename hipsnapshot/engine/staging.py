@@ -396,7 +396,12 @@ def managed_host_view(t: torch.Tensor, producer: Optional[int]) -> StagedBuffer:
     import ctypes
 
     mv = memoryview((ctypes.c_char * nbytes).from_address(t.data_ptr())).cast("B")
-    return StagedBuffer(mv, addr=t.data_ptr(), keepalive=t)
+    staged = StagedBuffer(mv, addr=t.data_ptr(), keepalive=t)
+    # the writer copies the pages into the page cache: on their node
+    from ..utils.affinity import pages_node
+
+    staged.numa_node = pages_node(t.data_ptr(), nbytes)
+    return staged
 
 
 def d2h_tensor(t: torch.Tensor, producer: Optional[int],

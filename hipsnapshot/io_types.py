@@ -39,7 +39,7 @@ def buffer_address(buf) -> int:
 class StagedBuffer:
     """Bytes ready for storage: ``view`` + raw ``addr`` + release hook."""
 
-    __slots__ = ("view", "addr", "_release", "keepalive", "checksum", "ready", "mapped")
+    __slots__ = ("view", "addr", "_release", "keepalive", "checksum", "ready", "numa_node")
 
     def __init__(self, view: BufferType, addr: Optional[int] = None,
                  release: Optional[Callable[[], None]] = None, keepalive: Any = None) -> None:
@@ -56,6 +56,9 @@ class StagedBuffer:
         # set when the bytes are still arriving (asynchronous SDMA copy):
         # call it (blocking, once) before reading the buffer
         self.ready: Optional[Callable[[], None]] = None
+        # NUMA node of the host pages ``view`` points into, when the writer
+        # should run there (host-resident UVM tables written in place)
+        self.numa_node: Optional[int] = None
 
     @property
     def nbytes(self) -> int:
@@ -207,6 +210,8 @@ class WriteIO:
     path: str
     buf: BufferType
     addr: Optional[int] = None
+    # ``StagedBuffer.numa_node``: run the write on that node's CPUs
+    numa_node: Optional[int] = None
 
 
 @dataclass

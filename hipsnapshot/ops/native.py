@@ -96,6 +96,7 @@ IO_DIRECT = 1
 IO_SYNC = 2
 IO_MKDIRS = 4
 IO_APPEND = 8
+IO_NODE_SHIFT = 16  # flags bits 16..23: NUMA node + 1 whose CPUs run the job
 
 
 class IOEngine:

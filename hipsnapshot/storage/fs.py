@@ -126,7 +126,10 @@ class FSStoragePlugin(StoragePlugin):
             await _uncancellable(asyncio.get_running_loop().run_in_executor(
                 None, _py_write, path, mv))
         else:
-            job = eng.submit_write(path, addr, n, 0, self._flags(mkdirs=True))
+            flags = self._flags(mkdirs=True)
+            if write_io.numa_node is not None and 0 <= write_io.numa_node < 255:
+                flags |= (write_io.numa_node + 1) << _native.IO_NODE_SHIFT  # csrc/hsio.cpp
+            job = eng.submit_write(path, addr, n, 0, flags)
             res = await self._await_job(job, mv)
             if res < 0:
                 raise OSError(-res, os.strerror(-res), path)

@@ -13,7 +13,7 @@ changes process state the trainer may manage itself; ``bench.py`` uses it.
 from __future__ import annotations
 
 import os
-from typing import List, Optional, Set
+from typing import Dict, List, Optional, Set
 
 _SYS_PCI = "/sys/bus/pci/devices"
 _SYS_NODE = "/sys/devices/system/node"
@@ -282,6 +282,43 @@ def gpu_node_mask(device: int, min_cpus: int = 4) -> Optional[Set[int]]:
     if len(local) < min_cpus or local == allowed:
         return None
     return local
+
+
+_SYS_MOVE_PAGES = {"x86_64": 279, "aarch64": 239}
+
+
+def pages_node(addr: int, nbytes: int, samples: int = 32) -> Optional[int]:
+    """The NUMA node holding most of the host pages of ``[addr, addr +
+    nbytes)``, from ``samples`` pages spread over the range (``move_pages``
+    with no target nodes only reports where pages are); None when unknown
+    (no pages faulted in yet, no NUMA, not Linux)."""
+    import ctypes
+    import platform
+
+    nr = _SYS_MOVE_PAGES.get(platform.machine())
+    if nr is None or nbytes <= 0:
+        return None
+    page = os.sysconf("SC_PAGE_SIZE")
+    first = addr // page * page
+    n_pages = max(1, (addr + nbytes - first + page - 1) // page)
+    k = max(1, min(samples, n_pages))
+    ptrs = (ctypes.c_void_p * k)(*[first + (i * n_pages // k) * page for i in range(k)])
+    status = (ctypes.c_int * k)()
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        rc = libc.syscall(ctypes.c_long(nr), ctypes.c_int(0), ctypes.c_ulong(k), ptrs, None,
+                          status, ctypes.c_int(0))
+    except Exception:  # noqa: BLE001
+        return None
+    if rc != 0:
+        return None
+    counts: Dict[int, int] = {}
+    for s in status:
+        if s >= 0:
+            counts[s] = counts.get(s, 0) + 1
+    if not counts:
+        return None
+    return max(counts, key=counts.get)
 
 
 class threads_with_mask:

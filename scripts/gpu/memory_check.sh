@@ -13,3 +13,6 @@ timeout -k 10 120 python scripts/probes/vmm_cost.py > $O/vmm_cost.json 2> $O/vmm
 cat $O/vmm_cost.json
 timeout -k 10 150 python scripts/probes/pool_churn_mp.py --mode both --procs 1 --iters 400 --out $O/churn_1p_kinds.json > $O/churn_1p_kinds.log 2>&1 || { tail -20 $O/churn_1p_kinds.log; exit 1; }
 tail -1 $O/churn_1p_kinds.log
+export HSBENCH_DIR=$PWD/bench_tmp
+timeout -k 10 420 python benchmarks/dlrm_uvm/main.py --total-gb 8 --uvm --sync-repeats 6 > $O/dlrm_uvm_repeat.json 2> $O/dlrm_uvm_repeat.err || { tail -20 $O/dlrm_uvm_repeat.err; exit 1; }
+tail -1 $O/dlrm_uvm_repeat.json | cut -c1-600

@@ -385,10 +385,9 @@ def _poison_reshard_worker(root):
 def test_pools_trimmed_to_zero_four_processes_bitwise(gpu, tmp_path):
     """The round-5 failure: 4 processes restoring on one GPU with the restore
     pools freed after EVERY job (and ``release_restore_memory()`` between
-    reads) got wrong bytes and hipErrorIllegalAddress faults, because a freed
-    hipMalloc / hipExtMallocWithFlags address came back as the other kind of
-    block and kernels wrote through its old translation
-    (profiles/r6/trim/).  The pools now allocate through the VMM hooks, whose
+    reads) got wrong bytes and hipErrorIllegalAddress faults: after freeing
+    both uncached and plain hipMalloc'd blocks, the process's kernels used
+    its next blocks through stale translations (profiles/r6/trim/).  The pools now allocate through the VMM hooks, whose
     freed addresses are never handed out again: every read is bitwise, with
     and without ``verify``, whole and in 2 KiB tiles."""
     import sys

@@ -300,3 +300,31 @@ def test_s3_out_of_process_parallel_parts_land_in_dest():
             await p.close()
 
         run(body())
+
+
+def test_fs_write_on_a_numa_node(tmp_path):
+    """A write carrying the NUMA node of its host pages (a host-resident UVM
+    table written in place) runs on that node's CPUs in the native engine
+    (csrc/hsio.cpp kNodeShift) and writes the same bytes; an unknown node is
+    ignored."""
+    import asyncio
+
+    import numpy as np
+
+    from hipsnapshot.io_types import WriteIO
+    from hipsnapshot.storage.fs import FSStoragePlugin
+    from hipsnapshot.utils.affinity import pages_node
+
+    data = np.random.default_rng(0).integers(0, 255, 3 << 20, dtype=np.uint8)
+    node = pages_node(data.ctypes.data, data.nbytes)
+    assert node is None or node >= 0
+    plugin = FSStoragePlugin(str(tmp_path))
+    loop = asyncio.new_event_loop()
+    try:
+        for i, n in enumerate((node if node is not None else 0, 254, None)):
+            loop.run_until_complete(plugin.write(WriteIO(path=f"b{i}", buf=memoryview(data),
+                                                         numa_node=n)))
+            assert (tmp_path / f"b{i}").read_bytes() == data.tobytes()
+        loop.run_until_complete(plugin.close())
+    finally:
+        loop.close()
