@@ -12,6 +12,7 @@ memory.
 import argparse
 import os
 import shutil
+import time
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -93,6 +94,7 @@ def main():
 
     for _ in range(max(1, args.sync_repeats)):
         before = _host_state()
+        nodes_before = _node_state()
         if sib is not None:
             sib.go()
         d = rank_diag.measure(lambda: (Snapshot.take(p_sync, {"model": model}), sync(dev)))
@@ -103,6 +105,7 @@ def main():
         d["dirty_kB_after"] = after["Dirty"]
         d["minflt"] = after["minflt"] - before["minflt"]
         d["majflt"] = after["majflt"] - before["majflt"]
+        d["nodes_before"] = nodes_before
         sync_each.append(d)
         if sib is not None:
             sib_ms.append(max(x[0] for x in sib.wait()) * 1e3)
@@ -185,6 +188,58 @@ def _host_state() -> dict:
         pass
     ru = resource.getrusage(resource.RUSAGE_SELF)
     out["minflt"], out["majflt"] = ru.ru_minflt, ru.ru_majflt
+    return out
+
+
+def _node_state() -> dict:
+    """Per NUMA node: free memory and page cache (kB, from sysfs), and the
+    rate (GB/s) one thread on that node copies 256 MiB between buffers it
+    first-touched there -- what the machine leaves a writer on each node."""
+    import threading
+
+    import numpy as np
+
+    base = "/sys/devices/system/node"
+    out: dict = {}
+    try:
+        nodes = sorted(d for d in os.listdir(base) if d.startswith("node"))
+    except OSError:
+        return out
+    for d in nodes:
+        info = {}
+        try:
+            with open(f"{base}/{d}/meminfo") as f:
+                for line in f:
+                    parts = line.split()
+                    if len(parts) >= 4 and parts[2].rstrip(":") in ("MemFree", "FilePages",
+                                                                      "Dirty"):
+                        info[parts[2].rstrip(":")] = int(parts[3])
+        except OSError:
+            pass
+        try:
+            from hipsnapshot.utils.affinity import node_cpus
+
+            cpus = node_cpus(int(d[4:])) & os.sched_getaffinity(0)
+        except Exception:  # noqa: BLE001
+            cpus = set()
+        if cpus:
+            res = {}
+
+            def copy_on_node(cpus=cpus, res=res):
+                os.sched_setaffinity(0, cpus)  # this thread only
+                a = np.ones(256 << 20, dtype=np.uint8)
+                b = np.empty_like(a)
+                np.copyto(b, a)
+                t0 = time.perf_counter()
+                for _ in range(4):
+                    np.copyto(b, a)
+                res["GBps"] = round(4 * a.nbytes / (time.perf_counter() - t0) / 1e9, 2)
+
+            th = threading.Thread(target=copy_on_node)
+            th.start()
+            th.join()
+            info["copy_GBps_1thread"] = res.get("GBps")
+        out[d] = info
     return out
 
 

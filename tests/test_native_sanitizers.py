@@ -12,6 +12,8 @@ import subprocess
 
 import pytest
 
+pytestmark = pytest.mark.slow
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = [os.path.join(ROOT, "hipsnapshot", "csrc", "hsio.cpp"),
        os.path.join(ROOT, "hipsnapshot", "csrc", "hsz_cpu.cpp"),
