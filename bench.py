@@ -149,6 +149,78 @@ def _check_resharded(model, old: list, dev: int) -> list:
     return bad
 
 
+def _hsdp_phase(cfg, dev, gpu_index, world, rank, reps, root, opts, args, total_bytes,
+                barrier_sync, log) -> dict:
+    """The model under HSDP on a (reps, world / reps) mesh: timed takes,
+    per-rank written bytes, and a bitwise restore of every local shard."""
+    import statistics
+
+    import torch
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+
+    from hipsnapshot import Snapshot, release_hbm_arena
+    from hipsnapshot.models.llama import build_fsdp_llama
+    from hipsnapshot.snapshot import TakeStats
+
+    release_hbm_arena()
+    mesh = init_device_mesh("cuda", (reps, world // reps), mesh_dim_names=("rep", "shard"))
+    model = build_fsdp_llama(cfg, dev, torch.bfloat16, mesh=mesh)
+    # replicas start identical: each shard-group member takes replica 0's bytes
+    rep_group = mesh.get_group("rep")
+    with torch.no_grad():
+        for p in model.parameters():
+            dist.broadcast(p._local_tensor, group=rep_group, group_src=0)
+    torch.cuda.synchronize()
+    path = os.path.join(root, "hsdp")
+    app = {"model": model}
+    Snapshot.take(path, app, storage_options=opts, compression=args.compression)
+    each, mine = [], []
+    for _ in range(max(1, args.hsdp_steps)):
+        barrier_sync()
+        t0 = time.perf_counter()
+        Snapshot.take(path, app, storage_options=opts, compression=args.compression)
+        mine.append(time.perf_counter() - t0)
+        barrier_sync()
+        e = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        each.append(float(e.item()))
+    written = int(TakeStats.last.get("bytes", 0))
+    before = {n: _hash_tensor(p._local_tensor, gpu_index) for n, p in model.named_parameters()}
+    for p in model.parameters():
+        p._local_tensor.zero_()
+    barrier_sync()
+    t0 = time.perf_counter()
+    Snapshot(path).restore(app)
+    barrier_sync()
+    restore_s = time.perf_counter() - t0
+    bad = sum(_hash_tensor(p._local_tensor, gpu_index) != before[n]
+              for n, p in model.named_parameters())
+    per = [None] * world
+    dist.all_gather_object(per, (written, statistics.mean(mine) * 1e3, bad))
+    wr = [r[0] for r in per]
+    # the model's logical bytes: one copy of the global state
+    logical = sum(p.numel() * p.element_size() for p in model.parameters())
+    out = {
+        "hsdp_mesh": [reps, world // reps],
+        "hsdp_GBps": round(logical / statistics.median(each) / 1e9, 2),
+        "hsdp_s_each": [round(x, 3) for x in each],
+        "hsdp_rank_written_bytes": wr,
+        "hsdp_rank_written_max_over_mean": round(max(wr) / (sum(wr) / world), 3) if sum(wr)
+        else None,
+        "hsdp_rank_take_ms": [round(r[1], 1) for r in per],
+        "hsdp_restore_GBps": round(logical / restore_s / 1e9, 2),
+        "hsdp_restore_bitwise_ok": all(r[2] == 0 for r in per),
+    }
+    log(f"HSDP {reps}x{world // reps}: {out}")
+    del model, app
+    torch.cuda.empty_cache()
+    if rank == 0:
+        shutil.rmtree(path, ignore_errors=True)
+    dist.barrier()
+    return out
+
+
 def _selftest_hook(rank: int) -> None:
     """``HSBENCH_SELFTEST`` (launcher tests on CPU, before any
     torch import): ``ok`` -- rank 0 prints a JSON line, every rank exits 0;
@@ -272,6 +344,12 @@ def main() -> None:
     ap.add_argument("--elastic-iters", type=int, default=1,
                     help="BASELINE config 3 (N >= 2, N even): restores of the N-rank FSDP "
                          "checkpoint into N/2 ranks, each checked bitwise (0 = skip)")
+    ap.add_argument("--hsdp", type=int, default=None,
+                    help="HSDP phase: the model on a (R, N/R) (replicate, shard) mesh, each "
+                         "replicated box written by the R replicas in row ranges "
+                         "(io/sharded.py); reports per-rank written bytes and a bitwise "
+                         "restore (default R = 2 when N >= 4 is even, 0 = skip)")
+    ap.add_argument("--hsdp-steps", type=int, default=2)
     ap.add_argument("--launch-timeout", type=float, default=3600.0,
                     help="self-launched ranks (--gpus N > 1 without torchrun): seconds before "
                          "every rank is stopped and the run fails")
@@ -577,6 +655,13 @@ def main() -> None:
         log(f"elastic restore {world} -> {half} ranks: {elastic}")
         dist.barrier()
 
+    # HSDP: replicated DTensor boxes split over the replica group
+    hsdp = {}
+    reps = args.hsdp if args.hsdp is not None else (2 if world >= 4 and world % 2 == 0 else 0)
+    if reps > 1 and world % reps == 0 and world // reps >= 1:
+        hsdp = _hsdp_phase(cfg, dev, gpu_index, world, rank, reps, root, opts, args, total_bytes,
+                           barrier_sync, log)
+
     # the same save with raw, reference-format blobs (no HSZ1): what the
     # headline would be without the codec, measured in the same process
     raw_gbps = None
@@ -816,6 +901,7 @@ def main() -> None:
                              "no published number for 2/4 GPUs",
             **ddp_llama,
             **elastic,
+            **hsdp,
             # what rank 0 holds between checkpoints (engine/memory.py): after
             # the async takes (arena, pools, pinned) and after the restores
             "hbm_held_between_takes_bytes": held_after_takes["hbm_held_bytes"],
