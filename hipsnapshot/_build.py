@@ -19,7 +19,24 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 HSIO_SO = os.path.join(PKG_DIR, "_hsio.so")
 HSGPU_SO = os.path.join(PKG_DIR, "_hsgpu.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
-GPU_ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+# The kernels use gfx950-only builtins (MFMA 32x32x16 bf16, fp8 conversions):
+# build for gfx950 whatever else PYTORCH_ROCM_ARCH lists (ROCm images often
+# start that list with older targets).  ``python -m
+# hipsnapshot._build --arch gfx950`` names the target explicitly.
+SUPPORTED_ARCHS = ("gfx950",)
+
+
+def gpu_archs(override: str = "") -> list:
+    want = [a.strip() for a in (override or os.environ.get("PYTORCH_ROCM_ARCH", "")).replace(
+        ",", ";").split(";") if a.strip()]
+    # feature suffixes (gfx950:xnack-) keep their base name's support
+    picked = [a for a in want if a.split(":")[0] in SUPPORTED_ARCHS]
+    if override and not picked:
+        raise ValueError(f"--arch {override!r}: the kernels build for {SUPPORTED_ARCHS} only")
+    return picked or list(SUPPORTED_ARCHS)
+
+
+GPU_ARCH = gpu_archs()[0]
 
 
 def _stale(out: str, srcs) -> bool:
@@ -51,7 +68,7 @@ def build_hsio(force: bool = False) -> str:
     return HSIO_SO
 
 
-def build_hsgpu(force: bool = False) -> str:
+def build_hsgpu(force: bool = False, arch: str = "") -> str:
     # hsdrain.cpp / hsrestore.cpp are host-only engines (their HIP calls sit
     # in hshost.hip); hipcc builds them as plain C++ into the same library
     srcs = [os.path.join(CSRC, "hsgpu.hip"), os.path.join(CSRC, "hsz.hip"),
@@ -61,18 +78,20 @@ def build_hsgpu(force: bool = False) -> str:
         hipcc = os.path.join(ROCM, "bin", "hipcc")
         if not os.path.exists(hipcc):
             hipcc = shutil.which("hipcc") or hipcc
-        _atomic_build(HSGPU_SO, lambda out: [hipcc, f"--offload-arch={GPU_ARCH}", "-O3",
-                                             "-std=c++17", "-fPIC", "-shared", "-Wall",
-                                             "-o", out] + srcs + ["-ldl"])
+        archs = [f"--offload-arch={a}" for a in gpu_archs(arch)]
+        _atomic_build(HSGPU_SO, lambda out: [hipcc] + archs + ["-O3", "-std=c++17", "-fPIC",
+                                                               "-shared", "-Wall", "-o", out]
+                      + srcs + ["-ldl"])
     return HSGPU_SO
 
 
-def build_all(force: bool = False) -> None:
+def build_all(force: bool = False, arch: str = "") -> None:
     build_hsio(force)
-    build_hsgpu(force)
+    build_hsgpu(force or bool(arch), arch)
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    _arch = sys.argv[sys.argv.index("--arch") + 1] if "--arch" in sys.argv else ""
+    build_all(force="--force" in sys.argv, arch=_arch)
     print(HSIO_SO)
     print(HSGPU_SO)

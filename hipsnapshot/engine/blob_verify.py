@@ -15,7 +15,9 @@ itself checks each blob it reads against the recorded checksum and raises
 * the Python pipeline hashes whole-blob host reads with the C++ hasher
   (``checksum.hs64_host``, multi-threaded) before they are consumed;
 * blobs only PART of which a restore reads (byte-range reads of one rank's
-  piece, budgeted tiles) are read once more in full and hashed at the end.
+  piece, budgeted tiles) are read once more and hashed at the end, in pieces
+  that keep the read within the caller's memory budget (hs64 is a sum over
+  8-byte words with their index: pieces at word boundaries add up).
 
 A flipped byte in a raw blob -- or in an HSZ1 blob's low-byte plane, which
 the HSZ1 frame checks cannot see -- then fails the restore instead of landing
@@ -82,22 +84,58 @@ class RestoreVerifier:
             if path not in self.verified:
                 self.partial.add(path)
 
-    async def finish(self, storage: StoragePlugin, concurrency: int = 4) -> None:
-        """Read and hash, in full, every blob only part of which was read."""
+    async def finish(self, storage: StoragePlugin, memory_budget_bytes: Optional[int] = None,
+                     concurrency: int = 4) -> None:
+        """Read and hash every blob only part of which was read.  At most
+        ``concurrency`` pieces of ``memory_budget_bytes / concurrency`` bytes
+        (capped at 64 MiB, at least 1 MiB) are in memory at once; a plugin
+        that cannot tell a blob's size is read whole."""
         with self._lock:
             todo = sorted(self.partial - self.verified)
+        piece = PIECE_MAX
+        if memory_budget_bytes:
+            # a small budget: fewer pieces at once rather than tiny pieces
+            concurrency = max(1, min(concurrency, int(memory_budget_bytes) // PIECE_MIN))
+            piece = max(PIECE_MIN, min(PIECE_MAX, int(memory_budget_bytes) // concurrency))
+        piece = piece // 8 * 8
         sem = asyncio.Semaphore(concurrency)
         loop = asyncio.get_running_loop()
 
-        async def one(path: str) -> None:
+        async def read_piece(path: str, lo: int, hi: Optional[int]) -> tuple:
             async with sem:
-                rio = ReadIO(path=path)
+                rio = ReadIO(path=path, byte_range=None if hi is None else (lo, hi))
                 await storage.read(rio)
                 mv = memoryview(rio.data()).cast("B")
-                h = await loop.run_in_executor(None, checksum.hs64_of, mv)
-                self.check_sum(path, h, mv.nbytes)
+                s = await loop.run_in_executor(None, _partial, mv, lo // 8)
+                return s, mv.nbytes
+
+        async def one(path: str) -> None:
+            size = await storage.size(path)
+            if size is None:
+                s, n = await read_piece(path, 0, None)
+            else:
+                parts = await asyncio.gather(*(read_piece(path, lo, min(size, lo + piece))
+                                               for lo in range(0, max(size, 1), piece)))
+                s, n = sum(p[0] for p in parts), sum(p[1] for p in parts)
+            self.check_sum(path, checksum.finish(s, n), n)
 
         await asyncio.gather(*(one(p) for p in todo))
+
+
+PIECE_MIN = 1 << 20
+PIECE_MAX = 64 << 20
+
+
+def _partial(mv: memoryview, first_word: int) -> int:
+    """hs64's partial sum of ``mv`` as the bytes starting at word
+    ``first_word`` of their blob (added over pieces, then ``finish``ed)."""
+    from ..io_types import buffer_address
+    from ..ops import native
+
+    n = mv.nbytes
+    if n == 0:
+        return 0
+    return int(native.hsio().hs64_partial(buffer_address(mv), n, first_word, 4))
 
 
 def whole_read(rr, stored_size: Optional[int]) -> bool:

@@ -648,7 +648,7 @@ async def execute_read_reqs(read_reqs: List[ReadReq], storage: StoragePlugin,
         stats.bytes_written += native_bytes[0]
         stats.n_reqs += sum(len(v) for v in native_jobs.values())
     if verifier is not None:
-        await verifier.finish(storage)
+        await verifier.finish(storage, memory_budget_bytes)
     return stats
 
 

@@ -247,6 +247,12 @@ class StoragePlugin(ABC):
     async def delete_dir(self, path: str) -> None:
         raise NotImplementedError(f"{type(self).__name__} does not implement delete_dir")
 
+    async def rename(self, src: str, dst: str) -> None:
+        """Atomically move blob ``src`` to ``dst`` (optional: a take that
+        replaces a committed snapshot stashes its metadata this way, and
+        otherwise keeps a copy of the bytes to put back)."""
+        raise NotImplementedError(f"{type(self).__name__} does not implement rename")
+
     async def size(self, path: str) -> Optional[int]:
         """Stored size of a blob, or None when the backend cannot tell
         cheaply (then compressed blobs are read header-first)."""

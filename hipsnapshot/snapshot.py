@@ -523,39 +523,67 @@ class Snapshot:
                            storage_options: Optional[Dict[str, Any]]):
         """Commit rule (reference `snapshot.py:226-234`): a snapshot exists
         iff its ``.snapshot_metadata`` exists.  A take into a path that holds
-        a committed snapshot overwrites its blobs, so rank 0 removes the old
-        commit (``_uncommit``) BEFORE it contributes to the coalesce gather:
-        no rank can finish that collective -- and so write its first blob --
-        while the old metadata still names the blobs being rewritten.  (Rank
-        0's path is the snapshot's path, so it can open storage first.)"""
+        a committed snapshot overwrites its blobs, so rank 0 takes the old
+        commit away (``_uncommit``) BEFORE it contributes to the coalesce
+        gather: no rank can finish that collective -- and so write its first
+        blob -- while the old metadata still names the blobs being rewritten.
+        The old metadata is stashed, not deleted: if the coalesce fails (app
+        states that do not match, a rank that never arrives) no rank has
+        written anything, and rank 0 puts the old commit back.
+        (Rank 0's path is the snapshot's path, so it can open storage first.)"""
         storage = None
+        stash = None
         try:
             if comm.get_rank() == 0:
                 with timeline.span("storage_open"):
                     storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
                 with timeline.span("uncommit"):
-                    cls._uncommit(storage, loop)
+                    stash = cls._uncommit(storage, loop)
             with timeline.span("coalesce"):
                 path, rep, keys, nonce = cls._coalesce(path, comm, app_state, replicated or [])
             if storage is None:
                 with timeline.span("storage_open"):
                     storage = url_to_storage_plugin_in_event_loop(path, loop, storage_options)
         except BaseException:
+            if stash is not None:
+                cls._recommit(storage, loop, stash)
             if storage is not None:
                 storage.sync_close(loop)
             loop.close()
             raise
+        if stash is not None and stash[0] == "renamed":
+            try:  # the stashed commit is obsolete now that every rank agreed
+                storage.sync_delete(stash[1], loop)
+            except Exception as e:  # noqa: BLE001
+                logger.debug(f"could not remove the stashed metadata: {e}")
         return path, rep, keys, nonce, storage
 
     @staticmethod
-    def _uncommit(storage: StoragePlugin, loop: asyncio.AbstractEventLoop) -> None:
-        """A snapshot exists iff its metadata exists: drop an older commit at
-        this path before its blobs get overwritten."""
+    def _uncommit(storage: StoragePlugin, loop: asyncio.AbstractEventLoop):
+        """A snapshot exists iff its metadata exists: take an older commit at
+        this path away before its blobs get overwritten.  Returns how to put
+        it back (``_recommit``): ``("renamed", stash path)`` where the plugin
+        renames atomically (FS), ``("bytes", data)`` where the old metadata
+        was read and deleted, or None when there was none."""
+        stash = f"{SNAPSHOT_METADATA_FNAME}.stash.{uuid.uuid4().hex[:12]}"
+        out = None
         try:
-            storage.sync_delete(SNAPSHOT_METADATA_FNAME, loop)
+            run_sync(loop, storage.rename(SNAPSHOT_METADATA_FNAME, stash))
+            out = ("renamed", stash)
         except (FileNotFoundError, KeyError):
             pass
-        except Exception as e:  # noqa: BLE001 - e.g. plugins without delete
+        except NotImplementedError:
+            try:
+                rio = ReadIO(path=SNAPSHOT_METADATA_FNAME)
+                storage.sync_read(rio, loop)
+                data = bytes(rio.data())
+                storage.sync_delete(SNAPSHOT_METADATA_FNAME, loop)
+                out = ("bytes", data)
+            except (FileNotFoundError, KeyError):
+                pass
+            except Exception as e:  # noqa: BLE001 - e.g. plugins without delete
+                logger.debug(f"could not remove previous metadata: {e}")
+        except Exception as e:  # noqa: BLE001
             logger.debug(f"could not remove previous metadata: {e}")
         # a take with checksums rewrites every rank's file (verify reads only
         # ranks < world size); one without them must not leave the previous
@@ -568,6 +596,25 @@ class Snapshot:
                 pass
             except Exception as e:  # noqa: BLE001
                 logger.debug(f"could not remove previous checksums: {e}")
+        return out
+
+    @staticmethod
+    def _recommit(storage: Optional[StoragePlugin], loop: asyncio.AbstractEventLoop,
+                  stash) -> None:
+        """Put back the commit ``_uncommit`` took away (the take failed
+        before any rank wrote a blob)."""
+        if storage is None or stash is None:
+            return
+        try:
+            if stash[0] == "renamed":
+                run_sync(loop, storage.rename(stash[1], SNAPSHOT_METADATA_FNAME))
+            else:
+                commit = getattr(storage, "commit_metadata", None)
+                run_sync(loop, commit(SNAPSHOT_METADATA_FNAME, stash[1]) if commit is not None
+                         else storage.write(WriteIO(path=SNAPSHOT_METADATA_FNAME,
+                                                    buf=memoryview(stash[1]))))
+        except Exception as e:  # noqa: BLE001 - the take's own error is the one raised
+            logger.warning(f"could not restore the previous snapshot's metadata: {e}")
 
     @classmethod
     def _take_impl(cls, path: str, app_state: AppState, replicated: Set[str],
@@ -875,7 +922,8 @@ class Snapshot:
                 with timeline.span("read_pipeline", cached=True):
                     restore_cache.run(plan, get_process_memory_budget_bytes(comm), verifier)
                     if verifier is not None:
-                        run_sync(loop, verifier.finish(storage))
+                        run_sync(loop, verifier.finish(storage,
+                                                       get_process_memory_budget_bytes(comm)))
                 return
         budget = get_process_memory_budget_bytes(comm)
         # the native job's pinned slots / device rings fill beside the planning

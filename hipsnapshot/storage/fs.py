@@ -184,6 +184,9 @@ class FSStoragePlugin(StoragePlugin):
     async def delete(self, path: str) -> None:
         os.remove(self._abs(path))
 
+    async def rename(self, src: str, dst: str) -> None:
+        os.replace(self._abs(src), self._abs(dst))
+
     async def delete_dir(self, path: str) -> None:
         shutil.rmtree(self._abs(path))
 

@@ -56,3 +56,19 @@ def test_plan_settings_ignore_tracing_and_threads(monkeypatch):
     with knobs.override_knob("RESTORE_SLOTS", 3):
         assert knobs.TUNING.restore_slots == 3
     assert knobs.TUNING.restore_slots == 6
+
+
+def test_build_targets_gfx950_whatever_pytorch_rocm_arch_lists(monkeypatch):
+    """the build took the first PYTORCH_ROCM_ARCH entry (often an
+    older target on ROCm images); the kernels need gfx950."""
+    import pytest
+
+    from hipsnapshot import _build
+
+    monkeypatch.setenv("PYTORCH_ROCM_ARCH", "gfx900;gfx906;gfx942")
+    assert _build.gpu_archs() == ["gfx950"]
+    monkeypatch.setenv("PYTORCH_ROCM_ARCH", "gfx90a;gfx950:xnack-")
+    assert _build.gpu_archs() == ["gfx950:xnack-"]
+    assert _build.gpu_archs("gfx950") == ["gfx950"]
+    with pytest.raises(ValueError):
+        _build.gpu_archs("gfx942")

@@ -122,3 +122,51 @@ def test_read_object_of_a_sharded_entry_without_obj_out(tmp_path):
     finally:
         if own:
             dist.destroy_process_group()
+
+
+def test_partial_blob_verification_stays_within_the_budget(tmp_path):
+    """the end-of-read check of partially read blobs read each blob
+    whole, ignoring the caller's budget.  It now reads budget-sized pieces
+    and adds their hs64 partial sums: a 5 MiB blob checked under a 2 MiB
+    budget never has more than the budget in flight, and the sum of the
+    pieces equals the whole-blob hash (and still finds a flipped byte)."""
+    import asyncio
+
+    from hipsnapshot.engine.blob_verify import RestoreVerifier
+    from hipsnapshot.ops import checksum
+    from hipsnapshot.storage.fs import FSStoragePlugin
+
+    data = torch.randint(0, 255, (5 << 20,), dtype=torch.uint8).numpy().tobytes() + b"xyz"
+    (tmp_path / "blob").write_bytes(data)
+    storage = FSStoragePlugin(str(tmp_path))
+    reads, live, peak = [], [0], [0]
+    orig = storage.read
+
+    async def spy(rio):
+        lo, hi = rio.byte_range if rio.byte_range else (0, len(data))
+        reads.append(hi - lo)
+        live[0] += hi - lo
+        peak[0] = max(peak[0], live[0])
+        await orig(rio)
+        await asyncio.sleep(0.01)  # the piece stays in memory while it is hashed
+        live[0] -= hi - lo
+
+    storage.read = spy
+    v = RestoreVerifier({"blob": checksum.hs64_of(data)})
+    v.note_partial("blob")
+    loop = asyncio.new_event_loop()
+    try:
+        loop.run_until_complete(v.finish(storage, memory_budget_bytes=2 << 20))
+        assert "blob" in v.verified
+        assert sum(reads) == len(data) and len(reads) > 1
+        assert peak[0] <= 2 << 20, peak
+        bad = bytearray(data)
+        bad[(3 << 20) + 5] ^= 1
+        (tmp_path / "blob").write_bytes(bytes(bad))
+        v2 = RestoreVerifier({"blob": checksum.hs64_of(data)})
+        v2.note_partial("blob")
+        with pytest.raises(CorruptBlobError):
+            loop.run_until_complete(v2.finish(storage, memory_budget_bytes=2 << 20))
+        loop.run_until_complete(storage.close())
+    finally:
+        loop.close()

@@ -301,3 +301,37 @@ def test_local_metadata_cache_follows_the_file(tmp_path):
     Snapshot(p).restore({"sd": out})
     assert out["n"] == 2 and torch.equal(out["extra"], torch.zeros(5))
     assert len(snap_mod._metadata_cache) <= 4
+
+
+@pytest.mark.parametrize("url", ["fs", "memory"])
+def test_failed_coalesce_keeps_the_committed_snapshot(tmp_path, monkeypatch, url):
+    """rank 0 takes the old commit away before the coalesce
+    gather (no rank may write a blob while it names them), but a take that
+    fails IN that gather has written nothing: the old commit comes back
+    (renamed back on FS, re-written from the kept bytes elsewhere)."""
+    import uuid
+
+    from hipsnapshot import Snapshot, StateDict
+
+    path = str(tmp_path / "s") if url == "fs" else f"memory://b{uuid.uuid4().hex[:8]}/s"
+    sd = StateDict(w=torch.arange(10.0))
+    Snapshot.take(path, {"sd": sd})
+
+    def boom(*a, **k):
+        raise RuntimeError("coalesce failed")
+
+    monkeypatch.setattr(Snapshot, "_coalesce", classmethod(boom))
+    with pytest.raises(RuntimeError, match="coalesce failed"):
+        Snapshot.take(path, {"sd": StateDict(w=torch.zeros(10))})
+    monkeypatch.undo()
+    out = StateDict(w=torch.zeros(10))
+    Snapshot(path).restore({"sd": out})
+    assert torch.equal(out["w"], torch.arange(10.0))
+    if url == "fs":
+        assert not [f for f in os.listdir(path) if ".stash." in f]
+    # a take that succeeds leaves no stash behind either
+    Snapshot.take(path, {"sd": StateDict(w=torch.ones(10))})
+    if url == "fs":
+        assert not [f for f in os.listdir(path) if ".stash." in f]
+    Snapshot(path).restore({"sd": out})
+    assert torch.equal(out["w"], torch.ones(10))
