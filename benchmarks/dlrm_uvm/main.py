@@ -161,6 +161,7 @@ def main():
           "writer_cpus": rank_diag.cpu_set(), "writer_cpu_nodes": _cpu_nodes(),
           "async_unblock_ms": round(unblock * 1e3, 1), "freeze_gpu_ms": round(freeze_ms, 2),
           "async_total_s": round(async_total, 3),
+          "uvm_capture_stats": _capture_stats(),
           "async_GBps": round(nbytes / async_total / 1e9, 2),
           "host_siblings": args.host_siblings, "sibling_take_ms": [round(x, 1) for x in sib_ms],
           "cold_async_total_s": round(cold_s, 3), "single_path": args.single_path,
@@ -171,6 +172,13 @@ def main():
     if rank == 0:
         shutil.rmtree(root, ignore_errors=True)
     dist.destroy_process_group()
+
+
+def _capture_stats() -> dict:
+    """The last async take's CPU capture of host UVM tables (seconds)."""
+    from hipsnapshot.engine import uvm_capture
+
+    return {k: round(v, 4) for k, v in uvm_capture.last.items()}
 
 
 def _host_state() -> dict:

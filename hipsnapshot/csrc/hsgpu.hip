@@ -30,6 +30,8 @@
 
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1421,6 +1423,7 @@ struct PinnedPool {
   std::unordered_map<void*, size_t> live;       // ptr -> size
   size_t cached_bytes = 0;                        // total allocated (live + free)
   size_t in_use_bytes = 0;
+  std::unordered_map<void*, int> node;            // blocks bound to a NUMA node
 };
 PinnedPool g_pool;
 
@@ -1547,12 +1550,20 @@ struct MappedBlock {
 std::mutex g_mapped_mu;
 std::unordered_map<void*, MappedBlock> g_mapped;  // registered block -> its mapping
 
-void* alloc_thp_registered(size_t want) {
+void* alloc_thp_registered(size_t want, int node = -1) {
   constexpr size_t kHuge = size_t(2) << 20;
   const size_t len = want + kHuge;
   void* base = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (base == MAP_FAILED) return nullptr;
   char* p = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(base) + kHuge - 1) & ~(kHuge - 1));
+  if (node >= 0 && node < 64) {
+    // pages on `node` whichever CPU touches them first (MPOL_BIND = 2)
+    unsigned long mask = 1ul << node;
+    if (syscall(SYS_mbind, p, want, 2, &mask, 65ul, 0u) != 0) {
+      munmap(base, len);
+      return nullptr;
+    }
+  }
   (void)madvise(p, want, MADV_HUGEPAGE);
   // fault every page in now (a huge page per 2 MiB where the kernel grants
   // one): registration then maps resident pages, and no copy pays a fault.
@@ -1592,6 +1603,10 @@ void* alloc_thp_registered(size_t want) {
 }
 
 void free_pinned_block(void* p) {
+  {
+    std::lock_guard<std::mutex> g(g_pool.mu);
+    g_pool.node.erase(p);
+  }
   MappedBlock mb{nullptr, 0};
   {
     std::lock_guard<std::mutex> g(g_mapped_mu);
@@ -1655,6 +1670,38 @@ void* hsg_pinned_acquire(uint64_t nbytes) {
 uint64_t g_pool_limit = ~uint64_t(0);
 
 void hsg_pinned_set_limit(uint64_t bytes) { g_pool_limit = bytes; }
+
+// A pinned block whose pages are bound to NUMA `node` (an async take's UVM
+// capture copies a table into a block on the table's own node, then writes
+// it from there: engine/uvm_capture.py).  Cached separately from the
+// unplaced blocks; node < 0 is hsg_pinned_acquire.
+void* hsg_pinned_acquire_on(uint64_t nbytes, int node) {
+  if (node < 0) return hsg_pinned_acquire(nbytes);
+  const size_t want =
+      (std::max<size_t>(nbytes, 1) + kPinnedGranule - 1) / kPinnedGranule * kPinnedGranule;
+  {
+    std::lock_guard<std::mutex> g(g_pool.mu);
+    for (auto it = g_pool.free_blocks.lower_bound(want);
+         it != g_pool.free_blocks.end() && it->first <= 2 * want; ++it) {
+      auto nd = g_pool.node.find(it->second);
+      if (nd == g_pool.node.end() || nd->second != node) continue;
+      void* p = it->second;
+      const size_t sz = it->first;
+      g_pool.free_blocks.erase(it);
+      g_pool.live[p] = sz;
+      g_pool.in_use_bytes += sz;
+      return p;
+    }
+  }
+  void* p = alloc_thp_registered(want, node);
+  if (p == nullptr) return nullptr;  // the caller falls back to an unplaced block
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  g_pool.live[p] = want;
+  g_pool.node[p] = node;
+  g_pool.cached_bytes += want;
+  g_pool.in_use_bytes += want;
+  return p;
+}
 
 int hsg_pinned_release(void* p) {
   void* drop = nullptr;
@@ -2286,6 +2333,78 @@ void* hsg_managed_alloc(int dev, uint64_t n) {
 int hsg_managed_free(void* p) {
   HS_CHECK(hipFree(p));
   return 0;
+}
+
+// ---- stream gates (engine/uvm_capture.py) ------------------------------------
+//
+// An async take of host-resident UVM tables copies them on the CPU (threads on
+// the pages' NUMA node: ~160-200 GB/s vs ~55 GB/s for the HBM freeze kernel
+// reading them over PCIe, profiles/r6/uvmcap/) while the trainer's stream
+// waits on a host word: hipStreamWaitValue32(word >= v) armed on the stream,
+// released by the CPU once the copy is done.  One word per device, values
+// increase per take, and a release only ever raises the word (an older
+// take's late release cannot re-block a newer gate).
+
+struct GateWord {
+  uint32_t* word = nullptr;
+  uint32_t next = 0;
+};
+std::mutex g_gate_mu;
+std::map<int, GateWord> g_gates;
+
+// 1 if hipStreamWaitValue32 works on `dev` (else the HBM freeze is used).
+int hsg_gate_supported(int dev) {
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return v ? 1 : 0;
+}
+
+// Arm a gate on `stream`: work queued on it from now on waits until the
+// gate's value is released.  *value gets the value to release (> 0).
+int hsg_gate_arm(int dev, void* stream, uint32_t* value) {
+  HS_CHECK(hipSetDevice(dev));
+  std::lock_guard<std::mutex> g(g_gate_mu);
+  GateWord& gw = g_gates[dev];
+  if (gw.word == nullptr) {
+    void* p = nullptr;
+    // signal memory: the command processor polls it, the CPU stores into it;
+    // allocated once per device and never freed
+    HS_CHECK(hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory));
+    gw.word = static_cast<uint32_t*>(p);
+    __atomic_store_n(gw.word, 0u, __ATOMIC_SEQ_CST);
+  }
+  const uint32_t v = ++gw.next;
+  HS_CHECK(hipStreamWaitValue32(static_cast<hipStream_t>(stream), gw.word, v,
+                                hipStreamWaitValueGte, 0xffffffffu));
+  *value = v;
+  return 0;
+}
+
+// Release every gate of `dev` armed with a value <= `value`.
+int hsg_gate_release(int dev, uint32_t value) {
+  uint32_t* w;
+  {
+    std::lock_guard<std::mutex> g(g_gate_mu);
+    auto it = g_gates.find(dev);
+    if (it == g_gates.end() || it->second.word == nullptr) return -1;
+    w = it->second.word;
+  }
+  uint32_t cur = __atomic_load_n(w, __ATOMIC_ACQUIRE);
+  while (cur < value && !__atomic_compare_exchange_n(w, &cur, value, false, __ATOMIC_SEQ_CST,
+                                                     __ATOMIC_ACQUIRE)) {
+  }
+  return 0;
+}
+
+// The gate word's current value (tests).
+uint32_t hsg_gate_value(int dev) {
+  std::lock_guard<std::mutex> g(g_gate_mu);
+  auto it = g_gates.find(dev);
+  if (it == g_gates.end() || it->second.word == nullptr) return 0;
+  return __atomic_load_n(it->second.word, __ATOMIC_ACQUIRE);
 }
 
 // Advised placement of a managed range: *preferred / *last_prefetch get a

@@ -150,6 +150,8 @@ def _layout(write_reqs: List[WriteReq]) -> Dict[int, list]:
     """device -> [(region bytes, member offsets, blob bytes, wr, stagers)]."""
     by_dev = defaultdict(list)
     for wr in write_reqs:
+        if wr.buffer_stager.__dict__.get("captured") is not None:
+            continue  # copied by the CPU (engine/uvm_capture.py)
         sts = _cuda_sources(wr)
         if not sts:
             continue
@@ -170,18 +172,27 @@ def _plan_layout(write_reqs: List[WriteReq], plan) -> Dict[int, list]:
                                       "launch": {}}
     ids = cache["ids"]
     extra = _layout([wr for wr in write_reqs if id(wr) not in ids])
+    base = cache["layout"]
+    if any(r[3].buffer_stager.__dict__.get("captured") is not None
+           for v in base.values() for r in v):
+        # tables the CPU captures this take (engine/uvm_capture.py) stay out
+        base = {d: [r for r in v if r[3].buffer_stager.__dict__.get("captured") is None]
+                for d, v in base.items()}
+        base = {d: v for d, v in base.items() if v}
     if not extra:
-        return cache["layout"]
-    merged = defaultdict(list, {d: list(v) for d, v in cache["layout"].items()})
+        return base
+    merged = defaultdict(list, {d: list(v) for d, v in base.items()})
     for d, v in extra.items():
         merged[d].extend(v)
     return merged
 
 
-def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]:
+def freeze_device_state(write_reqs: List[WriteReq], plan=None,
+                        keep: Optional[set] = None) -> Dict[int, int]:
     """Returns {device: arena_bytes} for the devices that were (partly) frozen.
     ``plan``: the reused take plan the requests come from (layout and the
-    freeze launch's descriptor table are cached on it)."""
+    freeze launch's descriptor table are cached on it).  ``keep``: ids of
+    stagers a reused plan must not reset (taken over by a UVM capture)."""
     if not native.gpu_available():
         return {}
     if plan is not None:
@@ -194,7 +205,7 @@ def freeze_device_state(write_reqs: List[WriteReq], plan=None) -> Dict[int, int]
         by_dev = _plan_layout(write_reqs, plan) if plan is not None else _layout(write_reqs)
     launch_cache = plan.freeze_layout["launch"] if plan is not None else None
     frozen = {}
-    placed: set = set()  # ids of the stagers re-pointed at an arena below
+    placed: set = set(keep or ())  # ids of the stagers re-pointed at an arena below
     try:
         _freeze_devices(by_dev, launch_cache, frozen, placed)
     finally:

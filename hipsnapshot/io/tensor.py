@@ -196,7 +196,11 @@ class TensorBufferStager(BufferStager):
 
     def reset_for_reuse(self) -> None:
         """Back to the planned state for a later take (engine/plan_cache.py):
-        undo an async HBM freeze and order after the caller's current stream."""
+        undo an async HBM freeze or UVM capture and order after the caller's
+        current stream."""
+        cap = self.__dict__.pop("captured", None)
+        if cap is not None:
+            cap[0].drop(cap[1])
         self.tensor = self._plan_tensor
         self.frozen = False
         self.wait_event = None
@@ -236,6 +240,9 @@ class TensorBufferStager(BufferStager):
         return self._tensor_prepare_func is None
 
     def stage_buffer_sync(self):
+        cap = self.__dict__.get("captured")
+        if cap is not None:  # an async take's CPU copy of a host UVM table
+            return cap[0].buffer(cap[1])
         return self._stage_source(self._source())
 
     def _stage_source(self, t: torch.Tensor):

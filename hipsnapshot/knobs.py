@@ -253,6 +253,14 @@ class _Tuning:
     rebalance_min_gain = 0.1
     # -- UVM ------------------------------------------------------------------------------
     uvm_assume_host = None     # None: unless the device runs with XNACK on
+    # async takes copy host-resident UVM tables with CPU threads on the pages'
+    # node while the trainer's stream waits on a gate (engine/uvm_capture.py):
+    # 160-196 GB/s vs 55 GB/s for the HBM freeze over PCIe (profiles/r6/uvmcap/)
+    uvm_async_capture = True
+    uvm_capture_threads = 32
+    # the drain writes a captured table as soon as it is copied (True) or
+    # once the whole capture released the trainer's stream (False)
+    uvm_capture_overlap = False
 
 
 TUNING = _Tuning()

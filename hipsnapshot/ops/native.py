@@ -244,6 +244,7 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
                  [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
         _declare(lib, "hsg_pinned_acquire", c_void_p, [c_uint64])
         _declare(lib, "hsg_pinned_release", c_int, [c_void_p])
+        _declare(lib, "hsg_pinned_acquire_on", c_void_p, [c_uint64, c_int])
         _declare(lib, "hsg_pinned_stats", None, [ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)])
         _declare(lib, "hsg_pinned_trim", c_uint64, [])
         _declare(lib, "hsg_pinned_set_limit", None, [c_uint64])
@@ -305,6 +306,10 @@ def _load_hsgpu() -> Optional[ctypes.CDLL]:
         _declare(lib, "hsg_managed_place", c_int, [c_int, c_void_p, c_uint64, c_int, c_void_p])
         _declare(lib, "hsg_managed_alloc", c_void_p, [c_int, c_uint64])
         _declare(lib, "hsg_managed_free", c_int, [c_void_p])
+        _declare(lib, "hsg_gate_supported", c_int, [c_int])
+        _declare(lib, "hsg_gate_arm", c_int, [c_int, c_void_p, ctypes.POINTER(ctypes.c_uint32)])
+        _declare(lib, "hsg_gate_release", c_int, [c_int, ctypes.c_uint32])
+        _declare(lib, "hsg_gate_value", ctypes.c_uint32, [c_int])
         _declare(lib, "hsg_hsz_last_error", c_char_p, [])
         _declare(lib, "hsg_set_thread_grid_cap", c_int, [c_int])
         _declare(lib, "hsg_hash64", c_int, [c_int, c_int, c_int, c_void_p, c_uint64, c_uint64,
@@ -394,9 +399,13 @@ class PinnedBuffer:
 
     __slots__ = ("ptr", "nbytes", "_released", "_cbuf", "__weakref__")
 
-    def __init__(self, nbytes: int) -> None:
+    def __init__(self, nbytes: int, node: Optional[int] = None) -> None:
         lib = require_gpu_lib()
-        ptr = lib.hsg_pinned_acquire(max(int(nbytes), 1))
+        ptr = None
+        if node is not None and node >= 0:  # pages bound to that NUMA node
+            ptr = lib.hsg_pinned_acquire_on(max(int(nbytes), 1), int(node))
+        if not ptr:
+            ptr = lib.hsg_pinned_acquire(max(int(nbytes), 1))
         if not ptr:
             raise MemoryError(f"pinned allocation of {nbytes} bytes failed: "
                               f"{lib.hsg_last_error().decode()}")
@@ -1078,6 +1087,28 @@ def restore_prewarm(dev: int, up_bytes: int, sc_bytes: int, slot_bytes: int, nsl
     ctypes drops the GIL): 0, or -1 when an allocation failed."""
     return int(require_gpu_lib().hsg_restore_prewarm(dev, up_bytes, sc_bytes, slot_bytes,
                                                      nslots, table_bytes))
+
+
+def gate_supported(dev: int) -> bool:
+    return bool(require_gpu_lib().hsg_gate_supported(dev))
+
+
+def gate_arm(dev: int, stream_handle: int) -> int:
+    """Make work queued on ``stream_handle`` from now on wait for
+    ``gate_release(dev, value)``; returns that value (csrc/hsgpu.hip).  The
+    caller MUST release it on every path."""
+    v = ctypes.c_uint32(0)
+    _check(require_gpu_lib().hsg_gate_arm(dev, stream_handle or None, ctypes.byref(v)),
+           "hsg_gate_arm")
+    return int(v.value)
+
+
+def gate_release(dev: int, value: int) -> None:
+    require_gpu_lib().hsg_gate_release(dev, value)
+
+
+def gate_value(dev: int) -> int:
+    return int(require_gpu_lib().hsg_gate_value(dev))
 
 
 def managed_location(ptr: int, nbytes: int) -> Tuple[int, int]:

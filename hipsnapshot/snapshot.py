@@ -779,9 +779,15 @@ class Snapshot:
         deferred: List[WriteReq] = []
         if is_async and knobs.async_hbm_staging_enabled():
             from .engine.hbm_staging import freeze_device_state, is_deferrable
+            from .engine.uvm_capture import capture_host_uvm
 
+            # host-resident UVM tables: copied by CPU threads while the
+            # trainer's stream waits on a gate, not frozen over PCIe
+            with timeline.span("uvm_capture"):
+                captured = capture_host_uvm(write_reqs, budget)
             with timeline.span("hbm_freeze"):
-                freeze_device_state(write_reqs, plan)
+                freeze_device_state(write_reqs, plan,
+                                    keep={id(wr.buffer_stager) for wr in captured})
             if progress is not None:
                 progress["arenas"] = list({
                     id(r[0]): r[0] for r in (getattr(wr.buffer_stager, "frozen_region", None)
