@@ -24,6 +24,9 @@ from .tracing import timeline
 # metadata / collective phases of a take (snapshot.py span names)
 META_PHASES = ("coalesce", "replicated_entries", "partition", "barrier", "gather_manifest",
                "commit_barrier", "committed_barrier", "write_metadata", "uncommit")
+# ... of which these run on a helper thread beside the writes (their time
+# includes waiting for the slowest rank, not the take's critical path)
+META_BACKGROUND = ("gather_manifest",)
 
 
 def _union_s(events: Sequence[dict]) -> float:
@@ -80,6 +83,8 @@ def summarize(events: List[dict], wall_s: float, cpu_s: float) -> Dict[str, obje
         "cpu_s_per_GB": round(cpu_s / (w_bytes / 1e9), 4) if w_bytes else None,
         "meta_ms": {k: round(v, 2) for k, v in sorted(meta.items())},
         "meta_total_ms": round(sum(meta.values()), 2),
+        "meta_critical_ms": round(sum(v for k, v in meta.items() if k not in META_BACKGROUND),
+                                  2),
     }
 
 
@@ -100,7 +105,8 @@ def measure(take: Callable[[], object]) -> Dict[str, object]:
 def skew(per_rank: List[Dict[str, object]]) -> Dict[str, object]:
     """One line over the ranks: max / median of each timing field, the
     slowest rank, and the phase where it lost the most against the median."""
-    fields = ("take_ms", "d2h_busy_s", "write_busy_s", "cpu_s", "meta_total_ms")
+    fields = ("take_ms", "d2h_busy_s", "write_busy_s", "cpu_s", "meta_total_ms",
+              "meta_critical_ms")
     out: Dict[str, object] = {}
     for f in fields:
         vals = [float(r[f]) for r in per_rank if r.get(f) is not None]
@@ -111,7 +117,7 @@ def skew(per_rank: List[Dict[str, object]]) -> Dict[str, object]:
     slow = max(range(len(takes)), key=lambda i: takes[i])
     out["slowest_rank"] = slow
     gaps = {}
-    for f, scale in (("d2h_busy_s", 1e3), ("write_busy_s", 1e3), ("meta_total_ms", 1.0)):
+    for f, scale in (("d2h_busy_s", 1e3), ("write_busy_s", 1e3), ("meta_critical_ms", 1.0)):
         vals = [float(r[f]) for r in per_rank if r.get(f) is not None]
         if len(vals) == len(per_rank):
             gaps[f] = (float(per_rank[slow][f]) - statistics.median(vals)) * scale

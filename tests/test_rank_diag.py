@@ -25,7 +25,8 @@ def _worker(tmp):
     sk = rank_diag.skew(allr)
     assert sk["take_ms_max_over_median"] >= 1.0
     assert sk["slowest_rank"] in (0, 1)
-    assert sk["slowest_rank_phase"] in ("d2h_busy_s", "write_busy_s", "meta_total_ms")
+    assert sk["slowest_rank_phase"] in ("d2h_busy_s", "write_busy_s", "meta_critical_ms")
+    assert d["meta_critical_ms"] <= d["meta_total_ms"]
 
 
 @pytest.mark.multiproc
