@@ -56,7 +56,15 @@ def _eligible(wr: WriteReq):
     t = st.tensor
     if not t.is_cuda or not t.is_contiguous() or t.numel() == 0:
         return None
-    if not staging._is_managed(t) or not staging.host_resident_managed(t):
+    # a tensor is managed or not for life: the pointer query (a HIP call)
+    # runs once per stager, not on every async take's unblock path
+    ptr = t.data_ptr()
+    if st.__dict__.get("_not_managed") == ptr:
+        return None
+    if not staging._is_managed(t):
+        st._not_managed = ptr
+        return None
+    if not staging.host_resident_managed(t):
         return None
     return t
 

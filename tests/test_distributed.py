@@ -15,7 +15,7 @@ def test_comm_collectives():
     run_distributed(W.comm_collectives, 3)
 
 
-@pytest.mark.parametrize("chunk", [None, 700])
+@pytest.mark.parametrize("chunk", [None, pytest.param(700, marks=pytest.mark.slow)])
 def test_ddp_take_restore_and_upscale(tmp_path, chunk):
     p = str(tmp_path / f"ddp_{chunk}")
     run_distributed(W.ddp_take, 2, p, chunk)
@@ -33,7 +33,8 @@ def test_partition_plan():
     run_distributed(W.partition_plan_check, 4)
 
 
-@pytest.mark.parametrize("save_ws,load_ws", [(2, 2), (2, 1), (2, 3), (4, 2)])
+@pytest.mark.parametrize("save_ws,load_ws", [(2, 2), (2, 1), pytest.param(2, 3, marks=pytest.mark.slow),
+                                              (4, 2)])
 def test_fsdp2_dtensor_resharding(tmp_path, save_ws, load_ws):
     p = str(tmp_path / "fsdp")
     run_distributed(W.fsdp_take, save_ws, p)

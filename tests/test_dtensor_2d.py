@@ -249,6 +249,7 @@ def _restore_worker(tmp: str, target: str, device: str = "cpu"):
 
 
 @pytest.mark.multiproc
+@pytest.mark.slow  # 25 s of CPU; its GPU twin runs in every GPU suite
 def test_fsdp_over_tp_save_and_reshard(tmp_path):
     run_distributed(_save_worker, 4, str(tmp_path))
     for target in ("2d_same", "2d_swapped", "fsdp"):

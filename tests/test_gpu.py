@@ -385,8 +385,8 @@ def test_async_take_partial_hbm_freeze(gpu, tmp_path):
     seen = {}
     orig = hbm_staging.freeze_device_state
 
-    def spy(write_reqs, plan=None):
-        out = orig(write_reqs, plan)
+    def spy(write_reqs, plan=None, **kw):
+        out = orig(write_reqs, plan, **kw)
         seen["frozen"] = out
         seen["kinds"] = [(type(wr.buffer_stager).__name__, hbm_staging.is_deferrable(wr))
                          for wr in write_reqs]
@@ -1149,8 +1149,8 @@ def test_reused_async_plan_full_then_partial_then_full_freeze(gpu, tmp_path, mon
     real_freeze = hbm_staging.freeze_device_state
     frozen_bytes = []
 
-    def spy(write_reqs, plan=None):
-        out = real_freeze(write_reqs, plan)
+    def spy(write_reqs, plan=None, **kw):
+        out = real_freeze(write_reqs, plan, **kw)
         frozen_bytes.append(sum(out.values()))
         return out
 

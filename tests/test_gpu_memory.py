@@ -16,6 +16,22 @@ pytestmark = pytest.mark.gpu
 GiB = 1 << 30
 
 
+@pytest.fixture(autouse=True)
+def _give_hbm_back():
+    """These tests fill the device on purpose: hand torch's cached blocks
+    back to the driver afterwards, or the next tests' worker processes (other
+    processes on the same GPU) find no free HBM."""
+    yield
+    import gc
+
+    from hipsnapshot import release_snapshot_memory
+
+    gc.collect()
+    release_snapshot_memory()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
 def _state(dev, nbytes):
     n = nbytes // 2 // 4
     g = torch.Generator(device=dev).manual_seed(3)
@@ -115,3 +131,18 @@ def test_memory_held_reports_pinned_pool(gpu, tmp_path):
     assert h["pinned_held_bytes"] >= h["pinned_in_use_bytes"] >= 0
     assert h["hbm_held_bytes"] == (h["hbm_arena_bytes"] + h["restore_pool_idle_bytes"]
                                    + h["restore_pool_live_bytes"] + h["uncached_pool_bytes"])
+
+
+def test_vmm_free_gives_the_memory_back(gpu):
+    """hsg_rt_vmm_free unmaps and releases the physical memory (the virtual
+    range stays reserved): 100 cycles of 4 GiB (400 GiB in all) leave the
+    device's free memory where it was."""
+    lib = __import__("hipsnapshot.ops.native", fromlist=["x"]).require_gpu_lib()
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    for i in range(100):
+        p = lib.hsg_rt_vmm_alloc(0, 4 * GiB, i % 2)
+        assert p, lib.hsg_rt_last_error()
+        assert lib.hsg_rt_vmm_free(p) == 0
+    free1, _ = torch.cuda.mem_get_info()
+    assert free1 >= free0 - GiB, (free0, free1)
