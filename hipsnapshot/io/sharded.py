@@ -41,6 +41,7 @@ import torch
 from ..format.manifest import Shard, ShardedTensorEntry, TensorEntry
 from ..format.serialization import SER, string_to_dtype
 from ..io_types import BufferConsumer, CompressedSpan, Future, ReadReq, StagedBuffer, WriteReq
+from .. import knobs
 from ..knobs import get_max_shard_size_bytes
 from ..engine import staging
 from .tensor import (
@@ -254,8 +255,6 @@ def split_for_replicas(boxes, j: int, r: int, itemsize: int, shape: Sequence[int
 
 
 def _dtensor_layout(dt, for_write: bool):
-    from .. import knobs
-
     key = (dt._spec, for_write, knobs.TUNING.replica_split_min_bytes)
     hit = _LAYOUT_CACHE.get(key)
     if hit is not None:
@@ -279,8 +278,6 @@ def _dtensor_layout(dt, for_write: bool):
 
 
 def _dtensor_boxes(dt, for_write: bool) -> List[LocalBox]:
-    from .. import knobs
-
     spec = dt._spec
     key = (id(spec), for_write, knobs.TUNING.replica_split_min_bytes)
     ent = _LAYOUT_BY_ID.get(key)

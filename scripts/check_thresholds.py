@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Regression guard for the single-GPU benchmark set (scripts/gpu_bench_all_r5.sh):
+"""Regression guard for the single-GPU benchmark set (scripts/gpu/benches.sh):
 ``check_thresholds.py <dir with one JSON per benchmark>`` compares each
 metric with its floor (or ceiling) in scripts/bench_thresholds.json and exits 1
 when any is missed.  Floors sit ~20 % under the round-5 measurements:
