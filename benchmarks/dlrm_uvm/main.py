@@ -122,6 +122,7 @@ def main():
     sync(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
+    cg0 = _cgroup_cpu()
     with Timer() as ta:
         with Timer() as tu:
             if sib is not None:
@@ -131,6 +132,9 @@ def main():
         e1.synchronize()
         pending.wait()
     freeze_ms = e0.elapsed_time(e1)  # the trainer stream's busy time (HBM freeze)
+    cg1 = _cgroup_cpu()
+    async_cgroup = {k: cg1[k] - cg0[k] for k in cg0 if isinstance(cg0[k], int) and k in cg1}
+    async_cgroup["cpu_max"] = cg1.get("cpu_max")
     unblock = max_over_ranks(tu.s, dev)
     async_total = max_over_ranks(ta.s, dev)
     if sib is not None:
@@ -162,6 +166,8 @@ def main():
           "async_unblock_ms": round(unblock * 1e3, 1), "freeze_gpu_ms": round(freeze_ms, 2),
           "async_total_s": round(async_total, 3),
           "uvm_capture_stats": _capture_stats(),
+          # CPU time and CFS throttling of the job's cgroup over the async take
+          "async_cgroup": async_cgroup,
           "async_GBps": round(nbytes / async_total / 1e9, 2),
           "host_siblings": args.host_siblings, "sibling_take_ms": [round(x, 1) for x in sib_ms],
           "cold_async_total_s": round(cold_s, 3), "single_path": args.single_path,
@@ -177,8 +183,55 @@ def main():
 def _capture_stats() -> dict:
     """The last async take's CPU capture of host UVM tables (seconds)."""
     from hipsnapshot.engine import uvm_capture
+    from hipsnapshot.utils.affinity import pages_node
 
-    return {k: round(v, 4) for k, v in uvm_capture.last.items()}
+    out = {k: round(v, 4) for k, v in uvm_capture.last.items() if isinstance(v, (int, float))}
+    tables = uvm_capture.last.get("tables") or []
+    if tables:
+        thp = _thp_of([ptr for *_x, ptr in tables])
+        out["tables"] = [
+            {"GB": round(n / 1e9, 3), "s": round(s, 4), "GBps": round(n / max(s, 1e-9) / 1e9, 1),
+             "src_node": node, "dst_node": pages_node(ptr, n), "dst_thp_frac": thp.get(ptr)}
+            for n, s, node, ptr in tables]
+    return out
+
+
+def _cgroup_cpu() -> dict:
+    """The cgroup's CPU quota and usage / throttling counters (cgroup v2)."""
+    out: dict = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                    out[k] = int(v)
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            out["cpu_max"] = f.read().strip()
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def _thp_of(ptrs) -> dict:
+    """Fraction of the mapping holding each address that is backed by
+    transparent huge pages (/proc/self/smaps AnonHugePages / Size)."""
+    want = sorted(set(ptrs))
+    out, cur = {}, None
+    try:
+        with open("/proc/self/smaps") as f:
+            for line in f:
+                head = line.split(None, 1)[0]
+                if "-" in head and not head.endswith(":"):
+                    lo, hi = (int(x, 16) for x in head.split("-"))
+                    cur = [p for p in want if lo <= p < hi] or None
+                    size = hi - lo
+                elif cur and head == "AnonHugePages:":
+                    kb = int(line.split()[1])
+                    for p in cur:
+                        out[p] = round(kb * 1024 / max(size, 1), 3)
+    except OSError:
+        pass
+    return out
 
 
 def _host_state() -> dict:

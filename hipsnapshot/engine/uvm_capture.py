@@ -93,7 +93,7 @@ class Capture:
         self.done = [threading.Event() for _ in items]
         self.error: Optional[BaseException] = None
         self.value: Optional[int] = None
-        self.stats: Dict[str, float] = {}
+        self.stats: Dict[str, object] = {}
         self._thread: Optional[threading.Thread] = None
         self._t_start = self._t_blocks = 0.0
 
@@ -150,7 +150,10 @@ class Capture:
             # sequential tables at 16 threads each copied at ~100 GB/s, this
             # at 160-196 (scripts/probes/uvm_capture_probe.py)
             per = max(1, nthreads // max(1, len(self.items)))
+            # (a work queue of 32 MiB pieces over the tables copied at 97-182
+            # GB/s where this split did 131-200: profiles/r6/uvmcap/r6b/)
             errs: List[BaseException] = []
+            per_table: List[Optional[tuple]] = [None] * len(self.items)
             sem = threading.Semaphore(nthreads)
 
             def copy(i: int, t, n: int) -> None:
@@ -165,8 +168,9 @@ class Capture:
                             os.sched_setaffinity(0, mask)  # this thread, then its helpers
                     ts = time.perf_counter()
                     lib.hsio_parallel_memcpy(self.blocks[i].ptr, t.data_ptr(), n, per)
-                    timeline.add("uvm_capture", "d2h", ts, time.perf_counter(), bytes=n,
-                                 node=node)
+                    te = time.perf_counter()
+                    timeline.add("uvm_capture", "d2h", ts, te, bytes=n, node=node)
+                    per_table[i] = (n, te - ts, node, self.blocks[i].ptr)
                     if knobs.TUNING.uvm_capture_overlap:
                         self.done[i].set()
                 except BaseException as e:  # noqa: BLE001
@@ -190,7 +194,10 @@ class Capture:
             self.stats = {"wait_s": t1 - t0, "copy_s": time.perf_counter() - t1,
                           "bytes": float(sum(n for _s, _t, n in self.items)),
                           "start_to_release_s": time.perf_counter() - self._t_start,
-                          "blocks_s": self._t_blocks - self._t_start}
+                          "blocks_s": self._t_blocks - self._t_start,
+                          "threads_per_table": per,
+                          # (bytes, seconds, pages' node, block address) per table
+                          "tables": [r for r in per_table if r is not None]}
         except BaseException as e:  # noqa: BLE001 - reported by the stagers
             self.error = e
         finally:
@@ -242,7 +249,7 @@ class Capture:
                 self.blocks[i] = None
 
 
-last: Dict[str, float] = {}  # the last capture's seconds (benchmarks)
+last: Dict[str, object] = {}  # the last capture's seconds (benchmarks)
 
 
 def capture_host_uvm(write_reqs: List[WriteReq], budget: Optional[int] = None) -> List[WriteReq]:

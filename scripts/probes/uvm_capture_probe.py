@@ -56,12 +56,12 @@ def main():
     out["gpu_freeze_GBps"] = round(total / min(times) / 1e9, 1)
     del arena
     # CPU capture into pinned blocks, threads on the pages' node
-    pbs = [native.PinnedBuffer(per) for _ in tabs]
+    pbs = [native.PinnedBuffer(per, node) for _ in tabs]
     mask = (node_cpus(node) & os.sched_getaffinity(0)) if node is not None else None
     lib = native.hsio()
-    for nthreads in (4, 8, 16, 32, 64):
+    for nthreads in (16, 32):
         times = []
-        for _ in range(3):
+        for _ in range(5):
             t0 = time.perf_counter()
             with threads_with_mask(mask):
                 import threading
@@ -77,6 +77,29 @@ def main():
                     th.join()
             times.append(time.perf_counter() - t0)
         out[f"cpu_capture_{nthreads}t_GBps"] = round(total / min(times) / 1e9, 1)
+        out[f"cpu_capture_{nthreads}t_GBps_median"] = round(
+            total / sorted(times)[len(times) // 2] / 1e9, 1)
+    # the library's capture loop (engine/uvm_capture.py): 32 MiB pieces that
+    # a pool of workers pulls, each worker on the pages' node
+    import statistics
+    import types
+
+    from hipsnapshot.engine import uvm_capture
+    from hipsnapshot.knobs import override_tuning
+
+    uvm_capture.native.gate_release = lambda dev, v: None  # no gate armed here
+    for nthreads in (16, 32):
+        times = []
+        for _ in range(5):
+            cap = uvm_capture.Capture(dev, [(types.SimpleNamespace(), t, per) for t in tabs])
+            cap.blocks = list(pbs)
+            with override_tuning(uvm_capture_threads=nthreads):
+                t0 = time.perf_counter()
+                cap._run([])
+                times.append(time.perf_counter() - t0)
+            assert cap.error is None, cap.error
+        out[f"pieces_{nthreads}t_GBps"] = round(total / min(times) / 1e9, 1)
+        out[f"pieces_{nthreads}t_GBps_median"] = round(total / statistics.median(times) / 1e9, 1)
     ok = all(torch.equal(torch.frombuffer(pb.view, dtype=torch.float32)[: per // 4],
                          t.cpu()) for pb, t in zip(pbs, tabs))
     out["capture_bitwise"] = ok

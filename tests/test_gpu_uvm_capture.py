@@ -71,7 +71,8 @@ def test_async_take_captures_host_uvm_tables_on_the_cpu(gpu, tmp_path):
     assert memory_held(gpu.index or 0)["hbm_arena_bytes"] == 0  # no HBM freeze
     assert all(torch.equal(t, r + 1.0) for t, r in zip(ts, ref))
     out = StateDict(**{f"t{i}": torch.zeros_like(r) for i, r in enumerate(ref)})
-    Snapshot(str(tmp_path / "a")).restore({"sd": out})
+    # verify=True: the checksums the capture computed while copying match
+    Snapshot(str(tmp_path / "a")).restore({"sd": out}, verify=True)
     for i, r in enumerate(ref):
         assert torch.equal(out[f"t{i}"], r), i
     # a second async take reuses the plan and captures again
