@@ -95,10 +95,21 @@ def main():
     for _ in range(max(1, args.sync_repeats)):
         before = _host_state()
         nodes_before = _node_state()
+        cg0 = _cgroup_cpu()
+        hb0 = _host_busy()
         if sib is not None:
             sib.go()
         d = rank_diag.measure(lambda: (Snapshot.take(p_sync, {"model": model}), sync(dev)))
+        hb1 = _host_busy()
+        cg1 = _cgroup_cpu()
+        wall = max(d["take_ms"] / 1e3, 1e-6)
+        # the whole host's busy CPUs per node during the take (this job's
+        # included: ``cgroup.usage_usec`` / wall is this job's share)
+        d["host_busy_cpus"] = {n: round((hb1[n] - hb0.get(n, 0)) / _HZ / wall, 1) for n in hb1}
         after = _host_state()
+        # the job's CPU quota: periods throttled and the whole cgroup's CPU
+        # time during this take (other processes of the job included)
+        d["cgroup"] = {k: cg1[k] - cg0[k] for k in cg0 if isinstance(cg0[k], int) and k in cg1}
         d["take_s"] = max_over_ranks(d["take_ms"] / 1e3, dev)
         d["GBps"] = round(nbytes / d["take_s"] / 1e9, 2)
         d["dirty_kB_before"], d["writeback_kB_before"] = before["Dirty"], before["Writeback"]
@@ -193,6 +204,57 @@ def _capture_stats() -> dict:
             {"GB": round(n / 1e9, 3), "s": round(s, 4), "GBps": round(n / max(s, 1e-9) / 1e9, 1),
              "src_node": node, "dst_node": pages_node(ptr, n), "dst_thp_frac": thp.get(ptr)}
             for n, s, node, ptr in tables]
+    return out
+
+
+_HZ = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
+
+
+def _host_busy() -> dict:
+    """Busy CPU jiffies (all but idle and iowait) per NUMA node, summed over
+    every CPU of the host (/proc/stat): load from other tenants shows here."""
+    node_of = {}
+    for n, ids in _node_cpu_ids().items():
+        for c in ids:
+            node_of[c] = n
+    out: dict = {}
+    try:
+        with open("/proc/stat") as f:
+            for line in f:
+                if not line.startswith("cpu") or line.startswith("cpu "):
+                    continue
+                parts = line.split()
+                c = int(parts[0][3:])
+                v = [int(x) for x in parts[1:9]]
+                busy = sum(v) - v[3] - v[4]
+                n = node_of.get(c, "?")
+                out[n] = out.get(n, 0) + busy
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def _node_cpu_ids() -> dict:
+    base = "/sys/devices/system/node"
+    out: dict = {}
+    try:
+        nodes = [d for d in os.listdir(base) if d.startswith("node")]
+    except OSError:
+        return out
+    for d in nodes:
+        try:
+            with open(f"{base}/{d}/cpulist") as f:
+                spec = f.read().strip()
+        except OSError:
+            continue
+        ids = set()
+        for part in spec.split(","):
+            if "-" in part:
+                a, b = part.split("-")
+                ids.update(range(int(a), int(b) + 1))
+            elif part:
+                ids.add(int(part))
+        out[d] = ids
     return out
 
 
