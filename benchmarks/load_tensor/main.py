@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=50000)
     ap.add_argument("--budget-mb", type=int, default=100)
+    ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--work-dir", default=os.environ.get("HSBENCH_DIR", "/tmp"))
     args = ap.parse_args()
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
@@ -34,18 +35,28 @@ def main():
     Snapshot.take(root, {"sd": StateDict(t=t)})
     nbytes = t.numel() * 4
     results = {}
-    for name, budget in (("no_budget", None), ("budget", args.budget_mb << 20)):
-        out = torch.empty_like(t)
-        deltas = []
-        t0 = time.perf_counter()
-        with measure_rss_deltas(deltas):
-            Snapshot(root).read_object("0/sd/t", obj_out=out, memory_budget_bytes=budget)
+    # alternated, twice each: the first read of a process pays its plans and
+    # pools, whichever mode goes first; "GBps" is the better of the two
+    out = torch.empty_like(t)
+    for rnd in range(args.rounds):
+        for name, budget in (("no_budget", None), ("budget", args.budget_mb << 20)):
+            out.zero_()
+            deltas = []
             if dev.type == "cuda":
                 torch.cuda.synchronize()
-        s = time.perf_counter() - t0
-        assert torch.equal(out, t)
-        results[name] = {"seconds": round(s, 3), "GBps": round(nbytes / s / 1e9, 2),
-                         "peak_rss_delta_MB": round(max(deltas) / 2 ** 20, 1)}
+            t0 = time.perf_counter()
+            with measure_rss_deltas(deltas):
+                Snapshot(root).read_object("0/sd/t", obj_out=out, memory_budget_bytes=budget)
+                if dev.type == "cuda":
+                    torch.cuda.synchronize()
+            s = time.perf_counter() - t0
+            assert torch.equal(out, t)
+            r = results.setdefault(name, {"GBps_each": [], "peak_rss_delta_MB": 0.0})
+            r["GBps_each"].append(round(nbytes / s / 1e9, 2))
+            r["peak_rss_delta_MB"] = max(r["peak_rss_delta_MB"], round(max(deltas) / 2 ** 20, 1))
+    for r in results.values():
+        r["GBps"] = max(r["GBps_each"])
+        r["seconds"] = round(nbytes / r["GBps"] / 1e9, 3)
     print(json.dumps({"bench": "load_tensor", "bytes": nbytes, **results}))
     shutil.rmtree(root, ignore_errors=True)
 
