@@ -159,7 +159,11 @@ def sizing(budget: Optional[int]) -> Tuple[int, int, int]:
                       knobs.get_restore_slots())
     if budget:
         cap = max(2 << 20, int(budget) // 2)
-        n = max(2, min(n, cap // slot))
+        # the knob's slot count, down to 4 MiB slots: the same pinned bytes in
+        # a deeper pipeline (2 slots of 25 MiB under a 100 MB budget kept one
+        # read and one DMA in flight: 37-40 GB/s, where unbudgeted reads run
+        # at 52 GB/s, profiles/r6/benches/)
+        n = max(2, min(n, cap // (4 << 20)))
         slot = max(1 << 20, min(slot, cap // n))
     return slot, min(first, slot), n
 

@@ -11,6 +11,7 @@ def test_sizing_defaults_and_budget():
     # a 100 MiB read budget: the pinned slots take at most half of it
     slot, first, n = native_restore.sizing(100 << 20)
     assert slot * n <= 50 << 20 and n >= 2 and first <= slot
+    assert n == 6 and slot >= 4 << 20  # a deep pipeline of small slots, not 2 big ones
     # tiny budgets still get two 1 MiB slots
     slot, first, n = native_restore.sizing(1 << 20)
     assert (slot, n) == (1 << 20, 2) and first == 1 << 20
