@@ -70,12 +70,6 @@ def flatten(obj: Any, prefix: str) -> Tuple[Manifest, Dict[str, Any]]:
     return manifest, flattened
 
 
-def _is_int_str(s: str) -> bool:
-    if s.isdigit():
-        return True
-    return len(s) > 1 and s[0] in "+-" and s[1:].isdigit()
-
-
 def _container_for(entry: Entry) -> Any:
     if isinstance(entry, ListEntry):
         return []
@@ -118,15 +112,15 @@ def inflate(manifest: Manifest, flattened: Dict[str, Any], prefix: str) -> Any:
         if isinstance(container, list):
             container.extend(v for _, v in sorted(vals.items(), key=lambda kv: int(kv[0])))
         elif isinstance(container, dict):
-            by_key: Dict[Any, Any] = {}
-            for k, v in vals.items():
-                dk = decode_key(k)
-                by_key[dk] = v
-                if _is_int_str(dk):
-                    by_key[int(dk)] = v
+            # flatten() names a child by str(key), and the str forms of one
+            # dict's keys are unique, so the match is exact.  (The reference
+            # also maps every int-looking segment to an int key, so
+            # {1: a, "+1": b} came back as {1: b, "+1": b}.)
+            by_key: Dict[str, Any] = {decode_key(k): v for k, v in vals.items()}
             for k in list(container.keys()):
-                if k in by_key:
-                    container[k] = by_key[k]
+                sk = str(k)
+                if sk in by_key:
+                    container[k] = by_key[sk]
                 else:
                     del container[k]
         else:
