@@ -80,6 +80,8 @@ class ChunkedTensorIOPreparer:
     def prepare_read(cls, entry: ChunkedTensorEntry, tensor_out: Optional[torch.Tensor] = None,
                      buffer_size_limit_bytes: Optional[int] = None
                      ) -> Tuple[List[ReadReq], Future]:
+        if _is_quantized_entry(entry) or (tensor_out is not None and tensor_out.is_quantized):
+            return _read_quantized_chunks(entry, tensor_out, buffer_size_limit_bytes)
         if tensor_out is None or not TensorIOPreparer.can_load_inplace(entry, tensor_out):
             tensor_out = TensorIOPreparer.empty_tensor_from_entry(entry)
         reqs: List[ReadReq] = []
@@ -88,3 +90,67 @@ class ChunkedTensorIOPreparer:
                                                    buffer_size_limit_bytes)
             reqs += rrs
         return reqs, Future(obj=tensor_out)
+
+
+def _is_quantized_entry(entry: ChunkedTensorEntry) -> bool:
+    from ..format.serialization import SUPPORTED_QUANTIZED_DTYPES, string_to_dtype
+
+    try:
+        return string_to_dtype(entry.dtype) in SUPPORTED_QUANTIZED_DTYPES
+    except Exception:  # noqa: BLE001 - an unknown dtype string: not quantized
+        return False
+
+
+class _JoinedQuantized(Future):
+    """A chunked quantized tensor.  Its chunks load as tensors of their own: a
+    chunk-sized view of the destination cannot take the saved scale / zero
+    point (``copy_`` moves qparams onto the view only), so the chunks are
+    joined on first access and copied into ``out`` whole."""
+
+    def __init__(self, parts: List[Future], entry: ChunkedTensorEntry,
+                 out: Optional[torch.Tensor]) -> None:
+        self._parts, self._entry, self._out, self._done = parts, entry, out, False
+
+    @property
+    def obj(self):
+        if not self._done:
+            self._out = _join_quantized([f.obj for f in self._parts], self._entry, self._out)
+            self._done = True
+        return self._out
+
+    @obj.setter
+    def obj(self, value) -> None:
+        self._out, self._done = value, True
+
+
+def _join_quantized(parts: List[torch.Tensor], entry: ChunkedTensorEntry,
+                    out: Optional[torch.Tensor]) -> torch.Tensor:
+    from .tensor import tensor_copy
+
+    shape = list(entry.shape)
+    flat0 = len(shape) == 0  # a 0-d tensor was chunked as a 1-d view
+    if parts[0].qscheme() in (torch.per_tensor_affine, torch.per_tensor_symmetric):
+        full = torch.cat(parts, dim=0)
+    else:
+        axis = parts[0].q_per_channel_axis()
+        cat = lambda f: torch.cat([f(p) for p in parts]) if axis == 0 else f(parts[0])  # noqa
+        full = torch._make_per_channel_quantized_tensor(
+            torch.cat([p.int_repr() for p in parts], dim=0),
+            cat(lambda p: p.q_per_channel_scales()),
+            cat(lambda p: p.q_per_channel_zero_points()), axis)
+    full = full.reshape(shape) if not flat0 else full.reshape([])
+    if out is None:
+        return full
+    tensor_copy(out, full)
+    return out
+
+
+def _read_quantized_chunks(entry: ChunkedTensorEntry, tensor_out: Optional[torch.Tensor],
+                           limit: Optional[int]) -> Tuple[List[ReadReq], Future]:
+    reqs: List[ReadReq] = []
+    parts: List[Future] = []
+    for ch in sorted(entry.chunks, key=lambda c: list(c.offsets)):
+        rrs, fut = TensorIOPreparer.prepare_read(ch.tensor, None, limit)
+        reqs += rrs
+        parts.append(fut)
+    return reqs, _JoinedQuantized(parts, entry, tensor_out)

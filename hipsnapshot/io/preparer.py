@@ -108,7 +108,9 @@ def _write_sharded(obj, path, is_async, prepare_func, serializer, max_chunk, max
 
 def _write_tensor(obj, path, is_async, prepare_func, serializer, max_chunk, max_shard):
     max_chunk = max_chunk or get_max_chunk_size_bytes()
-    if obj.numel() * obj.element_size() > max_chunk:
+    # quantized tensors stay whole (the reference chunks them too): a chunk
+    # restored into a view of the destination could not carry its qparams
+    if obj.numel() * obj.element_size() > max_chunk and not obj.is_quantized:
         return ChunkedTensorIOPreparer.prepare_write(
             storage_path=path, tensor=obj,
             chunking_instruction=ChunkedTensorIOPreparer.chunk_tensor(obj,

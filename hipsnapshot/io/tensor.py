@@ -446,4 +446,8 @@ def tensor_copy(dst: torch.Tensor, src: torch.Tensor) -> None:
             or (dst._is_view() and not _q_params_equal(dst, src))):
         src = src.dequantize()
     with torch.no_grad():
-        dst.detach().copy_(src)
+        # quantized -> quantized copy_ also moves the qparams onto its
+        # destination: that must be ``dst`` itself, not a detach()'d alias
+        # (the alias took the new scale / zero point, ``dst`` kept its old
+        # ones and read back wrong values)
+        (dst if dst.is_quantized else dst.detach()).copy_(src)
