@@ -1,0 +1,98 @@
+"""Randomised distributed round trips (4 gloo ranks on the CPU): random
+DTensor layouts -- 1-D and 2-D meshes, ``Shard`` / ``Replicate`` on any dim,
+uneven shapes -- saved, then restored into ANOTHER random layout (elastic
+resharding, HSDP replica splits, replicated <-> sharded) and read whole with
+``read_object``; every case is compared with the global tensor.  torch's own
+``distribute_tensor`` builds both layouts, so the ground truth is not ours.
+
+Reference: the hand-picked resharding matrix of
+`/root/reference/tests/test_sharded_tensor_resharding.py`.
+"""
+
+import os
+import random
+
+import pytest
+import torch
+
+from hipsnapshot.utils.test_utils import run_distributed
+
+pytestmark = pytest.mark.multiproc
+
+MESHES = [(4,), (2, 2), (1, 4), (4, 1)]
+
+
+def _layout(rng: random.Random, ndim: int):
+    from torch.distributed.tensor import Replicate, Shard
+
+    mesh = rng.choice(MESHES)
+    pl = [Shard(rng.randrange(ndim)) if rng.random() < 0.7 else Replicate() for _ in mesh]
+    return mesh, pl
+
+
+def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import DTensor, distribute_tensor
+
+    from hipsnapshot import Snapshot, StateDict, knobs
+
+    rng = random.Random(seed)  # the same stream on every rank
+    meshes = {}
+
+    def mesh_of(shape, dev_type="cpu"):
+        if (shape, dev_type) not in meshes:
+            meshes[(shape, dev_type)] = init_device_mesh(dev_type, shape)
+        return meshes[(shape, dev_type)]
+
+    def place(glob, shape, pl):
+        """``glob`` laid out by torch (on a CPU mesh), then, for a GPU run,
+        the same local pieces as DTensors of HIP tensors (no collectives on
+        them: gloo ranks share the one GPU)."""
+        cpu = distribute_tensor(glob, mesh_of(shape), pl)
+        if device == "cpu":
+            return cpu
+        if device.startswith("cuda"):
+            torch.cuda.set_device(torch.device(device))
+        return DTensor.from_local(cpu.to_local().to(device), mesh_of(shape, "cuda"), pl,
+                                  run_check=False, shape=cpu.shape, stride=cpu.stride())
+
+    for case in range(n_cases):
+        ndim = rng.randint(1, 3)
+        shape = [rng.randint(1, 13) for _ in range(ndim)]
+        dtype = rng.choice([torch.float32, torch.bfloat16, torch.int64, torch.float64])
+        g = torch.Generator().manual_seed(seed * 1000 + case)
+        glob = (torch.randn(shape, generator=g) * 100).to(dtype)
+        save_mesh, save_pl = _layout(rng, ndim)
+        load_mesh, load_pl = _layout(rng, ndim)
+        compression = rng.choice(["none", "hsz1"])
+        batching = rng.random() < 0.7
+        what = (case, shape, dtype, save_mesh, save_pl, load_mesh, load_pl, compression,
+                batching)
+        path = os.path.join(root, f"c{case}")
+        src = place(glob, save_mesh, save_pl)
+        with knobs.override_is_batching_disabled(not batching):
+            snap = Snapshot.take(path, {"s": StateDict(t=src, step=case)},
+                                 compression=compression)
+            dst = place(torch.zeros_like(glob), load_mesh, load_pl)
+            app = {"s": StateDict(t=dst, step=-1)}
+            Snapshot(path).restore(app)
+        got = app["s"]["t"].to_local().cpu()
+        assert torch.equal(got, place(glob, load_mesh, load_pl).to_local().cpu()), what
+        assert app["s"]["step"] == case, what
+        whole = torch.zeros_like(glob, device=device)
+        snap.read_object("0/s/t", obj_out=whole)
+        assert torch.equal(whole.cpu(), glob), what
+        dist.barrier()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_dtensor_layouts_reshard_exactly(tmp_path, seed):
+    run_distributed(_worker, 4, str(tmp_path), 14, seed, timeout=400)
+
+
+@pytest.mark.gpu
+def test_random_dtensor_layouts_reshard_exactly_gpu(gpu, tmp_path):
+    """The same with every local piece on cuda:0 (4 gloo ranks sharing it):
+    staging, HSZ1 and the native restore's scatter under random layouts."""
+    run_distributed(_worker, 4, str(tmp_path), 24, 7, "cuda:0", timeout=600)
