@@ -108,13 +108,21 @@ def _round_trip(tmp_path, seed: int, device: str) -> None:
                 if c is not None:
                     c.__exit__(None, None, None)
     assert_state_dict_eq(dict(target["app"]), state, f"case {case}")
-    # read_object of one leaf (a tensor leaf: into a fresh buffer)
-    flat = sorted(p for p in snap.get_manifest() if p.startswith("0/app/"))
-    leaves = [p for p in flat if snap.get_manifest()[p].type in ("Tensor", "ChunkedTensor")]
-    if leaves:
-        p = rng.choice(leaves)
-        got = snap.read_object(p)
-        assert isinstance(got, torch.Tensor), (case, p)
+    # read_object of top-level tensor leaves: into a fresh buffer, and into a
+    # zeroed obj_out under a random memory budget (tiled reads)
+    from hipsnapshot.format.flatten import encode_key
+
+    for key, v in state.items():
+        if not isinstance(v, torch.Tensor):
+            continue
+        p = f"0/app/{encode_key(key)}"
+        assert_state_dict_eq(snap.read_object(p), v, f"read_object {p} {case}")
+        if v.is_quantized or v.numel() == 0:
+            continue
+        budget = rng.choice([None, 4096, 100_000])
+        out = _blank(v)
+        snap.read_object(p, obj_out=out, memory_budget_bytes=budget)
+        assert_state_dict_eq(out, v, f"read_object {p} budget {budget} {case}")
 
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("HS_E2E_SEEDS", "100"))))
