@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import asyncio
 import datetime as _dt
+import random
 import re
 import threading
 import uuid
@@ -33,14 +34,26 @@ class _ServerThread:
         self._thread = threading.Thread(target=self.loop.run_forever, daemon=True)
         self.fail_queue: list = []
         self.requests = 0
+        self.fail_rate = 0.0
+        self.injected = 0  # requests failed by fail_randomly
+        self._fail_rng = random.Random(0)
 
     def fail_next(self, n: int = 1, status: int = 503) -> None:
         self.fail_queue.extend([status] * n)
+
+    def fail_randomly(self, rate: float, seed: int = 0) -> None:
+        """Fail each later request with probability ``rate`` (a transient
+        408 / 429 / 500 / 503, seeded): a flaky service for retry tests."""
+        self.fail_rate, self._fail_rng = float(rate), random.Random(seed)
 
     def _maybe_fail(self) -> Optional[web.Response]:
         self.requests += 1
         if self.fail_queue:
             return web.Response(status=self.fail_queue.pop(0), text="injected")
+        if self.fail_rate and self._fail_rng.random() < self.fail_rate:
+            self.injected += 1
+            return web.Response(status=self._fail_rng.choice((408, 429, 500, 503)),
+                                text="injected")
         return None
 
     def start(self, app: web.Application) -> "_ServerThread":
@@ -118,6 +131,9 @@ class FakeS3Server:
         self.uploads: Dict[str, Dict[int, bytearray]] = {}
         self.fail_queue: list = []
         self.requests = 0
+        self.fail_rate = 0.0
+        self.injected = 0  # requests failed by fail_randomly
+        self._fail_rng = random.Random(0)
         self._lock = threading.Lock()
         server = self
 
@@ -194,6 +210,12 @@ class FakeS3Server:
     def fail_next(self, n: int = 1, status: int = 503) -> None:
         self.fail_queue.extend([status] * n)
 
+    def fail_randomly(self, rate: float, seed: int = 0) -> None:
+        """Fail each later request with probability ``rate`` (a transient
+        429 / 500 / 503, seeded): a flaky service for retry tests."""
+        with self._lock:
+            self.fail_rate, self._fail_rng = float(rate), random.Random(seed)
+
     def stop(self) -> None:
         self._httpd.shutdown()
         self._httpd.server_close()
@@ -240,6 +262,9 @@ class FakeS3Server:
         with self._lock:
             self.requests += 1
             fail = self.fail_queue.pop(0) if self.fail_queue else None
+            if fail is None and self.fail_rate and self._fail_rng.random() < self.fail_rate:
+                fail = self._fail_rng.choice((429, 500, 503))
+                self.injected += 1
         if fail is not None:
             return fail, b"injected"
         bad = self._verify(h, path, q, body)

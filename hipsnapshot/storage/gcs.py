@@ -162,7 +162,14 @@ class GCSStoragePlugin(StoragePlugin):
                     headers=self._headers({"Content-Range": f"bytes {offset}-{end - 1}/{total}"}))
             except Exception as e:  # noqa: BLE001
                 await retry.backoff(e)
-                offset = await self._query_offset(session_url, total)
+                # where the service got to: the status query is retried the
+                # same way (a flaky service fails it too)
+                offset = None
+                while offset is None:
+                    try:
+                        offset = await self._query_offset(session_url, total)
+                    except Exception as e2:  # noqa: BLE001
+                        await retry.backoff(e2)
                 continue
             retry.refresh()  # progress made
             if status in (200, 201):
@@ -223,7 +230,13 @@ class GCSStoragePlugin(StoragePlugin):
     async def delete(self, path: str) -> None:
         name = self._name(path)
         url = f"{self.endpoint}/storage/v1/b/{self.bucket}/o/{quote(name, safe='')}"
-        await self._call("DELETE", url, headers=self._headers())
+        retry = _RetryStrategy(self.deadline_s)
+        while True:
+            try:
+                await self._call("DELETE", url, headers=self._headers())
+                return
+            except Exception as e:  # noqa: BLE001
+                await retry.backoff(e)
 
     async def close(self) -> None:
         if self._session is not None and not self._session.closed:

@@ -328,3 +328,43 @@ def test_fs_write_on_a_numa_node(tmp_path):
         loop.run_until_complete(plugin.close())
     finally:
         loop.close()
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_FLAKY_SEEDS", "3"))))
+def test_s3_snapshot_survives_a_flaky_service(seed):
+    """One request in five fails (429 / 500 / 503, seeded): take (multipart),
+    async_take, restore and a budgeted ranged read_object all get through on
+    retries, bit-exact."""
+    with FakeS3Server() as srv:
+        opts = dict(S3_OPTS, endpoint_url=srv.url, multipart_threshold=1 << 20,
+                    part_size=5 << 20, retries=8)
+        g = torch.Generator().manual_seed(seed)
+        sd = StateDict(w=torch.randn(3000, 1000, generator=g), b=torch.arange(10), step=seed)
+        srv.fail_randomly(0.2, seed)
+        Snapshot.take("s3://ckpt/flaky/a", {"sd": sd}, storage_options=opts)
+        Snapshot.async_take("s3://ckpt/flaky/b", {"sd": sd}, storage_options=opts).wait()
+        for name in ("a", "b"):
+            out = StateDict(w=torch.zeros(3000, 1000), b=torch.zeros(10, dtype=torch.long),
+                            step=-1)
+            snap = Snapshot(f"s3://ckpt/flaky/{name}", storage_options=opts)
+            snap.restore({"sd": out})
+            assert torch.equal(out["w"], sd["w"]) and torch.equal(out["b"], sd["b"])
+            assert out["step"] == seed
+            w = torch.zeros(3000, 1000)
+            snap.read_object("0/sd/w", obj_out=w, memory_budget_bytes=1 << 20)
+            assert torch.equal(w, sd["w"])
+        assert srv.injected >= 3, (srv.injected, srv.requests)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_FLAKY_SEEDS", "2"))))
+def test_gcs_snapshot_survives_a_flaky_service(seed):
+    with FakeGCSServer() as srv:
+        opts = {"endpoint_url": srv.url, "token": "fake-token", "chunk_size": 1 << 20}
+        g = torch.Generator().manual_seed(seed)
+        sd = StateDict(w=torch.randn(1500, 1000, generator=g), s="x")
+        srv.fail_randomly(0.3, 100 + seed)
+        Snapshot.take("gs://bkt/flaky", {"sd": sd}, storage_options=opts)
+        out = StateDict(w=torch.zeros(1500, 1000), s="")
+        Snapshot("gs://bkt/flaky", storage_options=opts).restore({"sd": out})
+        assert torch.equal(out["w"], sd["w"]) and out["s"] == "x"
+        assert srv.injected >= 1, (srv.injected, srv.requests)
