@@ -1,0 +1,101 @@
+"""Randomised training loops around ``async_take``: every step mutates the
+state in place; on random steps an ``async_take`` (or a blocking take) is
+started without waiting for the ones still draining, with random options
+(compression, HBM freeze vs host fallback; checksums on or off per loop).  At the end every
+snapshot must hold exactly the state of its own step -- the consistency
+guarantee of `/root/reference/torchsnapshot/snapshot.py` ``async_take``
+("changes to app_state after this returns do not affect the snapshot") --
+and pass ``verify``.
+"""
+
+import os
+import random
+
+import pytest
+import torch
+
+from hipsnapshot import Snapshot, StateDict
+from hipsnapshot.knobs import override_knob
+
+
+def _state(rng: random.Random, device: str) -> dict:
+    big = 2_000_000 if device != "cpu" else 300_000
+    out = {}
+    for i in range(rng.randint(3, 7)):
+        n = rng.choice([1, 17, 4096, big, rng.randint(1, big)])
+        dtype = rng.choice([torch.float32, torch.bfloat16, torch.float16])
+        out[f"t{i}"] = torch.randn(n, device=device).to(dtype)
+    out["m"] = torch.randn(rng.randint(2, 300), rng.randint(2, 300), device=device)
+    return out
+
+
+def _mutate(rng: random.Random, state: dict, step: int) -> None:
+    for k, t in state.items():
+        op = rng.randrange(3)
+        if op == 0:
+            t.add_(1.0 + step)
+        elif op == 1:
+            t.mul_(-0.5)
+        else:
+            t.index_fill_(0, torch.tensor([0], device=t.device), float(step))
+
+
+def _loop(tmp_path, seed: int, device: str, steps: int = 10) -> None:
+    rng = random.Random(seed)
+    torch.manual_seed(seed)
+    state = _state(rng, device)
+    taken = []  # (path, refs, how)
+    pending = []
+    # one value per loop: environment knobs are read while a take runs, and
+    # the async takes of earlier steps are still draining
+    checksum = rng.choice(["0", "1"])
+    with override_knob("CHECKSUM", checksum):
+        _steps(rng, state, steps, tmp_path, device, checksum, taken, pending)
+        for p in pending:
+            p.wait()
+    _check(taken)
+
+
+def _steps(rng, state, steps, tmp_path, device, checksum, taken, pending) -> None:
+    for step in range(steps):
+        _mutate(rng, state, step)
+        if rng.random() < 0.6:
+            path = os.path.join(str(tmp_path), f"step_{step}")
+            refs = {k: v.clone() for k, v in state.items()}
+            comp = rng.choice(["none", "hsz1"])
+            host_fallback = device != "cpu" and rng.random() < 0.3
+            how = (step, comp, host_fallback, checksum)
+            with override_knob("HBM_STAGING_RESERVE_BYTES",
+                               str(1 << 50) if host_fallback else "0"):
+                app = {"sd": StateDict(step=step, **state)}
+                if rng.random() < 0.2:
+                    Snapshot.take(path, app, compression=comp)
+                else:
+                    pending.append(Snapshot.async_take(path, app, compression=comp))
+            taken.append((path, refs, how))
+            if pending and rng.random() < 0.3:
+                pending.pop(rng.randrange(len(pending))).wait()
+
+
+def _check(taken) -> None:
+    from hipsnapshot.verify import verify_snapshot
+
+    for path, refs, how in taken:
+        out = StateDict(step=-1, **{k: torch.zeros_like(v) for k, v in refs.items()})
+        Snapshot(path).restore({"sd": out})
+        assert out["step"] == how[0], how
+        for k, v in refs.items():
+            assert torch.equal(out[k], v), (how, k)
+        if how[3] == "1":
+            assert verify_snapshot(path).ok, how
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_async_training_loop_cpu(tmp_path, seed):
+    _loop(tmp_path, seed, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(100, 100 + int(os.environ.get("HS_ASYNC_GPU_SEEDS", "6"))))
+def test_random_async_training_loop_gpu(tmp_path, gpu, seed):
+    _loop(tmp_path, seed, "cuda:0")
