@@ -234,12 +234,12 @@ class _Tuning:
     restore_readers = 0        # 0: max(4, min(12, I/O threads))
     restore_device_budget = 2 << 30
     # idle restore blocks kept per pool after a restore (HBM outside torch's
-    # allocator): the two 2 GiB rings.  Trimming them to 0 after every job
-    # was measured in round 5: alone on a GPU it restored bitwise, but with 4
-    # processes restoring on one GPU it gave wrong bytes and device-work
-    # errors (profiles/r5/trim/); released pool memory is reused at once by
-    # the other processes' uncached SDMA targets.  ``release_restore_memory()``
-    # frees them on request.
+    # allocator): the two 2 GiB rings, so the next restore does not allocate.
+    # The blocks are VMM mappings on never-reused address ranges, so freeing
+    # them is safe at any time (the round-5 wrong bytes after trims were
+    # stale translations of reused ranges: profiles/r6/trim/); the memory
+    # policy trims them to 0 when the trainer's headroom runs short
+    # (engine/memory.py), ``release_restore_memory()`` on request.
     restore_keep_bytes = (2 << 30) + (256 << 20)
     # -- distributed -------------------------------------------------------------------
     # a DTensor box replicated R ways (HSDP, DTensor DDP) at least this large

@@ -78,8 +78,30 @@ def _blank(v):
     return "placeholder"
 
 
-def _round_trip(tmp_path, seed: int, device: str) -> None:
+def _random_tuning(rng: random.Random) -> dict:
+    """Engine constants far from their defaults: tiny rings that wrap many
+    times per blob, one slot, one copy in flight, no idle pool kept."""
+    slot = rng.choice([1 << 20, 4 << 20, 128 << 20])
+    return {
+        "restore_slot_bytes": slot,
+        "restore_slots": rng.choice([1, 2, 3, 6]),
+        "restore_first_bytes": min(slot, rng.choice([1 << 20, 16 << 20])),
+        "restore_piece_bytes": min(slot, rng.choice([64 << 10, 1 << 20, 4 << 20])),
+        "read_head_bytes": rng.choice([256 << 10, 16 << 20]),
+        "restore_keep_bytes": rng.choice([0, (2 << 30) + (256 << 20)]),
+        "drain_slot_bytes": rng.choice([1 << 20, 8 << 20, 64 << 20]),
+        "drain_slots": rng.choice([1, 2, 16]),
+        "dma_inflight": rng.choice([1, 2, 8]),
+        "stage_threads": rng.choice([1, 4]),
+        "plan_cache": rng.random() < 0.5,
+    }
+
+
+def _round_trip(tmp_path, seed: int, device: str, tuning: bool = False) -> None:
     rng = random.Random(seed)
+    if tuning:
+        with knobs.override_tuning(**_random_tuning(random.Random(seed + 7))):
+            return _round_trip(tmp_path, seed, device)
     state = _random_state(rng, device)
     compression = rng.choice(["none", "hsz1"])
     batching = rng.random() < 0.7
@@ -169,3 +191,16 @@ def test_chunked_quantized_restores_its_qparams(tmp_path, monkeypatch, qscheme):
     Snapshot(path).restore(target)
     assert_state_dict_eq(dict(target["app"]), {"q": q})
     assert_state_dict_eq({"q": snap.read_object("0/app/q")}, {"q": q})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(500, 500 + int(os.environ.get("HS_E2E_GPU_SEEDS", "24"))))
+def test_random_state_round_trip_gpu_engine_tuning(tmp_path, gpu, seed):
+    """The same under random engine constants (``_random_tuning``): the native
+    drain's and restore's rings with 1 MiB slots, 1 slot, 1 DMA in flight."""
+    _round_trip(tmp_path, seed, "cuda:0", tuning=True)
+
+
+@pytest.mark.parametrize("seed", range(500, 512))
+def test_random_state_round_trip_cpu_engine_tuning(tmp_path, seed):
+    _round_trip(tmp_path, seed, "cpu", tuning=True)
