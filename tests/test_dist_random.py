@@ -65,7 +65,7 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
         glob = (torch.randn(shape, generator=g) * 100).to(dtype)
         save_mesh, save_pl = _layout(rng, ndim)
         load_mesh, load_pl = _layout(rng, ndim)
-        compression = rng.choice(["none", "hsz1"])
+        compression = rng.choice(["none", "hsz1", "hsz1+host"])
         batching = rng.random() < 0.7
         what = (case, shape, dtype, save_mesh, save_pl, load_mesh, load_pl, compression,
                 batching)

@@ -103,7 +103,7 @@ def _round_trip(tmp_path, seed: int, device: str, tuning: bool = False) -> None:
         with knobs.override_tuning(**_random_tuning(random.Random(seed + 7))):
             return _round_trip(tmp_path, seed, device)
     state = _random_state(rng, device)
-    compression = rng.choice(["none", "hsz1"])
+    compression = rng.choice(["none", "hsz1", "hsz1+host"])
     batching = rng.random() < 0.7
     chunk = rng.choice([None, 64 << 10, 1 << 20])
     slab = rng.choice([None, 16 << 10, 256 << 10])
