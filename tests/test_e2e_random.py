@@ -34,6 +34,8 @@ def _tensor(rng: random.Random, device: str):
         shape = [0, rng.randint(1, 4)]
     elif r < 0.24:
         shape = [rng.randint(40_000, 400_000)]  # several chunks / its own slab
+    elif r < 0.28 and device != "cpu":
+        shape = [rng.randint(1 << 21, 1 << 24)]  # many ring slots of the native engines
     else:
         shape = [rng.randint(1, 33) for _ in range(rng.randint(1, 3))]
     t = rand_tensor(shape, dtype, device="cpu")
