@@ -96,3 +96,60 @@ def test_random_dtensor_layouts_reshard_exactly_gpu(gpu, tmp_path):
     """The same with every local piece on cuda:0 (4 gloo ranks sharing it):
     staging, HSZ1 and the native restore's scatter under random layouts."""
     run_distributed(_worker, 4, str(tmp_path), 24, 7, "cuda:0", timeout=600)
+
+
+def _elastic_state(seed: int, world: int):
+    """Replicated tensors (the same on every rank; large ones chunked and
+    spread by the partitioner) and a Shard(0) DTensor over the world."""
+    import torch.distributed as dist  # noqa: F401
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import Shard, distribute_tensor
+
+    rng = random.Random(seed)
+    g = torch.Generator().manual_seed(seed)
+    rep = {f"r{i}": (torch.randn(rng.choice([3, 1000, 70_000]), generator=g) * 10).to(
+        rng.choice([torch.float32, torch.bfloat16])) for i in range(rng.randint(1, 6))}
+    rows = rng.randint(1, 40)
+    glob = torch.randn(rows, rng.randint(1, 9), generator=g)
+    mesh = init_device_mesh("cpu", (world,))
+    return rep, glob, distribute_tensor(glob, mesh, [Shard(0)])
+
+
+def _elastic_save(root: str, seed: int) -> None:
+    import torch.distributed as dist
+
+    from hipsnapshot import Snapshot, StateDict, knobs
+
+    rep, _glob, dt = _elastic_state(seed, dist.get_world_size())
+    with knobs.override_max_chunk_size_bytes(64 << 10):
+        Snapshot.take(root, {"rep": StateDict(**rep), "sh": StateDict(w=dt)},
+                      replicated=["rep/**"],
+                      compression=random.Random(seed).choice(["none", "hsz1+host"]))
+
+
+def _elastic_restore(root: str, seed: int) -> None:
+    import torch.distributed as dist
+
+    from hipsnapshot import Snapshot, StateDict
+
+    rep, glob, dt = _elastic_state(seed, dist.get_world_size())
+    out_rep = StateDict(**{k: torch.zeros_like(v) for k, v in rep.items()})
+    dt.to_local().zero_()
+    out_sh = StateDict(w=dt)
+    Snapshot(root).restore({"rep": out_rep, "sh": out_sh})
+    for k, v in rep.items():
+        assert torch.equal(out_rep[k], v), (seed, k)
+    assert torch.equal(out_sh["w"].full_tensor(), glob), seed
+
+
+@pytest.mark.parametrize("seed", range(11, 11 + int(os.environ.get("HS_ELASTIC_SEEDS", "1"))))
+def test_random_elastic_world_sizes(tmp_path, seed):
+    """Save with W1 ranks, restore with W2 (random in 1-4): replicated state
+    partitioned over the savers comes back whole on every restoring rank, a
+    Shard(0) DTensor re-cut for W2."""
+    rng = random.Random(seed)
+    for i in range(2):
+        w1, w2 = rng.randint(1, 4), rng.randint(1, 4)
+        path = str(tmp_path / f"e{i}")
+        run_distributed(_elastic_save, w1, path, seed * 10 + i, timeout=240)
+        run_distributed(_elastic_restore, w2, path, seed * 10 + i, timeout=240)
