@@ -521,6 +521,32 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Non-finite inputs of the blockwise (f32-scale) formats, as in the MX ones:
+// they do not set their block's scale (|x| of inf / nan counts as 0), and
+// their code is the e4m3fn NaN with the input's sign (torch's cast).  So one
+// inf no longer turns every element of its block into NaN, and the GPU codes
+// equal ops/quant.py's reference for every input.
+__device__ __forceinline__ float finite_abs(float x) {
+  const float a = fabsf(x);
+  return a < __builtin_huge_valf() ? a : 0.f;
+}
+
+// `word` holds the codes of x[0..3] (byte j <- x[j]); j >= nvalid are left as is
+__device__ __forceinline__ uint32_t fp8_fix_nonfinite(uint32_t word, const float* x,
+                                                      int nvalid = 4) {
+  uint32_t fix = 0, mask = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j >= nvalid) break;
+    const uint32_t b = __float_as_uint(x[j]);
+    if ((b & 0x7f800000u) == 0x7f800000u) {
+      mask |= 0xffu << (8 * j);
+      fix |= ((b >> 31) ? 0xffu : 0x7fu) << (8 * j);
+    }
+  }
+  return (word & ~mask) | fix;
+}
+
 template <int VPT>
 __global__ void __launch_bounds__(kBlock)
 hs_fp8_quant(const char* __restrict__ src, int32_t src_dtype, int64_t n,
@@ -539,7 +565,7 @@ hs_fp8_quant(const char* __restrict__ src, int32_t src_dtype, int64_t n,
     for (int j = 0; j < VPT; ++j) {
       const int64_t e = e0 + j;
       v[j] = (e < n) ? load_as_f32(src + e * ses, src_dtype) : 0.f;
-      amax = fmaxf(amax, fabsf(v[j]));
+      amax = fmaxf(amax, finite_abs(v[j]));
     }
     amax = wave_max(amax);
     // two correctly rounded divisions per BLOCK (scale, then its reciprocal)
@@ -558,7 +584,8 @@ hs_fp8_quant(const char* __restrict__ src, int32_t src_dtype, int64_t n,
       float a3 = (4 * w + 3 < VPT) ? fminf(fmaxf(v[4 * w + 3] * inv, -kFp8Max), kFp8Max) : 0.f;
       int word = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
       word = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, word, true);
-      words[w] = static_cast<uint32_t>(word);
+      words[w] = fp8_fix_nonfinite(static_cast<uint32_t>(word), v + 4 * w,
+                                   VPT - 4 * w < 4 ? VPT - 4 * w : 4);
     }
     if (e0 + VPT <= n && (VPT % 4) == 0) {
 #pragma unroll
@@ -933,7 +960,7 @@ hs_fp8_quant_v(const char* __restrict__ src, int64_t n, uint8_t* __restrict__ ou
       }
       float amax = 0.f;
 #pragma unroll
-      for (int j = 0; j < EPL; ++j) amax = fmaxf(amax, fabsf(v[j]));
+      for (int j = 0; j < EPL; ++j) amax = fmaxf(amax, finite_abs(v[j]));
 #pragma unroll
       for (int o = 1; o < LPB; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
       const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
@@ -949,7 +976,7 @@ hs_fp8_quant_v(const char* __restrict__ src, int64_t n, uint8_t* __restrict__ ou
         word = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4 * w + 2] * inv, -kFp8Max), kFp8Max),
                                                fminf(fmaxf(v[4 * w + 3] * inv, -kFp8Max), kFp8Max),
                                                word, true);
-        q[w] = static_cast<uint32_t>(word);
+        q[w] = fp8_fix_nonfinite(static_cast<uint32_t>(word), v + 4 * w);
       }
       if (full) {
         if constexpr (EPL == 8) {
@@ -1061,8 +1088,8 @@ hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[t], hada(16 * h + t, r), acc, 0, 0, 0);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      float amax = fmaxf(fmaxf(fabsf(acc[4 * g4]), fabsf(acc[4 * g4 + 1])),
-                         fmaxf(fabsf(acc[4 * g4 + 2]), fabsf(acc[4 * g4 + 3])));
+      float amax = fmaxf(fmaxf(finite_abs(acc[4 * g4]), finite_abs(acc[4 * g4 + 1])),
+                         fmaxf(finite_abs(acc[4 * g4 + 2]), finite_abs(acc[4 * g4 + 3])));
       amax = max_over_32(amax);
       const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
       const float inv = 1.f / scale;
@@ -1078,6 +1105,10 @@ hs_fp8_hadamard_quant(const char* __restrict__ src, int64_t n, int64_t n_pad,
       // instead of 4 one-byte stores.
       uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false));
       w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], static_cast<int>(w), true));
+      {
+        const float a4[4] = {acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]};
+        w = fp8_fix_nonfinite(w, a4);
+      }
       uint32_t o = static_cast<uint32_t>(
           __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0xB1, 0xF, 0xF, false));  // lane ^ 1
       w = __builtin_amdgcn_perm(o, w, (r & 1) ? 0x03070105u : 0x06020400u);
@@ -1137,8 +1168,8 @@ __device__ __forceinline__ void hadamard_tile_store(const floatx16& acc, int64_t
                                                     float* __restrict__ scales) {
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
-    float amax = fmaxf(fmaxf(fabsf(acc[4 * g4]), fabsf(acc[4 * g4 + 1])),
-                       fmaxf(fabsf(acc[4 * g4 + 2]), fabsf(acc[4 * g4 + 3])));
+    float amax = fmaxf(fmaxf(finite_abs(acc[4 * g4]), finite_abs(acc[4 * g4 + 1])),
+                       fmaxf(finite_abs(acc[4 * g4 + 2]), finite_abs(acc[4 * g4 + 3])));
     amax = max_over_32(amax);
     const float scale = amax > 0.f ? amax / kFp8Max : 1.f;
     const float inv = 1.f / scale;
@@ -1149,6 +1180,10 @@ __device__ __forceinline__ void hadamard_tile_store(const floatx16& acc, int64_t
     for (int q = 0; q < 4; ++q) v[q] = fminf(fmaxf(acc[4 * g4 + q] * inv, -kFp8Max), kFp8Max);
     uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false));
     w = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], static_cast<int>(w), true));
+    {
+      const float a4[4] = {acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]};
+      w = fp8_fix_nonfinite(w, a4);
+    }
     uint32_t o = static_cast<uint32_t>(
         __builtin_amdgcn_mov_dpp(static_cast<int>(w), 0xB1, 0xF, 0xF, false));  // lane ^ 1
     w = __builtin_amdgcn_perm(o, w, (r & 1) ? 0x03070105u : 0x06020400u);

@@ -143,13 +143,18 @@ def fp8_entry_quant_info(t: torch.Tensor, vpt: int = DEFAULT_VPT,
 # ---------------------------------------------------------------------------
 
 def _scale_and_quant(blocks: torch.Tensor):
-    amax = blocks.abs().amax(dim=1)
+    # over the finite elements: an inf / nan does not set its block's scale,
+    # and its code is the e4m3fn NaN with its sign (torch's cast of inf / nan),
+    # as in the MX format and the GPU kernels (``csrc/hsgpu.hip`` fp8_fix_nonfinite)
+    finite = torch.isfinite(blocks)
+    amax = torch.where(finite, blocks.abs(), torch.zeros_like(blocks)).amax(dim=1)
     # tensor/tensor division (correctly rounded; a Python-scalar divisor is
     # lowered to a reciprocal multiply by torch and differs by 1 ulp)
     scale = torch.where(amax > 0, amax / torch.full_like(amax, FP8_MAX), torch.ones_like(amax))
     # one reciprocal per block, one multiply per element (the kernels' rule)
     inv = torch.ones_like(scale) / scale
-    q = (blocks * inv[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    q = torch.where(finite, (blocks * inv[:, None]).clamp(-FP8_MAX, FP8_MAX),
+                    blocks).to(torch.float8_e4m3fn)
     return q, scale
 
 
