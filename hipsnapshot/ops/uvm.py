@@ -87,23 +87,17 @@ def new_managed_tensor(shape: List[int], dtype: torch.dtype = torch.float32,
     class _Holder:
         pass
 
+    # the pages as bytes, then viewed as ``dtype``: the array interface has no
+    # type string torch accepts for bf16 / fp8 (a "<V2" bf16 table failed to
+    # wrap -- tests/test_uvm_random.py)
     holder = _Holder()
     holder.__cuda_array_interface__ = {
-        "shape": tuple(int(s) for s in shape),
-        "typestr": _typestr(dtype),
-        "data": (ptr, False),
-        "version": 3,
+        "shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3,
         "strides": None,
     }
     with torch.cuda.device(device):
-        t = torch.as_tensor(holder, device=f"cuda:{device}")
+        raw = torch.as_tensor(holder, device=f"cuda:{device}")
+    t = raw[: numel * torch.empty(0, dtype=dtype).element_size()].view(dtype).view(
+        [int(s) for s in shape])
     weakref.finalize(t.untyped_storage(), _free)
     return t
-
-
-def _typestr(dtype: torch.dtype) -> str:
-    return {
-        torch.float32: "<f4", torch.float16: "<f2", torch.float64: "<f8",
-        torch.int64: "<i8", torch.int32: "<i4", torch.int16: "<i2", torch.int8: "|i1",
-        torch.uint8: "|u1", torch.bool: "|b1", torch.bfloat16: "<V2",
-    }[dtype]
