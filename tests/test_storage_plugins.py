@@ -368,3 +368,26 @@ def test_gcs_snapshot_survives_a_flaky_service(seed):
         Snapshot("gs://bkt/flaky", storage_options=opts).restore({"sd": out})
         assert torch.equal(out["w"], sd["w"]) and out["s"] == "x"
         assert srv.injected >= 1, (srv.injected, srv.requests)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_FLAKY_SEEDS", "3"))))
+def test_s3_gpu_snapshot_survives_a_flaky_service(gpu, seed):
+    """HIP tensors through a flaky S3: SDMA staging + HSZ1 on the way out,
+    ranged reads and the device-side decode on the way back."""
+    with FakeS3Server() as srv:
+        opts = dict(S3_OPTS, endpoint_url=srv.url, multipart_threshold=1 << 20,
+                    part_size=5 << 20, retries=8)
+        g = torch.Generator(device=gpu).manual_seed(seed)
+        sd = StateDict(w=torch.randn(3000, 1000, device=gpu, generator=g).bfloat16(),
+                       b=torch.randn(1000, device=gpu, generator=g), step=seed)
+        srv.fail_randomly(0.25, 100 + seed)
+        Snapshot.take("s3://ckpt/g/a", {"sd": sd}, storage_options=opts, compression="hsz1")
+        Snapshot.async_take("s3://ckpt/g/b", {"sd": sd}, storage_options=opts).wait()
+        for name in ("a", "b"):
+            out = StateDict(w=torch.zeros_like(sd["w"]), b=torch.zeros_like(sd["b"]), step=-1)
+            Snapshot(f"s3://ckpt/g/{name}", storage_options=opts).restore({"sd": out},
+                                                                           verify=True)
+            assert torch.equal(out["w"], sd["w"]) and torch.equal(out["b"], sd["b"])
+            assert out["step"] == seed
+        assert srv.injected >= 1, (srv.injected, srv.requests)
