@@ -51,7 +51,7 @@ def _loop(tmp_path, seed: int, device: str, steps: int = 10) -> None:
     checksum = rng.choice(["0", "1"])
     with override_knob("CHECKSUM", checksum):
         _steps(rng, state, steps, tmp_path, device, checksum, taken, pending)
-        for p in pending:
+        for _path, p in pending:
             p.wait()
     _check(taken)
 
@@ -71,10 +71,19 @@ def _steps(rng, state, steps, tmp_path, device, checksum, taken, pending) -> Non
                 if rng.random() < 0.2:
                     Snapshot.take(path, app, compression=comp)
                 else:
-                    pending.append(Snapshot.async_take(path, app, compression=comp))
+                    pending.append((path, Snapshot.async_take(path, app, compression=comp)))
             taken.append((path, refs, how))
             if pending and rng.random() < 0.3:
-                pending.pop(rng.randrange(len(pending))).wait()
+                pending.pop(rng.randrange(len(pending)))[1].wait()
+        # read back a committed snapshot while later async takes still drain
+        busy = {pp for pp, p in pending if not p.done()}
+        done = [t for t in taken if t[0] not in busy]
+        if done and rng.random() < 0.25:
+            path, refs, how = rng.choice(done)
+            out = StateDict(step=-1, **{k: torch.zeros_like(v) for k, v in refs.items()})
+            Snapshot(path).restore({"sd": out})
+            assert out["step"] == how[0] and all(torch.equal(out[k], v) for k, v in refs.items()), \
+                ("restore during drains", how)
 
 
 def _check(taken) -> None:
