@@ -67,13 +67,17 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
         load_mesh, load_pl = _layout(rng, ndim)
         compression = rng.choice(["none", "hsz1", "hsz1+host"])
         batching = rng.random() < 0.7
+        use_async = rng.random() < 0.4
         what = (case, shape, dtype, save_mesh, save_pl, load_mesh, load_pl, compression,
-                batching)
+                batching, use_async)
         path = os.path.join(root, f"c{case}")
         src = place(glob, save_mesh, save_pl)
         with knobs.override_is_batching_disabled(not batching):
-            snap = Snapshot.take(path, {"s": StateDict(t=src, step=case)},
-                                 compression=compression)
+            app = {"s": StateDict(t=src, step=case)}
+            if use_async:
+                snap = Snapshot.async_take(path, app, compression=compression).wait()
+            else:
+                snap = Snapshot.take(path, app, compression=compression)
             dst = place(torch.zeros_like(glob), load_mesh, load_pl)
             app = {"s": StateDict(t=dst, step=-1)}
             Snapshot(path).restore(app)
