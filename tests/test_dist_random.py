@@ -90,7 +90,7 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
         dist.barrier()
 
 
-@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("seed", [1])
 def test_random_dtensor_layouts_reshard_exactly(tmp_path, seed):
     run_distributed(_worker, 4, str(tmp_path), 14, seed, timeout=400)
 
@@ -146,13 +146,14 @@ def _elastic_restore(root: str, seed: int) -> None:
     assert torch.equal(out_sh["w"].full_tensor(), glob), seed
 
 
+@pytest.mark.slow  # 10 s of spawned ranks; --run-slow (CI) runs it
 @pytest.mark.parametrize("seed", range(11, 11 + int(os.environ.get("HS_ELASTIC_SEEDS", "1"))))
 def test_random_elastic_world_sizes(tmp_path, seed):
     """Save with W1 ranks, restore with W2 (random in 1-4): replicated state
     partitioned over the savers comes back whole on every restoring rank, a
     Shard(0) DTensor re-cut for W2."""
     rng = random.Random(seed)
-    for i in range(2):
+    for i in range(1):
         w1, w2 = rng.randint(1, 4), rng.randint(1, 4)
         path = str(tmp_path / f"e{i}")
         run_distributed(_elastic_save, w1, path, seed * 10 + i, timeout=240)

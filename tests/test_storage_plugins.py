@@ -330,7 +330,7 @@ def test_fs_write_on_a_numa_node(tmp_path):
         loop.close()
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_FLAKY_SEEDS", "3"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_FLAKY_SEEDS", "2"))))
 def test_s3_snapshot_survives_a_flaky_service(seed):
     """One request in five fails (429 / 500 / 503, seeded): take (multipart),
     async_take, restore and a budgeted ranged read_object all get through on
@@ -356,7 +356,7 @@ def test_s3_snapshot_survives_a_flaky_service(seed):
         assert srv.injected >= 3, (srv.injected, srv.requests)
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_FLAKY_SEEDS", "2"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_FLAKY_SEEDS", "1"))))
 def test_gcs_snapshot_survives_a_flaky_service(seed):
     with FakeGCSServer() as srv:
         opts = {"endpoint_url": srv.url, "token": "fake-token", "chunk_size": 1 << 20}
