@@ -15,6 +15,7 @@ if __name__ == "__main__":
     ap.add_argument("--seeds", type=int, nargs=2, default=[20, 30])
     ap.add_argument("--cases", type=int, default=24)
     ap.add_argument("--device", default="cpu")
+    ap.add_argument("--strided", action="store_true", help="mix _StridedShard placements in")
     a = ap.parse_args()
     import test_dist_random as t
 
@@ -22,5 +23,5 @@ if __name__ == "__main__":
 
     for seed in range(*a.seeds):
         with tempfile.TemporaryDirectory() as d:
-            run_distributed(t._worker, 4, d, a.cases, seed, a.device, timeout=600)
+            run_distributed(t._worker, 4, d, a.cases, seed, a.device, a.strided, timeout=600)
         print(f"seed {seed}: {a.cases} cases ok", flush=True)

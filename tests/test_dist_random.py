@@ -22,15 +22,42 @@ pytestmark = pytest.mark.multiproc
 MESHES = [(4,), (2, 2), (1, 4), (4, 1)]
 
 
-def _layout(rng: random.Random, ndim: int):
+def _layout(rng: random.Random, ndim: int, strided: bool = False):
     from torch.distributed.tensor import Replicate, Shard
+    from torch.distributed.tensor.placement_types import _StridedShard
 
     mesh = rng.choice(MESHES)
-    pl = [Shard(rng.randrange(ndim)) if rng.random() < 0.7 else Replicate() for _ in mesh]
+    pl = []
+    for _ in mesh:
+        r = rng.random()
+        if strided and r < 0.3:
+            pl.append(_StridedShard(rng.randrange(ndim), split_factor=rng.randint(2, 3)))
+        elif r < 0.75:
+            pl.append(Shard(rng.randrange(ndim)))
+        else:
+            pl.append(Replicate())
     return mesh, pl
 
 
-def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
+def _truth_index(shape, mesh_shape, coord, placements):
+    """Global indices per dim of a coordinate's local tensor, by torch's own
+    splitting code (``_split_tensor``): the ground truth, not ours."""
+    from torch.distributed.tensor import Shard
+    from torch.distributed.tensor.placement_types import _StridedShard
+
+    idx = [torch.arange(n) for n in shape]
+    for mdim, p in enumerate(placements):
+        if not hasattr(p, "dim"):
+            continue
+        p1 = _StridedShard(0, split_factor=p.split_factor) if isinstance(p, _StridedShard) \
+            else Shard(0)
+        shards, _ = p1._split_tensor(idx[p.dim], mesh_shape[mdim], with_padding=False)
+        idx[p.dim] = shards[coord[mdim]]
+    return idx
+
+
+def _worker(root: str, n_cases: int, seed: int, device: str = "cpu",
+            strided: bool = False) -> None:
     import torch.distributed as dist
     from torch.distributed.device_mesh import init_device_mesh
     from torch.distributed.tensor import DTensor, distribute_tensor
@@ -39,6 +66,8 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
 
     rng = random.Random(seed)  # the same stream on every rank
     meshes = {}
+    if device.startswith("cuda"):  # before any "cuda" mesh picks rank % n_gpus
+        torch.cuda.set_device(torch.device(device))
 
     def mesh_of(shape, dev_type="cpu"):
         if (shape, dev_type) not in meshes:
@@ -48,12 +77,18 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
     def place(glob, shape, pl):
         """``glob`` laid out by torch (on a CPU mesh), then, for a GPU run,
         the same local pieces as DTensors of HIP tensors (no collectives on
-        them: gloo ranks share the one GPU)."""
+        them: gloo ranks share the one GPU).  Layouts with a _StridedShard
+        (FSDP2 over TP) are cut by torch's ``_split_tensor``."""
+        if any(type(p).__name__ == "_StridedShard" for p in pl):
+            mesh = mesh_of(shape, "cuda" if device != "cpu" else "cpu")
+            coord = mesh.get_coordinate()
+            local = glob[torch.meshgrid(*_truth_index(list(glob.shape), shape, coord, pl),
+                                        indexing="ij")].contiguous()
+            return DTensor.from_local(local.to(device), mesh, pl, run_check=False,
+                                      shape=glob.shape, stride=glob.stride())
         cpu = distribute_tensor(glob, mesh_of(shape), pl)
         if device == "cpu":
             return cpu
-        if device.startswith("cuda"):
-            torch.cuda.set_device(torch.device(device))
         return DTensor.from_local(cpu.to_local().to(device), mesh_of(shape, "cuda"), pl,
                                   run_check=False, shape=cpu.shape, stride=cpu.stride())
 
@@ -63,8 +98,8 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
         dtype = rng.choice([torch.float32, torch.bfloat16, torch.int64, torch.float64])
         g = torch.Generator().manual_seed(seed * 1000 + case)
         glob = (torch.randn(shape, generator=g) * 100).to(dtype)
-        save_mesh, save_pl = _layout(rng, ndim)
-        load_mesh, load_pl = _layout(rng, ndim)
+        save_mesh, save_pl = _layout(rng, ndim, strided)
+        load_mesh, load_pl = _layout(rng, ndim, strided)
         compression = rng.choice(["none", "hsz1", "hsz1+host"])
         batching = rng.random() < 0.7
         use_async = rng.random() < 0.4
@@ -93,6 +128,12 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu") -> None:
 @pytest.mark.parametrize("seed", [1])
 def test_random_dtensor_layouts_reshard_exactly(tmp_path, seed):
     run_distributed(_worker, 4, str(tmp_path), 14, seed, timeout=400)
+
+
+def test_random_strided_dtensor_layouts_reshard_exactly(tmp_path):
+    """The same with _StridedShard placements (FSDP2 over TP) mixed in: a
+    local tensor holds several disjoint runs of a dim."""
+    run_distributed(_worker, 4, str(tmp_path), 8, 3, "cpu", True, timeout=400)
 
 
 @pytest.mark.gpu
