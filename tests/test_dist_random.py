@@ -127,7 +127,7 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu",
 
 @pytest.mark.parametrize("seed", [1])
 def test_random_dtensor_layouts_reshard_exactly(tmp_path, seed):
-    run_distributed(_worker, 4, str(tmp_path), 14, seed, timeout=400)
+    run_distributed(_worker, 4, str(tmp_path), 10, seed, timeout=400)
 
 
 def test_random_strided_dtensor_layouts_reshard_exactly(tmp_path):
@@ -268,5 +268,5 @@ def test_random_sharded_tensor_specs_reshard_exactly(tmp_path, world):
     ranks, saved (with and without forced sub-division) and restored into
     another random spec, then read whole.  The reference's own test crosses 3
     fixed specs (`/root/reference/tests/test_sharded_tensor_resharding.py`)."""
-    run_distributed(_sharded_worker, world, str(tmp_path), 16,
+    run_distributed(_sharded_worker, world, str(tmp_path), 10,
                     int(os.environ.get("HS_ST_SEED", "5")) + world, timeout=400)
