@@ -99,7 +99,7 @@ def _check(taken) -> None:
             assert verify_snapshot(path).ok, how
 
 
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(3))
 def test_random_async_training_loop_cpu(tmp_path, seed):
     _loop(tmp_path, seed, "cpu")
 
