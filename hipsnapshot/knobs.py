@@ -31,6 +31,7 @@ from __future__ import annotations
 import functools
 import math
 import os
+import threading
 from contextlib import contextmanager
 from typing import Any, Generator, Optional
 
@@ -48,12 +49,35 @@ _DEFAULT_SLAB_SIZE_THRESHOLD_BYTES = 128 * 1024 * 1024
 MAX_PER_RANK_MEMORY_BUDGET_BYTES = 32 * 1024 * 1024 * 1024
 
 
+_pins = threading.local()  # .env: the knob values an async take's commit thread runs with
+
+
 def _get(name: str) -> Optional[str]:
+    env = getattr(_pins, "env", None)
+    src = env if env is not None else os.environ
     for p in _PREFIXES:
-        v = os.environ.get(p + name)
+        v = src.get(p + name)
         if v is not None:
             return v
     return None
+
+
+def env_snapshot() -> dict:
+    """The ``HIPSNAPSHOT_*`` / ``TORCHSNAPSHOT_*`` variables as they are now."""
+    return {k: v for k, v in os.environ.items() if k.startswith(_PREFIXES)}
+
+
+@contextmanager
+def pinned(env: Optional[dict]) -> Generator[None, None, None]:
+    """Read knobs from ``env`` (an ``env_snapshot()``) on this thread: an
+    ``async_take`` drains with the configuration it was called with, even if
+    the environment changes before its drain is done."""
+    prev = getattr(_pins, "env", None)
+    _pins.env = env
+    try:
+        yield
+    finally:
+        _pins.env = prev
 
 
 def _get_int(name: str, default: int) -> int:

@@ -1462,6 +1462,9 @@ class PendingSnapshot:
         self._go = threading.Event()  # set by async_take once it is returning
         self._finished = threading.Event()
         self._gc_after = False  # run the new plan's full GC pass after the commit
+        # the drain runs with the knobs of the async_take call, whatever the
+        # environment says by the time it writes (knobs.pinned)
+        self._env = knobs.env_snapshot()
         store = None if comm.solo() else get_or_create_store(comm)
         self._pending_io_work = pending_io_work
         # a pooled thread: starting one cost ~0.2 ms of every unblock
@@ -1473,7 +1476,8 @@ class PendingSnapshot:
 
     def _run_commit(self, **kwargs) -> None:
         try:
-            self._complete_snapshot(**kwargs)
+            with knobs.pinned(self._env):
+                self._complete_snapshot(**kwargs)
         except BaseException:  # noqa: BLE001 - reported by wait()
             if self.exc_info is None:
                 self.exc_info = sys.exc_info()

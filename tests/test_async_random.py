@@ -1,7 +1,7 @@
 """Randomised training loops around ``async_take``: every step mutates the
 state in place; on random steps an ``async_take`` (or a blocking take) is
 started without waiting for the ones still draining, with random options
-(compression, HBM freeze vs host fallback; checksums on or off per loop).  At the end every
+(compression, HBM freeze vs host fallback, checksums on or off per take).  At the end every
 snapshot must hold exactly the state of its own step -- the consistency
 guarantee of `/root/reference/torchsnapshot/snapshot.py` ``async_take``
 ("changes to app_state after this returns do not affect the snapshot") --
@@ -46,17 +46,13 @@ def _loop(tmp_path, seed: int, device: str, steps: int = 10) -> None:
     state = _state(rng, device)
     taken = []  # (path, refs, how)
     pending = []
-    # one value per loop: environment knobs are read while a take runs, and
-    # the async takes of earlier steps are still draining
-    checksum = rng.choice(["0", "1"])
-    with override_knob("CHECKSUM", checksum):
-        _steps(rng, state, steps, tmp_path, device, checksum, taken, pending)
-        for _path, p in pending:
-            p.wait()
+    _steps(rng, state, steps, tmp_path, device, taken, pending)
+    for _path, p in pending:
+        p.wait()
     _check(taken)
 
 
-def _steps(rng, state, steps, tmp_path, device, checksum, taken, pending) -> None:
+def _steps(rng, state, steps, tmp_path, device, taken, pending) -> None:
     for step in range(steps):
         _mutate(rng, state, step)
         if rng.random() < 0.6:
@@ -64,9 +60,13 @@ def _steps(rng, state, steps, tmp_path, device, checksum, taken, pending) -> Non
             refs = {k: v.clone() for k, v in state.items()}
             comp = rng.choice(["none", "hsz1"])
             host_fallback = device != "cpu" and rng.random() < 0.3
+            # CHECKSUM changes between takes while earlier ones still drain:
+            # each async take drains with the knobs of its own call
+            checksum = rng.choice(["0", "1"])
             how = (step, comp, host_fallback, checksum)
             with override_knob("HBM_STAGING_RESERVE_BYTES",
-                               str(1 << 50) if host_fallback else "0"):
+                               str(1 << 50) if host_fallback else "0"), \
+                    override_knob("CHECKSUM", checksum):
                 app = {"sd": StateDict(step=step, **state)}
                 if rng.random() < 0.2:
                     Snapshot.take(path, app, compression=comp)
@@ -108,3 +108,29 @@ def test_random_async_training_loop_cpu(tmp_path, seed):
 @pytest.mark.parametrize("seed", range(100, 100 + int(os.environ.get("HS_ASYNC_GPU_SEEDS", "6"))))
 def test_random_async_training_loop_gpu(tmp_path, gpu, seed):
     _loop(tmp_path, seed, "cuda:0")
+
+
+def test_async_take_drains_with_the_knobs_of_its_call(tmp_path, monkeypatch):
+    """The environment changes after ``async_take`` returns but before its
+    drain writes (the commit thread is held back 0.3 s here): the drain still
+    uses the call's knobs -- its checksums are written (``knobs.pinned``).
+    The random loops above flip CHECKSUM between overlapping takes."""
+    import time
+
+    from hipsnapshot.snapshot import PendingSnapshot
+    from hipsnapshot.verify import verify_snapshot
+
+    orig = PendingSnapshot._complete_snapshot
+
+    def late(self, *a, **kw):
+        time.sleep(0.3)
+        return orig(self, *a, **kw)
+
+    monkeypatch.setattr(PendingSnapshot, "_complete_snapshot", late)
+    sd = StateDict(w=torch.randn(1000, 100), step=3)
+    with override_knob("CHECKSUM", "1"):
+        pending = Snapshot.async_take(str(tmp_path / "a"), {"sd": sd})
+    with override_knob("CHECKSUM", "0"):  # while the drain has not started
+        pending.wait()
+    rep = verify_snapshot(str(tmp_path / "a"))
+    assert rep.has_checksums and rep.ok, rep
