@@ -270,3 +270,47 @@ def test_random_sharded_tensor_specs_reshard_exactly(tmp_path, world):
     fixed specs (`/root/reference/tests/test_sharded_tensor_resharding.py`)."""
     run_distributed(_sharded_worker, world, str(tmp_path), 10,
                     int(os.environ.get("HS_ST_SEED", "5")) + world, timeout=400)
+
+
+def _comm_worker(n_rounds: int, seed: int) -> None:
+    """Comm's framed all-gather / broadcast / scatter with random payload
+    sizes per rank (0 B to ~3 frames, the frame size itself random): every
+    take's metadata exchange rides on them."""
+    import torch.distributed as dist
+
+    from hipsnapshot.parallel.comm import Comm
+
+    comm = Comm()
+    rank, ws = comm.get_rank(), comm.get_world_size()
+    rng = random.Random(seed)  # the same draws on every rank
+    for i in range(n_rounds):
+        frame = rng.choice([64, 1000, 1 << 16])
+        sizes = [rng.choice([0, 1, frame - 1, frame, frame + 1, rng.randint(0, 3 * frame)])
+                 for _ in range(ws)]
+        payload = {"r": rank, "i": i, "b": bytes([rank % 256]) * sizes[rank]}
+        out = [None] * ws
+        comm.all_gather_object(out, payload, frame=frame)
+        for r in range(ws):
+            assert out[r] == {"r": r, "i": i, "b": bytes([r % 256]) * sizes[r]}, (i, r, frame)
+        src = rng.randrange(ws)
+        obj = [("from", rank, "x" * sizes[rank])]
+        comm.broadcast_object_list(obj, src=src)
+        assert obj == [("from", src, "x" * sizes[src])], (i, "broadcast")
+        res = [None]
+        comm.scatter_object_list(res, [(r, "y" * sizes[r]) for r in range(ws)]
+                                 if rank == src else None, src=src)
+        assert res[0] == (rank, "y" * sizes[rank]), (i, "scatter")
+    dist.barrier()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_random_comm_payloads(world):
+    run_distributed(_comm_worker, world, 40, 17 + world, timeout=240)
+
+
+@pytest.mark.gpu
+def test_random_comm_payloads_rccl_forced(gpu, monkeypatch):
+    """The same payloads over a one-rank RCCL group with
+    HIPSNAPSHOT_FORCE_COLLECTIVES (device-tensor frames, overflow rounds)."""
+    monkeypatch.setenv("HIPSNAPSHOT_FORCE_COLLECTIVES", "1")
+    run_distributed(_comm_worker, 1, 40, 23, backend="nccl", timeout=240)
