@@ -126,7 +126,7 @@ def _round_trip(tmp_path, seed: int, device: str, tuning: bool = False) -> None:
             else:
                 snap = Snapshot.take(path, app, compression=compression)
             target = {"app": StateDict(**_blank(state))}
-            Snapshot(path).restore(target)
+            Snapshot(path).restore(target, verify=rng.random() < 0.3)
         finally:
             for c in reversed(ctx):
                 if c is not None:
@@ -145,7 +145,8 @@ def _round_trip(tmp_path, seed: int, device: str, tuning: bool = False) -> None:
             continue
         budget = rng.choice([None, 4096, 100_000])
         out = _blank(v)
-        snap.read_object(p, obj_out=out, memory_budget_bytes=budget)
+        snap.read_object(p, obj_out=out, memory_budget_bytes=budget,
+                         verify=rng.random() < 0.3)
         assert_state_dict_eq(out, v, f"read_object {p} budget {budget} {case}")
 
 
