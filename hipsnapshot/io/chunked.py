@@ -133,11 +133,15 @@ def _join_quantized(parts: List[torch.Tensor], entry: ChunkedTensorEntry,
         full = torch.cat(parts, dim=0)
     else:
         axis = parts[0].q_per_channel_axis()
-        cat = lambda f: torch.cat([f(p) for p in parts]) if axis == 0 else f(parts[0])  # noqa
+        # per-channel qparams along the chunked dim are cut with it; along
+        # another dim every chunk carries the same ones
+        if axis == 0:
+            scales = torch.cat([p.q_per_channel_scales() for p in parts])
+            zeros = torch.cat([p.q_per_channel_zero_points() for p in parts])
+        else:
+            scales, zeros = parts[0].q_per_channel_scales(), parts[0].q_per_channel_zero_points()
         full = torch._make_per_channel_quantized_tensor(
-            torch.cat([p.int_repr() for p in parts], dim=0),
-            cat(lambda p: p.q_per_channel_scales()),
-            cat(lambda p: p.q_per_channel_zero_points()), axis)
+            torch.cat([p.int_repr() for p in parts], dim=0), scales, zeros, axis)
     full = full.reshape(shape) if not flat0 else full.reshape([])
     if out is None:
         return full
