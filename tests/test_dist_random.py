@@ -113,11 +113,15 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu",
                 snap = Snapshot.async_take(path, app, compression=compression).wait()
             else:
                 snap = Snapshot.take(path, app, compression=compression)
-            dst = place(torch.zeros_like(glob), load_mesh, load_pl)
+            # a DTensor target of another float dtype is cast in place
+            tdt = rng.choice([torch.float32, torch.bfloat16, torch.float64]) \
+                if dtype.is_floating_point and rng.random() < 0.3 else dtype
+            dst = place(torch.zeros(glob.shape, dtype=tdt), load_mesh, load_pl)
             app = {"s": StateDict(t=dst, step=-1)}
             Snapshot(path).restore(app)
         got = app["s"]["t"].to_local().cpu()
-        assert torch.equal(got, place(glob, load_mesh, load_pl).to_local().cpu()), what
+        want = place(glob.to(tdt), load_mesh, load_pl).to_local().cpu()
+        assert got.dtype == tdt and torch.equal(got, want), (what, tdt)
         assert app["s"]["step"] == case, what
         whole = torch.zeros_like(glob, device=device)
         snap.read_object("0/s/t", obj_out=whole)

@@ -80,6 +80,35 @@ def _blank(v):
     return "placeholder"
 
 
+FLOAT_CASTS = [torch.float32, torch.bfloat16, torch.float16, torch.float64]
+
+
+def _cross(v, rng: random.Random):
+    """(target, expected): like ``_blank``, but a floating tensor's target
+    may have another float dtype and / or live on the other device.  Same
+    dtype and shape: restored in place, across devices.  Another dtype:
+    TorchSnapshot's rule -- the value is read into a new tensor of the saved
+    dtype, which a ``StateDict`` takes as is (``nn.Module.load_state_dict``
+    would then cast it into its parameter; DTensor targets are cast in place
+    by the scatter, ``tests/test_dist_random.py``)."""
+    if isinstance(v, torch.Tensor):
+        if v.is_quantized or not v.is_floating_point() or v.dtype not in FLOAT_CASTS:
+            return _blank(v), v
+        dtype = rng.choice(FLOAT_CASTS) if rng.random() < 0.4 else v.dtype
+        dev = v.device
+        if rng.random() < 0.3:
+            dev = torch.device("cpu") if v.is_cuda else torch.device("cuda", 0)
+        z = torch.zeros(v.shape, dtype=dtype, device=dev)
+        return z, (v.to(device=dev) if dtype == v.dtype else v)
+    if isinstance(v, dict):
+        pairs = {k: _cross(x, rng) for k, x in v.items()}
+        return {k: a for k, (a, _b) in pairs.items()}, {k: b for k, (_a, b) in pairs.items()}
+    if isinstance(v, list):
+        pairs = [_cross(x, rng) for x in v]
+        return [a for a, _b in pairs], [b for _a, b in pairs]
+    return "placeholder", v
+
+
 def _random_tuning(rng: random.Random) -> dict:
     """Engine constants far from their defaults: tiny rings that wrap many
     times per blob, one slot, one copy in flight, no idle pool kept."""
@@ -99,11 +128,12 @@ def _random_tuning(rng: random.Random) -> dict:
     }
 
 
-def _round_trip(tmp_path, seed: int, device: str, tuning: bool = False) -> None:
+def _round_trip(tmp_path, seed: int, device: str, tuning: bool = False,
+                cross: bool = False) -> None:
     rng = random.Random(seed)
     if tuning:
         with knobs.override_tuning(**_random_tuning(random.Random(seed + 7))):
-            return _round_trip(tmp_path, seed, device)
+            return _round_trip(tmp_path, seed, device, cross=cross)
     state = _random_state(rng, device)
     compression = rng.choice(["none", "hsz1", "hsz1+host"])
     batching = rng.random() < 0.7
@@ -125,13 +155,17 @@ def _round_trip(tmp_path, seed: int, device: str, tuning: bool = False) -> None:
                 snap = Snapshot.async_take(path, app, compression=compression).wait()
             else:
                 snap = Snapshot.take(path, app, compression=compression)
-            target = {"app": StateDict(**_blank(state))}
+            if cross:
+                tgt, expect = _cross(state, random.Random(seed + 11))
+            else:
+                tgt, expect = _blank(state), state
+            target = {"app": StateDict(**tgt)}
             Snapshot(path).restore(target, verify=rng.random() < 0.3)
         finally:
             for c in reversed(ctx):
                 if c is not None:
                     c.__exit__(None, None, None)
-    assert_state_dict_eq(dict(target["app"]), state, f"case {case}")
+    assert_state_dict_eq(dict(target["app"]), expect, f"case {case}")
     # read_object of top-level tensor leaves: into a fresh buffer, and into a
     # zeroed obj_out under a random memory budget (tiled reads)
     from hipsnapshot.format.flatten import encode_key
@@ -207,3 +241,11 @@ def test_random_state_round_trip_gpu_engine_tuning(tmp_path, gpu, seed):
 @pytest.mark.parametrize("seed", range(500, 506))
 def test_random_state_round_trip_cpu_engine_tuning(tmp_path, seed):
     _round_trip(tmp_path, seed, "cpu", tuning=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(700, 700 + int(os.environ.get("HS_E2E_GPU_SEEDS", "24"))))
+def test_random_state_round_trip_gpu_cross_dtype_device(tmp_path, gpu, seed):
+    """Restore targets of another float dtype and / or on the other device
+    (GPU -> host, host -> GPU): cast kernels and H2D / D2H on restore."""
+    _round_trip(tmp_path, seed, "cuda:0", cross=True)
