@@ -249,3 +249,44 @@ def test_random_state_round_trip_gpu_cross_dtype_device(tmp_path, gpu, seed):
     """Restore targets of another float dtype and / or on the other device
     (GPU -> host, host -> GPU): cast kernels and H2D / D2H on restore."""
     _round_trip(tmp_path, seed, "cuda:0", cross=True)
+
+
+def _alias_case(tmp_path, seed: int, device: str) -> None:
+    """Entries that share storage: a tied weight listed twice, overlapping
+    slices and a transpose of one base tensor (slab gather, HBM freeze and
+    in-place restore must each see consistent bytes)."""
+    rng = random.Random(seed)
+    n = rng.randint(8, 600)
+    base = torch.randn(n, 16, device=device).to(rng.choice([torch.float32, torch.bfloat16]))
+    a0, a1 = sorted(rng.sample(range(n), 2))
+    b0 = rng.randrange(a0, a1 + 1)
+    def views(t):
+        return {"tied_a": t, "tied_b": t, "s1": t[a0:a1 + 1], "s2": t[b0:],
+                "tr": t.t(), "col": t[:, 3:9]}
+    state = views(base)
+    comp = rng.choice(["none", "hsz1"])
+    path = os.path.join(str(tmp_path), f"al{seed}")
+    ref = base.clone()
+    if rng.random() < 0.5:
+        pend = Snapshot.async_take(path, {"sd": StateDict(**state)}, compression=comp)
+        base.add_(1)  # after the take: not in the snapshot
+        pend.wait()
+    else:
+        Snapshot.take(path, {"sd": StateDict(**state)}, compression=comp)
+    fresh = torch.zeros_like(base)
+    out = StateDict(**views(fresh))
+    Snapshot(path).restore({"sd": out})
+    assert torch.equal(fresh, ref), (seed, device, comp)
+    for k, v in views(ref).items():
+        assert torch.equal(out[k], v), (seed, k)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_aliased_entries_round_trip_cpu(tmp_path, seed):
+    _alias_case(tmp_path, seed, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(100, 100 + int(os.environ.get("HS_E2E_GPU_SEEDS", "24"))))
+def test_aliased_entries_round_trip_gpu(tmp_path, gpu, seed):
+    _alias_case(tmp_path, seed, "cuda:0")
