@@ -129,6 +129,7 @@ def _worker(root: str, n_cases: int, seed: int, device: str = "cpu",
         dist.barrier()
 
 
+@pytest.mark.slow  # the strided test below covers plain placements too (CPU time)
 @pytest.mark.parametrize("seed", [1])
 def test_random_dtensor_layouts_reshard_exactly(tmp_path, seed):
     run_distributed(_worker, 4, str(tmp_path), 10, seed, timeout=400)
@@ -307,6 +308,7 @@ def _comm_worker(n_rounds: int, seed: int) -> None:
     dist.barrier()
 
 
+@pytest.mark.slow  # 4 s of spawned ranks; --run-slow (CI) runs it
 @pytest.mark.parametrize("world", [3])
 def test_random_comm_payloads(world):
     run_distributed(_comm_worker, world, 40, 17 + world, timeout=240)

@@ -100,7 +100,7 @@ def _resume_case(tmp_path, seed: int, device: str) -> None:
         assert torch.equal(v, ref_state[n]), (case, n)
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_RESUME_SEEDS", "6"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("HS_RESUME_SEEDS", "4"))))
 def test_random_resume_is_bit_identical_cpu(tmp_path, seed):
     _resume_case(tmp_path, seed, "cpu")
 
