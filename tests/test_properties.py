@@ -22,6 +22,7 @@ The reference tests the same behaviour on hand-picked cases
 `test_partitioner.py`); these search the space.
 """
 
+import os
 from collections import OrderedDict
 from itertools import product
 
@@ -41,7 +42,7 @@ from hipsnapshot.io.sharded import (  # noqa: E402
 )
 from hipsnapshot.parallel.partitioner import plan_partition  # noqa: E402
 
-SETTINGS = settings(max_examples=150, deadline=None)
+SETTINGS = settings(max_examples=int(os.environ.get("HS_PROP_EXAMPLES", "150")), deadline=None)
 
 
 # ---- DTensor layouts -------------------------------------------------------------
@@ -289,7 +290,7 @@ def codec_inputs(draw):
     return raw.tobytes(), w, frame
 
 
-@settings(max_examples=60, deadline=None)
+@settings(max_examples=int(os.environ.get("HS_PROP_EXAMPLES", "60")), deadline=None)
 @given(codec_inputs())
 def test_hsz1_native_matches_reference_and_is_lossless(inp):
     from hipsnapshot.ops import codec
